@@ -1,0 +1,223 @@
+/* me_hip.h — C ABI of the MI355X-native stereo-VO hot path (libme_hip.so).
+ *
+ * Drop-in boundary for abeauvisage/uasl_motion_estimation.  Every entry point
+ * names the reference interface it replaces (paths relative to the reference
+ * root).  Plain pointers and sizes only: no OpenCV / Eigen / Ceres / torch
+ * types cross this boundary.  The C++ adapters that keep the reference's
+ * include/MotionEstimation signatures live in include/MotionEstimationAMD/.
+ *
+ * Conventions
+ *  - Every function returns ME_OK (0) or a negative ME_ERR_* code; the
+ *    message of the last error on a context is returned by me_last_error().
+ *  - One me_ctx per host thread (the reference is single-threaded).  A ctx
+ *    owns a HIP device, a stream and scratch memory.
+ *  - `mem` = ME_HOST: pointers are host memory, the call copies in/out and
+ *    returns when results are on the host.  ME_DEVICE: pointers are device
+ *    memory on the ctx device; the call is asynchronous on the ctx stream
+ *    (call me_synchronize() before reading results on the host).
+ *  - Images are 8-bit grayscale, row-major with a stride in bytes (the
+ *    reference reads CV_8U images, src/core/file_IO.cpp:300,304).
+ */
+#ifndef ME_HIP_H
+#define ME_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ME_ABI_VERSION 1
+
+enum {
+  ME_OK = 0,
+  ME_ERR_INVALID = -1,     /* bad argument / shape (reference: assert / cv::Exception) */
+  ME_ERR_HIP = -2,         /* HIP runtime error */
+  ME_ERR_NOMEM = -3,
+  ME_ERR_UNSUPPORTED = -4,
+  ME_ERR_STATE = -5,       /* misuse of a stateful object (reference: std::cerr + status) */
+  ME_ERR_NO_DEVICE = -6    /* no HIP device: the product path never falls back to the CPU */
+};
+
+typedef enum { ME_HOST = 0, ME_DEVICE = 1 } me_mem;
+
+typedef struct me_ctx me_ctx;
+
+/* ---- context ---------------------------------------------------------- */
+int me_abi_version(void);
+int me_device_count(int* n);
+int me_create(me_ctx** out, int hip_device);
+void me_destroy(me_ctx* ctx);
+const char* me_last_error(const me_ctx* ctx);
+/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
+   NULL restores the ctx-owned stream. */
+int me_set_stream(me_ctx* ctx, void* hip_stream);
+void* me_get_stream(me_ctx* ctx);
+int me_synchronize(me_ctx* ctx);
+int me_malloc(me_ctx* ctx, void** dptr, size_t bytes);
+int me_free(me_ctx* ctx, void* dptr);
+int me_memcpy_h2d(me_ctx* ctx, void* dst, const void* src, size_t bytes);
+int me_memcpy_d2h(me_ctx* ctx, void* dst, const void* src, size_t bytes);
+int me_memcpy_d2d(me_ctx* ctx, void* dst, const void* src, size_t bytes);
+
+/* Per-kernel timing with HIP events on the ctx stream (for bench.py's
+   roofline): enable, then read the number of launches and the summed
+   milliseconds of a kernel family. */
+enum { ME_KT_MI = 0, ME_KT_SCALE_RES = 1, ME_KT_SCALE_NEQ = 2, ME_KT_BA_LINEARIZE = 3, ME_KT_BA_POINTS = 4,
+       ME_KT_BA_SCHUR = 5, ME_KT_BA_SOLVE = 6, ME_KT_BA_STEP = 7, ME_KT_KLT = 8, ME_KT_PYR = 9, ME_KT_NMS = 10,
+       ME_KT_COUNT = 16 };
+int me_timing_enable(me_ctx* ctx, int on);
+int me_timing_read(me_ctx* ctx, int kernel, long* launches, double* total_ms);
+int me_timing_reset(me_ctx* ctx);
+
+/* ---- A1/A2: mutual information ---------------------------------------
+ * Replaces float me::computeMutualInformation(const cv::Mat&, const cv::Mat&)
+ * (include/MotionEstimation/core/mutual_information.h:20,
+ *  src/core/mutual_information.cpp:55-86), batched: n patch pairs of
+ * patch_w x patch_h pixels whose top-left corners are xyL[2k],xyL[2k+1] in imgL
+ * and xyR[2k],xyR[2k+1] in imgR (the reference truncates ROI corners to int,
+ * SURVEY A-4).  Bit-exact with the reference's float result (20-bin calcHist,
+ * fl32(c*fl32(1/N)) normalisation, row-major float sum, glibc log2f). */
+int me_mi_scores(me_ctx* ctx, me_mem mem, const uint8_t* imgL, int strideL, const uint8_t* imgR, int strideR,
+                 int width, int height, const int32_t* xyL, const int32_t* xyR, int n, int patch_w, int patch_h,
+                 float* mi_out);
+/* Whole-patch form (any size, the literal computeMutualInformation(L, R)). */
+int me_mutual_information(me_ctx* ctx, me_mem mem, const uint8_t* L, int strideL, const uint8_t* R, int strideR,
+                          int w, int h, float* mi_out);
+/* me::computeEntropy (src/core/mutual_information.cpp:28-45). */
+int me_entropy(me_ctx* ctx, me_mem mem, const uint8_t* img, int stride, int w, int h, float* out);
+
+/* ---- A4-A9: ScaleState optimiser --------------------------------------
+ * Replaces me::optimisation::Optimiser<ScaleState, std::vector<std::pair<cv::Mat,cv::Mat>>>
+ * (include/MotionEstimation/optimisation/optimisation.h:76-125,
+ *  src/optimisation/optimisation.cpp:29-228,435-747).  The state is the
+ * flattened ScaleState: tracks (WBA_Ptf) as homogeneous points + flags, the
+ * last poses of the window, intrinsics, scale, baseline, window size and the
+ * last keyframe image pair (m_obs[poses.first.size()-1]). */
+typedef struct {
+  int n_left, n_right;
+  const double* X_left;      /* 4*n_left, WBA_Point::get3DLocation() */
+  const double* X_right;     /* 4*n_right */
+  const uint8_t* tri_left;   /* WBA_Point::isTriangulated() */
+  const uint8_t* tri_right;
+  const uint32_t* last_left; /* WBA_Point::getLastFrameIdx() */
+  const uint32_t* last_right;
+  uint32_t lframe;           /* poses.first[0].ID + poses.first.size()-1 */
+  double K1[9], K2[9];       /* state.K.first / .second, row-major */
+  double q1[4], t1[3];       /* poses.first.back(): Quat (w,x,y,z), position */
+  double q2[4], t2[3];       /* poses.second.back() */
+  double scale, baseline;
+  int window_size;
+  const uint8_t* imgL;       /* m_obs[f_idx].first  (mem = img_mem) */
+  const uint8_t* imgR;       /* m_obs[f_idx].second */
+  int stride, cols, rows;
+  int bb_cols, bb_rows;      /* m_obs[0].first.cols, m_obs[1].first.rows */
+  const uint8_t* mask;       /* optional Eigen::VectorXi mask as 0/1 bytes (host) */
+  int mask_len;
+  me_mem img_mem;
+} me_scale_state;
+
+typedef struct {
+  int type;                  /* 0 = OptimType::GN, 1 = OptimType::LM */
+  int minim;
+  int max_nb_iter;
+  double v, tau, mu, abs_tol, grad_tol, incr_tol, rel_tol, alpha;
+  int weighting;
+} me_optim_params;
+
+/* OptimisationParams() defaults (optimisation.h:31) */
+void me_optim_default_params(me_optim_params* p);
+/* Optimiser::compute_residuals (optimisation.cpp:149-228): res has
+   n_left+n_right slots; *n_rows receives the row count. */
+int me_scale_residuals(me_ctx* ctx, const me_scale_state* s, int weighting, double* res, int* n_rows);
+/* Optimiser::compute_normal_equations (optimisation.cpp:435-537). */
+int me_scale_normal_equations(me_ctx* ctx, const me_scale_state* s, int weighting, const double* res, double* JJ,
+                              double* e);
+/* Optimiser::compute_jacobian / getJacobian (optimisation.cpp:539-634). */
+int me_scale_jacobian(me_ctx* ctx, const me_scale_state* s, int weighting, double* JJ);
+/* Optimiser::optimise (optimisation.cpp:29-147): updates s->scale, returns the
+   StopCondition (rotation_utils.h:20) in *stop. trace: {e1, scale} per outer
+   iteration (optional). */
+int me_scale_optimise(me_ctx* ctx, me_scale_state* s, const me_optim_params* p, int test, int* stop,
+                      int* iterations, double* trace, int trace_cap, long* mi_evals);
+/* Optimiser::compute_inliers (optimisation.cpp:732-747): row indices. */
+int me_scale_inliers(me_ctx* ctx, const me_scale_state* s, int weighting, double threshold, int* idx, int cap,
+                     int* n_out);
+
+/* ---- A13-A17: windowed stereo bundle adjustment ----------------------
+ * Replaces me::optimisation::BundleAdjuster<4>::optimise(int fixedFrames)
+ * (include/MotionEstimation/optimisation/BundleAdjuster.h:142-180,431-476)
+ * and the Ceres solve it wraps: StereoReprojectionError residual/Jacobian,
+ * HuberLoss(1.0), LM trust region with Jacobi scaling, point-first Schur
+ * elimination, box bounds on points.  cams are Matx61d {t, angle-axis}
+ * (BundleAdjuster.h:297-310), observations Observation<4>. */
+typedef struct {
+  int n_cams, n_pts, n_obs;
+  double* cams;              /* n_cams*6, updated in place */
+  double* pts;               /* n_pts*3, updated in place */
+  const double* obs;         /* n_obs*4 {xL, yL, xR, yR} */
+  const int32_t* cam_idx;    /* Observation::camIdx */
+  const int32_t* pt_idx;     /* Observation::ptIdx */
+  double K0[9], K1[9];       /* CalibrationParameters::K[0], K[1] */
+  double baseline, feat_var;
+  int fixed_frames;          /* optimise(fixedFrames) */
+} me_ba_problem;
+
+typedef struct {
+  int max_num_iterations;          /* Ceres default 50 */
+  double function_tolerance;       /* 1e-3 (BundleAdjuster.h:465) */
+  double gradient_tolerance;       /* 1e-10 */
+  double parameter_tolerance;      /* 1e-8 */
+  double initial_trust_region_radius, max_trust_region_radius, min_trust_region_radius;
+  double min_lm_diagonal, max_lm_diagonal, min_relative_decrease;
+  int max_num_consecutive_invalid_steps;
+  int jacobi_scaling;
+} me_ba_options;
+
+typedef struct {
+  int status;                /* BundleAdjuster::Status: 2 SUCCESSFUL, 3 FAILED */
+  int termination;           /* 0 CONVERGENCE, 1 NO_CONVERGENCE, 2 FAILURE */
+  int iterations;
+  int successful_steps;
+  double initial_cost, final_cost;
+} me_ba_summary;
+
+void me_ba_default_options(me_ba_options* o);
+int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_summary* s);
+/* Cost (Ceres ½Σρ) at the problem's current parameters. */
+int me_ba_cost(me_ctx* ctx, const me_ba_problem* p, double* cost);
+/* Residuals (sigma-scaled, uncorrected) and Jacobian blocks per observation:
+   res 4/obs, Jc 24/obs (row-major 4x6), Jp 12/obs (4x3). */
+int me_ba_evaluate(me_ctx* ctx, const me_ba_problem* p, double* res, double* Jc, double* Jp);
+/* Reduced camera system of the first LM step at trust radius `radius`
+   (scaled coordinates), S (6m x 6m row-major) and b (6m), m = non-fixed cams. */
+int me_ba_reduced_system(me_ctx* ctx, const me_ba_problem* p, double radius, double* S, double* b);
+
+/* Landmark-sharded solve: this rank holds all cameras and a
+   subset of the points with their observations.  At each exchange point the
+   solver calls allreduce(dev_ptr, n_doubles, user) which must sum the device
+   buffer over ranks in place (e.g. RCCL all_reduce through torch.distributed)
+   on the ctx stream. */
+typedef int (*me_allreduce_fn)(double* dev_buf, int n, void* user);
+int me_ba_solve_sharded(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn allreduce,
+                        void* user, me_ba_summary* s);
+
+/* ---- A12: KLT feature tracking (build-defined; no reference) ---------- */
+typedef struct { int win; int max_level; int max_iters; double eps; double min_eig; } me_klt_params;
+void me_klt_default_params(me_klt_params* p);
+int me_klt_track(me_ctx* ctx, me_mem mem, const uint8_t* prev, const uint8_t* next, int width, int height,
+                 int stride, const float* pts_in, float* pts_out, uint8_t* status, int n, const me_klt_params* p);
+
+/* ---- A11: non-maximum suppression ------------------------------------
+ * Replaces std::vector<pt2D> me::nonMaxSupScanline3x3(const cv::Mat& input,
+ * cv::Mat& output) (include/MotionEstimation/core/feature_types.h:270,
+ * src/core/feature_types.cpp:253-351): response is CV_64F (h x w doubles),
+ * mask_out h*w bytes (255 = maximum), maxima 2*cap doubles (row-major scan
+ * order, (row+0.5+dr, col+0.5+dc)). */
+int me_nms_scanline3x3(me_ctx* ctx, me_mem mem, const double* response, int width, int height, uint8_t* mask_out,
+                       double* maxima, int cap, int* n_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ME_HIP_H */

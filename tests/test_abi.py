@@ -1,0 +1,55 @@
+"""CPU tests of the drop-in boundary: the C ABI library loads and exports every
+symbol include/me_hip.h declares; without a device the product path fails
+loudly (no CPU fallback)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "me_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(me_[a-z0-9_]+)\s*\(", src))
+    names.discard("me_allreduce_fn")
+    return names
+
+
+def test_library_builds_and_loads():
+    from uasl_motion_estimation_amd import _lib
+
+    lib = _lib.load_library()
+    assert lib.me_abi_version() == 1
+
+
+def test_exports_every_header_symbol():
+    from uasl_motion_estimation_amd import _lib
+
+    so = _lib.LIB_PATH
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (me_[a-z0-9_]+)", out))
+    declared = _header_symbols()
+    assert declared, "no declarations parsed"
+    missing = declared - exported
+    assert not missing, f"declared in me_hip.h but not exported: {missing}"
+    assert declared == set(_lib.EXPORTS), declared ^ set(_lib.EXPORTS)
+
+
+def test_code_object_is_gfx950():
+    from uasl_motion_estimation_amd import _lib
+
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob, "libme_hip.so carries no gfx950 code object"
+
+
+def test_no_device_fails_loudly():
+    """On a machine without a GPU, creating a context must raise, never fall back to the CPU."""
+    from uasl_motion_estimation_amd import _lib
+
+    if _lib.device_count() > 0:
+        pytest.skip("a device is present")
+    with pytest.raises(_lib.MEError):
+        _lib.Context(0)

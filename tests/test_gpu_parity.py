@@ -1,0 +1,260 @@
+"""GPU parity tests: libme_hip.so (through the C ABI) vs the CPU restatement.
+
+Bars (north star):
+  * MI scores, histograms, NMS maxima/order, KLT positions/status, ROI
+    decisions of the scale optimiser: bit-exact;
+  * BA pose / point parameters: 1e-6 relative (FP64, reduction order differs);
+  * scale optimiser: identical stop condition and scale within 1e-9.
+"""
+import numpy as np
+import pytest
+
+from uasl_motion_estimation_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+# ------------------------------------------------------------------ MI (A1/A2)
+@pytest.mark.parametrize("patch", [(11, 11), (10, 10), (15, 15), (3, 7), (1, 1)])
+def test_mi_scores_bit_exact(ctx, oracle, patch):
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    pw, ph = patch
+    L, R, xyL, xyR = S.random_patches(100 + pw, 320, 240, 4099, pw, ph)
+    got = mi_scores(L, R, xyL, xyR, patch, ctx=ctx)
+    ref = oracle.mi_scores(L, R, xyL, xyR, pw, ph)
+    assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
+
+
+def test_mi_edge_patches(ctx, oracle):
+    from uasl_motion_estimation_amd.mutual_information import computeEntropy, computeMutualInformation
+
+    rng = np.random.default_rng(5)
+    cases = [np.full((11, 11), 200, np.uint8), np.zeros((11, 11), np.uint8), rng.integers(0, 256, (11, 11)),
+             rng.integers(0, 256, (10, 10)), rng.integers(0, 256, (37, 53)), rng.integers(0, 256, (480, 640))]
+    for A in cases:
+        A = A.astype(np.uint8)
+        B = np.roll(A, 3, axis=1)
+        for X, Y in ((A, B), (A, A), (B, 255 - A)):
+            got = computeMutualInformation(X, Y, ctx)
+            assert np.float32(got).view(np.uint32) == np.float32(oracle.mutual_information(X, Y)).view(np.uint32)
+        assert np.float32(computeEntropy(A, ctx)) == np.float32(oracle.entropy(A))
+
+
+def test_mi_batch_empty_and_single(ctx, oracle):
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    L, R, xyL, xyR = S.random_patches(3, 64, 48, 1, 11, 11)
+    assert mi_scores(L, R, xyL[:0], xyR[:0], (11, 11), ctx=ctx).shape == (0,)
+    got = mi_scores(L, R, xyL, xyR, (11, 11), ctx=ctx)
+    assert np.array_equal(bits(got), bits(oracle.mi_scores(L, R, xyL, xyR, 11, 11)))
+
+
+def test_mi_rejects_out_of_image(ctx):
+    from uasl_motion_estimation_amd import MEError
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    L = np.zeros((20, 20), np.uint8)
+    with pytest.raises(MEError):
+        mi_scores(L, L, np.array([[15, 0]], np.int32), np.array([[0, 0]], np.int32), (11, 11), ctx=ctx)
+
+
+# ------------------------------------------------------------------ ScaleState (A4-A8)
+@pytest.fixture(scope="module")
+def scale_prob():
+    return S.scale_problem(3, 640, 480, 300)
+
+
+def test_scale_residuals_bit_exact(ctx, oracle, scale_prob):
+    from uasl_motion_estimation_amd.optimisation import scale_residuals
+
+    got = scale_residuals(scale_prob, ctx=ctx)
+    ref = oracle.scale_residuals(scale_prob)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref), np.flatnonzero(got != ref)[:10]
+
+
+def test_scale_residuals_with_mask_and_weighting(ctx, oracle, scale_prob):
+    import dataclasses
+
+    from uasl_motion_estimation_amd.optimisation import scale_residuals
+
+    n = len(scale_prob.X_left) + len(scale_prob.X_right)
+    mask = (np.random.default_rng(1).random(n) < 0.8).astype(np.uint8)
+    sp = dataclasses.replace(scale_prob, mask=mask)
+    try:
+        ref = oracle.scale_residuals(sp)
+    except RuntimeError:
+        pytest.skip("mask selects fewer rows than tracks (reference UB)")
+    got = scale_residuals(sp, ctx=ctx)
+    assert np.array_equal(got, ref)
+    got_w = scale_residuals(scale_prob, weighting=True, ctx=ctx)
+    ref_w = oracle.scale_residuals(scale_prob, weighting=1)
+    assert np.array_equal(got_w, ref_w)
+
+
+def test_scale_normal_equations(ctx, oracle, scale_prob):
+    from uasl_motion_estimation_amd.optimisation import scale_normal_equations
+
+    r = oracle.scale_residuals(scale_prob)
+    JJ, e = scale_normal_equations(scale_prob, r, ctx=ctx)
+    rJJ, re = oracle.scale_normal_equations(scale_prob, r)
+    np.testing.assert_allclose([JJ, e], [rJJ, re], rtol=1e-12)
+
+
+def test_scale_jacobian(ctx, oracle, scale_prob):
+    from uasl_motion_estimation_amd.optimisation import scale_jacobian
+
+    np.testing.assert_allclose(scale_jacobian(scale_prob, ctx=ctx), oracle.scale_jacobian(scale_prob), rtol=1e-12)
+
+
+@pytest.mark.parametrize("seed,scale0", [(3, 1.02), (4, 0.97), (5, 1.0)])
+def test_scale_optimise(ctx, oracle, seed, scale0):
+    import dataclasses
+
+    from uasl_motion_estimation_amd.optimisation import scale_optimise
+
+    sp = dataclasses.replace(S.scale_problem(seed, 640, 480, 300), scale=scale0)
+    got = scale_optimise(sp, ctx=ctx)
+    ref = oracle.scale_optimise(sp)
+    assert int(got["stop"]) == ref["stop"]
+    assert got["iterations"] == ref["iterations"]
+    np.testing.assert_allclose(got["scale"], ref["scale"], rtol=1e-9)
+    np.testing.assert_allclose(got["trace"], ref["trace"], rtol=1e-9)
+
+
+def test_scale_optimise_test_mode(ctx, oracle, scale_prob):
+    from uasl_motion_estimation_amd.optimisation import scale_optimise
+
+    got = scale_optimise(scale_prob, test=True, ctx=ctx)
+    ref = oracle.scale_optimise(scale_prob, test=1)
+    assert int(got["stop"]) == ref["stop"] and got["iterations"] == ref["iterations"]
+    np.testing.assert_allclose(got["scale"], ref["scale"], rtol=1e-12)
+
+
+def test_scale_inliers(ctx, oracle, scale_prob):
+    from uasl_motion_estimation_amd.optimisation import scale_inliers
+
+    assert np.array_equal(scale_inliers(scale_prob, 1.5, ctx=ctx), oracle.scale_inliers(scale_prob, 1.5))
+
+
+# ------------------------------------------------------------------ BA (A13-A17)
+@pytest.fixture(scope="module")
+def ba_small():
+    return S.ba_problem(21, 250, 8, 640, 480)
+
+
+def test_ba_residuals_and_jacobians(ctx, oracle, ba_small):
+    from uasl_motion_estimation_amd.optimisation import ba_evaluate
+
+    r, Jc, Jp = ba_evaluate(ba_small, ctx=ctx)
+    rr, rJc, rJp = oracle.ba_evaluate(ba_small)
+    np.testing.assert_allclose(r, rr, rtol=1e-12, atol=1e-9)
+    scale_c = np.abs(rJc).max()
+    scale_p = np.abs(rJp).max()
+    np.testing.assert_allclose(Jc, rJc, rtol=1e-9, atol=1e-12 * scale_c)
+    np.testing.assert_allclose(Jp, rJp, rtol=1e-9, atol=1e-12 * scale_p)
+
+
+def test_ba_cost(ctx, oracle, ba_small):
+    from uasl_motion_estimation_amd.optimisation import ba_cost
+
+    np.testing.assert_allclose(ba_cost(ba_small, ctx=ctx), oracle.ba_cost(ba_small), rtol=1e-12)
+
+
+def test_ba_reduced_system(ctx, oracle, ba_small):
+    from uasl_motion_estimation_amd.optimisation import ba_reduced_system
+
+    S_, b = ba_reduced_system(ba_small, 1e4, ctx=ctx)
+    rS, rb, rc = oracle.ba_reduced_system(ba_small, 1e4)
+    assert rc == 0
+    np.testing.assert_allclose(S_, rS, rtol=1e-9, atol=1e-9 * np.abs(rS).max())
+    np.testing.assert_allclose(b, rb, rtol=1e-9, atol=1e-9 * np.abs(rb).max())
+
+
+@pytest.mark.parametrize("seed,n,w,fixed", [(21, 250, 8, 2), (22, 120, 5, 2), (23, 400, 12, 1), (24, 60, 4, 0)])
+def test_ba_solve_default_options(ctx, oracle, seed, n, w, fixed):
+    from uasl_motion_estimation_amd.optimisation import ba_solve
+
+    bp = S.ba_problem(seed, n, w, 640, 480, fixed=fixed)
+    cams, pts, s = ba_solve(bp, ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp)
+    assert s["iterations"] == rs["iterations"] and s["termination"] == rs["termination"], (s, rs)
+    assert s["status"] == rs["status"] == 2
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(s["final_cost"], rs["final_cost"], rtol=1e-9)
+
+
+def test_ba_fixed_iterations_config2(ctx, oracle):
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    c = S.CONFIGS[2]
+    bp = S.ba_problem(S.SEED0 + 2, c["n_feats"], c["window"], c["width"], c["height"])
+    cams, pts, s = ba_solve(bp, SolverOptions.fixed_iterations(10), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert s["iterations"] == rs["iterations"] == 10
+    assert s["successful_steps"] == rs["successful_steps"]
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+def test_ba_infeasible_start_fails(ctx):
+    from uasl_motion_estimation_amd.optimisation import ba_solve
+
+    bp = S.ba_problem(25, 30, 4, 320, 240)
+    bp.pts[0, 2] = 1e9  # beyond Zmax -> Ceres refuses the problem
+    cams, pts, s = ba_solve(bp, ctx=ctx)
+    assert s["status"] == 3
+    assert np.array_equal(cams, bp.cams)
+
+
+# ------------------------------------------------------------------ NMS (A11)
+@pytest.mark.parametrize("kind", ["smooth", "plateaus", "ties", "tiny"])
+def test_nms_bit_exact(ctx, oracle, kind):
+    from uasl_motion_estimation_amd.feature_types import nonMaxSupScanline3x3
+
+    rng = np.random.default_rng({"smooth": 1, "plateaus": 2, "ties": 3, "tiny": 4}[kind])
+    if kind == "smooth":
+        resp = rng.random((300, 400))
+    elif kind == "plateaus":
+        resp = np.floor(rng.random((200, 260)) * 4.0)
+    elif kind == "ties":
+        resp = np.kron(rng.integers(0, 3, (50, 70)), np.ones((2, 3))).astype(np.float64)
+    else:
+        resp = rng.random((3, 3))
+    got, gmask = nonMaxSupScanline3x3(resp, ctx)
+    ref, rmask = oracle.nms(resp)
+    assert got.shape == ref.shape
+    assert np.array_equal(got, ref)
+    assert np.array_equal(gmask, rmask)
+
+
+def test_nms_tall_image_multi_pass(ctx, oracle):
+    from uasl_motion_estimation_amd.feature_types import nonMaxSupScanline3x3
+
+    rng = np.random.default_rng(9)
+    resp = np.floor(rng.random((2100, 40)) * 3.0)
+    got, gm = nonMaxSupScanline3x3(resp, ctx)
+    ref, rm = oracle.nms(resp)
+    assert np.array_equal(got, ref) and np.array_equal(gm, rm)
+
+
+# ------------------------------------------------------------------ KLT (A12)
+def test_klt_bit_exact(ctx, oracle):
+    from uasl_motion_estimation_amd.klt import calcOpticalFlowPyrLK
+
+    scene, K, frames = S.stereo_stream(31, 640, 480, 2)
+    rng = np.random.default_rng(0)
+    pts = S.grid_features(rng, 500, 640, 480, 8).astype(np.float32)
+    pts[:5] = [[1, 1], [639, 479], [-5, 10], [320.5, 240.25], [630, 10]]  # border cases
+    got, gst = calcOpticalFlowPyrLK(frames[0].left, frames[1].left, pts, ctx=ctx)
+    ref, rst = oracle.klt(frames[0].left, frames[1].left, pts)
+    assert np.array_equal(gst, rst)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst.mean() > 0.8

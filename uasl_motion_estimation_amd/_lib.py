@@ -1,0 +1,279 @@
+"""ctypes binding of libme_hip.so (the C ABI declared in include/me_hip.h).
+
+The product path has no CPU fallback: if the HIP library is missing or no
+device is present, every entry point raises ``MEError``.
+
+torch is imported (when available) before the library is loaded so that the
+process uses a single HIP runtime: libme_hip.so resolves ``libamdhip64.so.7``
+to the copy torch already mapped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_float, c_int, c_int32, c_long, c_size_t, c_uint8, c_uint32, c_void_p
+
+import numpy as np
+
+try:  # one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the ctypes path
+    torch = None
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libme_hip.so")
+
+ME_OK = 0
+ME_HOST = 0
+ME_DEVICE = 1
+ERRORS = {
+    -1: "ME_ERR_INVALID",
+    -2: "ME_ERR_HIP",
+    -3: "ME_ERR_NOMEM",
+    -4: "ME_ERR_UNSUPPORTED",
+    -5: "ME_ERR_STATE",
+    -6: "ME_ERR_NO_DEVICE",
+}
+
+# kernel timing families (me_hip.h ME_KT_*)
+KT = dict(MI=0, SCALE_RES=1, SCALE_NEQ=2, BA_LINEARIZE=3, BA_POINTS=4, BA_SCHUR=5, BA_SOLVE=6, BA_STEP=7,
+          KLT=8, PYR=9, NMS=10)
+
+
+class MEError(RuntimeError):
+    def __init__(self, code, msg=""):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class ScaleStateC(ctypes.Structure):
+    _fields_ = [
+        ("n_left", c_int), ("n_right", c_int),
+        ("X_left", POINTER(c_double)), ("X_right", POINTER(c_double)),
+        ("tri_left", POINTER(c_uint8)), ("tri_right", POINTER(c_uint8)),
+        ("last_left", POINTER(c_uint32)), ("last_right", POINTER(c_uint32)),
+        ("lframe", c_uint32),
+        ("K1", c_double * 9), ("K2", c_double * 9),
+        ("q1", c_double * 4), ("t1", c_double * 3),
+        ("q2", c_double * 4), ("t2", c_double * 3),
+        ("scale", c_double), ("baseline", c_double),
+        ("window_size", c_int),
+        ("imgL", c_void_p), ("imgR", c_void_p),
+        ("stride", c_int), ("cols", c_int), ("rows", c_int),
+        ("bb_cols", c_int), ("bb_rows", c_int),
+        ("mask", POINTER(c_uint8)), ("mask_len", c_int),
+        ("img_mem", c_int),
+    ]
+
+
+class OptimParamsC(ctypes.Structure):
+    _fields_ = [
+        ("type", c_int), ("minim", c_int), ("max_nb_iter", c_int),
+        ("v", c_double), ("tau", c_double), ("mu", c_double), ("abs_tol", c_double), ("grad_tol", c_double),
+        ("incr_tol", c_double), ("rel_tol", c_double), ("alpha", c_double),
+        ("weighting", c_int),
+    ]
+
+
+class BAProblemC(ctypes.Structure):
+    _fields_ = [
+        ("n_cams", c_int), ("n_pts", c_int), ("n_obs", c_int),
+        ("cams", POINTER(c_double)), ("pts", POINTER(c_double)), ("obs", POINTER(c_double)),
+        ("cam_idx", POINTER(c_int32)), ("pt_idx", POINTER(c_int32)),
+        ("K0", c_double * 9), ("K1", c_double * 9),
+        ("baseline", c_double), ("feat_var", c_double),
+        ("fixed_frames", c_int),
+    ]
+
+
+class BAOptionsC(ctypes.Structure):
+    _fields_ = [
+        ("max_num_iterations", c_int),
+        ("function_tolerance", c_double), ("gradient_tolerance", c_double), ("parameter_tolerance", c_double),
+        ("initial_trust_region_radius", c_double), ("max_trust_region_radius", c_double),
+        ("min_trust_region_radius", c_double),
+        ("min_lm_diagonal", c_double), ("max_lm_diagonal", c_double), ("min_relative_decrease", c_double),
+        ("max_num_consecutive_invalid_steps", c_int),
+        ("jacobi_scaling", c_int),
+    ]
+
+
+class BASummaryC(ctypes.Structure):
+    _fields_ = [
+        ("status", c_int), ("termination", c_int), ("iterations", c_int), ("successful_steps", c_int),
+        ("initial_cost", c_double), ("final_cost", c_double),
+    ]
+
+
+class KLTParamsC(ctypes.Structure):
+    _fields_ = [("win", c_int), ("max_level", c_int), ("max_iters", c_int), ("eps", c_double),
+                ("min_eig", c_double)]
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
+
+# every symbol include/me_hip.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
+    "me_get_stream", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
+    "me_timing_enable", "me_timing_read", "me_timing_reset",
+    "me_mi_scores", "me_mutual_information", "me_entropy",
+    "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
+    "me_scale_optimise", "me_scale_inliers",
+    "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
+    "me_ba_solve_sharded",
+    "me_klt_default_params", "me_klt_track",
+    "me_nms_scanline3x3",
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libme_hip.so and declare prototypes.  Raises MEError if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise MEError(-4, f"{path} not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    P = POINTER
+    sig = {
+        "me_abi_version": (c_int, []),
+        "me_device_count": (c_int, [P(c_int)]),
+        "me_create": (c_int, [P(c_void_p), c_int]),
+        "me_destroy": (None, [c_void_p]),
+        "me_last_error": (ctypes.c_char_p, [c_void_p]),
+        "me_set_stream": (c_int, [c_void_p, c_void_p]),
+        "me_get_stream": (c_void_p, [c_void_p]),
+        "me_synchronize": (c_int, [c_void_p]),
+        "me_malloc": (c_int, [c_void_p, P(c_void_p), c_size_t]),
+        "me_free": (c_int, [c_void_p, c_void_p]),
+        "me_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+        "me_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+        "me_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+        "me_timing_enable": (c_int, [c_void_p, c_int]),
+        "me_timing_read": (c_int, [c_void_p, c_int, P(c_long), P(c_double)]),
+        "me_timing_reset": (c_int, [c_void_p]),
+        "me_mi_scores": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                                 c_void_p, c_int, c_int, c_int, c_void_p]),
+        "me_mutual_information": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
+                                          c_void_p]),
+        "me_entropy": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
+        "me_optim_default_params": (None, [P(OptimParamsC)]),
+        "me_scale_residuals": (c_int, [c_void_p, P(ScaleStateC), c_int, P(c_double), P(c_int)]),
+        "me_scale_normal_equations": (c_int, [c_void_p, P(ScaleStateC), c_int, P(c_double), P(c_double),
+                                              P(c_double)]),
+        "me_scale_jacobian": (c_int, [c_void_p, P(ScaleStateC), c_int, P(c_double)]),
+        "me_scale_optimise": (c_int, [c_void_p, P(ScaleStateC), P(OptimParamsC), c_int, P(c_int), P(c_int),
+                                      P(c_double), c_int, P(c_long)]),
+        "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
+        "me_ba_default_options": (None, [P(BAOptionsC)]),
+        "me_ba_solve": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), P(BASummaryC)]),
+        "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
+        "me_ba_evaluate": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_double), P(c_double)]),
+        "me_ba_reduced_system": (c_int, [c_void_p, P(BAProblemC), c_double, P(c_double), P(c_double)]),
+        "me_ba_solve_sharded": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), ALLREDUCE_FN, c_void_p,
+                                        P(BASummaryC)]),
+        "me_klt_default_params": (None, [P(KLTParamsC)]),
+        "me_klt_track": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_int, P(KLTParamsC)]),
+        "me_nms_scanline3x3": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
+                                       P(c_int)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def dptr(a: np.ndarray, ctype=c_double):
+    """POINTER(ctype) to a C-contiguous numpy array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return a.ctypes.data_as(POINTER(ctype))
+
+
+def vptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return c_void_p(a)
+    assert a.flags["C_CONTIGUOUS"], "array must be C-contiguous"
+    return c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One me_ctx (HIP device + stream + scratch).  One per host thread."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = c_void_p()
+        rc = self.lib.me_create(ctypes.byref(h), device)
+        if rc != ME_OK:
+            raise MEError(rc, f"me_create(device={device}) failed: no usable HIP device "
+                              "(the product path has no CPU fallback)")
+        self.h = h
+        self.device = device
+
+    def check(self, rc: int, what: str = ""):
+        if rc != ME_OK:
+            msg = self.lib.me_last_error(self.h)
+            raise MEError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.me_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_stream(self, stream_handle: int | None):
+        self.check(self.lib.me_set_stream(self.h, c_void_p(stream_handle) if stream_handle else None),
+                   "me_set_stream")
+
+    def synchronize(self):
+        self.check(self.lib.me_synchronize(self.h), "me_synchronize")
+
+    # --- kernel timing (HIP events on the ctx stream) ---
+    def timing(self, on: bool = True):
+        self.check(self.lib.me_timing_enable(self.h, 1 if on else 0))
+
+    def timing_reset(self):
+        self.check(self.lib.me_timing_reset(self.h))
+
+    def timing_read(self, family: str):
+        n = c_long()
+        ms = c_double()
+        self.check(self.lib.me_timing_read(self.h, KT[family], ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+
+_default_ctx = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(int(os.environ.get("ME_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+    return _default_ctx
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = c_int()
+    lib.me_device_count(ctypes.byref(n))
+    return n.value

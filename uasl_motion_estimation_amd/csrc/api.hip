@@ -1,0 +1,203 @@
+// api.hip — context, memory and timing entry points of the C ABI (me_hip.h).
+#include "me_internal.hpp"
+#include <cstring>
+
+int me_set_error(me_ctx* ctx, int code, const char* fmt, ...) {
+  if (ctx) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    ctx->err = buf;
+  }
+  return code;
+}
+
+int me_scratch(me_ctx* ctx, int slot, size_t bytes, void** out) {
+  if ((int)ctx->slot_ptr.size() <= slot) {
+    ctx->slot_ptr.resize(slot + 1, nullptr);
+    ctx->slot_size.resize(slot + 1, 0);
+  }
+  if (bytes == 0) bytes = 16;
+  if (ctx->slot_size[slot] < bytes) {
+    if (ctx->slot_ptr[slot]) {
+      ME_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      ME_HIP(ctx, hipFree(ctx->slot_ptr[slot]));
+      ctx->slot_ptr[slot] = nullptr;
+      ctx->slot_size[slot] = 0;
+    }
+    size_t sz = bytes + bytes / 4;
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) return me_set_error(ctx, ME_ERR_NOMEM, "hipMalloc(%zu) failed: %s", sz, hipGetErrorString(e));
+    ctx->slot_ptr[slot] = p;
+    ctx->slot_size[slot] = sz;
+  }
+  *out = ctx->slot_ptr[slot];
+  return ME_OK;
+}
+
+int me_pinned(me_ctx* ctx, size_t bytes, void** out) {
+  if (ctx->pinned_size < bytes) {
+    if (ctx->pinned) {
+      ME_HIP(ctx, hipStreamSynchronize(ctx->stream));
+      ME_HIP(ctx, hipHostFree(ctx->pinned));
+    }
+    ctx->pinned = nullptr;
+    ctx->pinned_size = 0;
+    size_t sz = bytes < 4096 ? 4096 : bytes;
+    ME_HIP(ctx, hipHostMalloc(&ctx->pinned, sz, hipHostMallocDefault));
+    ctx->pinned_size = sz;
+  }
+  *out = ctx->pinned;
+  return ME_OK;
+}
+
+int me_check_launch(me_ctx* ctx, const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return me_set_error(ctx, ME_ERR_HIP, "launch of %s failed: %s", what, hipGetErrorString(e));
+  return ME_OK;
+}
+
+static hipEvent_t pool_get(me_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+me_ktimer::me_ktimer(me_ctx* ctx, int kernel) : c(ctx), k(kernel) {
+  if (c && c->timing) {
+    a = pool_get(c);
+    b = pool_get(c);
+    if (a) hipEventRecord(a, c->stream);
+  }
+}
+me_ktimer::~me_ktimer() {
+  if (c && c->timing && a && b) {
+    hipEventRecord(b, c->stream);
+    c->pending.push_back({a, b, k});
+  }
+}
+
+static void drain_timers(me_ctx* c) {
+  for (auto& p : c->pending) {
+    hipEventSynchronize(p.b);
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      c->launches[p.kernel] += 1;
+      c->total_ms[p.kernel] += ms;
+    }
+    c->event_pool.push_back(p.a);
+    c->event_pool.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+extern "C" {
+
+int me_abi_version(void) { return ME_ABI_VERSION; }
+
+int me_device_count(int* n) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *n = c;
+  return ME_OK;
+}
+
+int me_create(me_ctx** out, int dev) {
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ME_ERR_NO_DEVICE;
+  if (dev < 0 || dev >= n) return ME_ERR_INVALID;
+  me_ctx* c = new me_ctx();
+  c->device = dev;
+  if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return ME_ERR_HIP;
+  }
+  c->stream = c->own_stream;
+  c->slot_ptr.assign(SLOT_COUNT, nullptr);
+  c->slot_size.assign(SLOT_COUNT, 0);
+  *out = c;
+  return ME_OK;
+}
+
+void me_destroy(me_ctx* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  drain_timers(c);
+  for (void* p : c->slot_ptr)
+    if (p) hipFree(p);
+  if (c->pinned) hipHostFree(c->pinned);
+  for (auto e : c->event_pool) hipEventDestroy(e);
+  if (c->own_stream) hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+const char* me_last_error(const me_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int me_set_stream(me_ctx* c, void* s) {
+  if (!c) return ME_ERR_INVALID;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return ME_OK;
+}
+void* me_get_stream(me_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int me_synchronize(me_ctx* c) {
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  return ME_OK;
+}
+
+int me_malloc(me_ctx* c, void** p, size_t bytes) {
+  ME_HIP(c, hipSetDevice(c->device));
+  ME_HIP(c, hipMalloc(p, bytes ? bytes : 16));
+  return ME_OK;
+}
+int me_free(me_ctx* c, void* p) {
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  ME_HIP(c, hipFree(p));
+  return ME_OK;
+}
+int me_memcpy_h2d(me_ctx* c, void* d, const void* s, size_t n) {
+  ME_HIP(c, hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  return ME_OK;
+}
+int me_memcpy_d2h(me_ctx* c, void* d, const void* s, size_t n) {
+  ME_HIP(c, hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  return ME_OK;
+}
+int me_memcpy_d2d(me_ctx* c, void* d, const void* s, size_t n) {
+  ME_HIP(c, hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, c->stream));
+  return ME_OK;
+}
+
+int me_timing_enable(me_ctx* c, int on) {
+  c->timing = on != 0;
+  return ME_OK;
+}
+int me_timing_read(me_ctx* c, int k, long* launches, double* ms) {
+  if (k < 0 || k >= ME_KT_COUNT) return ME_ERR_INVALID;
+  drain_timers(c);
+  *launches = c->launches[k];
+  *ms = c->total_ms[k];
+  return ME_OK;
+}
+int me_timing_reset(me_ctx* c) {
+  drain_timers(c);
+  for (int i = 0; i < ME_KT_COUNT; ++i) {
+    c->launches[i] = 0;
+    c->total_ms[i] = 0;
+  }
+  return ME_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1234 @@
+// ba.hip — windowed stereo bundle adjustment on MI355X.
+// Kernel map in ba_kernels.hpp.  Host side: problem upload + CSR build, the
+// per-iteration launch sequence (LM control lives on the device: every kernel
+// reads the State flags, so a whole solve can be enqueued — or captured in a
+// hipGraph — without host round trips), and the landmark-sharded variant with
+// a caller-provided all-reduce.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <vector>
+#include "me_internal.hpp"
+#include "ba_kernels.hpp"
+
+using namespace ba;
+
+namespace {
+
+constexpr double kDblMin = 2.2250738585072014e-308;
+constexpr double kDblEps = 2.220446049250313e-16;
+
+// ---------------------------------------------------------------- helpers
+template <int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* lds /* 4*NV */) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    double x = v[i];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+    v[i] = x;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      double s = 0;
+      for (int w = 0; w < nw; ++w) s += lds[w * NV + i];
+      out[i] = s;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double block_max(double v, double* lds) {
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  double r = 0;
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    r = lds[0];
+    for (int w = 1; w < nw; ++w) r = fmax(r, lds[w]);
+  }
+  __syncthreads();
+  return r;
+}
+
+// p = R(aa) X + t with dp/daa and dp/dX (ceres::AngleAxisRotatePoint values;
+// derivative: Gallego & Yezzi, d(Ru)/dw = -R[u]x (w w^T + (R^T - I)[w]x)/theta^2)
+__device__ __forceinline__ void rotate(const double* aa, const double* X, double* P, double* dPdw, double* dPdX) {
+  const double t2 = aa[0] * aa[0] + aa[1] * aa[1] + aa[2] * aa[2];
+  if (t2 > kDblEps) {
+    const double th = sqrt(t2), c = cos(th), s = sin(th), ti = 1.0 / th;
+    const double w0 = aa[0] * ti, w1 = aa[1] * ti, w2 = aa[2] * ti;
+    const double wx0 = w1 * X[2] - w2 * X[1], wx1 = w2 * X[0] - w0 * X[2], wx2 = w0 * X[1] - w1 * X[0];
+    const double tmp = (w0 * X[0] + w1 * X[1] + w2 * X[2]) * (1.0 - c);
+    P[0] = X[0] * c + wx0 * s + w0 * tmp;
+    P[1] = X[1] * c + wx1 * s + w1 * tmp;
+    P[2] = X[2] * c + wx2 * s + w2 * tmp;
+    if (dPdX) {
+      const double oc = 1.0 - c;
+      double R[9] = {c + oc * w0 * w0,      oc * w0 * w1 - s * w2, oc * w0 * w2 + s * w1,
+                     oc * w1 * w0 + s * w2, c + oc * w1 * w1,      oc * w1 * w2 - s * w0,
+                     oc * w2 * w0 - s * w1, oc * w2 * w1 + s * w0, c + oc * w2 * w2};
+      for (int i = 0; i < 9; ++i) dPdX[i] = R[i];
+      // M = (w w^T + (R^T - I)[w]x) / theta^2 with w = aa (unnormalised)
+      const double a0 = aa[0], a1 = aa[1], a2 = aa[2];
+      double Wx[9] = {0, -a2, a1, a2, 0, -a0, -a1, a0, 0};
+      double M[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          double acc = aa[i] * aa[j];
+          for (int k = 0; k < 3; ++k) acc += (R[k * 3 + i] - (i == k ? 1.0 : 0.0)) * Wx[k * 3 + j];
+          M[i * 3 + j] = acc / t2;
+        }
+      // -R [X]x M
+      double Xx[9] = {0, -X[2], X[1], X[2], 0, -X[0], -X[1], X[0], 0};
+      double RX[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) RX[i * 3 + j] = R[i * 3 + 0] * Xx[0 * 3 + j] + R[i * 3 + 1] * Xx[1 * 3 + j] + R[i * 3 + 2] * Xx[2 * 3 + j];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+          dPdw[i * 3 + j] = -(RX[i * 3 + 0] * M[0 * 3 + j] + RX[i * 3 + 1] * M[1 * 3 + j] + RX[i * 3 + 2] * M[2 * 3 + j]);
+    }
+  } else {
+    const double wx0 = aa[1] * X[2] - aa[2] * X[1], wx1 = aa[2] * X[0] - aa[0] * X[2], wx2 = aa[0] * X[1] - aa[1] * X[0];
+    P[0] = X[0] + wx0;
+    P[1] = X[1] + wx1;
+    P[2] = X[2] + wx2;
+    if (dPdX) {
+      double D[9] = {1, -aa[2], aa[1], aa[2], 1, -aa[0], -aa[1], aa[0], 1};
+      for (int i = 0; i < 9; ++i) dPdX[i] = D[i];
+      double N[9] = {0, X[2], -X[1], -X[2], 0, X[0], X[1], -X[0], 0};  // -[X]x
+      for (int i = 0; i < 9; ++i) dPdw[i] = N[i];
+    }
+  }
+}
+
+// StereoReprojectionError (BundleAdjuster.h:153-171): residual, optional J
+__device__ __forceinline__ void stereo_residual(const Geo& g, const double* cam, const double* X, const double* f,
+                                                double* r, double* Jc, double* Jp) {
+  double P[3], dPdw[9], dPdX[9];
+  rotate(cam + 3, X, P, Jc ? dPdw : nullptr, Jc ? dPdX : nullptr);
+  P[0] = P[0] + cam[0];
+  P[1] = P[1] + cam[1];
+  P[2] = P[2] + cam[2];
+  const double x1 = g.K0[0] * (P[0] / P[2]) + g.K0[2];
+  const double x2 = g.K1[0] * ((P[0] - g.baseline) / P[2]) + g.K1[2];
+  const double y = g.K0[4] * (P[1] / P[2]) + g.K0[5];
+  r[0] = g.sinv * (x1 - f[0]);
+  r[1] = g.sinv * (y - f[1]);
+  r[2] = g.sinv * (x2 - f[2]);
+  r[3] = g.sinv * (y - f[3]);
+  if (!Jc) return;
+  const double iz = 1.0 / P[2], iz2 = iz * iz;
+  double dr[4][3] = {{g.sinv * g.K0[0] * iz, 0.0, -g.sinv * g.K0[0] * P[0] * iz2},
+                     {0.0, g.sinv * g.K0[4] * iz, -g.sinv * g.K0[4] * P[1] * iz2},
+                     {g.sinv * g.K1[0] * iz, 0.0, -g.sinv * g.K1[0] * (P[0] - g.baseline) * iz2},
+                     {0.0, g.sinv * g.K0[4] * iz, -g.sinv * g.K0[4] * P[1] * iz2}};
+  for (int k = 0; k < 4; ++k) {
+    for (int j = 0; j < 3; ++j) Jc[k * 6 + j] = dr[k][j];
+    for (int j = 0; j < 3; ++j) {
+      Jc[k * 6 + 3 + j] = dr[k][0] * dPdw[0 * 3 + j] + dr[k][1] * dPdw[1 * 3 + j] + dr[k][2] * dPdw[2 * 3 + j];
+      Jp[k * 3 + j] = dr[k][0] * dPdX[0 * 3 + j] + dr[k][1] * dPdX[1 * 3 + j] + dr[k][2] * dPdX[2 * 3 + j];
+    }
+  }
+}
+
+// ceres::HuberLoss(1.0): rho0 and sqrt(rho1) (Corrector with rho'' <= 0)
+__device__ __forceinline__ void huber(double s, double* rho0, double* sqrt_rho1) {
+  if (s > 1.0) {
+    const double rr = sqrt(s);
+    *rho0 = 2.0 * rr - 1.0;
+    *sqrt_rho1 = sqrt(fmax(kDblMin, 1.0 / rr));
+  } else {
+    *rho0 = s;
+    *sqrt_rho1 = 1.0;
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+__global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
+  __shared__ double lds[4];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  const int o = blockIdx.x * kBlock + threadIdx.x;
+  double cost = 0;
+  if (o < g.no) {
+    const int cur = st->cur;
+    const int ci = b.cam_idx[o], pi = b.pt_idx[o];
+    double* L = b.lin + (long)o * kLinStride;
+    double r[4], Jc[24], Jp[12];
+    stereo_residual(g, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, b.obs + 4 * (long)o, r, Jc, Jp);
+    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    double rho0, sc;
+    huber(s, &rho0, &sc);
+    cost = 0.5 * rho0;
+    for (int k = 0; k < 4; ++k) L[k] = r[k] * sc;
+    for (int k = 0; k < 24; ++k) L[4 + k] = Jc[k] * sc;
+    for (int k = 0; k < 12; ++k) L[28 + k] = Jp[k] * sc;
+  }
+  double v[1] = {cost};
+  double out[1];
+  block_sum<1>(v, out, lds);
+  if (threadIdx.x == 0) b.part[R_COST * g.pstride + blockIdx.x] = out[0];
+}
+
+// phase 0: camera Jacobian column norms -> colnorm (6m); phase 1: U, g
+__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, int phase, double* colnorm,
+                                                              double* gc_raw) {
+  __shared__ double lds[4 * 33];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  if (phase == 0 && st->scaled) return;
+  const int ci = blockIdx.x;
+  const int beg = b.c_off[ci], end = b.c_off[ci + 1];
+  if (phase == 0) {
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    for (int q = beg + threadIdx.x; q < end; q += kBlock) {
+      const double* L = b.lin + (long)b.c_obs[q] * kLinStride;
+      for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 6; ++j) v[j] += L[4 + k * 6 + j] * L[4 + k * 6 + j];
+    }
+    double out[6];
+    block_sum<6>(v, out, lds);
+    if (threadIdx.x == 0)
+      for (int j = 0; j < 6; ++j) colnorm[6 * ci + j] = out[j];
+    return;
+  }
+  // 21 unique JtJ + 6 gradient entries, unscaled, then scaled on write
+  double v[27];
+  for (int i = 0; i < 27; ++i) v[i] = 0;
+  for (int q = beg + threadIdx.x; q < end; q += kBlock) {
+    const double* L = b.lin + (long)b.c_obs[q] * kLinStride;
+    int u = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int c = a; c < 6; ++c, ++u) {
+        double s = 0;
+        for (int k = 0; k < 4; ++k) s += L[4 + k * 6 + a] * L[4 + k * 6 + c];
+        v[u] += s;
+      }
+    for (int a = 0; a < 6; ++a) {
+      double s = 0;
+      for (int k = 0; k < 4; ++k) s += L[4 + k * 6 + a] * L[k];
+      v[21 + a] += s;
+    }
+  }
+  double out[27];
+  block_sum<27>(v, out, lds);
+  if (threadIdx.x == 0) {
+    const double* cs = b.csc + 6 * ci;
+    double* U = b.U + 36 * (long)ci;
+    int u = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int c = a; c < 6; ++c, ++u) {
+        const double x = out[u] * cs[a] * cs[c];
+        U[a * 6 + c] = x;
+        U[c * 6 + a] = x;
+      }
+    for (int a = 0; a < 6; ++a) {
+      b.gcs[6 * ci + a] = out[21 + a] * cs[a];
+      gc_raw[6 * ci + a] = out[21 + a];
+    }
+  }
+}
+
+__global__ void cam_scaling_kernel(Geo g, Bufs b, const double* colnorm) {
+  const State* st = b.st;
+  if (st->done || !st->need_lin || st->scaled) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < g.n6) b.csc[i] = 1.0 / (1.0 + sqrt(colnorm[i]));
+}
+
+__global__ __launch_bounds__(kBlock) void pt_assemble_kernel(Geo g, Bufs b, int jacobi) {
+  __shared__ double lds[4];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  double gm = 0;
+  if (j < g.np) {
+    const int beg = b.p_off[j], end = b.p_off[j + 1];
+    double* ps = b.psc + 3 * (long)j;
+    if (!st->scaled) {
+      double cn[3] = {0, 0, 0};
+      for (int q = beg; q < end; ++q) {
+        const double* L = b.lin + (long)b.p_obs[q] * kLinStride;
+        for (int k = 0; k < 4; ++k)
+          for (int a = 0; a < 3; ++a) cn[a] += L[28 + k * 3 + a] * L[28 + k * 3 + a];
+      }
+      for (int a = 0; a < 3; ++a) ps[a] = jacobi ? 1.0 / (1.0 + sqrt(cn[a])) : 1.0;
+    }
+    const double p0 = ps[0], p1 = ps[1], p2 = ps[2];
+    const double pscv[3] = {p0, p1, p2};
+    double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
+    for (int q = beg; q < end; ++q) {
+      const int o = b.p_obs[q];
+      const double* L = b.lin + (long)o * kLinStride;
+      const double* Jp = L + 28;
+      V[0] += Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
+      V[1] += Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
+      V[2] += Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
+      V[3] += Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
+      V[4] += Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
+      V[5] += Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
+      for (int a = 0; a < 3; ++a) gr[a] += Jp[a] * L[0] + Jp[3 + a] * L[1] + Jp[6 + a] * L[2] + Jp[9 + a] * L[3];
+      const int ci = b.cam_idx[o] - g.nf;
+      if (ci >= 0) {
+        const double* Jc = L + 4;
+        const double* cs = b.csc + 6 * ci;
+        double* W = b.Wo + 18 * (long)o;
+        for (int a = 0; a < 6; ++a)
+          for (int c = 0; c < 3; ++c) {
+            double s = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
+            W[a * 3 + c] = s * cs[a] * pscv[c];
+          }
+      }
+    }
+    double* Vo = b.V + 9 * (long)j;
+    Vo[0] = V[0] * p0 * p0; Vo[1] = V[1] * p0 * p1; Vo[2] = V[2] * p0 * p2;
+    Vo[3] = Vo[1];          Vo[4] = V[3] * p1 * p1; Vo[5] = V[4] * p1 * p2;
+    Vo[6] = Vo[2];          Vo[7] = Vo[5];          Vo[8] = V[5] * p2 * p2;
+    for (int a = 0; a < 3; ++a) b.gps[3 * (long)j + a] = gr[a] * pscv[a];
+    // projected gradient max-norm contribution ||x - Plus(x, -g)||_inf
+    const double* x = b.pts[st->cur] + 3 * (long)j;
+    for (int a = 0; a < 3; ++a) {
+      double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
+      gm = fmax(gm, fabs(x[a] - xp));
+    }
+  }
+  double r = block_max(gm, lds);
+  if (threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+}
+
+// Reduce linearisation partials into scal[R_COST], scal[R_GMAX_PT]
+__global__ __launch_bounds__(1024) void lin_reduce_kernel(Geo g, Bufs b) {
+  __shared__ double lds[32];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  double c = 0, m = 0;
+  for (int i = threadIdx.x; i < g.nblk_obs; i += 1024) c += b.part[R_COST * g.pstride + i];
+  for (int i = threadIdx.x; i < g.nblk_pts; i += 1024) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+  double v[1] = {c}, out[1];
+  block_sum<1>(v, out, lds);
+  double mm = block_max(m, lds + 20);
+  if (threadIdx.x == 0) {
+    b.scal[R_COST] = out[0];
+    b.scal[R_GMAX_PT] = mm;
+  }
+}
+
+// Linearisation bookkeeping + iteration start (Ceres IterationZero /
+// HandleSuccessfulStep gradient test, FinalizeIteration max-iteration and
+// min-radius tests).
+__global__ void lin_check_kernel(Geo g, Bufs b, Opts o, const double* gc_raw) {
+  if (threadIdx.x != 0) return;
+  State* st = b.st;
+  if (st->done) return;
+  if (st->need_lin) {
+    st->x_cost = b.scal[R_COST];
+    double gm = b.scal[R_GMAX_PT];
+    for (int i = 0; i < g.n6; ++i) gm = fmax(gm, fabs(gc_raw[i]));
+    if (!st->scaled) {
+      st->initial_cost = st->x_cost;
+      st->scaled = 1;
+    }
+    st->need_lin = 0;
+    if (gm <= o.gradient_tolerance) {
+      st->done = 1;
+      st->termination = 0;
+      return;
+    }
+  }
+  if (st->iterations >= o.max_num_iterations) {
+    st->done = 1;
+    st->termination = 1;
+    return;
+  }
+  if (st->radius <= o.min_radius) {
+    st->done = 1;
+    st->termination = 0;
+    return;
+  }
+  st->iterations += 1;
+  st->fail = 0;
+}
+
+__device__ __forceinline__ bool chol3(const double* A, double* L) {
+  // lower-triangular L (row-major 3x3) of SPD A
+  double d0 = A[0];
+  if (!(d0 > 0)) return false;
+  d0 = sqrt(d0);
+  const double l10 = A[3] / d0, l20 = A[6] / d0;
+  double d1 = A[4] - l10 * l10;
+  if (!(d1 > 0)) return false;
+  d1 = sqrt(d1);
+  const double l21 = (A[7] - l20 * l10) / d1;
+  double d2 = A[8] - l20 * l20 - l21 * l21;
+  if (!(d2 > 0)) return false;
+  d2 = sqrt(d2);
+  L[0] = d0; L[1] = 0; L[2] = 0;
+  L[3] = l10; L[4] = d1; L[5] = 0;
+  L[6] = l20; L[7] = l21; L[8] = d2;
+  return true;
+}
+__device__ __forceinline__ void fwd3(const double* L, const double* b, double* y) {
+  y[0] = b[0] / L[0];
+  y[1] = (b[1] - L[3] * y[0]) / L[4];
+  y[2] = (b[2] - L[6] * y[0] - L[7] * y[1]) / L[8];
+}
+__device__ __forceinline__ void bwd3(const double* L, const double* y, double* x) {
+  x[2] = y[2] / L[8];
+  x[1] = (y[1] - L[7] * x[2]) / L[4];
+  x[0] = (y[0] - L[3] * x[1] - L[6] * x[2]) / L[0];
+}
+
+__global__ __launch_bounds__(kBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+  State* st = b.st;
+  if (st->done) return;
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= g.np) return;
+  const double radius = st->radius;
+  double A[9];
+  const double* V = b.V + 9 * (long)j;
+  for (int i = 0; i < 9; ++i) A[i] = V[i];
+  for (int a = 0; a < 3; ++a) A[4 * a] += fmin(fmax(V[4 * a], o.min_diag), o.max_diag) / radius;
+  double* L = b.Lp + 9 * (long)j;
+  if (!chol3(A, L)) {
+    st->fail = 1;
+    return;
+  }
+  fwd3(L, b.gps + 3 * (long)j, b.zp + 3 * (long)j);
+  const int beg = b.p_off[j], end = b.p_off[j + 1];
+  for (int q = beg; q < end; ++q) {
+    const int ob = b.p_obs[q];
+    if (b.cam_idx[ob] - g.nf < 0) continue;
+    const double* W = b.Wo + 18 * (long)ob;
+    double* Y = b.Yo + 18 * (long)ob;
+    for (int a = 0; a < 6; ++a) fwd3(L, W + 3 * a, Y + 3 * a);
+  }
+}
+
+// Dense Y[k][r] (k = 3*point + comp, r = 6*varcam + row): sum of Y_o over the
+// point's observations in that camera (duplicates add, as Ceres would).
+__global__ __launch_bounds__(kBlock) void y_scatter_kernel(Geo g, Bufs b) {
+  const State* st = b.st;
+  if (st->done || st->fail) return;
+  const long idx = (long)blockIdx.x * kBlock + threadIdx.x;
+  const long total = (long)g.Kpad * g.Rpad;
+  if (idx >= total) return;
+  const int k = (int)(idx / g.Rpad), r = (int)(idx - (long)k * g.Rpad);
+  double v = 0;
+  if (k < g.K3 && r < g.n6) {
+    const int j = k / 3, c = k - 3 * j;
+    const int cam = r / 6 + g.nf, a = r - 6 * (r / 6);
+    int lo = b.p_off[j], hi = b.p_off[j + 1];
+    while (lo < hi) {  // lower_bound on camera index
+      int mid = (lo + hi) >> 1;
+      if (b.cam_idx[b.p_obs[mid]] < cam) lo = mid + 1;
+      else hi = mid;
+    }
+    for (int q = lo; q < b.p_off[j + 1] && b.cam_idx[b.p_obs[q]] == cam; ++q)
+      v += b.Yo[18 * (long)b.p_obs[q] + a * 3 + c];
+  }
+  b.Y[idx] = v;
+}
+
+// S partial tiles on the FP64 matrix cores: D(16x16) += A(16x4) B(4x16) with
+// A[i][k] = Y[k][16I+i], B[k][j] = Y[k][16J+j] (or z[k] for the b column).
+// Operand map of v_mfma_f64_16x16x4f64: lane l holds A[l&15][l>>4] and
+// B[l>>4][l&15]; result reg i holds D[(l>>4) + 4i][l&15].
+__global__ __launch_bounds__(kBlock) void schur_gemm_kernel(Geo g, Bufs b) {
+  __shared__ double tile[4][256];
+  const State* st = b.st;
+  if (st->done || st->fail) return;
+  const int p = blockIdx.x, s = blockIdx.y;
+  const int ntri = g.T * (g.T + 1) / 2;
+  int I, J;
+  if (p < ntri) {
+    int rem = p;
+    I = 0;
+    while (rem >= g.T - I) {
+      rem -= g.T - I;
+      ++I;
+    }
+    J = I + rem;
+  } else {
+    I = p - ntri;
+    J = g.T;
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int KC = g.Kpad / g.ksplit, KW = KC / 4;
+  const int k0 = s * KC + wave * KW;
+  double4_t acc = {0.0, 0.0, 0.0, 0.0};
+  const int col = lane & 15, kr = lane >> 4;
+  const double* Ya = b.Y + 16 * I + col;
+  if (J < g.T) {
+    const double* Yb = b.Y + 16 * J + col;
+    for (int k = k0; k < k0 + KW; k += 4) {
+      const long row = (long)(k + kr) * g.Rpad;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ya[row], Yb[row], acc, 0, 0, 0);
+    }
+  } else {
+    for (int k = k0; k < k0 + KW; k += 4) {
+      const int kk = k + kr;
+      const long row = (long)kk * g.Rpad;
+      const double z = (col == 0 && kk < g.K3) ? b.zp[kk] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ya[row], z, acc, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tile[wave][(kr + 4 * i) * 16 + col] = acc[i];
+  __syncthreads();
+  const int e = threadIdx.x;
+  const double v = ((tile[0][e] + tile[1][e]) + tile[2][e]) + tile[3][e];
+  b.Spart[((long)s * g.npairs + p) * 256 + e] = v;
+}
+
+__device__ __forceinline__ double gemm_part(const Geo& g, const double* Spart, int r, int c) {
+  // S element (r, c) of sum_k Y[k][r] Y[k][c]
+  int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
+  if (I > J) {
+    int t = I; I = J; J = t;
+    t = rr; rr = cc; cc = t;
+  }
+  const int p = I * g.T - I * (I - 1) / 2 + (J - I);
+  double s = 0;
+  for (int q = 0; q < g.ksplit; ++q) s += Spart[((long)q * g.npairs + p) * 256 + rr * 16 + cc];
+  return s;
+}
+__device__ __forceinline__ double gemm_zpart(const Geo& g, const double* Spart, int r) {
+  const int ntri = g.T * (g.T + 1) / 2;
+  const int p = ntri + (r >> 4);
+  double s = 0;
+  for (int q = 0; q < g.ksplit; ++q) s += Spart[((long)q * g.npairs + p) * 256 + (r & 15) * 16];
+  return s;
+}
+
+// Sharded mode: S_local = U - YY^T, b_local = g - Yz, diag(U) (no LM diagonal)
+__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b) {
+  const State* st = b.st;
+  if (st->done) return;
+  const int n = g.n6;
+  const long idx = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (idx < (long)n * n) {
+    const int r = (int)(idx / n), c = (int)(idx - (long)r * n);
+    double v = 0;
+    if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
+    b.S[idx] = st->fail ? 0.0 : v - gemm_part(g, b.Spart, r, c);
+  } else if (idx < (long)n * n + n) {
+    const int r = (int)(idx - (long)n * n);
+    b.bvec[r] = st->fail ? 0.0 : b.gcs[r] - gemm_zpart(g, b.Spart, r);
+    b.diagU[r] = b.U[36 * (r / 6) + (r % 6) * 7];
+  } else if (idx == (long)n * n + n) {
+    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
+  }
+}
+
+// One workgroup: assemble S (mode 0) or take the all-reduced S (mode 1), add
+// the LM diagonal, dense Cholesky, y_c = -S^-1 b, candidate cameras.
+constexpr int kSolveBlock = 1024;
+__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int mode, int use_lds) {
+  extern __shared__ double smem[];
+  __shared__ double red[64];
+  __shared__ int sfail;
+  State* st = b.st;
+  if (st->done) return;
+  const int n = g.n6;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  double* A = use_lds ? smem : b.S;
+  const double radius = st->radius;
+  if (tid == 0) sfail = st->fail || (mode == 1 && b.scal[R_COUNT] != 0.0);
+  __syncthreads();
+  if (sfail) {
+    if (tid == 0) st->fail = 1;
+    return;
+  }
+  for (long idx = tid; idx < (long)n * n; idx += nt) {
+    const int r = (int)(idx / n), c = (int)(idx - (long)r * n);
+    double v;
+    if (mode == 0) {
+      v = 0;
+      if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
+      v -= gemm_part(g, b.Spart, r, c);
+      if (r == c) v += fmin(fmax(b.U[36 * (r / 6) + (r % 6) * 7], o.min_diag), o.max_diag) / radius;
+    } else {
+      v = b.S[idx];
+      if (r == c) v += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
+    }
+    A[idx] = v;
+  }
+  for (int r = tid; r < n; r += nt) b.yc[r] = -(mode == 0 ? b.gcs[r] - gemm_zpart(g, b.Spart, r) : b.bvec[r]);
+  __syncthreads();
+  // right-looking Cholesky, lower triangle
+  for (int j = 0; j < n; ++j) {
+    if (tid == 0) {
+      double d = A[(long)j * n + j];
+      if (!(d > 0)) sfail = 1;
+      A[(long)j * n + j] = sqrt(d);
+    }
+    __syncthreads();
+    if (sfail) break;
+    const double d = A[(long)j * n + j];
+    for (int i = j + 1 + tid; i < n; i += nt) A[(long)i * n + j] /= d;
+    __syncthreads();
+    const int m = n - j - 1;
+    for (long q = tid; q < (long)m * m; q += nt) {
+      const int i = j + 1 + (int)(q / m), k = j + 1 + (int)(q % m);
+      if (k <= i) A[(long)i * n + k] -= A[(long)i * n + j] * A[(long)k * n + j];
+    }
+    __syncthreads();
+  }
+  if (sfail) {
+    if (tid == 0) st->fail = 1;
+    return;
+  }
+  // forward: L u = -b ; backward: L^T y = u
+  for (int i = 0; i < n; ++i) {
+    if (tid == 0) b.yc[i] /= A[(long)i * n + i];
+    __syncthreads();
+    const double ui = b.yc[i];
+    for (int r = i + 1 + tid; r < n; r += nt) b.yc[r] -= A[(long)r * n + i] * ui;
+    __syncthreads();
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    if (tid == 0) b.yc[i] /= A[(long)i * n + i];
+    __syncthreads();
+    const double yi = b.yc[i];
+    for (int r = tid; r < i; r += nt) b.yc[r] -= A[(long)i * n + r] * yi;
+    __syncthreads();
+  }
+  // candidate cameras
+  const int cur = st->cur;
+  const double* x = b.cams[cur];
+  double* xc = b.cams[1 - cur];
+  double s2 = 0, xn2 = 0;
+  for (int i = tid; i < 6 * g.nc; i += nt) {
+    const int ci = i / 6 - g.nf;
+    if (ci < 0) {
+      xc[i] = x[i];
+      continue;
+    }
+    const double d = b.yc[i - 6 * g.nf] * b.csc[i - 6 * g.nf];
+    b.dc[i - 6 * g.nf] = d;
+    const double v = x[i] + d;
+    xc[i] = v;
+    const double dd = v - x[i];
+    s2 += dd * dd;
+    xn2 += x[i] * x[i];
+  }
+  double v2[2] = {s2, xn2}, out[2];
+  block_sum<2>(v2, out, red);
+  if (tid == 0) {
+    st->cam_step2 = out[0];
+    st->cam_xn2 = out[1];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void pt_backsub_kernel(Geo g, Bufs b) {
+  __shared__ double lds[8];
+  const State* st = b.st;
+  if (st->done) return;
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  double s2 = 0, xn2 = 0;
+  if (j < g.np && !st->fail) {
+    double rhs[3] = {-b.gps[3 * (long)j], -b.gps[3 * (long)j + 1], -b.gps[3 * (long)j + 2]};
+    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
+      const int ob = b.p_obs[q];
+      const int ci = b.cam_idx[ob] - g.nf;
+      if (ci < 0) continue;
+      const double* W = b.Wo + 18 * (long)ob;
+      const double* y = b.yc + 6 * ci;
+      for (int c = 0; c < 3; ++c)
+        rhs[c] -= W[c] * y[0] + W[3 + c] * y[1] + W[6 + c] * y[2] + W[9 + c] * y[3] + W[12 + c] * y[4] + W[15 + c] * y[5];
+    }
+    const double* L = b.Lp + 9 * (long)j;
+    double u[3], yp[3];
+    fwd3(L, rhs, u);
+    bwd3(L, u, yp);
+    const int cur = st->cur;
+    const double* x = b.pts[cur] + 3 * (long)j;
+    double* xc = b.pts[1 - cur] + 3 * (long)j;
+    for (int a = 0; a < 3; ++a) {
+      const double d = yp[a] * b.psc[3 * (long)j + a];
+      b.dp[3 * (long)j + a] = d;
+      double v = x[a] + d;
+      v = fmin(fmax(v, g.lo[a]), g.hi[a]);
+      xc[a] = v;
+      const double dd = v - x[a];
+      s2 += dd * dd;
+      xn2 += x[a] * x[a];
+    }
+  }
+  double v2[2] = {s2, xn2}, out[2];
+  block_sum<2>(v2, out, lds);
+  if (threadIdx.x == 0) {
+    b.part[R_STEP2 * g.pstride + blockIdx.x] = out[0];
+    b.part[R_XN2 * g.pstride + blockIdx.x] = out[1];
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void obs_step_kernel(Geo g, Bufs b) {
+  __shared__ double lds[8];
+  const State* st = b.st;
+  if (st->done) return;
+  const int o = blockIdx.x * kBlock + threadIdx.x;
+  double mc = 0, cc = 0;
+  if (o < g.no && !st->fail) {
+    const double* L = b.lin + (long)o * kLinStride;
+    const int ci = b.cam_idx[o] - g.nf, pi = b.pt_idx[o];
+    const double* dp = b.dp + 3 * (long)pi;
+    for (int k = 0; k < 4; ++k) {
+      double jd = 0;
+      if (ci >= 0) {
+        const double* dc = b.dc + 6 * ci;
+        for (int j = 0; j < 6; ++j) jd += L[4 + k * 6 + j] * dc[j];
+      }
+      jd += L[28 + k * 3 + 0] * dp[0] + L[28 + k * 3 + 1] * dp[1] + L[28 + k * 3 + 2] * dp[2];
+      mc -= jd * (L[k] + jd / 2.0);
+    }
+    const int nb = 1 - st->cur;
+    double r[4];
+    stereo_residual(g, b.cams[nb] + 6 * b.cam_idx[o], b.pts[nb] + 3 * pi, b.obs + 4 * (long)o, r, nullptr, nullptr);
+    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    double rho0, sc;
+    huber(s, &rho0, &sc);
+    cc = 0.5 * rho0;
+  }
+  double v2[2] = {mc, cc}, out[2];
+  block_sum<2>(v2, out, lds);
+  if (threadIdx.x == 0) {
+    b.part[R_MODEL * g.pstride + blockIdx.x] = out[0];
+    b.part[R_CAND * g.pstride + blockIdx.x] = out[1];
+  }
+}
+
+__global__ __launch_bounds__(1024) void step_reduce_kernel(Geo g, Bufs b) {
+  __shared__ double lds[64];
+  const State* st = b.st;
+  if (st->done) return;
+  double v[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < g.nblk_obs; i += 1024) {
+    v[0] += b.part[R_MODEL * g.pstride + i];
+    v[1] += b.part[R_CAND * g.pstride + i];
+  }
+  for (int i = threadIdx.x; i < g.nblk_pts; i += 1024) {
+    v[2] += b.part[R_STEP2 * g.pstride + i];
+    v[3] += b.part[R_XN2 * g.pstride + i];
+  }
+  double out[4];
+  block_sum<4>(v, out, lds);
+  if (threadIdx.x == 0) {
+    b.scal[R_MODEL] = out[0];
+    b.scal[R_CAND] = out[1];
+    b.scal[R_STEP2] = out[2];
+    b.scal[R_XN2] = out[3];
+    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
+  }
+}
+
+// TrustRegionMinimizer step handling + LevenbergMarquardtStrategy radius update
+__global__ void decide_kernel(Geo g, Bufs b, Opts o) {
+  if (threadIdx.x != 0) return;
+  State* st = b.st;
+  if (st->done) return;
+  st->accepted = 0;
+  const double model_change = b.scal[R_MODEL];
+  const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
+  if (fail || !(model_change > 0.0)) {
+    st->invalid_count += 1;
+    if (st->invalid_count >= o.max_invalid) {
+      st->done = 1;
+      st->termination = 2;
+      return;
+    }
+    st->radius = st->radius / st->decrease;
+    st->decrease *= 2.0;
+    return;
+  }
+  st->invalid_count = 0;
+  const double cand_cost = b.scal[R_CAND];
+  const double step_norm = sqrt(b.scal[R_STEP2] + st->cam_step2);
+  const double x_norm = sqrt(b.scal[R_XN2] + st->cam_xn2);
+  st->cand_cost = cand_cost;
+  st->model_change = model_change;
+  if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) {
+    st->done = 1;
+    st->termination = 0;
+    return;
+  }
+  if (fabs(st->x_cost - cand_cost) <= o.function_tolerance * st->x_cost) {
+    st->done = 1;
+    st->termination = 0;
+    return;
+  }
+  const double q = (st->x_cost - cand_cost) / model_change;
+  st->last_q = q;
+  if (q > o.min_rel_decrease) {
+    st->cur = 1 - st->cur;
+    st->x_cost = cand_cost;
+    st->successful += 1;
+    st->accepted = 1;
+    const double t = 2.0 * q - 1.0;
+    st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - pow(t, 3.0));
+    st->radius = fmin(o.max_radius, st->radius);
+    st->decrease = 2.0;
+    st->need_lin = 1;
+  } else {
+    st->radius = st->radius / st->decrease;
+    st->decrease *= 2.0;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void cost_kernel(Geo g, Bufs b, int which, double* part) {
+  __shared__ double lds[4];
+  const int o = blockIdx.x * kBlock + threadIdx.x;
+  double c = 0;
+  if (o < g.no) {
+    double r[4];
+    stereo_residual(g, b.cams[which] + 6 * b.cam_idx[o], b.pts[which] + 3 * b.pt_idx[o], b.obs + 4 * (long)o, r,
+                    nullptr, nullptr);
+    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    double rho0, sc;
+    huber(s, &rho0, &sc);
+    c = 0.5 * rho0;
+  }
+  double v[1] = {c}, out[1];
+  block_sum<1>(v, out, lds);
+  if (threadIdx.x == 0) part[blockIdx.x] = out[0];
+}
+
+__global__ __launch_bounds__(kBlock) void eval_kernel(Geo g, Bufs b, double* res, double* Jc, double* Jp) {
+  const int o = blockIdx.x * kBlock + threadIdx.x;
+  if (o >= g.no) return;
+  double r[4], jc[24], jp[12];
+  stereo_residual(g, b.cams[0] + 6 * b.cam_idx[o], b.pts[0] + 3 * b.pt_idx[o], b.obs + 4 * (long)o, r, jc, jp);
+  for (int k = 0; k < 4; ++k) res[4 * (long)o + k] = r[k];
+  if (Jc)
+    for (int k = 0; k < 24; ++k) Jc[24 * (long)o + k] = jc[k];
+  if (Jp)
+    for (int k = 0; k < 12; ++k) Jp[12 * (long)o + k] = jp[k];
+}
+
+// ---------------------------------------------------------------- host plan
+struct Plan {
+  me_ctx* c = nullptr;
+  Geo g;
+  Bufs b;
+  Opts o;
+  double* colnorm = nullptr;
+  double* gc_raw = nullptr;
+  double* host = nullptr;  // pinned State copy
+  size_t solve_lds = 0;
+  int use_lds = 0;
+};
+
+inline long rup(long x, long m) { return (x + m - 1) / m * m; }
+
+int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base) {
+  ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
+  ME_CHECK(c, p->feat_var > 0 && p->baseline != 0.0, "BA: wrong calibration parameters (BundleAdjuster.h:147)");
+  for (int i = 0; i < p->n_obs; ++i) {
+    ME_CHECK(c, p->cam_idx[i] >= 0 && p->cam_idx[i] < p->n_cams && p->pt_idx[i] >= 0 && p->pt_idx[i] < p->n_pts,
+             "BA: observation %d indexes outside the window", i);
+  }
+  P.c = c;
+  Geo& g = P.g;
+  g.nc = p->n_cams;
+  g.np = p->n_pts;
+  g.no = p->n_obs;
+  g.nf = std::min(std::max(p->fixed_frames, 0), p->n_cams);
+  g.m = g.nc - g.nf;
+  g.n6 = 6 * g.m;
+  g.Rpad = (int)rup(std::max(g.n6, 1), 16);
+  g.T = g.Rpad / 16;
+  g.K3 = 3 * g.np;
+  g.ksplit = (int)std::max(1L, std::min(64L, rup(std::max(g.K3, 1), 512) / 512));
+  g.Kpad = (int)rup(std::max(g.K3, 1), 16L * g.ksplit);
+  g.npairs = g.T * (g.T + 1) / 2 + g.T;
+  g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
+  g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kBlock) / kBlock);
+  g.pstride = std::max(g.nblk_obs, g.nblk_pts);
+  std::memcpy(g.K0, p->K0, sizeof(g.K0));
+  std::memcpy(g.K1, p->K1, sizeof(g.K1));
+  g.baseline = p->baseline;
+  g.sinv = 1.0 / std::sqrt(p->feat_var);
+  const double Zmax = p->K0[0] * p->baseline / 0.1;
+  const double Zmin = p->K0[0] * p->baseline / (2 * p->K0[2]);
+  g.hi[0] = Zmax / p->K0[0] * p->K0[2];
+  g.hi[1] = Zmax / p->K0[4] * p->K0[5];
+  g.hi[2] = Zmax;
+  g.lo[0] = -Zmax / p->K0[0] * p->K0[2];
+  g.lo[1] = -Zmax / p->K0[4] * p->K0[5];
+  g.lo[2] = Zmin;
+  Opts& o = P.o;
+  o.max_num_iterations = opt->max_num_iterations;
+  o.function_tolerance = opt->function_tolerance;
+  o.gradient_tolerance = opt->gradient_tolerance;
+  o.parameter_tolerance = opt->parameter_tolerance;
+  o.initial_radius = opt->initial_trust_region_radius;
+  o.max_radius = opt->max_trust_region_radius;
+  o.min_radius = opt->min_trust_region_radius;
+  o.min_diag = opt->min_lm_diagonal;
+  o.max_diag = opt->max_lm_diagonal;
+  o.min_rel_decrease = opt->min_relative_decrease;
+  o.max_invalid = opt->max_num_consecutive_invalid_steps;
+  // CSR by point (obs ordered by camera inside each point), CSR by variable camera
+  std::vector<int> p_off(g.np + 1, 0), c_off(g.m + 1, 0);
+  for (int i = 0; i < g.no; ++i) {
+    p_off[p->pt_idx[i] + 1]++;
+    int ci = p->cam_idx[i] - g.nf;
+    if (ci >= 0) c_off[ci + 1]++;
+  }
+  for (int j = 0; j < g.np; ++j) p_off[j + 1] += p_off[j];
+  for (int j = 0; j < g.m; ++j) c_off[j + 1] += c_off[j];
+  std::vector<int> p_obs(std::max(g.no, 1)), c_obs(std::max(g.no, 1));
+  {
+    std::vector<int> fp(p_off.begin(), p_off.end() - 1), fc(c_off.begin(), c_off.end() - 1);
+    for (int i = 0; i < g.no; ++i) {
+      p_obs[fp[p->pt_idx[i]]++] = i;
+      int ci = p->cam_idx[i] - g.nf;
+      if (ci >= 0) c_obs[fc[ci]++] = i;
+    }
+    for (int j = 0; j < g.np; ++j)
+      std::stable_sort(p_obs.begin() + p_off[j], p_obs.begin() + p_off[j + 1],
+                       [&](int a, int bb) { return p->cam_idx[a] < p->cam_idx[bb]; });
+  }
+  // one arena
+  const long nb = std::max(g.nblk_obs, g.nblk_pts);
+  struct Item { size_t bytes; void** dst; };
+  Bufs& b = P.b;
+  std::vector<std::pair<size_t, void**>> items;
+  auto add = [&](size_t bytes, void* dst) { items.push_back({rup((long)std::max<size_t>(bytes, 8), 256), (void**)dst}); };
+  add(8 * 6 * (size_t)g.nc, &b.cams[0]);
+  add(8 * 6 * (size_t)g.nc, &b.cams[1]);
+  add(8 * 3 * (size_t)g.np, &b.pts[0]);
+  add(8 * 3 * (size_t)g.np, &b.pts[1]);
+  add(8 * 4 * (size_t)g.no, &b.obs);
+  add(4 * (size_t)g.no, &b.cam_idx);
+  add(4 * (size_t)g.no, &b.pt_idx);
+  add(4 * (size_t)(g.np + 1), &b.p_off);
+  add(4 * (size_t)g.no, &b.p_obs);
+  add(4 * (size_t)(g.m + 1), &b.c_off);
+  add(4 * (size_t)g.no, &b.c_obs);
+  add(8 * kLinStride * (size_t)g.no, &b.lin);
+  add(8 * 18 * (size_t)g.no, &b.Wo);
+  add(8 * (size_t)g.n6, &b.csc);
+  add(8 * 3 * (size_t)g.np, &b.psc);
+  add(8 * 36 * (size_t)g.m, &b.U);
+  add(8 * (size_t)g.n6, &b.gcs);
+  add(8 * 9 * (size_t)g.np, &b.V);
+  add(8 * 3 * (size_t)g.np, &b.gps);
+  add(8 * 9 * (size_t)g.np, &b.Lp);
+  add(8 * 3 * (size_t)g.np, &b.zp);
+  add(8 * 18 * (size_t)g.no, &b.Yo);
+  add(8 * (size_t)g.Kpad * g.Rpad, &b.Y);
+  add(8 * 256 * (size_t)g.ksplit * g.npairs, &b.Spart);
+  add(8 * (size_t)g.n6 * g.n6 + 8 * (size_t)(2 * g.n6 + 2), &b.S);  // S | b | diagU | fail (contiguous for all-reduce)
+  add(8 * (size_t)g.n6, &b.yc);
+  add(8 * (size_t)g.n6, &b.dc);
+  add(8 * 3 * (size_t)g.np, &b.dp);
+  add(8 * R_COUNT * (size_t)nb, &b.part);
+  add(8 * (R_COUNT + 2), &b.scal);
+  add(sizeof(State), &b.st);
+  add(8 * (size_t)g.n6, &P.colnorm);
+  add(8 * (size_t)g.n6, &P.gc_raw);
+  size_t total = 0;
+  for (auto& it : items) total += it.first;
+  void* arena;
+  ME_TRY(me_scratch(c, SLOT_COUNT + slot_base, total, &arena));
+  char* ptr = (char*)arena;
+  for (auto& it : items) {
+    *it.second = ptr;
+    ptr += it.first;
+  }
+  b.bvec = b.S + (size_t)g.n6 * g.n6;
+  b.diagU = b.bvec + g.n6;
+  // uploads
+  hipStream_t s = c->stream;
+  ME_HIP(c, hipMemcpyAsync(b.cams[0], p->cams, 8 * 6 * (size_t)g.nc, hipMemcpyHostToDevice, s));
+  if (g.np) ME_HIP(c, hipMemcpyAsync(b.pts[0], p->pts, 8 * 3 * (size_t)g.np, hipMemcpyHostToDevice, s));
+  if (g.no) {
+    ME_HIP(c, hipMemcpyAsync((void*)b.obs, p->obs, 8 * 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.cam_idx, p->cam_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.pt_idx, p->pt_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.p_obs, p_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.c_obs, c_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+  }
+  ME_HIP(c, hipMemcpyAsync((void*)b.p_off, p_off.data(), 4 * (size_t)(g.np + 1), hipMemcpyHostToDevice, s));
+  ME_HIP(c, hipMemcpyAsync((void*)b.c_off, c_off.data(), 4 * (size_t)(g.m + 1), hipMemcpyHostToDevice, s));
+  State st0;
+  std::memset(&st0, 0, sizeof(st0));
+  st0.cur = 0;
+  st0.need_lin = 1;
+  st0.termination = 1;
+  st0.radius = o.initial_radius;
+  st0.decrease = 2.0;
+  void* hp;
+  ME_TRY(me_pinned(c, sizeof(State) + 64, &hp));
+  P.host = (double*)hp;
+  std::memcpy(hp, &st0, sizeof(st0));
+  ME_HIP(c, hipMemcpyAsync(b.st, hp, sizeof(State), hipMemcpyHostToDevice, s));
+  ME_HIP(c, hipMemsetAsync(b.csc, 0, 8 * (size_t)std::max(g.n6, 1), s));
+  ME_HIP(c, hipMemsetAsync(P.gc_raw, 0, 8 * (size_t)std::max(g.n6, 1), s));
+  ME_HIP(c, hipMemsetAsync(b.dc, 0, 8 * (size_t)std::max(g.n6, 1), s));
+  if (!opt->jacobi_scaling) {
+    std::vector<double> ones(std::max(g.n6, 1), 1.0);
+    ME_HIP(c, hipMemcpyAsync(b.csc, ones.data(), 8 * ones.size(), hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipStreamSynchronize(s));
+  }
+  // feasibility (Ceres Problem::IsFeasible): host-side, before any launch
+  for (int j = 0; j < g.np; ++j)
+    for (int a = 0; a < 3; ++a) {
+      double x = p->pts[3 * j + a];
+      if (x < g.lo[a] || x > g.hi[a]) return 1;  // infeasible
+    }
+  // LDS for the camera solve
+  P.solve_lds = 8 * (size_t)g.n6 * g.n6;
+  P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
+  if (!P.use_lds) P.solve_lds = 0;
+  else
+    ME_HIP(c, hipFuncSetAttribute((const void*)cam_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)P.solve_lds));
+  return ME_OK;
+}
+
+int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
+
+// Linearisation part of an iteration (skipped on device when need_lin == 0)
+int enqueue_linearize(Plan& P, int jacobi, me_allreduce_fn ar, void* user) {
+  me_ctx* c = P.c;
+  const Geo& g = P.g;
+  hipStream_t s = c->stream;
+  {
+    me_ktimer t(c, ME_KT_BA_LINEARIZE);
+    hipLaunchKernelGGL(linearize_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+  }
+  if (g.m > 0) {
+    if (jacobi) {
+      hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, 0, P.colnorm, P.gc_raw);
+      if (ar) ME_TRY(ar(P.colnorm, g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+      hipLaunchKernelGGL(cam_scaling_kernel, dim3(blocks(g.n6, 256)), dim3(256), 0, s, g, P.b,
+                         (const double*)P.colnorm);
+    }
+    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, 1, P.colnorm, P.gc_raw);
+  }
+  {
+    me_ktimer t(c, ME_KT_BA_POINTS);
+    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b, jacobi);
+  }
+  hipLaunchKernelGGL(lin_reduce_kernel, dim3(1), dim3(1024), 0, s, g, P.b);
+  return me_check_launch(c, "BA linearize");
+}
+
+int enqueue_iteration(Plan& P, int jacobi, me_allreduce_fn ar, void* user) {
+  me_ctx* c = P.c;
+  const Geo& g = P.g;
+  hipStream_t s = c->stream;
+  ME_TRY(enqueue_linearize(P, jacobi, ar, user));
+  if (ar) {
+    // sum the cost / unscaled camera gradient, max of the point gradient
+    // (gradient max is a max: the callback gets n < 0 to request MAX)
+    ME_TRY(ar(P.b.scal + R_COST, 1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+    ME_TRY(ar(P.b.scal + R_GMAX_PT, -1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+    ME_TRY(ar(P.gc_raw, g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+  }
+  hipLaunchKernelGGL(lin_check_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o, (const double*)P.gc_raw);
+  {
+    me_ktimer t(c, ME_KT_BA_POINTS);
+    hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b, P.o);
+  }
+  if (g.m > 0) {
+    me_ktimer t(c, ME_KT_BA_SCHUR);
+    hipLaunchKernelGGL(y_scatter_kernel, dim3(blocks((long)g.Kpad * g.Rpad, kBlock)), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, s, g, P.b);
+  }
+  if (g.m > 0) {
+    int mode = 0;
+    if (ar) {
+      hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0, s,
+                         g, P.b);
+      // S | b | diagU are contiguous; the failure flag lives in scal[R_COUNT]
+      ME_TRY(ar(P.b.S, g.n6 * g.n6 + 2 * g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+      ME_TRY(ar(P.b.scal + R_COUNT, 1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+      mode = 1;
+    }
+    me_ktimer t(c, ME_KT_BA_SOLVE);
+    hipLaunchKernelGGL(cam_solve_kernel, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, mode, P.use_lds);
+  }
+  {
+    me_ktimer t(c, ME_KT_BA_STEP);
+    hipLaunchKernelGGL(pt_backsub_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(obs_step_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+  }
+  hipLaunchKernelGGL(step_reduce_kernel, dim3(1), dim3(1024), 0, s, g, P.b);
+  if (ar) ME_TRY(ar(P.b.scal + R_MODEL, 5, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
+  hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o);
+  return me_check_launch(c, "BA iteration");
+}
+
+int read_state(Plan& P, State* st) {
+  me_ctx* c = P.c;
+  ME_HIP(c, hipMemcpyAsync(P.host, P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  std::memcpy(st, P.host, sizeof(State));
+  return ME_OK;
+}
+
+int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
+  me_ctx* c = P.c;
+  State st;
+  ME_TRY(read_state(P, &st));
+  ME_HIP(c, hipMemcpyAsync(p->cams, P.b.cams[st.cur], 8 * 6 * (size_t)P.g.nc, hipMemcpyDeviceToHost, c->stream));
+  if (P.g.np)
+    ME_HIP(c, hipMemcpyAsync(p->pts, P.b.pts[st.cur], 8 * 3 * (size_t)P.g.np, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  if (sum) {
+    sum->termination = st.termination;
+    sum->iterations = st.iterations;
+    sum->successful_steps = st.successful;
+    sum->initial_cost = st.initial_cost;
+    sum->final_cost = st.x_cost;
+    sum->status = st.termination == 2 ? 3 : 2;
+  }
+  return ME_OK;
+}
+
+int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allreduce_fn ar, void* user,
+               me_ba_summary* sum) {
+  if (!c || !p || !opt) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  Plan P;
+  int rc = plan_build(c, p, opt, P, 0);
+  if (rc < 0) return rc;
+  if (rc == 1) {  // infeasible start -> Ceres FAILURE, parameters untouched
+    if (sum) {
+      sum->status = 3;
+      sum->termination = 2;
+      sum->iterations = 0;
+      sum->successful_steps = 0;
+      sum->initial_cost = sum->final_cost = NAN;
+    }
+    return ME_OK;
+  }
+  const int jacobi = opt->jacobi_scaling ? 1 : 0;
+  // enqueue the whole solve; poll the device state every `chunk` iterations
+  const int chunk = 4;
+  for (int it = 0; it <= opt->max_num_iterations; it += chunk) {
+    for (int k = 0; k < chunk && it + k <= opt->max_num_iterations; ++k) ME_TRY(enqueue_iteration(P, jacobi, ar, user));
+    State st;
+    ME_TRY(read_state(P, &st));
+    if (st.done) break;
+  }
+  return finish(P, p, sum);
+}
+
+}  // namespace
+
+extern "C" void me_ba_default_options(me_ba_options* o) {
+  o->max_num_iterations = 50;
+  o->function_tolerance = 1e-3;
+  o->gradient_tolerance = 1e-10;
+  o->parameter_tolerance = 1e-8;
+  o->initial_trust_region_radius = 1e4;
+  o->max_trust_region_radius = 1e16;
+  o->min_trust_region_radius = 1e-32;
+  o->min_lm_diagonal = 1e-6;
+  o->max_lm_diagonal = 1e32;
+  o->min_relative_decrease = 1e-3;
+  o->max_num_consecutive_invalid_steps = 5;
+  o->jacobi_scaling = 1;
+}
+
+extern "C" int me_ba_solve(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_ba_summary* s) {
+  return solve_impl(c, p, o, nullptr, nullptr, s);
+}
+
+extern "C" int me_ba_solve_sharded(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn ar,
+                                   void* user, me_ba_summary* s) {
+  if (!ar) return me_set_error(c, ME_ERR_INVALID, "me_ba_solve_sharded: null allreduce");
+  return solve_impl(c, p, o, ar, user, s);
+}
+
+extern "C" int me_ba_cost(me_ctx* c, const me_ba_problem* p, double* cost) {
+  if (!c || !p) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  me_ba_options o;
+  me_ba_default_options(&o);
+  Plan P;
+  int rc = plan_build(c, p, &o, P, 0);
+  if (rc < 0) return rc;
+  std::vector<double> part(P.g.nblk_obs);
+  hipLaunchKernelGGL(cost_kernel, dim3(P.g.nblk_obs), dim3(kBlock), 0, c->stream, P.g, P.b, 0, P.b.part);
+  ME_TRY(me_check_launch(c, "cost_kernel"));
+  ME_HIP(c, hipMemcpyAsync(part.data(), P.b.part, 8 * part.size(), hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  double s = 0;
+  for (double v : part) s += v;
+  *cost = s;
+  return ME_OK;
+}
+
+extern "C" int me_ba_evaluate(me_ctx* c, const me_ba_problem* p, double* res, double* Jc, double* Jp) {
+  if (!c || !p) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  me_ba_options o;
+  me_ba_default_options(&o);
+  Plan P;
+  int rc = plan_build(c, p, &o, P, 0);
+  if (rc < 0) return rc;
+  const int no = P.g.no;
+  void* d;
+  ME_TRY(me_scratch(c, SLOT_GENERIC, 8 * 40 * (size_t)std::max(no, 1), &d));
+  double* dres = (double*)d;
+  double* djc = dres + 4 * (size_t)no;
+  double* djp = djc + 24 * (size_t)no;
+  hipLaunchKernelGGL(eval_kernel, dim3(blocks(no, kBlock)), dim3(kBlock), 0, c->stream, P.g, P.b, dres, djc, djp);
+  ME_TRY(me_check_launch(c, "eval_kernel"));
+  ME_HIP(c, hipMemcpyAsync(res, dres, 8 * 4 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  if (Jc) ME_HIP(c, hipMemcpyAsync(Jc, djc, 8 * 24 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  if (Jp) ME_HIP(c, hipMemcpyAsync(Jp, djp, 8 * 12 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  return ME_OK;
+}
+
+extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double radius, double* S, double* bout) {
+  if (!c || !p) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  me_ba_options o;
+  me_ba_default_options(&o);
+  o.initial_trust_region_radius = radius;
+  Plan P;
+  int rc = plan_build(c, p, &o, P, 0);
+  if (rc < 0) return rc;
+  const Geo& g = P.g;
+  ME_TRY(enqueue_linearize(P, 1, nullptr, nullptr));
+  hipLaunchKernelGGL(lin_check_kernel, dim3(1), dim3(64), 0, c->stream, g, P.b, P.o, (const double*)P.gc_raw);
+  hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, c->stream, g, P.b, P.o);
+  if (g.m > 0) {
+    hipLaunchKernelGGL(y_scatter_kernel, dim3(blocks((long)g.Kpad * g.Rpad, kBlock)), dim3(kBlock), 0, c->stream, g,
+                       P.b);
+    hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, c->stream, g, P.b);
+    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0,
+                       c->stream, g, P.b);
+  }
+  ME_TRY(me_check_launch(c, "reduced system"));
+  std::vector<double> Sh((size_t)g.n6 * g.n6 + 2 * g.n6);
+  if (g.m > 0)
+    ME_HIP(c, hipMemcpyAsync(Sh.data(), P.b.S, 8 * Sh.size(), hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  const int n = g.n6;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double v = Sh[(size_t)i * n + j];
+      if (i == j) v += std::min(std::max(Sh[(size_t)n * n + n + i], o.min_lm_diagonal), o.max_lm_diagonal) / radius;
+      S[(size_t)i * n + j] = v;
+    }
+  for (int i = 0; i < n; ++i) bout[i] = Sh[(size_t)n * n + i];
+  return ME_OK;
+}

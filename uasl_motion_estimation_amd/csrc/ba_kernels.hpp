@@ -1,0 +1,100 @@
+// ba_kernels.hpp — device kernels of the windowed stereo bundle adjuster
+// (SURVEY §8a A13-A17).  Included by ba.hip only.
+//
+// Replaces the Ceres solve behind BundleAdjuster<4>::optimise
+// (include/MotionEstimation/optimisation/BundleAdjuster.h:431-476):
+//   linearize      per observation: StereoReprojectionError (:153-171) value +
+//                  analytic Jacobian, HuberLoss(1.0) corrector, cost.
+//   cam_assemble   one workgroup per variable camera: Jacobi column norms
+//                  (iteration 0), scaled U = Jc'Jc, g_c = Jc'r.
+//   pt_assemble    one lane per point: V = Jp'Jp, g_p, W_o = Jc'Jp per obs.
+//   pt_schur       one lane per point: V + D/radius -> Cholesky L_p,
+//                  Y_o = W_o L_p^-T, z_p = L_p^-1 g_p.
+//   y_scatter      dense Y (3 rows per point x 6m cols, K-major) for the GEMM.
+//   schur_gemm     S -= Y Y^T and b -= Y z on v_mfma_f64_16x16x4f64 tiles,
+//                  split-K partials (deterministic, no atomics).
+//   cam_solve      one workgroup: S = U + D/radius - sum(partials), dense
+//                  Cholesky, y_c = -S^-1 b, candidate cameras.
+//   pt_backsub     one lane per point: y_p, candidate points (bounds
+//                  projection), step norms.
+//   obs_step       per observation: model cost change and candidate cost.
+//   decide         one workgroup: Ceres LM acceptance / radius / termination.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ba {
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;
+constexpr int kLinStride = 40;   // r[4], Jc[24], Jp[12] per observation (corrected, unscaled)
+
+struct Opts {
+  int max_num_iterations;
+  double function_tolerance, gradient_tolerance, parameter_tolerance;
+  double initial_radius, max_radius, min_radius, min_diag, max_diag, min_rel_decrease;
+  int max_invalid;
+};
+
+struct State {
+  int cur;            // parameter buffer holding x
+  int need_lin;       // linearize at the start of this iteration
+  int done;
+  int termination;    // 0 CONVERGENCE, 1 NO_CONVERGENCE, 2 FAILURE
+  int iterations, successful, invalid_count;
+  int fail;           // linear solver failure in this iteration
+  int scaled;         // jacobi scaling computed
+  int accepted;
+  int pad[6];
+  double radius, decrease;
+  double x_cost, cand_cost, model_change, initial_cost;
+  double cam_step2, cam_xn2, cam_gmax;
+  double last_q;
+};
+
+// Scalars reduced from block partials (one slot per quantity).
+enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
+
+struct Geo {
+  int nc, np, no, nf, m, n6, Rpad, T, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride;
+  double K0[9], K1[9];
+  double baseline, sinv;
+  double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
+};
+
+struct Bufs {
+  double* cams[2];
+  double* pts[2];
+  const double* obs;
+  const int* cam_idx;
+  const int* pt_idx;
+  const int* p_off;   // CSR by point (obs sorted by cam inside a point)
+  const int* p_obs;
+  const int* c_off;   // CSR by variable camera
+  const int* c_obs;
+  double* lin;        // no * 40
+  double* Wo;         // no * 18 (scaled Jc^T Jp, row-major 6x3)
+  double* csc;        // 6m jacobi scaling (cameras)
+  double* psc;        // 3np (points)
+  double* U;          // m * 36 scaled Jc^T Jc
+  double* gcs;        // 6m scaled gradient
+  double* V;          // np * 9 scaled Jp^T Jp
+  double* gps;        // 3np scaled gradient
+  double* Lp;         // np * 9 Cholesky of V + D/radius
+  double* zp;         // 3np
+  double* Yo;         // no * 18 (W_o L^-T)
+  double* Y;          // Kpad * Rpad dense, K-major
+  double* Spart;      // ksplit * npairs * 256
+  double* S;          // n6 * n6 (assembled / reduced)
+  double* bvec;       // n6
+  double* diagU;      // n6 (for the sharded all-reduce)
+  double* yc;         // n6
+  double* dc;         // n6 camera step (unscaled)
+  double* dp;         // 3np point step (unscaled)
+  double* part;       // R_COUNT * max(nblk_obs, nblk_pts)
+  double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
+  State* st;
+};
+
+}  // namespace ba

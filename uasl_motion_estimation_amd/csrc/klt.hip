@@ -1,0 +1,307 @@
+// klt.hip — pyramidal Lucas-Kanade feature tracking.
+//
+// The reference contains NO tracker (the app that drove it is absent); this
+// is the build-defined tracker, specified by oracle/klt.cpp (the CPU
+// restatement used as its checker).  MI355X design:
+//  * pyramids (pyrDown 5x5 binomial) and Scharr derivatives built once per
+//    image by 2-D kernels; levels resident in HBM;
+//  * one wavefront per feature: the 21x21 window is spread over 64 lanes
+//    (7 pixels each), template values / gradients stay in VGPRs across the
+//    LK iterations, the 2x2 normal matrix and the mismatch vector are int64
+//    sums reduced with wave shuffles (exact, so order-independent and
+//    bit-identical to the serial restatement);
+//  * the 2x2 solve runs redundantly in every lane (wave-uniform control).
+#include <algorithm>
+#include <cstring>
+#include <vector>
+#include "me_internal.hpp"
+
+namespace {
+
+__device__ __forceinline__ int refl(int i, int n) {
+  if (n == 1) return 0;
+  while (i < 0 || i >= n) {
+    if (i < 0) i = -i;
+    if (i >= n) i = 2 * n - 2 - i;
+  }
+  return i;
+}
+
+__global__ void pyr_down_kernel(const uint8_t* __restrict__ src, int w, int h, int ss, uint8_t* __restrict__ dst,
+                                int dw, int dh, int ds) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= dw || y >= dh) return;
+  const int k[5] = {1, 4, 6, 4, 1};
+  int s = 0;
+#pragma unroll
+  for (int a = 0; a < 5; ++a) {
+    const uint8_t* row = src + (long)refl(2 * y + a - 2, h) * ss;
+    int rs = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) rs += k[b] * row[refl(2 * x + b - 2, w)];
+    s += k[a] * rs;
+  }
+  dst[(long)y * ds + x] = (uint8_t)((s + 128) >> 8);
+}
+
+__global__ void scharr_kernel(const uint8_t* __restrict__ I, int w, int h, int stride, int16_t* __restrict__ dx,
+                              int16_t* __restrict__ dy) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
+  if (x >= w || y >= h) return;
+  const uint8_t* r0 = I + (long)refl(y - 1, h) * stride;
+  const uint8_t* r1 = I + (long)y * stride;
+  const uint8_t* r2 = I + (long)refl(y + 1, h) * stride;
+  const int xm = refl(x - 1, w), xp = refl(x + 1, w);
+  const int t0m = 3 * (r0[xm] + r2[xm]) + 10 * r1[xm], t0p = 3 * (r0[xp] + r2[xp]) + 10 * r1[xp];
+  const int t1m = r2[xm] - r0[xm], t1p = r2[xp] - r0[xp], t1 = r2[x] - r0[x];
+  dx[(long)y * w + x] = (int16_t)(t0p - t0m);
+  dy[(long)y * w + x] = (int16_t)(3 * (t1p + t1m) + 10 * t1);
+}
+
+constexpr int kMaxLevels = 8;
+struct Pyr {
+  int nl;
+  int w[kMaxLevels], h[kMaxLevels];
+  const uint8_t* I[kMaxLevels];      // prev levels (stride = w)
+  const int16_t* dx[kMaxLevels];
+  const int16_t* dy[kMaxLevels];
+  const uint8_t* J[kMaxLevels];      // next levels
+};
+
+__device__ __forceinline__ long wave_sum64(long v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ int descale(long v, int n) { return (int)((v + (1L << (n - 1))) >> n); }
+
+constexpr int kMaxWinPx = 7;  // pixels per lane: ceil(21*21/64)
+
+__global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict__ pin, float* __restrict__ pout,
+                                                  uint8_t* __restrict__ status, int n, int win, int max_iters,
+                                                  double eps2, double min_eig) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= n) return;  // wave-uniform
+  const int half = (win - 1) / 2, npx = win * win;
+  const double FLT_SCALE = 1.0 / (1 << 20);
+  uint8_t st = 1;
+  float nx = 0, ny = 0;
+  int iv[kMaxWinPx], ixv[kMaxWinPx], iyv[kMaxWinPx];
+  const float px0 = pin[2 * f], py0 = pin[2 * f + 1];
+  for (int L = P.nl - 1; L >= 0; --L) {
+    const int W = P.w[L], H = P.h[L];
+    const float sc = 1.0f / (float)(1 << L);
+    const float px = px0 * sc, py = py0 * sc;
+    if (L == P.nl - 1) {
+      nx = px;
+      ny = py;
+    } else {
+      nx = nx * 2.0f;
+      ny = ny * 2.0f;
+    }
+    const float pxw = px - (float)half, pyw = py - (float)half;
+    const int ix0 = (int)floorf(pxw), iy0 = (int)floorf(pyw);
+    if (ix0 < 0 || iy0 < 0 || ix0 + win >= W || iy0 + win >= H) {
+      if (L == 0) st = 0;
+      continue;
+    }
+    const float a = pxw - (float)ix0, b = pyw - (float)iy0;
+    const int iw00 = (int)rintf((1.f - a) * (1.f - b) * 16384.f);
+    const int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
+    const int iw10 = (int)rintf((1.f - a) * b * 16384.f);
+    const int iw11 = 16384 - iw00 - iw01 - iw10;
+    const uint8_t* I = P.I[L];
+    const int16_t* DX = P.dx[L];
+    const int16_t* DY = P.dy[L];
+    long A11 = 0, A12 = 0, A22 = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxWinPx; ++q) {
+      const int k = lane + 64 * q;
+      iv[q] = 0;
+      ixv[q] = 0;
+      iyv[q] = 0;
+      if (k < npx) {
+        const int y = k / win, x = k - y * win;
+        const long o = (long)(iy0 + y) * W + ix0 + x;
+        const long v = (long)I[o] * iw00 + (long)I[o + 1] * iw01 + (long)I[o + W] * iw10 + (long)I[o + W + 1] * iw11;
+        const long gx = (long)DX[o] * iw00 + (long)DX[o + 1] * iw01 + (long)DX[o + W] * iw10 + (long)DX[o + W + 1] * iw11;
+        const long gy = (long)DY[o] * iw00 + (long)DY[o + 1] * iw01 + (long)DY[o + W] * iw10 + (long)DY[o + W + 1] * iw11;
+        iv[q] = descale(v, 9);
+        ixv[q] = descale(gx, 14);
+        iyv[q] = descale(gy, 14);
+        A11 += (long)ixv[q] * ixv[q];
+        A12 += (long)ixv[q] * iyv[q];
+        A22 += (long)iyv[q] * iyv[q];
+      }
+    }
+    A11 = wave_sum64(A11);
+    A12 = wave_sum64(A12);
+    A22 = wave_sum64(A22);
+    const double a11 = (double)A11 * FLT_SCALE, a12 = (double)A12 * FLT_SCALE, a22 = (double)A22 * FLT_SCALE;
+    const double D = a11 * a22 - a12 * a12;
+    const double minEig = (a22 + a11 - sqrt((a11 - a22) * (a11 - a22) + 4.0 * a12 * a12)) / (2.0 * win * win);
+    if (minEig < min_eig || D < 1.1920928955078125e-07) {
+      if (L == 0) st = 0;
+      continue;
+    }
+    const double Dinv = 1.0 / D;
+    float nxw = nx - (float)half, nyw = ny - (float)half;
+    float pdx = 0, pdy = 0;
+    const uint8_t* J = P.J[L];
+    for (int j = 0; j < max_iters; ++j) {
+      const int jx0 = (int)floorf(nxw), jy0 = (int)floorf(nyw);
+      if (jx0 < 0 || jy0 < 0 || jx0 + win >= W || jy0 + win >= H) {
+        if (L == 0) st = 0;
+        break;
+      }
+      const float c = nxw - (float)jx0, d = nyw - (float)jy0;
+      const int jw00 = (int)rintf((1.f - c) * (1.f - d) * 16384.f);
+      const int jw01 = (int)rintf(c * (1.f - d) * 16384.f);
+      const int jw10 = (int)rintf((1.f - c) * d * 16384.f);
+      const int jw11 = 16384 - jw00 - jw01 - jw10;
+      long b1 = 0, b2 = 0;
+#pragma unroll
+      for (int q = 0; q < kMaxWinPx; ++q) {
+        const int k = lane + 64 * q;
+        if (k < npx) {
+          const int y = k / win, x = k - y * win;
+          const long o = (long)(jy0 + y) * W + jx0 + x;
+          const long v = (long)J[o] * jw00 + (long)J[o + 1] * jw01 + (long)J[o + W] * jw10 + (long)J[o + W + 1] * jw11;
+          const long diff = descale(v, 9) - iv[q];
+          b1 += diff * ixv[q];
+          b2 += diff * iyv[q];
+        }
+      }
+      b1 = wave_sum64(b1);
+      b2 = wave_sum64(b2);
+      const double b1d = (double)b1 * FLT_SCALE, b2d = (double)b2 * FLT_SCALE;
+      const float ddx = (float)((a12 * b2d - a22 * b1d) * Dinv);
+      const float ddy = (float)((a12 * b1d - a11 * b2d) * Dinv);
+      nxw += ddx;
+      nyw += ddy;
+      nx = nxw + (float)half;
+      ny = nyw + (float)half;
+      if ((double)ddx * ddx + (double)ddy * ddy <= eps2) break;
+      if (j > 0 && fabsf(ddx + pdx) < 0.01f && fabsf(ddy + pdy) < 0.01f) {
+        nx -= ddx * 0.5f;
+        ny -= ddy * 0.5f;
+        break;
+      }
+      pdx = ddx;
+      pdy = ddy;
+    }
+  }
+  if (lane == 0) {
+    pout[2 * f] = nx;
+    pout[2 * f + 1] = ny;
+    status[f] = st;
+  }
+}
+
+}  // namespace
+
+extern "C" void me_klt_default_params(me_klt_params* p) {
+  p->win = 21;
+  p->max_level = 3;
+  p->max_iters = 30;
+  p->eps = 0.01;
+  p->min_eig = 1e-4;
+}
+
+// Builds the pyramids of prev (with derivatives) and next into scratch.
+static int build_pyramids(me_ctx* c, const uint8_t* dprev, const uint8_t* dnext, int w, int h, int stride, int nl,
+                          Pyr& P) {
+  std::vector<int> W(nl), H(nl);
+  W[0] = w;
+  H[0] = h;
+  for (int l = 1; l < nl; ++l) {
+    W[l] = (W[l - 1] + 1) / 2;
+    H[l] = (H[l - 1] + 1) / 2;
+  }
+  size_t bytes = 0;
+  for (int l = 0; l < nl; ++l) bytes += 2 * (size_t)W[l] * H[l] + 4 * (size_t)W[l] * H[l] + 64;
+  void* base;
+  ME_TRY(me_scratch(c, SLOT_KLT_PYR, bytes + 1024, &base));
+  char* p = (char*)base;
+  P.nl = nl;
+  uint8_t* Ilev[kMaxLevels];
+  uint8_t* Jlev[kMaxLevels];
+  for (int l = 0; l < nl; ++l) {
+    P.w[l] = W[l];
+    P.h[l] = H[l];
+    size_t npx = (size_t)W[l] * H[l];
+    Ilev[l] = (uint8_t*)p;
+    p += (npx + 63) / 64 * 64;
+    Jlev[l] = (uint8_t*)p;
+    p += (npx + 63) / 64 * 64;
+    P.dx[l] = (int16_t*)p;
+    p += (2 * npx + 63) / 64 * 64;
+    P.dy[l] = (int16_t*)p;
+    p += (2 * npx + 63) / 64 * 64;
+    P.I[l] = Ilev[l];
+    P.J[l] = Jlev[l];
+  }
+  hipStream_t s = c->stream;
+  ME_HIP(c, hipMemcpy2DAsync(Ilev[0], w, dprev, stride, w, h, hipMemcpyDeviceToDevice, s));
+  ME_HIP(c, hipMemcpy2DAsync(Jlev[0], w, dnext, stride, w, h, hipMemcpyDeviceToDevice, s));
+  me_ktimer t(c, ME_KT_PYR);
+  for (int l = 1; l < nl; ++l) {
+    dim3 blk(32, 8), grd((W[l] + 31) / 32, (H[l] + 7) / 8);
+    hipLaunchKernelGGL(pyr_down_kernel, grd, blk, 0, s, Ilev[l - 1], W[l - 1], H[l - 1], W[l - 1], Ilev[l], W[l], H[l],
+                       W[l]);
+    hipLaunchKernelGGL(pyr_down_kernel, grd, blk, 0, s, Jlev[l - 1], W[l - 1], H[l - 1], W[l - 1], Jlev[l], W[l], H[l],
+                       W[l]);
+  }
+  for (int l = 0; l < nl; ++l) {
+    dim3 blk(32, 8), grd((W[l] + 31) / 32, (H[l] + 7) / 8);
+    hipLaunchKernelGGL(scharr_kernel, grd, blk, 0, s, P.I[l], W[l], H[l], W[l], (int16_t*)P.dx[l], (int16_t*)P.dy[l]);
+  }
+  return me_check_launch(c, "pyramid kernels");
+}
+
+extern "C" int me_klt_track(me_ctx* c, me_mem mem, const uint8_t* prev, const uint8_t* next, int w, int h,
+                            int stride, const float* pin, float* pout, uint8_t* status, int n,
+                            const me_klt_params* kp) {
+  if (!c || !kp) return ME_ERR_INVALID;
+  ME_CHECK(c, w > 0 && h > 0 && stride >= w && n >= 0, "me_klt_track: bad image");
+  ME_CHECK(c, kp->win >= 3 && (kp->win & 1) && kp->win * kp->win <= 64 * kMaxWinPx,
+           "me_klt_track: window must be odd and <= 21");
+  ME_CHECK(c, kp->max_level >= 0 && kp->max_level < kMaxLevels, "me_klt_track: max_level out of range");
+  ME_HIP(c, hipSetDevice(c->device));
+  const int nl = kp->max_level + 1;
+  const uint8_t *dprev = prev, *dnext = next;
+  const float* dpin = pin;
+  float* dpout = pout;
+  uint8_t* dst = status;
+  if (mem == ME_HOST) {
+    void *a, *b, *pts;
+    size_t bytes = (size_t)stride * (h - 1) + w;
+    ME_TRY(me_scratch(c, SLOT_IMG_L, bytes, &a));
+    ME_TRY(me_scratch(c, SLOT_IMG_R, bytes, &b));
+    ME_TRY(me_scratch(c, SLOT_KLT_PTS, 17 * (size_t)std::max(n, 1) + 64, &pts));
+    ME_HIP(c, hipMemcpyAsync(a, prev, bytes, hipMemcpyHostToDevice, c->stream));
+    ME_HIP(c, hipMemcpyAsync(b, next, bytes, hipMemcpyHostToDevice, c->stream));
+    dprev = (const uint8_t*)a;
+    dnext = (const uint8_t*)b;
+    dpin = (const float*)pts;
+    dpout = (float*)pts + 2 * (size_t)std::max(n, 1);
+    dst = (uint8_t*)((float*)pts + 4 * (size_t)std::max(n, 1));
+    if (n) ME_HIP(c, hipMemcpyAsync((void*)dpin, pin, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
+  }
+  Pyr P;
+  ME_TRY(build_pyramids(c, dprev, dnext, w, h, stride, nl, P));
+  if (n > 0) {
+    me_ktimer t(c, ME_KT_KLT);
+    hipLaunchKernelGGL(klt_kernel, dim3((n + 3) / 4), dim3(256), 0, c->stream, P, dpin, dpout, dst, n, kp->win,
+                       kp->max_iters, kp->eps * kp->eps, kp->min_eig);
+  }
+  ME_TRY(me_check_launch(c, "klt_kernel"));
+  if (mem == ME_HOST) {
+    if (n) {
+      ME_HIP(c, hipMemcpyAsync(pout, dpout, 8 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
+      ME_HIP(c, hipMemcpyAsync(status, dst, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    }
+    ME_HIP(c, hipStreamSynchronize(c->stream));
+  }
+  return ME_OK;
+}

@@ -1,0 +1,180 @@
+// me_device.hpp — device-side building blocks shared by the kernels.
+//
+// Numerics contract (bit-exact parity with the reference's x86-64 build):
+//  * this whole library is compiled with -ffp-contract=off, so every float /
+//    double expression rounds exactly as written (no implicit FMA);
+//  * fp32 division/sqrt are the correctly rounded HIP defaults;
+//  * log2f is the glibc 2.35 algorithm (ARM optimized-routines log2f: a
+//    16-entry {1/c, log2 c} table and a degree-4 polynomial evaluated in
+//    double).  Verified equal to the host libm on all 2^31 positive floats
+//    (tests/test_oracle.py::test_log2f_exhaustive runs the same check).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace me_dev {
+
+__constant__ const double kLog2fInvc[16] = {
+    0x1.661ec79f8f3bep+0, 0x1.571ed4aaf883dp+0, 0x1.49539f0f010b0p+0, 0x1.3c995b0b80385p+0,
+    0x1.30d190c8864a5p+0, 0x1.25e227b0b8ea0p+0, 0x1.1bb4a4a1a343fp+0, 0x1.12358f08ae5bap+0,
+    0x1.0953f419900a7p+0, 0x1.0000000000000p+0, 0x1.e608cfd9a47acp-1, 0x1.ca4b31f026aa0p-1,
+    0x1.b2036576afce6p-1, 0x1.9c2d163a1aa2dp-1, 0x1.886e6037841edp-1, 0x1.767dcf5534862p-1};
+__constant__ const double kLog2fLogc[16] = {
+    -0x1.efec65b963019p-2, -0x1.b0b6832d4fca4p-2, -0x1.7418b0a1fb77bp-2, -0x1.39de91a6dcf7bp-2,
+    -0x1.01d9bf3f2b631p-2, -0x1.97c1d1b3b7af0p-3, -0x1.2f9e393af3c9fp-3, -0x1.960cbbf788d5cp-4,
+    -0x1.a6f9db6475fcep-5, 0x0.0p+0,              0x1.338ca9f24f53dp-4,  0x1.476a9543891bap-3,
+    0x1.e840b4ac4e4d2p-3,  0x1.40645f0c6651cp-2,  0x1.88e9c2c1b9ff8p-2,  0x1.ce0a44eb17bccp-2};
+
+// glibc log2f for the finite positive normal/subnormal inputs MI produces
+// (q = pJ/(pL*pR) > 0).  FMA form = glibc's __log2f_fma ifunc variant; both
+// variants agree with libm on every float (checked exhaustively).
+__device__ __forceinline__ float log2f_glibc(float x) {
+  uint32_t ix = __float_as_uint(x);
+  if (ix == 0x3f800000u) return 0.0f;
+  if (ix < 0x00800000u) {  // subnormal
+    ix = __float_as_uint(x * 0x1p23f);
+    ix -= 23u << 23;
+  }
+  uint32_t tmp = ix - 0x3f330000u;
+  int i = (tmp >> 19) & 15;
+  uint32_t top = tmp & 0xff800000u;
+  uint32_t iz = ix - top;
+  int k = (int32_t)tmp >> 23;
+  double z = (double)__uint_as_float(iz);
+  double r = __builtin_fma(z, kLog2fInvc[i], -1.0);
+  double y0 = kLog2fLogc[i] + (double)k;
+  double r2 = r * r;
+  double y = __builtin_fma(0x1.ecabf496832e0p-2, r, -0x1.715479ffae3dep-1);
+  y = __builtin_fma(-0x1.712b6f70a7e4dp-2, r2, y);
+  double p = __builtin_fma(0x1.715475f35c8b8p+0, r, y0);
+  y = __builtin_fma(y, r2, p);
+  return (float)y;
+}
+
+// calcHist 8U, 20 uniform bins over [0,256): floor(v*20/256) = (5v)>>6
+__device__ __forceinline__ int bin20(int v) { return (v * 5) >> 6; }
+
+// One MI term of mutual_information.cpp:82-83.
+__device__ __forceinline__ float mi_term(int cJ, int cL, int cR, float invN) {
+  float pJ = (float)cJ * invN;
+  float pL = (float)cL * invN;
+  float pR = (float)cR * invN;
+  float den = pL * pR;
+  float q = pJ / den;
+  return pJ * log2f_glibc(q);
+}
+
+// ---------------------------------------------------------------------
+// Lane-private MI histogram in LDS.  Word w of lane t lives at
+// lds[w * LANES + t] so a wave's accesses to one word hit 64 distinct banks.
+//   words [0,100)   joint counts, 4 x u8 per word (code = bl*20 + br)
+//   words [100,105) left marginal, [105,110) right marginal
+//   words [110,123) occupancy bitmap of the 400 joint bins
+// u8 counts limit a patch to 255 pixels (P <= 15).
+constexpr int kHistWords = 123;
+
+template <int LANES>
+struct LaneHist {
+  uint32_t* base;  // &lds[tid]
+  __device__ __forceinline__ uint32_t& w(int i) { return base[i * LANES]; }
+  __device__ __forceinline__ void clear() {
+#pragma unroll 4
+    for (int i = 0; i < kHistWords; ++i) w(i) = 0u;
+  }
+  __device__ __forceinline__ void add(int vl, int vr) {
+    int bl = bin20(vl), br = bin20(vr);
+    int code = bl * 20 + br;
+    // lane-private words: LDS atomics only to get single ds_add/ds_or ops
+    atomicAdd(&w(code >> 2), 1u << ((code & 3) * 8));
+    atomicAdd(&w(100 + (bl >> 2)), 1u << ((bl & 3) * 8));
+    atomicAdd(&w(105 + (br >> 2)), 1u << ((br & 3) * 8));
+    atomicOr(&w(110 + (code >> 5)), 1u << (code & 31));
+  }
+  // Row-major (i = L bin outer, j = R bin inner) float sum over non-empty bins.
+  __device__ __forceinline__ float mi(float invN) {
+    float MI = 0.0f;
+    for (int wd = 0; wd < 13; ++wd) {
+      uint32_t bits = w(110 + wd);
+      while (bits) {
+        int b = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        int code = wd * 32 + b;
+        int i = code / 20, j = code - i * 20;
+        int cJ = (w(code >> 2) >> ((code & 3) * 8)) & 0xff;
+        int cL = (w(100 + (i >> 2)) >> ((i & 3) * 8)) & 0xff;
+        int cR = (w(105 + (j >> 2)) >> ((j & 3) * 8)) & 0xff;
+        MI += mi_term(cJ, cL, cR, invN);
+      }
+    }
+    return MI;
+  }
+};
+
+// ---------------------------------------------------------------------
+// Pose / projection math for the ScaleState residuals, restating the
+// OpenCV Matx evaluation order of optimisation.cpp:172-215 (s = 0; s += ...).
+struct Pose44 { double T[16]; };
+
+__device__ __forceinline__ void quat_pose(const double* q, const double* t, double* T) {
+  const double w = q[0], x = q[1], y = q[2], z = q[3];
+  T[0] = w * w + x * x - y * y - z * z; T[1] = 2 * (x * y - w * z); T[2] = 2 * (x * z + w * y); T[3] = t[0];
+  T[4] = 2 * (x * y + w * z); T[5] = w * w - x * x + y * y - z * z; T[6] = 2 * (y * z - w * x); T[7] = t[1];
+  T[8] = 2 * (x * z - w * y); T[9] = 2 * (y * z + w * x); T[10] = w * w - x * x - y * y + z * z; T[11] = t[2];
+  T[12] = 0; T[13] = 0; T[14] = 0; T[15] = 1;
+}
+
+__device__ __forceinline__ void mat44_vec(const double* T, const double* X, double* Y) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double s = 0;
+    s += T[i * 4 + 0] * X[0];
+    s += T[i * 4 + 1] * X[1];
+    s += T[i * 4 + 2] * X[2];
+    s += T[i * 4 + 3] * X[3];
+    Y[i] = s;
+  }
+}
+
+// ((K * I34) * s) * Y
+__device__ __forceinline__ void project_scaled(const double* K, double s, const double* Y, double* f) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double a = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double kij = 0;
+      kij += K[i * 3 + 0] * (k == 0 ? 1.0 : 0.0);
+      kij += K[i * 3 + 1] * (k == 1 ? 1.0 : 0.0);
+      kij += K[i * 3 + 2] * (k == 2 ? 1.0 : 0.0);
+      a += (kij * s) * Y[k];
+    }
+    f[i] = a;
+  }
+}
+
+// (K * I34) * Z
+__device__ __forceinline__ void project(const double* K, const double* Z, double* f) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    double a = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double kij = 0;
+      kij += K[i * 3 + 0] * (k == 0 ? 1.0 : 0.0);
+      kij += K[i * 3 + 1] * (k == 1 ? 1.0 : 0.0);
+      kij += K[i * 3 + 2] * (k == 2 ? 1.0 : 0.0);
+      a += kij * Z[k];
+    }
+    f[i] = a;
+  }
+}
+
+// cv::Rect::contains(Point2f): cvRound (half-even) then half-open test
+__device__ __forceinline__ bool rect_contains(int rx, int ry, int rw, int rh, float px, float py) {
+  int ix = (int)rintf(px), iy = (int)rintf(py);
+  return rx <= ix && ix < rx + rw && ry <= iy && iy < ry + rh;
+}
+// Rect(feat.x - w, ...): float - int in float, then truncation to int
+__device__ __forceinline__ int roi_corner(float c, int w) { return (int)(c - (float)w); }
+
+}  // namespace me_dev

@@ -1,0 +1,76 @@
+// me_internal.hpp — host-side internals of libme_hip.so (context, errors,
+// scratch memory, kernel timing).  Not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+#include <vector>
+#include "../../include/me_hip.h"
+
+struct me_timer_pair {
+  hipEvent_t a, b;
+  int kernel;
+};
+
+struct me_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // growable device scratch slots (allocated outside timed/captured regions)
+  std::vector<void*> slot_ptr;
+  std::vector<size_t> slot_size;
+  // pinned host staging for small scalar read-backs
+  void* pinned = nullptr;
+  size_t pinned_size = 0;
+  // kernel timing
+  bool timing = false;
+  std::vector<me_timer_pair> pending;
+  std::vector<hipEvent_t> event_pool;
+  long launches[ME_KT_COUNT] = {0};
+  double total_ms[ME_KT_COUNT] = {0};
+};
+
+int me_set_error(me_ctx* ctx, int code, const char* fmt, ...);
+
+#define ME_HIP(ctx, call)                                                                    \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      return me_set_error((ctx), ME_ERR_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), \
+                          __FILE__, __LINE__);                                               \
+  } while (0)
+
+#define ME_CHECK(ctx, cond, ...)                                     \
+  do {                                                               \
+    if (!(cond)) return me_set_error((ctx), ME_ERR_INVALID, __VA_ARGS__); \
+  } while (0)
+
+#define ME_TRY(expr)            \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != ME_OK) return rc_; \
+  } while (0)
+
+// Returns a device buffer of at least `bytes` for scratch slot `slot`.
+int me_scratch(me_ctx* ctx, int slot, size_t bytes, void** out);
+int me_pinned(me_ctx* ctx, size_t bytes, void** out);
+int me_check_launch(me_ctx* ctx, const char* what);
+
+// RAII event pair around one launch when timing is enabled.
+struct me_ktimer {
+  me_ctx* c;
+  int k;
+  hipEvent_t a = nullptr, b = nullptr;
+  me_ktimer(me_ctx* ctx, int kernel);
+  ~me_ktimer();
+};
+
+// Scratch slot ids (one owner per slot)
+enum {
+  SLOT_IMG_L = 0, SLOT_IMG_R, SLOT_XY_L, SLOT_XY_R, SLOT_MI_OUT, SLOT_RED, SLOT_GENERIC,
+  SLOT_SC_TRACKS, SLOT_SC_RES, SLOT_SC_RES2, SLOT_SC_NEQ, SLOT_SC_IMGL, SLOT_SC_IMGR,
+  SLOT_KLT_PYR, SLOT_KLT_PTS, SLOT_NMS,
+  SLOT_COUNT
+};

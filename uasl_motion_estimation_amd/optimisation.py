@@ -1,0 +1,489 @@
+"""Optimisers mirroring include/MotionEstimation/optimisation/{optimisation,BundleAdjuster}.h.
+
+* ``Optimiser`` — Optimiser<ScaleState, vector<pair<Mat,Mat>>> (optimisation.h:100-125,
+  src/optimisation/optimisation.cpp:29-747): the MI stereo-scale LM.  Residual /
+  normal-equation evaluations run in scale.hip; the scalar LM control is the
+  reference's, in libme_hip.so's host code.
+* ``BundleAdjuster`` — BundleAdjuster<4> (BundleAdjuster.h:182-476): windowed
+  stereo BA; the whole Ceres-style LM runs on the device (ba.hip).
+* Array-level helpers (``scale_*``, ``ba_*``) take the flattened problems of
+  synthetic.py and are what the parity tests and bench.py call.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, byref, c_double, c_int, c_int32, c_long, c_uint8, c_uint32
+from dataclasses import dataclass, field
+from enum import Enum, IntEnum
+
+import numpy as np
+
+from ._lib import (ALLREDUCE_FN, BAOptionsC, BAProblemC, BASummaryC, ME_DEVICE, ME_HOST, Context, OptimParamsC,
+                   ScaleStateC, default_context)
+from .feature_types import CamPose, WBA_Point
+from .rotation_utils import Quat, StopCondition, exp_map_Quat, log_map_Quat
+
+
+def _p(a, t=c_double):
+    return None if a is None else a.ctypes.data_as(POINTER(t))
+
+
+# ============================================================ ScaleState LM
+class OptimType(IntEnum):
+    GN = 0
+    LM = 1
+
+
+@dataclass
+class OptimisationParams:
+    """OptimisationParams (optimisation.h:22-32) with the same defaults."""
+    type: OptimType = OptimType.LM
+    minim: bool = True
+    MAX_NB_ITER: int = 20
+    v: float = 2.0
+    tau: float = 1e-3
+    mu: float = 1e-20
+    abs_tol: float = 1e-4
+    grad_tol: float = 1e-4
+    incr_tol: float = 1e-3
+    rel_tol: float = 1e-4
+    alpha: float = 1.0
+    weighting: bool = False
+
+    def to_c(self) -> OptimParamsC:
+        p = OptimParamsC()
+        p.type, p.minim, p.max_nb_iter = int(self.type), int(self.minim), int(self.MAX_NB_ITER)
+        p.v, p.tau, p.mu = self.v, self.tau, self.mu
+        p.abs_tol, p.grad_tol, p.incr_tol, p.rel_tol = self.abs_tol, self.grad_tol, self.incr_tol, self.rel_tol
+        p.alpha, p.weighting = self.alpha, int(self.weighting)
+        return p
+
+
+def scale_struct(sp, keep: list, img_mem: int = ME_HOST, dev_imgs=None) -> ScaleStateC:
+    """ScaleStateC from a flattened problem (synthetic.ScaleProblem or ScaleState.flatten())."""
+    s = ScaleStateC()
+    s.n_left, s.n_right = len(sp.X_left), len(sp.X_right)
+    for name in ("X_left", "X_right"):
+        a = np.ascontiguousarray(getattr(sp, name), np.float64).reshape(-1)
+        keep.append(a)
+        setattr(s, name, _p(a))
+    for name in ("tri_left", "tri_right"):
+        a = np.ascontiguousarray(getattr(sp, name), np.uint8)
+        keep.append(a)
+        setattr(s, name, _p(a, c_uint8))
+    for name in ("last_left", "last_right"):
+        a = np.ascontiguousarray(getattr(sp, name), np.uint32)
+        keep.append(a)
+        setattr(s, name, _p(a, c_uint32))
+    s.lframe = int(sp.lframe)
+    s.K1[:] = [float(x) for x in np.asarray(sp.K1).ravel()]
+    s.K2[:] = [float(x) for x in np.asarray(sp.K2).ravel()]
+    s.q1[:] = [float(x) for x in sp.q1]
+    s.t1[:] = [float(x) for x in sp.t1]
+    s.q2[:] = [float(x) for x in sp.q2]
+    s.t2[:] = [float(x) for x in sp.t2]
+    s.scale, s.baseline, s.window_size = float(sp.scale), float(sp.baseline), int(sp.window_size)
+    h, w = sp.imgL.shape
+    if img_mem == ME_DEVICE:
+        s.imgL, s.imgR = dev_imgs
+    else:
+        L = np.ascontiguousarray(sp.imgL, np.uint8)
+        R = np.ascontiguousarray(sp.imgR, np.uint8)
+        keep += [L, R]
+        s.imgL, s.imgR = L.ctypes.data, R.ctypes.data
+    s.stride, s.cols, s.rows = w, w, h
+    s.bb_cols = getattr(sp, "bb_cols", None) or w
+    s.bb_rows = getattr(sp, "bb_rows", None) or h
+    mask = getattr(sp, "mask", None)
+    if mask is not None:
+        m = np.ascontiguousarray(mask, np.uint8)
+        keep.append(m)
+        s.mask, s.mask_len = _p(m, c_uint8), len(m)
+    s.img_mem = img_mem
+    return s
+
+
+def scale_residuals(sp, weighting=False, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or default_context()
+    keep = []
+    s = scale_struct(sp, keep)
+    res = np.zeros(len(sp.X_left) + len(sp.X_right) + 1)
+    n = c_int()
+    ctx.check(ctx.lib.me_scale_residuals(ctx.h, byref(s), int(weighting), _p(res), byref(n)), "me_scale_residuals")
+    return res[:n.value]
+
+
+def scale_normal_equations(sp, residuals, weighting=False, ctx: Context | None = None):
+    ctx = ctx or default_context()
+    keep = []
+    s = scale_struct(sp, keep)
+    r = np.ascontiguousarray(residuals, np.float64)
+    JJ, e = c_double(), c_double()
+    ctx.check(ctx.lib.me_scale_normal_equations(ctx.h, byref(s), int(weighting), _p(r), byref(JJ), byref(e)),
+              "me_scale_normal_equations")
+    return JJ.value, e.value
+
+
+def scale_jacobian(sp, weighting=False, ctx: Context | None = None) -> float:
+    ctx = ctx or default_context()
+    keep = []
+    s = scale_struct(sp, keep)
+    JJ = c_double()
+    ctx.check(ctx.lib.me_scale_jacobian(ctx.h, byref(s), int(weighting), byref(JJ)), "me_scale_jacobian")
+    return JJ.value
+
+
+def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx: Context | None = None,
+                   img_mem: int = ME_HOST, dev_imgs=None) -> dict:
+    ctx = ctx or default_context()
+    params = params or OptimisationParams()
+    keep = []
+    s = scale_struct(sp, keep, img_mem, dev_imgs)
+    p = params.to_c()
+    stop, it, nmi = c_int(), c_int(), c_long()
+    trace = np.zeros(2 * 400)
+    ctx.check(ctx.lib.me_scale_optimise(ctx.h, byref(s), byref(p), int(test), byref(stop), byref(it), _p(trace), 400,
+                                        byref(nmi)), "me_scale_optimise")
+    n = min(it.value, 400)
+    return dict(stop=StopCondition(stop.value), scale=s.scale, iterations=it.value,
+                trace=trace[:2 * n].reshape(-1, 2), track_evals=nmi.value)
+
+
+def scale_inliers(sp, threshold: float, weighting=False, ctx: Context | None = None) -> np.ndarray:
+    ctx = ctx or default_context()
+    keep = []
+    s = scale_struct(sp, keep)
+    cap = len(sp.X_left) + len(sp.X_right) + 1
+    idx = np.zeros(cap, np.int32)
+    n = c_int()
+    ctx.check(ctx.lib.me_scale_inliers(ctx.h, byref(s), int(weighting), threshold, _p(idx, c_int), cap, byref(n)),
+              "me_scale_inliers")
+    return idx[:n.value]
+
+
+@dataclass
+class ScaleState:
+    """ScaleState (optimisation.h:76-98)."""
+    pts: tuple = field(default_factory=lambda: ([], []))          # (vector<WBA_Ptf>, vector<WBA_Ptf>)
+    K: tuple = field(default_factory=lambda: (np.eye(3), np.eye(3)))
+    poses: tuple = field(default_factory=lambda: ([], []))        # (vector<CamPose_qd>, vector<CamPose_qd>)
+    scale: float = 1.0
+    baseline: float = 0.0
+    window_size: int = 5
+    nb_params: int = 1
+
+    def update(self, dX):
+        self.scale += float(np.asarray(dX).ravel()[0])
+
+
+@dataclass
+class _Flat:
+    X_left: np.ndarray
+    X_right: np.ndarray
+    tri_left: np.ndarray
+    tri_right: np.ndarray
+    last_left: np.ndarray
+    last_right: np.ndarray
+    lframe: int
+    K1: np.ndarray
+    K2: np.ndarray
+    q1: np.ndarray
+    t1: np.ndarray
+    q2: np.ndarray
+    t2: np.ndarray
+    scale: float
+    baseline: float
+    window_size: int
+    imgL: np.ndarray
+    imgR: np.ndarray
+    bb_cols: int
+    bb_rows: int
+    mask: np.ndarray | None = None
+
+
+class Optimiser:
+    """Optimiser<ScaleState, std::vector<std::pair<cv::Mat,cv::Mat>>> (optimisation.h:100-125)."""
+
+    def __init__(self, observations, params: OptimisationParams | None = None, ctx: Context | None = None):
+        self.m_obs = [(np.ascontiguousarray(L, np.uint8), np.ascontiguousarray(R, np.uint8)) for L, R in observations]
+        self.m_params = params or OptimisationParams()
+        self.m_state: ScaleState | None = None
+        self.m_mask = None
+        self.ctx = ctx or default_context()
+
+    def _flatten(self, st: ScaleState, use_mask=True) -> _Flat:
+        def arr(tracks):
+            X = np.array([t.get3DLocation() for t in tracks], np.float64).reshape(-1, 4)
+            tri = np.array([t.isTriangulated() for t in tracks], np.uint8)
+            last = np.array([t.getLastFrameIdx() for t in tracks], np.uint32)
+            return X, tri, last
+
+        XL, tl, ll = arr(st.pts[0])
+        XR, tr, lr = arr(st.pts[1])
+        f_idx = len(st.poses[0]) - 1
+        L, R = self.m_obs[f_idx]
+        pl, pr = st.poses[0][-1], st.poses[1][-1]
+        return _Flat(XL, XR, tl, tr, ll, lr, st.poses[0][0].ID + len(st.poses[0]) - 1,
+                     np.asarray(st.K[0], np.float64), np.asarray(st.K[1], np.float64),
+                     pl.orientation.coeffs(), np.asarray(pl.position, np.float64),
+                     pr.orientation.coeffs(), np.asarray(pr.position, np.float64),
+                     st.scale, st.baseline, st.window_size, L, R,
+                     self.m_obs[0][0].shape[1], self.m_obs[1][0].shape[0] if len(self.m_obs) > 1 else L.shape[0],
+                     (np.asarray(self.m_mask, np.uint8) if (use_mask and self.m_mask is not None and
+                                                            len(self.m_mask)) else None))
+
+    def optimise(self, state: ScaleState, test: bool = False, mask=None) -> StopCondition:
+        self.m_state = state
+        self.m_mask = mask
+        r = scale_optimise(self._flatten(state), self.m_params, test, self.ctx)
+        state.scale = r["scale"]
+        self.last_result = r
+        return r["stop"]
+
+    def compute_residuals(self, state: ScaleState) -> np.ndarray:
+        return scale_residuals(self._flatten(state), self.m_params.weighting, self.ctx).reshape(-1, 1)
+
+    def getJacobian(self) -> np.ndarray:
+        return np.array([[scale_jacobian(self._flatten(self.m_state), self.m_params.weighting, self.ctx)]])
+
+    def compute_inliers(self, threshold: float) -> list:
+        return list(scale_inliers(self._flatten(self.m_state, use_mask=False), threshold, self.m_params.weighting,
+                                  self.ctx))
+
+
+# ============================================================ Bundle adjustment
+class Status(Enum):
+    UNINITIALISED = 0
+    INITIALISED = 1
+    SUCCESSFUL = 2
+    FAILED = 3
+
+
+@dataclass
+class CalibrationParameters:
+    """CalibrationParameters (BundleAdjuster.h:35-45)."""
+    K: list
+    feat_var: float
+    baseline: float = 0.0
+    compute_cov: bool = False
+
+
+@dataclass
+class SolverOptions:
+    """The Ceres options BundleAdjuster<4>::optimise sets (BundleAdjuster.h:463-466) + Ceres defaults.
+
+    max_solver_time_in_seconds = 1.0 is replaced by max_num_iterations (deterministic)."""
+    max_num_iterations: int = 50
+    function_tolerance: float = 1e-3
+    gradient_tolerance: float = 1e-10
+    parameter_tolerance: float = 1e-8
+    initial_trust_region_radius: float = 1e4
+    max_trust_region_radius: float = 1e16
+    min_trust_region_radius: float = 1e-32
+    min_lm_diagonal: float = 1e-6
+    max_lm_diagonal: float = 1e32
+    min_relative_decrease: float = 1e-3
+    max_num_consecutive_invalid_steps: int = 5
+    jacobi_scaling: bool = True
+
+    def to_c(self) -> BAOptionsC:
+        o = BAOptionsC()
+        for k, v in self.__dict__.items():
+            setattr(o, k, int(v) if isinstance(v, bool) else v)
+        return o
+
+    @staticmethod
+    def fixed_iterations(n: int) -> "SolverOptions":
+        """Fixed work per solve (bench): tolerances off, exactly n LM iterations."""
+        return SolverOptions(max_num_iterations=n, function_tolerance=0.0, gradient_tolerance=0.0,
+                             parameter_tolerance=0.0)
+
+
+def ba_struct(bp, keep: list):
+    p = BAProblemC()
+    p.n_cams, p.n_pts, p.n_obs = len(bp.cams), len(bp.pts), len(bp.obs)
+    cams = np.ascontiguousarray(bp.cams, np.float64).copy()
+    pts = np.ascontiguousarray(bp.pts, np.float64).copy()
+    obs = np.ascontiguousarray(bp.obs, np.float64)
+    ci = np.ascontiguousarray(bp.cam_idx, np.int32)
+    pi = np.ascontiguousarray(bp.pt_idx, np.int32)
+    keep += [cams, pts, obs, ci, pi]
+    p.cams, p.pts, p.obs = _p(cams), _p(pts), _p(obs)
+    p.cam_idx, p.pt_idx = _p(ci, c_int32), _p(pi, c_int32)
+    p.K0[:] = [float(x) for x in np.asarray(bp.K0).ravel()]
+    p.K1[:] = [float(x) for x in np.asarray(bp.K1).ravel()]
+    p.baseline, p.feat_var, p.fixed_frames = float(bp.baseline), float(bp.feat_var), int(bp.fixed_frames)
+    return p, cams, pts
+
+
+def _summary(s: BASummaryC) -> dict:
+    return dict(status=s.status, termination=s.termination, iterations=s.iterations,
+                successful_steps=s.successful_steps, initial_cost=s.initial_cost, final_cost=s.final_cost)
+
+
+def ba_solve(bp, options: SolverOptions | None = None, ctx: Context | None = None):
+    """Returns (cams, pts, summary) after the device LM solve."""
+    ctx = ctx or default_context()
+    keep = []
+    p, cams, pts = ba_struct(bp, keep)
+    o = (options or SolverOptions()).to_c()
+    s = BASummaryC()
+    ctx.check(ctx.lib.me_ba_solve(ctx.h, byref(p), byref(o), byref(s)), "me_ba_solve")
+    return cams, pts, _summary(s)
+
+
+def ba_solve_sharded(bp_local, allreduce, options: SolverOptions | None = None, ctx: Context | None = None):
+    """Landmark-sharded solve; ``allreduce(dev_ptr, n)`` sums n doubles in place (n < 0: max over |n|)."""
+    ctx = ctx or default_context()
+    keep = []
+    p, cams, pts = ba_struct(bp_local, keep)
+    o = (options or SolverOptions()).to_c()
+    s = BASummaryC()
+
+    def _cb(ptr, n, user):
+        try:
+            allreduce(ctypes.cast(ptr, ctypes.c_void_p).value, int(n))
+            return 0
+        except Exception:  # pragma: no cover
+            import traceback
+            traceback.print_exc()
+            return -1
+
+    cb = ALLREDUCE_FN(_cb)
+    keep.append(cb)
+    ctx.check(ctx.lib.me_ba_solve_sharded(ctx.h, byref(p), byref(o), cb, None, byref(s)), "me_ba_solve_sharded")
+    return cams, pts, _summary(s)
+
+
+def ba_cost(bp, ctx: Context | None = None) -> float:
+    ctx = ctx or default_context()
+    keep = []
+    p, _, _ = ba_struct(bp, keep)
+    c = c_double()
+    ctx.check(ctx.lib.me_ba_cost(ctx.h, byref(p), byref(c)), "me_ba_cost")
+    return c.value
+
+
+def ba_evaluate(bp, ctx: Context | None = None):
+    ctx = ctx or default_context()
+    keep = []
+    p, _, _ = ba_struct(bp, keep)
+    no = len(bp.obs)
+    r = np.zeros(4 * no)
+    Jc = np.zeros(24 * no)
+    Jp = np.zeros(12 * no)
+    ctx.check(ctx.lib.me_ba_evaluate(ctx.h, byref(p), _p(r), _p(Jc), _p(Jp)), "me_ba_evaluate")
+    return r.reshape(no, 4), Jc.reshape(no, 4, 6), Jp.reshape(no, 4, 3)
+
+
+def ba_reduced_system(bp, radius: float = 1e4, ctx: Context | None = None):
+    ctx = ctx or default_context()
+    keep = []
+    p, _, _ = ba_struct(bp, keep)
+    m = len(bp.cams) - min(max(bp.fixed_frames, 0), len(bp.cams))
+    S = np.zeros((6 * m) * (6 * m))
+    b = np.zeros(6 * m)
+    ctx.check(ctx.lib.me_ba_reduced_system(ctx.h, byref(p), radius, _p(S), _p(b)), "me_ba_reduced_system")
+    return S.reshape(6 * m, 6 * m), b
+
+
+@dataclass
+class _BAArrays:
+    cams: np.ndarray
+    pts: np.ndarray
+    obs: np.ndarray
+    cam_idx: np.ndarray
+    pt_idx: np.ndarray
+    K0: np.ndarray
+    K1: np.ndarray
+    baseline: float
+    feat_var: float
+    fixed_frames: int
+
+
+class BundleAdjuster:
+    """BundleAdjuster<4> (stereo windowed BA, BundleAdjuster.h:182-476)."""
+
+    def __init__(self, params: CalibrationParameters, cams: list, obs: list, ctx: Context | None = None,
+                 options: SolverOptions | None = None):
+        self.calib_params = params
+        self.m_status = Status.UNINITIALISED
+        self.m_camera_params = []
+        self.m_point_params = []
+        self.m_observations = []
+        self.options = options or SolverOptions()
+        self.ctx = ctx or default_context()
+        self.initialiseParameters(cams)
+        self.initialiseObservations(obs, cams[0].ID if cams else 0)
+
+    def initialiseParameters(self, cams, pts=None):
+        if self.m_status != Status.UNINITIALISED:
+            print("[Bundle Adjuster] system should be uninitialised!")
+            return
+        self.m_point_params = [] if pts is None else [np.asarray(p, np.float64) for p in pts]
+        self.m_camera_params = []
+        for pose in cams:  # BundleAdjuster.h:306-309
+            rv = log_map_Quat(pose.orientation)
+            self.m_camera_params.append(np.array([pose.position[0], pose.position[1], pose.position[2],
+                                                  rv[0], rv[1], rv[2]], np.float64))
+
+    def initialiseObservations(self, observations, first_frame: int):
+        if self.m_status != Status.UNINITIALISED or not self.m_camera_params:
+            print("[Bundle Adjuster] system should be uninitialised and cameras not empty!")
+            return
+        init_points = not self.m_point_params
+        self.m_observations = []
+        for pt_idx, track in enumerate(observations):  # BundleAdjuster.h:359-374
+            if init_points:
+                p = track.get3DLocation()
+                self.m_point_params.append(np.array([p[0] / p[3], p[1] / p[3], p[2] / p[3]]))
+            for i in range(track.getNbFeatures()):
+                fi = track.getFrameIdx(i)
+                if fi - first_frame >= 0:
+                    (xl, yl), (xr, yr) = track.getFeat(i)
+                    self.m_observations.append(((xl, yl, xr, yr), fi - first_frame, pt_idx, track.getCameraID()))
+        self.m_status = Status.INITIALISED
+
+    def _arrays(self, fixed: int) -> _BAArrays:
+        K = self.calib_params.K
+        K0 = np.asarray(K[0], np.float64)
+        if len(K) < 2:
+            raise ValueError("StereoReprojectionError reads K[1] (BundleAdjuster.h:163): give two intrinsics")
+        K1 = np.asarray(K[1], np.float64)
+        obs = np.array([o[0] for o in self.m_observations], np.float64).reshape(-1, 4)
+        ci = np.array([o[1] for o in self.m_observations], np.int32)
+        pi = np.array([o[2] for o in self.m_observations], np.int32)
+        return _BAArrays(np.array(self.m_camera_params).reshape(-1, 6), np.array(self.m_point_params).reshape(-1, 3),
+                         obs, ci, pi, K0, K1, self.calib_params.baseline, self.calib_params.feat_var, fixed)
+
+    def optimise(self, fixedFrames: int) -> Status:
+        if self.m_status != Status.INITIALISED:
+            print("[Bundle Adjuster] system should be initiliased to perform optimisation!")
+            return self.m_status
+        cams, pts, summ = ba_solve(self._arrays(fixedFrames), self.options, self.ctx)
+        self.m_camera_params = [c.copy() for c in cams]
+        self.m_point_params = [p.copy() for p in pts]
+        self.summary = summ
+        self.m_status = Status.SUCCESSFUL if summ["status"] == 2 else Status.FAILED
+        return self.m_status
+
+    def getPoints(self):
+        return [p.copy() for p in self.m_point_params]
+
+    def getCameraPoses(self):
+        out = []
+        for idx, c in enumerate(self.m_camera_params):  # IDs renumbered 0..W-1 (BundleAdjuster.h:231-236)
+            out.append(CamPose(idx, Quat(*exp_map_Quat(c[3:]).coeffs()), np.array(c[:3])))
+        return out
+
+    def getNbPoints(self):
+        return len(self.m_point_params)
+
+    def getNbCameras(self):
+        return len(self.m_camera_params)
+
+    def getNbObservations(self):
+        return len(self.m_observations)
+
+    def getStatus(self):
+        return self.m_status

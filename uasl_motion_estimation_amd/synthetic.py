@@ -1,0 +1,381 @@
+"""Deterministic synthetic stereo streams (SURVEY §8d generator).
+
+The reference ships no data and no tests, so every input of the parity tests
+and of bench.py is generated here from a seed (seed = 20261015 + config):
+
+* intrinsics fx = fy = 0.9 W, cx = W/2, cy = H/2, K0 = K1, baseline b = 0.5 m
+  (the reference's default for a zero baseline, BundleAdjuster.h:389-390);
+* camera path: forward 0.5 m / keyframe, yaw 0.3 deg / keyframe; poses are
+  world->camera (p_cam = R X + t), the convention of both StereoReprojectionError
+  (BundleAdjuster.h:153-160) and ScaleState (optimisation.cpp:175-178);
+* landmarks Z ~ U[5, 50] m, track lengths U[2, W], sigma = 0.5 px noise
+  (feat_var = 0.25 = TrackingInfo::feat_cov, file_IO.h:73), fixedFrames = 2;
+* images: 8-bit 4-octave value-noise texture on piecewise fronto-parallel
+  planes; the right image goes through a NON-monotone tone map, the
+  multi-spectral case mutual information is meant for.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+CONFIGS = {
+    1: dict(width=640, height=480, n_feats=200, window=5),
+    2: dict(width=640, height=480, n_feats=500, window=10),
+    3: dict(width=1280, height=720, n_feats=2000, window=20),
+    4: dict(width=3840, height=2160, n_feats=8000, window=30),
+    5: dict(width=1280, height=720, n_feats=2000, window=50),
+}
+SEED0 = 20261015
+BASELINE = 0.5
+
+
+def intrinsics(width: int, height: int) -> np.ndarray:
+    f = 0.9 * width
+    return np.array([[f, 0.0, width / 2.0], [0.0, f, height / 2.0], [0.0, 0.0, 1.0]])
+
+
+# ------------------------------------------------------------------ rotations
+def rot_y(a: float) -> np.ndarray:
+    c, s = math.cos(a), math.sin(a)
+    return np.array([[c, 0.0, s], [0.0, 1.0, 0.0], [-s, 0.0, c]])
+
+
+def aa_to_R(aa: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(aa))
+    if th < 1e-12:
+        return np.eye(3)
+    w = aa / th
+    Wx = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+    return np.eye(3) + math.sin(th) * Wx + (1 - math.cos(th)) * Wx @ Wx
+
+
+def R_to_aa(R: np.ndarray) -> np.ndarray:
+    c = max(-1.0, min(1.0, (np.trace(R) - 1) / 2))
+    th = math.acos(c)
+    if th < 1e-12:
+        return np.zeros(3)
+    v = np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    return v * th / (2 * math.sin(th))
+
+
+def R_to_quat(R: np.ndarray) -> np.ndarray:
+    """(w, x, y, z) with w >= 0, matching Quat::getR3 (rotation_utils.h:232-237)."""
+    aa = R_to_aa(R)
+    th = float(np.linalg.norm(aa))
+    if th < 1e-12:
+        return np.array([1.0, 0.0, 0.0, 0.0])
+    ax = aa / th
+    return np.concatenate([[math.cos(th / 2)], ax * math.sin(th / 2)])
+
+
+def trajectory(window: int, first_id: int = 0):
+    """World->camera poses (R, t) of `window` keyframes."""
+    poses = []
+    for i in range(window):
+        k = first_id + i
+        Rw = rot_y(math.radians(0.3 * k))  # camera->world rotation
+        C = np.array([0.0, 0.0, 0.5 * k])
+        R = Rw.T
+        t = -R @ C
+        poses.append((R, t))
+    return poses
+
+
+def project(K, b, R, t, X):
+    p = R @ X + t
+    xl = K[0, 0] * p[0] / p[2] + K[0, 2]
+    y = K[1, 1] * p[1] / p[2] + K[1, 2]
+    xr = K[0, 0] * (p[0] - b) / p[2] + K[0, 2]
+    return np.array([xl, y, xr, y]), p
+
+
+# ------------------------------------------------------------------ BA window
+@dataclass
+class BAProblem:
+    cams: np.ndarray          # (W, 6) {t, angle-axis}
+    pts: np.ndarray           # (N, 3)
+    obs: np.ndarray           # (O, 4)
+    cam_idx: np.ndarray       # (O,) int32
+    pt_idx: np.ndarray        # (O,) int32
+    K0: np.ndarray
+    K1: np.ndarray
+    baseline: float
+    feat_var: float
+    fixed_frames: int
+    cams_true: np.ndarray = field(default=None)
+    pts_true: np.ndarray = field(default=None)
+
+    def copy(self):
+        return BAProblem(self.cams.copy(), self.pts.copy(), self.obs, self.cam_idx, self.pt_idx, self.K0, self.K1,
+                         self.baseline, self.feat_var, self.fixed_frames, self.cams_true, self.pts_true)
+
+
+def ba_problem(seed: int, n_pts: int, window: int, width: int, height: int, noise: float = 0.5,
+               fixed: int = 2, alive_frac: float = 0.7, outlier_frac: float = 0.02) -> BAProblem:
+    rng = np.random.default_rng(seed)
+    K = intrinsics(width, height)
+    b = BASELINE
+    poses = trajectory(window)
+    margin = 12.0
+    pts_true, obs, cidx, pidx = [], [], [], []
+    j = 0
+    tries = 0
+    while j < n_pts and tries < 50 * n_pts:
+        tries += 1
+        L = int(rng.integers(2, window + 1))
+        if rng.random() < alive_frac:
+            end = window - 1
+        else:
+            end = int(rng.integers(L - 1, window))
+        start = end - L + 1
+        u = rng.uniform(margin, width - margin)
+        v = rng.uniform(margin, height - margin)
+        Z = rng.uniform(5.0, 50.0)
+        R, t = poses[start]
+        pc = np.array([(u - K[0, 2]) * Z / K[0, 0], (v - K[1, 2]) * Z / K[1, 1], Z])
+        X = R.T @ (pc - t)
+        ok = True
+        rows = []
+        for f in range(start, end + 1):
+            m, p = project(K, b, poses[f][0], poses[f][1], X)
+            if p[2] < 1.0 or not (margin <= m[0] < width - margin and margin <= m[1] < height - margin
+                                  and margin <= m[2] < width - margin):
+                ok = False
+                break
+            rows.append((f, m))
+        if not ok:
+            continue
+        for f, m in rows:
+            mm = m + rng.normal(0.0, noise, 4)
+            mm[3] = mm[1] + rng.normal(0.0, noise)  # y of the right image observed independently
+            if rng.random() < outlier_frac:
+                mm[:2] += rng.normal(0.0, 8.0, 2)
+            obs.append(mm)
+            cidx.append(f)
+            pidx.append(j)
+        pts_true.append(X)
+        j += 1
+    pts_true = np.array(pts_true)
+    cams_true = np.zeros((window, 6))
+    for i, (R, t) in enumerate(poses):
+        cams_true[i, :3] = t
+        cams_true[i, 3:] = R_to_aa(R)
+    # initial estimate: perturbed poses (2 cm, 0.2 deg) except the fixed ones,
+    # points triangulated from the noisy first stereo observation
+    cams = cams_true.copy()
+    for i in range(fixed, window):
+        cams[i, :3] += rng.normal(0.0, 0.02, 3)
+        cams[i, 3:] += np.radians(rng.normal(0.0, 0.2, 3))
+    obs = np.array(obs)
+    cidx = np.array(cidx, dtype=np.int32)
+    pidx = np.array(pidx, dtype=np.int32)
+    pts = np.zeros_like(pts_true)
+    first = np.full(len(pts_true), -1)
+    for o in range(len(obs)):
+        if first[pidx[o]] < 0:
+            first[pidx[o]] = o
+    for jj in range(len(pts_true)):
+        o = first[jj]
+        xl, yl, xr, _ = obs[o]
+        d = max(xl - xr, 0.5)
+        Z = K[0, 0] * b / d
+        pc = np.array([(xl - K[0, 2]) * Z / K[0, 0], (yl - K[1, 2]) * Z / K[1, 1], Z])
+        R = aa_to_R(cams[cidx[o], 3:])
+        pts[jj] = R.T @ (pc - cams[cidx[o], :3])
+    # keep the start feasible for the Ceres-style bounds (BundleAdjuster.h:455-460)
+    Zmax = K[0, 0] * b / 0.1
+    pts[:, 2] = np.clip(pts[:, 2], K[0, 0] * b / (2 * K[0, 2]) + 1e-3, Zmax - 1e-3)
+    return BAProblem(cams, pts, obs, cidx, pidx, K.copy(), K.copy(), b, noise ** 2, fixed, cams_true, pts_true)
+
+
+# ------------------------------------------------------------------ images
+def _value_noise(X, Y, rng_seed: int, octaves: int = 4, base: float = 0.35):
+    out = np.zeros_like(X)
+    amp, tot = 1.0, 0.0
+    for o in range(octaves):
+        cell = base / (2 ** o)
+        gx, gy = X / cell, Y / cell
+        ix, iy = np.floor(gx).astype(np.int64), np.floor(gy).astype(np.int64)
+        fx, fy = gx - ix, gy - iy
+        sx, sy = fx * fx * (3 - 2 * fx), fy * fy * (3 - 2 * fy)
+
+        def h(a, c):
+            v = (a * 73856093) ^ (c * 19349663) ^ (rng_seed * 83492791 + o * 2654435761)
+            v = (v ^ (v >> 13)) * 1274126177
+            v = v ^ (v >> 16)
+            return (v & 0xFFFF).astype(np.float64) / 65535.0
+
+        v00, v10, v01, v11 = h(ix, iy), h(ix + 1, iy), h(ix, iy + 1), h(ix + 1, iy + 1)
+        val = (v00 * (1 - sx) + v10 * sx) * (1 - sy) + (v01 * (1 - sx) + v11 * sx) * sy
+        out += amp * val
+        tot += amp
+        amp *= 0.55
+    return out / tot
+
+
+@dataclass
+class Scene:
+    planes: list           # (x0, x1, Z) world strips
+    seed: int
+
+
+def make_scene(seed: int) -> Scene:
+    rng = np.random.default_rng(seed)
+    edges = np.sort(rng.uniform(-40, 40, 9))
+    planes = [(-1e9, edges[0], float(rng.uniform(8, 40)))]
+    for a, c in zip(edges[:-1], edges[1:]):
+        planes.append((float(a), float(c), float(rng.uniform(6, 45))))
+    planes.append((float(edges[-1]), 1e9, float(rng.uniform(8, 40))))
+    planes.append((-1e9, 1e9, 60.0))  # background: rays passing between strips
+    return Scene(planes, seed)
+
+
+def tone_map():
+    v = np.arange(256, dtype=np.float64)
+    lut = 127.5 + 120.0 * np.sin(2 * np.pi * v / 255.0 * 1.3 + 0.7)  # non-monotone
+    return np.clip(np.rint(lut), 0, 255).astype(np.uint8)
+
+
+def render(scene: Scene, K, R, t, width, height, shift=0.0):
+    """8-bit image of the scene seen by camera (R, t) shifted by `shift` along its x axis."""
+    u, v = np.meshgrid(np.arange(width, dtype=np.float64), np.arange(height, dtype=np.float64))
+    d = np.stack([(u - K[0, 2]) / K[0, 0], (v - K[1, 2]) / K[1, 1], np.ones_like(u)], -1)
+    Rw = R.T
+    C = -Rw @ t + Rw @ np.array([shift, 0.0, 0.0])
+    dw = d @ Rw.T
+    best = np.full(u.shape, np.inf)
+    tex = np.zeros(u.shape)
+    for (x0, x1, Z) in scene.planes:
+        s = (Z - C[2]) / dw[..., 2]
+        X = C[0] + s * dw[..., 0]
+        Y = C[1] + s * dw[..., 1]
+        hit = (s > 0) & (X >= x0) & (X < x1) & (s < best)
+        if hit.any():
+            best = np.where(hit, s, best)
+            val = _value_noise(X, Y, scene.seed)
+            tex = np.where(hit, val, tex)
+    img = np.clip(np.rint(tex * 255.0), 0, 255).astype(np.uint8)
+    return img
+
+
+def depth_at(scene: Scene, K, R, t, u, v):
+    """Depth along the optical axis and world point for pixels (u, v)."""
+    d = np.stack([(u - K[0, 2]) / K[0, 0], (v - K[1, 2]) / K[1, 1], np.ones_like(u)], -1)
+    Rw = R.T
+    C = -Rw @ t
+    dw = d @ Rw.T
+    best = np.full(u.shape, np.inf)
+    for (x0, x1, Z) in scene.planes:
+        s = (Z - C[2]) / dw[..., 2]
+        X = C[0] + s * dw[..., 0]
+        hit = (s > 0) & (X >= x0) & (X < x1) & (s < best)
+        best = np.where(hit, s, best)
+    Xw = C[None, :] + best[:, None] * dw
+    return best, Xw
+
+
+@dataclass
+class StereoFrame:
+    left: np.ndarray
+    right: np.ndarray
+    R: np.ndarray
+    t: np.ndarray
+
+
+def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: int = 0):
+    scene = make_scene(seed)
+    K = intrinsics(width, height)
+    lut = tone_map()
+    frames = []
+    for (R, t) in trajectory(n_frames, first_id):
+        L = render(scene, K, R, t, width, height)
+        Rraw = render(scene, K, R, t, width, height, shift=BASELINE)
+        frames.append(StereoFrame(L, lut[Rraw], R, t))
+    return scene, K, frames
+
+
+def grid_features(rng, n, width, height, margin):
+    """Jittered grid of n feature positions at least `margin` px from the border."""
+    aspect = width / height
+    ny = max(1, int(round(math.sqrt(n / aspect))))
+    nx = max(1, int(math.ceil(n / ny)))
+    xs = np.linspace(margin, width - margin - 1, nx)
+    ys = np.linspace(margin, height - margin - 1, ny)
+    gx, gy = np.meshgrid(xs, ys)
+    pts = np.stack([gx.ravel(), gy.ravel()], -1)[:n]
+    jit = rng.uniform(-0.45, 0.45, pts.shape) * np.array([xs[1] - xs[0] if nx > 1 else 0,
+                                                           ys[1] - ys[0] if ny > 1 else 0])
+    pts = np.clip(pts + jit, margin, np.array([width - margin - 1, height - margin - 1]))
+    return pts
+
+
+@dataclass
+class ScaleProblem:
+    """Flattened ScaleState (optimisation.h:76-98) of the last keyframe."""
+    X_left: np.ndarray
+    X_right: np.ndarray
+    tri_left: np.ndarray
+    tri_right: np.ndarray
+    last_left: np.ndarray
+    last_right: np.ndarray
+    lframe: int
+    K1: np.ndarray
+    K2: np.ndarray
+    q1: np.ndarray
+    t1: np.ndarray
+    q2: np.ndarray
+    t2: np.ndarray
+    scale: float
+    baseline: float
+    window_size: int
+    imgL: np.ndarray
+    imgR: np.ndarray
+    mask: np.ndarray | None = None
+
+
+def scale_problem(seed: int, width: int, height: int, n_feats: int, window: int = 5, w: int = 5,
+                  scale0: float = 1.02, frames=None, scene=None, right_frac: float = 0.25,
+                  untriangulated_frac: float = 0.03, stale_frac: float = 0.05) -> ScaleProblem:
+    """Tracks seen in the last keyframe of a window, 3-D points from the scene."""
+    rng = np.random.default_rng(seed + 7)
+    if frames is None:
+        scene, K, frames = stereo_stream(seed, width, height, 2)
+    K = intrinsics(width, height)
+    fr = frames[-1]
+    R, t = fr.R, fr.t
+    pts = grid_features(rng, n_feats, width, height, 4 * w + 4)
+    depth, Xw = depth_at(scene, K, R, t, pts[:, 0], pts[:, 1])
+    Xh = np.concatenate([Xw, np.ones((len(Xw), 1))], 1)
+    n_right = int(round(right_frac * n_feats))
+    n_left = n_feats - n_right
+    XL = Xh[:n_left].copy()
+    XR = Xh[n_left:].copy()
+    # right-detected tracks store the point shifted by the baseline in the
+    # camera frame (optimisation.cpp:202-207 undoes exactly that)
+    XR[:, :3] = XR[:, :3] - (R.T @ np.array([BASELINE, 0.0, 0.0]))[None, :]
+    tri_l = (rng.random(n_left) >= untriangulated_frac).astype(np.uint8)
+    tri_r = (rng.random(n_right) >= untriangulated_frac).astype(np.uint8)
+    XL[tri_l == 0] = np.array([0, 0, 0, 1.0])
+    XR[tri_r == 0] = np.array([0, 0, 0, 1.0])
+    lframe = window - 1
+    last_l = np.where(rng.random(n_left) < stale_frac, lframe - 1, lframe).astype(np.uint32)
+    last_r = np.where(rng.random(n_right) < stale_frac, lframe - 1, lframe).astype(np.uint32)
+    q = R_to_quat(R)
+    return ScaleProblem(np.ascontiguousarray(XL), np.ascontiguousarray(XR), tri_l, tri_r, last_l, last_r, lframe,
+                        K.copy(), K.copy(), q, t.copy(), q.copy(), t.copy(), scale0, BASELINE, w,
+                        np.ascontiguousarray(fr.left), np.ascontiguousarray(fr.right))
+
+
+def random_patches(seed: int, width: int, height: int, n: int, pw: int, ph: int):
+    """Random images + corner lists for batched MI tests/benchmarks."""
+    rng = np.random.default_rng(seed)
+    scene, K, frames = stereo_stream(seed, width, height, 1)
+    L, Rimg = frames[0].left, frames[0].right
+    xyL = np.stack([rng.integers(0, width - pw + 1, n), rng.integers(0, height - ph + 1, n)], -1).astype(np.int32)
+    d = rng.integers(-3, 40, n)
+    xyR = np.stack([np.clip(xyL[:, 0] - d, 0, width - pw), np.clip(xyL[:, 1] + rng.integers(-1, 2, n), 0,
+                                                                     height - ph)], -1).astype(np.int32)
+    return L, Rimg, np.ascontiguousarray(xyL), np.ascontiguousarray(xyR)
