@@ -1,0 +1,255 @@
+#!/usr/bin/env python3
+"""Headline benchmark: frames/s + BA iter/s, 2000 feats x 20-keyframe window (BASELINE.json, config 3).
+
+One step = one stereo frame of the hot path on one batch of synthetic input,
+inputs resident in HBM when the timed region starts:
+  1. KLT: 2000 features tracked from the previous to the current left image
+     (3 pyramid levels, 21x21 window)            -> klt.hip
+  2. MI stereo-scale optimisation of the current keyframe (2000 tracks,
+     11x11 MI patches, reference OptimisationParams defaults) -> scale.hip / mi
+  3. windowed stereo BA: 2000 landmarks x 20 keyframes, 10 LM iterations
+     (fixed work, tolerances off)   -> ba.hip (FP64 MFMA Schur)
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process
+per GPU, each rank processes its own independent stereo stream (weak scaling,
+no collective on the data path; config-3 windows are below the landmark count
+at which the RCCL-sharded BA pays).  The barrier and the MAX over
+ranks of the timed region stay; value = frames of all ranks / that time.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=4, help="distinct synthetic frames cycled per rank")
+    ap.add_argument("--ba-iters", type=int, default=10)
+    ap.add_argument("--cpu-frames", type=int, default=2, help="frames of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+class FrameData:
+    pass
+
+
+def make_frames(cfg: dict, seed: int, n_frames: int):
+    from uasl_motion_estimation_amd import synthetic as S
+
+    W, H, N, win = cfg["width"], cfg["height"], cfg["n_feats"], cfg["window"]
+    scene, K, stream = S.stereo_stream(seed, W, H, n_frames + 1)
+    frames = []
+    rng = np.random.default_rng(seed)
+    for f in range(n_frames):
+        fd = FrameData()
+        fd.prev = stream[f].left
+        fd.cur = stream[f + 1]
+        fd.klt_pts = S.grid_features(rng, N, W, H, 12).astype(np.float32)
+        fd.scale = S.scale_problem(seed + f, W, H, N, window=win, w=5, frames=stream[: f + 2], scene=scene)
+        fd.ba = S.ba_problem(seed * 7 + f, N, win, W, H)
+        frames.append(fd)
+    return frames
+
+
+def upload_images(ctx, frames):
+    """Device copies of every image (inputs resident in HBM before timing)."""
+    keep = []
+    for fd in frames:
+        for name, img in (("d_prev", fd.prev), ("d_curL", fd.cur.left), ("d_curR", fd.cur.right)):
+            img = np.ascontiguousarray(img)
+            p = ctypes.c_void_p()
+            ctx.check(ctx.lib.me_malloc(ctx.h, ctypes.byref(p), img.nbytes))
+            ctx.check(ctx.lib.me_memcpy_h2d(ctx.h, p, img.ctypes.data, img.nbytes))
+            setattr(fd, name, p.value)
+            keep.append(p.value)
+        n = len(fd.klt_pts)
+        for name, nbytes in (("d_pts_in", 8 * n), ("d_pts_out", 8 * n), ("d_status", n)):
+            p = ctypes.c_void_p()
+            ctx.check(ctx.lib.me_malloc(ctx.h, ctypes.byref(p), max(nbytes, 16)))
+            setattr(fd, name, p.value)
+        ctx.check(ctx.lib.me_memcpy_h2d(ctx.h, ctypes.c_void_p(fd.d_pts_in), fd.klt_pts.ctypes.data, 8 * n))
+    return keep
+
+
+def gpu_step(ctx, fd, kp, ba_opts, stats):
+    from uasl_motion_estimation_amd._lib import ME_DEVICE
+    from uasl_motion_estimation_amd.optimisation import ba_solve, scale_optimise
+
+    H, W = fd.prev.shape
+    n = len(fd.klt_pts)
+    ctx.check(ctx.lib.me_klt_track(ctx.h, ME_DEVICE, ctypes.c_void_p(fd.d_prev), ctypes.c_void_p(fd.d_curL), W, H, W,
+                                   ctypes.c_void_p(fd.d_pts_in), ctypes.c_void_p(fd.d_pts_out),
+                                   ctypes.c_void_p(fd.d_status), n, ctypes.byref(kp)), "klt")
+    r = scale_optimise(fd.scale, ctx=ctx, img_mem=ME_DEVICE, dev_imgs=(fd.d_curL, fd.d_curR))
+    stats["scale_iters"] += r["iterations"]
+    cams, pts, s = ba_solve(fd.ba, ba_opts, ctx=ctx)
+    stats["ba_iters"] += s["iterations"]
+    stats["frames"] += 1
+
+
+def cpu_step(fd, ba_iters, stats):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle as O  # CPU baseline leg only
+
+    O.klt(fd.prev, fd.cur.left, fd.klt_pts)
+    O.scale_optimise(fd.scale)
+    _, _, s = O.ba_solve(fd.ba, max_num_iterations=ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                         parameter_tolerance=0.0)
+    stats["ba_iters"] += s["iterations"]
+
+
+# algorithmic bytes per launch of each kernel family
+def alg_bytes(family: str, cfg: dict, frames) -> float:
+    N, win = cfg["n_feats"], cfg["window"]
+    if family == "SCALE_RES":
+        return 262.0 * N                  # 2x121 px + 2 corners + out per track
+    if family == "SCALE_NEQ":
+        return 234.0 * N                  # x0 100 B + x1∪x2 110 B + corners + out
+    if family == "KLT":
+        return (2 * 22 * 22 + 2 * 2 * 22 * 22 + 16) * 4.0 * N  # I, dIx, dIy windows (+1 border) + 3 levels
+    fd = frames[0].ba
+    no, npt = len(fd.obs), len(fd.pts)
+    if family == "BA_LINEARIZE":
+        return no * (32 + 8 + 24 + 48 + 320.0)   # obs, idx, point, camera in; r + J out
+    if family == "BA_POINTS":
+        return no * (320 + 144.0) + npt * 72.0  # J in, W out, V/g per point
+    if family == "BA_SCHUR":
+        m = win - fd.fixed_frames
+        return 2 * 8.0 * (3 * npt) * (6 * m)    # dense Y written + read by the MFMA GEMM
+    if family == "BA_STEP":
+        return no * (320 + 32 + 8 + 72.0)
+    return 0.0
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    from uasl_motion_estimation_amd import synthetic as S
+    from uasl_motion_estimation_amd._lib import Context, KT
+    from uasl_motion_estimation_amd.klt import klt_params
+    from uasl_motion_estimation_amd.optimisation import SolverOptions
+
+    cfg = S.CONFIGS[args.config]
+    seed = S.SEED0 + args.config + 1000 * rank
+    t0 = time.time()
+    frames = make_frames(cfg, seed, args.frames)
+    gen_s = time.time() - t0
+    ctx = Context(local_rank)
+    upload_images(ctx, frames)
+    kp = klt_params()
+    ba_opts = SolverOptions.fixed_iterations(args.ba_iters)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    stats = dict(frames=0, ba_iters=0, scale_iters=0)
+    for i in range(args.warmup):
+        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+    ctx.synchronize()
+    # kernel timing with HIP events on the ctx stream, live in the timed region
+    ctx.timing_reset()
+    ctx.timing(True)
+    stats = dict(frames=0, ba_iters=0, scale_iters=0)
+    barrier()
+    torch.cuda.synchronize()
+    ctx.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t_start
+    barrier()
+    ctx.timing(False)
+    fams = {f: ctx.timing_read(f) for f in ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_POINTS", "BA_SCHUR",
+                                            "BA_SOLVE", "BA_STEP", "KLT", "PYR")}
+    t_max = elapsed
+    frames_total = stats["frames"]
+    ba_total = stats["ba_iters"]
+    if dist is not None:
+        tt = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        cnt = torch.tensor([stats["frames"], stats["ba_iters"]], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(cnt)
+        frames_total, ba_total = int(cnt[0].item()), int(cnt[1].item())
+    value = frames_total / t_max
+    # dominant kernel family by measured device time
+    dom = max((f for f in fams if fams[f][0] > 0 and alg_bytes(f, cfg, frames) > 0), key=lambda f: fams[f][1])
+    n_l, ms_l = fams[dom]
+    avg_ms = ms_l / n_l
+    bytes_launch = alg_bytes(dom, cfg, frames)
+    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
+    peak = 8000.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
+                "frac": round(achieved / peak, 5), "traffic": None, "kernel": dom,
+                "avg_launch_ms": round(avg_ms, 5), "alg_bytes_per_launch": bytes_launch}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cstats = dict(ba_iters=0)
+        t1 = time.perf_counter()
+        nf = max(1, args.cpu_frames)
+        for i in range(nf):
+            cpu_step(frames[i % len(frames)], args.ba_iters, cstats)
+        ct = time.perf_counter() - t1
+        cpu = {"value": round(nf / ct, 4), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"{nf} config-{args.config} frames (KLT + MI scale LM + {args.ba_iters}-iteration BA) on the "
+                         f"oracle restatement, 1 thread; {ct:.1f} s",
+               "ba_iter_per_s": round(cstats['ba_iters'] / ct, 3)}
+    if rank == 0:
+        out = {
+            "metric": "frames/sec + BA iter/sec, 2000 feats x 20-keyframe window, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * t_max / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8+f32 (MI), f64 (BA)",
+            "data": "synthetic",
+            "config": {"workload": f"config {args.config}: {cfg['width']}x{cfg['height']} stereo, "
+                                   f"{cfg['n_feats']} feats, {cfg['window']}-keyframe window, 11x11 MI patches",
+                       "frame": f"KLT + MI scale LM + {args.ba_iters} BA LM iterations",
+                       "parallelism": f"{world} independent streams (one per GPU)"},
+            "ba_iter_per_s": round(ba_total / t_max, 2),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "kernel_ms": {f: [fams[f][0], round(fams[f][1], 3)] for f in fams},
+            "gen_s": round(gen_s, 1),
+        }
+        print(json.dumps(out))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
