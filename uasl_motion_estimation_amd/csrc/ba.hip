@@ -11,6 +11,9 @@
 #include <vector>
 #include "me_internal.hpp"
 #include "ba_kernels.hpp"
+#include "me_device.hpp"
+
+using me_dev::wave_sync;
 
 using namespace ba;
 
@@ -154,6 +157,11 @@ __device__ __forceinline__ void huber(double s, double* rho0, double* sqrt_rho1)
 }
 
 // ---------------------------------------------------------------- kernels
+constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups over the CUs
+
+// Per observation: corrected residual / Jacobian, cost, and the unscaled
+// per-observation normal-equation pieces W_o = Jc^T Jp (6x3), V_o = Jp^T Jp
+// (6 unique), g_o = Jp^T r, so the per-point stage only sums.
 __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
   __shared__ double lds[4];
   const State* st = b.st;
@@ -170,9 +178,27 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
     double rho0, sc;
     huber(s, &rho0, &sc);
     cost = 0.5 * rho0;
-    for (int k = 0; k < 4; ++k) L[k] = r[k] * sc;
-    for (int k = 0; k < 24; ++k) L[4 + k] = Jc[k] * sc;
-    for (int k = 0; k < 12; ++k) L[28 + k] = Jp[k] * sc;
+    for (int k = 0; k < 4; ++k) r[k] *= sc;
+    for (int k = 0; k < 24; ++k) Jc[k] *= sc;
+    for (int k = 0; k < 12; ++k) Jp[k] *= sc;
+    for (int k = 0; k < 4; ++k) L[k] = r[k];
+    for (int k = 0; k < 24; ++k) L[4 + k] = Jc[k];
+    for (int k = 0; k < 12; ++k) L[28 + k] = Jp[k];
+    const long slot = b.pos[o];  // CSR-by-point slot: per-point stages read contiguously
+    double* X = b.obsx + slot * kObsxStride;
+    X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
+    X[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
+    X[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
+    X[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
+    X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
+    X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
+    for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
+    if (ci - g.nf >= 0) {
+      double* W = b.Wo + 18 * slot;
+      for (int a = 0; a < 6; ++a)
+        for (int c = 0; c < 3; ++c)
+          W[a * 3 + c] = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
+    }
   }
   double v[1] = {cost};
   double out[1];
@@ -180,171 +206,150 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
   if (threadIdx.x == 0) b.part[R_COST * g.pstride + blockIdx.x] = out[0];
 }
 
-// phase 0: camera Jacobian column norms -> colnorm (6m); phase 1: U, g
-__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, int phase, double* colnorm,
-                                                              double* gc_raw) {
-  __shared__ double lds[4 * 33];
+// One workgroup per variable camera: unscaled U = Jc^T Jc and g = Jc^T r over
+// its observations (fixed order), then (unless sharded) the Jacobi scaling at
+// iteration 0 from diag(U) = squared column norms, and the scaled blocks.
+__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, int sharded, double* colnorm,
+                                                              double* gc_raw, double* Uraw) {
+  __shared__ double lds[4 * 27];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
-  if (phase == 0 && st->scaled) return;
   const int ci = blockIdx.x;
   const int beg = b.c_off[ci], end = b.c_off[ci + 1];
-  if (phase == 0) {
-    double v[6] = {0, 0, 0, 0, 0, 0};
-    for (int q = beg + threadIdx.x; q < end; q += kBlock) {
-      const double* L = b.lin + (long)b.c_obs[q] * kLinStride;
-      for (int k = 0; k < 4; ++k)
-        for (int j = 0; j < 6; ++j) v[j] += L[4 + k * 6 + j] * L[4 + k * 6 + j];
-    }
-    double out[6];
-    block_sum<6>(v, out, lds);
-    if (threadIdx.x == 0)
-      for (int j = 0; j < 6; ++j) colnorm[6 * ci + j] = out[j];
-    return;
-  }
-  // 21 unique JtJ + 6 gradient entries, unscaled, then scaled on write
   double v[27];
   for (int i = 0; i < 27; ++i) v[i] = 0;
   for (int q = beg + threadIdx.x; q < end; q += kBlock) {
     const double* L = b.lin + (long)b.c_obs[q] * kLinStride;
     int u = 0;
     for (int a = 0; a < 6; ++a)
-      for (int c = a; c < 6; ++c, ++u) {
-        double s = 0;
-        for (int k = 0; k < 4; ++k) s += L[4 + k * 6 + a] * L[4 + k * 6 + c];
-        v[u] += s;
-      }
-    for (int a = 0; a < 6; ++a) {
-      double s = 0;
-      for (int k = 0; k < 4; ++k) s += L[4 + k * 6 + a] * L[k];
-      v[21 + a] += s;
-    }
+      for (int c = a; c < 6; ++c, ++u)
+        v[u] += L[4 + a] * L[4 + c] + L[10 + a] * L[10 + c] + L[16 + a] * L[16 + c] + L[22 + a] * L[22 + c];
+    for (int a = 0; a < 6; ++a) v[21 + a] += L[4 + a] * L[0] + L[10 + a] * L[1] + L[16 + a] * L[2] + L[22 + a] * L[3];
   }
   double out[27];
   block_sum<27>(v, out, lds);
   if (threadIdx.x == 0) {
-    const double* cs = b.csc + 6 * ci;
-    double* U = b.U + 36 * (long)ci;
+    double* Ur = Uraw + 21 * (long)ci;
+    for (int u = 0; u < 21; ++u) Ur[u] = out[u];
     int u = 0;
-    for (int a = 0; a < 6; ++a)
-      for (int c = a; c < 6; ++c, ++u) {
-        const double x = out[u] * cs[a] * cs[c];
-        U[a * 6 + c] = x;
-        U[c * 6 + a] = x;
-      }
     for (int a = 0; a < 6; ++a) {
-      b.gcs[6 * ci + a] = out[21 + a] * cs[a];
+      colnorm[6 * ci + a] = out[u];  // diagonal entry (a, a)
+      u += 6 - a;
       gc_raw[6 * ci + a] = out[21 + a];
+    }
+    if (!sharded) {
+      double* cs = b.csc + 6 * ci;
+      if (!st->scaled)
+        for (int a = 0; a < 6; ++a) cs[a] = g.jacobi ? 1.0 / (1.0 + sqrt(colnorm[6 * ci + a])) : 1.0;
+      double* U = b.U + 36 * (long)ci;
+      u = 0;
+      for (int a = 0; a < 6; ++a)
+        for (int c = a; c < 6; ++c, ++u) {
+          const double x = out[u] * cs[a] * cs[c];
+          U[a * 6 + c] = x;
+          U[c * 6 + a] = x;
+        }
+      for (int a = 0; a < 6; ++a) b.gcs[6 * ci + a] = out[21 + a] * cs[a];
     }
   }
 }
 
-__global__ void cam_scaling_kernel(Geo g, Bufs b, const double* colnorm) {
+// Sharded mode: scaling from the all-reduced column norms, then scale the
+// (local) U / g blocks.
+__global__ void cam_finish_kernel(Geo g, Bufs b, const double* colnorm, const double* gc_raw, const double* Uraw) {
   const State* st = b.st;
-  if (st->done || !st->need_lin || st->scaled) return;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < g.n6) b.csc[i] = 1.0 / (1.0 + sqrt(colnorm[i]));
+  if (st->done || !st->need_lin) return;
+  const int ci = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ci >= g.m) return;
+  double* cs = b.csc + 6 * ci;
+  if (!st->scaled)
+    for (int a = 0; a < 6; ++a) cs[a] = g.jacobi ? 1.0 / (1.0 + sqrt(colnorm[6 * ci + a])) : 1.0;
+  const double* Ur = Uraw + 21 * (long)ci;
+  double* U = b.U + 36 * (long)ci;
+  int u = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int c = a; c < 6; ++c, ++u) {
+      const double x = Ur[u] * cs[a] * cs[c];
+      U[a * 6 + c] = x;
+      U[c * 6 + a] = x;
+    }
+  for (int a = 0; a < 6; ++a) b.gcs[6 * ci + a] = gc_raw[6 * ci + a] * cs[a];
 }
 
-__global__ __launch_bounds__(kBlock) void pt_assemble_kernel(Geo g, Bufs b, int jacobi) {
+// One lane per point: sum V_o, g_o; point Jacobi scaling at iteration 0
+// (diag V = squared column norms); projected-gradient max-norm contribution.
+__global__ __launch_bounds__(kPtBlock) void pt_assemble_kernel(Geo g, Bufs b) {
   __shared__ double lds[4];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
-  const int j = blockIdx.x * kBlock + threadIdx.x;
+  const int j = blockIdx.x * kPtBlock + threadIdx.x;
   double gm = 0;
   if (j < g.np) {
-    const int beg = b.p_off[j], end = b.p_off[j + 1];
+    double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
+    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
+      const double* X = b.obsx + (long)q * kObsxStride;
+      for (int i = 0; i < 6; ++i) V[i] += X[i];
+      for (int a = 0; a < 3; ++a) gr[a] += X[6 + a];
+    }
     double* ps = b.psc + 3 * (long)j;
     if (!st->scaled) {
-      double cn[3] = {0, 0, 0};
-      for (int q = beg; q < end; ++q) {
-        const double* L = b.lin + (long)b.p_obs[q] * kLinStride;
-        for (int k = 0; k < 4; ++k)
-          for (int a = 0; a < 3; ++a) cn[a] += L[28 + k * 3 + a] * L[28 + k * 3 + a];
-      }
-      for (int a = 0; a < 3; ++a) ps[a] = jacobi ? 1.0 / (1.0 + sqrt(cn[a])) : 1.0;
+      ps[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
+      ps[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
+      ps[2] = g.jacobi ? 1.0 / (1.0 + sqrt(V[5])) : 1.0;
     }
     const double p0 = ps[0], p1 = ps[1], p2 = ps[2];
-    const double pscv[3] = {p0, p1, p2};
-    double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
-    for (int q = beg; q < end; ++q) {
-      const int o = b.p_obs[q];
-      const double* L = b.lin + (long)o * kLinStride;
-      const double* Jp = L + 28;
-      V[0] += Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
-      V[1] += Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
-      V[2] += Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
-      V[3] += Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
-      V[4] += Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
-      V[5] += Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
-      for (int a = 0; a < 3; ++a) gr[a] += Jp[a] * L[0] + Jp[3 + a] * L[1] + Jp[6 + a] * L[2] + Jp[9 + a] * L[3];
-      const int ci = b.cam_idx[o] - g.nf;
-      if (ci >= 0) {
-        const double* Jc = L + 4;
-        const double* cs = b.csc + 6 * ci;
-        double* W = b.Wo + 18 * (long)o;
-        for (int a = 0; a < 6; ++a)
-          for (int c = 0; c < 3; ++c) {
-            double s = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
-            W[a * 3 + c] = s * cs[a] * pscv[c];
-          }
-      }
-    }
     double* Vo = b.V + 9 * (long)j;
     Vo[0] = V[0] * p0 * p0; Vo[1] = V[1] * p0 * p1; Vo[2] = V[2] * p0 * p2;
     Vo[3] = Vo[1];          Vo[4] = V[3] * p1 * p1; Vo[5] = V[4] * p1 * p2;
     Vo[6] = Vo[2];          Vo[7] = Vo[5];          Vo[8] = V[5] * p2 * p2;
-    for (int a = 0; a < 3; ++a) b.gps[3 * (long)j + a] = gr[a] * pscv[a];
-    // projected gradient max-norm contribution ||x - Plus(x, -g)||_inf
+    b.gps[3 * (long)j + 0] = gr[0] * p0;
+    b.gps[3 * (long)j + 1] = gr[1] * p1;
+    b.gps[3 * (long)j + 2] = gr[2] * p2;
     const double* x = b.pts[st->cur] + 3 * (long)j;
     for (int a = 0; a < 3; ++a) {
-      double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
+      const double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
       gm = fmax(gm, fabs(x[a] - xp));
     }
   }
-  double r = block_max(gm, lds);
+  const double r = block_max(gm, lds);
   if (threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
 }
 
-// Reduce linearisation partials into scal[R_COST], scal[R_GMAX_PT]
-__global__ __launch_bounds__(1024) void lin_reduce_kernel(Geo g, Bufs b) {
-  __shared__ double lds[32];
-  const State* st = b.st;
-  if (st->done || !st->need_lin) return;
-  double c = 0, m = 0;
-  for (int i = threadIdx.x; i < g.nblk_obs; i += 1024) c += b.part[R_COST * g.pstride + i];
-  for (int i = threadIdx.x; i < g.nblk_pts; i += 1024) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
-  double v[1] = {c}, out[1];
-  block_sum<1>(v, out, lds);
-  double mm = block_max(m, lds + 20);
-  if (threadIdx.x == 0) {
-    b.scal[R_COST] = out[0];
-    b.scal[R_GMAX_PT] = mm;
-  }
-}
-
-// Linearisation bookkeeping + iteration start (Ceres IterationZero /
-// HandleSuccessfulStep gradient test, FinalizeIteration max-iteration and
-// min-radius tests).
-__global__ void lin_check_kernel(Geo g, Bufs b, Opts o, const double* gc_raw) {
-  if (threadIdx.x != 0) return;
+// Linearisation bookkeeping + iteration start: reduce the cost / gradient
+// partials (fixed order), Ceres gradient-tolerance test (IterationZero /
+// HandleSuccessfulStep), max-iteration and min-radius tests.
+constexpr int kFinBlock = 256;
+__global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, Opts o, const double* gc_raw,
+                                                                 int use_scal) {
+  __shared__ double lds[16];
   State* st = b.st;
   if (st->done) return;
   if (st->need_lin) {
-    st->x_cost = b.scal[R_COST];
-    double gm = b.scal[R_GMAX_PT];
-    for (int i = 0; i < g.n6; ++i) gm = fmax(gm, fabs(gc_raw[i]));
-    if (!st->scaled) {
-      st->initial_cost = st->x_cost;
-      st->scaled = 1;
+    double c = 0, m = 0;
+    if (!use_scal) {
+      for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
+      for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
     }
-    st->need_lin = 0;
-    if (gm <= o.gradient_tolerance) {
-      st->done = 1;
-      st->termination = 0;
-      return;
+    for (int i = threadIdx.x; i < g.n6; i += kFinBlock) m = fmax(m, fabs(gc_raw[i]));
+    double v[1] = {c}, out[1];
+    block_sum<1>(v, out, lds);
+    const double mm = block_max(m, lds + 8);
+    if (threadIdx.x == 0) {
+      st->x_cost = use_scal ? b.scal[R_COST] : out[0];
+      const double gm = use_scal ? fmax(mm, b.scal[R_GMAX_PT]) : mm;
+      if (!st->scaled) {
+        st->initial_cost = st->x_cost;
+        st->scaled = 1;
+      }
+      st->need_lin = 0;
+      if (gm <= o.gradient_tolerance) {
+        st->done = 1;
+        st->termination = 0;
+      }
     }
+    __syncthreads();
   }
+  if (threadIdx.x != 0 || st->done) return;
   if (st->iterations >= o.max_num_iterations) {
     st->done = 1;
     st->termination = 1;
@@ -359,8 +364,26 @@ __global__ void lin_check_kernel(Geo g, Bufs b, Opts o, const double* gc_raw) {
   st->fail = 0;
 }
 
+// Sharded mode: local partial sums into scal (all-reduced by the host callback)
+__global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) {
+  __shared__ double lds[16];
+  const State* st = b.st;
+  if (st->done) return;
+  double c = 0, m = 0;
+  if (st->need_lin) {
+    for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
+    for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+  }
+  double v[1] = {c}, out[1];
+  block_sum<1>(v, out, lds);
+  const double mm = block_max(m, lds + 8);
+  if (threadIdx.x == 0) {
+    b.scal[R_COST] = out[0];
+    b.scal[R_GMAX_PT] = mm;
+  }
+}
+
 __device__ __forceinline__ bool chol3(const double* A, double* L) {
-  // lower-triangular L (row-major 3x3) of SPD A
   double d0 = A[0];
   if (!(d0 > 0)) return false;
   d0 = sqrt(d0);
@@ -388,10 +411,11 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
   x[0] = (y[0] - L[3] * x[1] - L[6] * x[2]) / L[0];
 }
 
-__global__ __launch_bounds__(kBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+// One lane per point: V + D/radius -> Cholesky L_p, z_p = L_p^-1 g_p
+__global__ __launch_bounds__(kPtBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
   State* st = b.st;
   if (st->done) return;
-  const int j = blockIdx.x * kBlock + threadIdx.x;
+  const int j = blockIdx.x * kPtBlock + threadIdx.x;
   if (j >= g.np) return;
   const double radius = st->radius;
   double A[9];
@@ -404,39 +428,34 @@ __global__ __launch_bounds__(kBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o)
     return;
   }
   fwd3(L, b.gps + 3 * (long)j, b.zp + 3 * (long)j);
-  const int beg = b.p_off[j], end = b.p_off[j + 1];
-  for (int q = beg; q < end; ++q) {
-    const int ob = b.p_obs[q];
-    if (b.cam_idx[ob] - g.nf < 0) continue;
-    const double* W = b.Wo + 18 * (long)ob;
-    double* Y = b.Yo + 18 * (long)ob;
-    for (int a = 0; a < 6; ++a) fwd3(L, W + 3 * a, Y + 3 * a);
-  }
 }
 
-// Dense Y[k][r] (k = 3*point + comp, r = 6*varcam + row): sum of Y_o over the
-// point's observations in that camera (duplicates add, as Ceres would).
-__global__ __launch_bounds__(kBlock) void y_scatter_kernel(Geo g, Bufs b) {
+// One lane per observation with a variable camera: Y_o = (Dc W_o Dp) L_p^-T
+// written straight into the dense K-major Y (pre-zeroed).  A point seen twice
+// by one camera (duplicate residual blocks) accumulates with an FP64 atomic.
+__global__ __launch_bounds__(kBlock) void y_obs_kernel(Geo g, Bufs b) {
   const State* st = b.st;
   if (st->done || st->fail) return;
-  const long idx = (long)blockIdx.x * kBlock + threadIdx.x;
-  const long total = (long)g.Kpad * g.Rpad;
-  if (idx >= total) return;
-  const int k = (int)(idx / g.Rpad), r = (int)(idx - (long)k * g.Rpad);
-  double v = 0;
-  if (k < g.K3 && r < g.n6) {
-    const int j = k / 3, c = k - 3 * j;
-    const int cam = r / 6 + g.nf, a = r - 6 * (r / 6);
-    int lo = b.p_off[j], hi = b.p_off[j + 1];
-    while (lo < hi) {  // lower_bound on camera index
-      int mid = (lo + hi) >> 1;
-      if (b.cam_idx[b.p_obs[mid]] < cam) lo = mid + 1;
-      else hi = mid;
+  const int o = blockIdx.x * kBlock + threadIdx.x;
+  if (o >= g.no) return;
+  const int ci = b.cam_idx[o] - g.nf;
+  if (ci < 0) return;
+  const int j = b.pt_idx[o];
+  const double* W = b.Wo + 18 * (long)b.pos[o];
+  const double* L = b.Lp + 9 * (long)j;
+  const double* cs = b.csc + 6 * ci;
+  const double* ps = b.psc + 3 * (long)j;
+  const bool dup = b.dup[o] != 0;
+  for (int a = 0; a < 6; ++a) {
+    const double w[3] = {W[a * 3 + 0] * cs[a] * ps[0], W[a * 3 + 1] * cs[a] * ps[1], W[a * 3 + 2] * cs[a] * ps[2]};
+    double y[3];
+    fwd3(L, w, y);
+    for (int c = 0; c < 3; ++c) {
+      double* dst = b.Y + (long)(3 * j + c) * g.Rpad + 6 * ci + a;
+      if (dup) atomicAdd(dst, y[c]);
+      else *dst = y[c];
     }
-    for (int q = lo; q < b.p_off[j + 1] && b.cam_idx[b.p_obs[q]] == cam; ++q)
-      v += b.Yo[18 * (long)b.p_obs[q] + a * 3 + c];
   }
-  b.Y[idx] = v;
 }
 
 // S partial tiles on the FP64 matrix cores: D(16x16) += A(16x4) B(4x16) with
@@ -490,24 +509,38 @@ __global__ __launch_bounds__(kBlock) void schur_gemm_kernel(Geo g, Bufs b) {
   b.Spart[((long)s * g.npairs + p) * 256 + e] = v;
 }
 
+// Sum of the split-K partials of one S element, in split order.  The loads
+// are issued four at a time (independent addresses) so the latency of these
+// cross-XCD reads is paid once per group, not once per split.
+__device__ __forceinline__ double sum_splits(const Geo& g, const double* Spart, long off) {
+  const long stride = (long)g.npairs * 256;
+  double s = 0;
+  int q = 0;
+  for (; q + 4 <= g.ksplit; q += 4) {
+    const double a0 = Spart[off + (q + 0) * stride], a1 = Spart[off + (q + 1) * stride];
+    const double a2 = Spart[off + (q + 2) * stride], a3 = Spart[off + (q + 3) * stride];
+    s += a0;
+    s += a1;
+    s += a2;
+    s += a3;
+  }
+  for (; q < g.ksplit; ++q) s += Spart[off + q * stride];
+  return s;
+}
+
 __device__ __forceinline__ double gemm_part(const Geo& g, const double* Spart, int r, int c) {
-  // S element (r, c) of sum_k Y[k][r] Y[k][c]
   int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
   if (I > J) {
     int t = I; I = J; J = t;
     t = rr; rr = cc; cc = t;
   }
   const int p = I * g.T - I * (I - 1) / 2 + (J - I);
-  double s = 0;
-  for (int q = 0; q < g.ksplit; ++q) s += Spart[((long)q * g.npairs + p) * 256 + rr * 16 + cc];
-  return s;
+  return sum_splits(g, Spart, (long)p * 256 + rr * 16 + cc);
 }
 __device__ __forceinline__ double gemm_zpart(const Geo& g, const double* Spart, int r) {
   const int ntri = g.T * (g.T + 1) / 2;
   const int p = ntri + (r >> 4);
-  double s = 0;
-  for (int q = 0; q < g.ksplit; ++q) s += Spart[((long)q * g.npairs + p) * 256 + (r & 15) * 16];
-  return s;
+  return sum_splits(g, Spart, (long)p * 256 + (r & 15) * 16);
 }
 
 // Sharded mode: S_local = U - YY^T, b_local = g - Yz, diag(U) (no LM diagonal)
@@ -515,94 +548,233 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b) {
   const State* st = b.st;
   if (st->done) return;
   const int n = g.n6;
-  const long idx = (long)blockIdx.x * kBlock + threadIdx.x;
-  if (idx < (long)n * n) {
-    const int r = (int)(idx / n), c = (int)(idx - (long)r * n);
+  const int idx = blockIdx.x * kBlock + threadIdx.x;
+  if (idx < n * n) {
+    const int r = idx / n, c = idx - r * n;
     double v = 0;
     if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
     b.S[idx] = st->fail ? 0.0 : v - gemm_part(g, b.Spart, r, c);
-  } else if (idx < (long)n * n + n) {
-    const int r = (int)(idx - (long)n * n);
+  } else if (idx < n * n + n) {
+    const int r = idx - n * n;
     b.bvec[r] = st->fail ? 0.0 : b.gcs[r] - gemm_zpart(g, b.Spart, r);
     b.diagU[r] = b.U[36 * (r / 6) + (r % 6) * 7];
-  } else if (idx == (long)n * n + n) {
+  } else if (idx == n * n + n) {
     b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
   }
 }
 
-// One workgroup: assemble S (mode 0) or take the all-reduced S (mode 1), add
-// the LM diagonal, dense Cholesky, y_c = -S^-1 b, candidate cameras.
-constexpr int kSolveBlock = 1024;
-__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int mode, int use_lds) {
+// One workgroup: S (assembled by s_assemble_kernel, all-reduced in sharded
+// mode) + LM diagonal, blocked right-looking Cholesky with 16x16 blocks and
+// block-inverse triangular solves.  Every sequential chain is O(T = n/16):
+//  * diagonal block: 16 lanes, one row per lane in registers, shuffles;
+//  * panel: one lane per row, reciprocal pivots;
+//  * trailing update A_IK -= L_IJ L_KJ^T on v_mfma_f64_16x16x4f64;
+//  * solves: L_JJ^-1 of all diagonal blocks in parallel, then T block steps of
+//    16-term dot products forward and backward.
+// S is padded to N = 16T with an identity block.
+constexpr int kSolveBlock = 256;
+constexpr int kLoadBatch = 16;
+#define SOLVE_STAMP(i)                                                        \
+  do {                                                                        \
+    if ((skip & 256) && tid == 0) st->stamps[(i)] += (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+#define SOLVE_START(i)                                                        \
+  do {                                                                        \
+    if ((skip & 256) && tid == 0) st->stamps[(i)] -= (long long)__builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+__device__ __forceinline__ int solve_ld(int T) { return ((16 * T + 31) / 32) * 32 + 2; }  // == 2 mod 32
+
+__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int use_lds) {
   extern __shared__ double smem[];
   __shared__ double red[64];
   __shared__ int sfail;
   State* st = b.st;
   if (st->done) return;
-  const int n = g.n6;
+  const int n = g.n6, T = g.T, N = 16 * T;
+  const int ld = solve_ld(T);
   const int tid = threadIdx.x, nt = blockDim.x;
-  double* A = use_lds ? smem : b.S;
+  const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  // workspace: A (N x ld) | Linv (T x 256) | invd (N) | u (N)
+  double* A = use_lds ? smem : b.Abuf;
+  double* Linv = A + (long)N * ld;
+  double* invd = Linv + 256 * (long)T;
+  double* u = invd + N;
   const double radius = st->radius;
-  if (tid == 0) sfail = st->fail || (mode == 1 && b.scal[R_COUNT] != 0.0);
+  if (tid == 0) sfail = st->fail || b.scal[R_COUNT] != 0.0;
   __syncthreads();
   if (sfail) {
     if (tid == 0) st->fail = 1;
     return;
   }
-  for (long idx = tid; idx < (long)n * n; idx += nt) {
-    const int r = (int)(idx / n), c = (int)(idx - (long)r * n);
-    double v;
-    if (mode == 0) {
-      v = 0;
-      if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
-      v -= gemm_part(g, b.Spart, r, c);
-      if (r == c) v += fmin(fmax(b.U[36 * (r / 6) + (r % 6) * 7], o.min_diag), o.max_diag) / radius;
-    } else {
-      v = b.S[idx];
-      if (r == c) v += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
+  if ((skip & 256) && tid == 0) st->stamps[15] += 1;
+  SOLVE_START(0);
+  // S -> A with kLoadBatch independent (coalesced) loads in flight per thread
+  // (32-bit index math: a 64-bit division per element costs more than the load)
+  const int NN = N * N;
+  for (int base = tid; base < ((skip & 1) ? 0 : NN); base += nt * kLoadBatch) {
+    double v[kLoadBatch];
+    int rr[kLoadBatch], cc[kLoadBatch];
+#pragma unroll
+    for (int k = 0; k < kLoadBatch; ++k) {
+      const int idx = base + k * nt;
+      rr[k] = idx / N;
+      cc[k] = idx - rr[k] * N;
+      v[k] = (idx < NN && rr[k] < n && cc[k] < n) ? b.S[rr[k] * n + cc[k]] : 0.0;
     }
-    A[idx] = v;
+#pragma unroll
+    for (int k = 0; k < kLoadBatch; ++k) {
+      if (base + k * nt < NN) {
+        const int r = rr[k], c = cc[k];
+        double x = v[k];
+        if (r == c) x = r < n ? x + fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius : 1.0;
+        A[r * ld + c] = x;
+      }
+    }
   }
-  for (int r = tid; r < n; r += nt) b.yc[r] = -(mode == 0 ? b.gcs[r] - gemm_zpart(g, b.Spart, r) : b.bvec[r]);
+  for (int r = tid; r < N; r += nt) u[r] = r < n ? -b.bvec[r] : 0.0;
   __syncthreads();
-  // right-looking Cholesky, lower triangle
-  for (int j = 0; j < n; ++j) {
-    if (tid == 0) {
-      double d = A[(long)j * n + j];
-      if (!(d > 0)) sfail = 1;
-      A[(long)j * n + j] = sqrt(d);
+  SOLVE_STAMP(0);
+  SOLVE_START(1);
+  for (int J = 0; J < T; ++J) {
+    const int j0 = 16 * J;
+    // (a) diagonal block: lane i (< 16) of wave 0 holds row i in registers
+    if (wave == 0 && !(skip & 2)) {
+      const int i = lane & 15;
+      double r[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) r[m] = A[(long)(j0 + i) * ld + j0 + m];
+      bool ok = true;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const double piv = __shfl(r[k], k, 16);
+        ok = ok && (piv > 0);
+        const double d = sqrt(piv), inv = 1.0 / d;
+        if (i > k) r[k] *= inv;
+        else if (i == k) r[k] = d;
+#pragma unroll
+        for (int m = k + 1; m < 16; ++m) {
+          const double lmk = __shfl(r[k], m, 16);
+          if (i >= m) r[m] -= r[k] * lmk;
+        }
+      }
+      if (!ok && lane == 0) sfail = 1;
+      if (lane < 16) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if (m <= i) A[(long)(j0 + i) * ld + j0 + m] = r[m];
+        invd[j0 + i] = 1.0 / r[i];
+      }
     }
     __syncthreads();
+    SOLVE_STAMP(1);
+    SOLVE_START(2);
     if (sfail) break;
-    const double d = A[(long)j * n + j];
-    for (int i = j + 1 + tid; i < n; i += nt) A[(long)i * n + j] /= d;
-    __syncthreads();
-    const int m = n - j - 1;
-    for (long q = tid; q < (long)m * m; q += nt) {
-      const int i = j + 1 + (int)(q / m), k = j + 1 + (int)(q % m);
-      if (k <= i) A[(long)i * n + k] -= A[(long)i * n + j] * A[(long)k * n + j];
+    // (b) panel: L_IJ = A_IJ L_JJ^-T, one thread per row below the block
+    for (int rr = j0 + 16 + tid; rr < ((skip & 4) ? 0 : N); rr += nt) {
+      double x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = A[(long)rr * ld + j0 + k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        double s = x[k];
+#pragma unroll
+        for (int m = 0; m < k; ++m) s -= x[m] * A[(long)(j0 + k) * ld + j0 + m];
+        x[k] = s * invd[j0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) A[(long)rr * ld + j0 + k] = x[k];
     }
     __syncthreads();
+    SOLVE_STAMP(2);
+    SOLVE_START(3);
+    // (c) trailing update on the matrix cores: A_IK -= L_IJ L_KJ^T, J < K <= I
+    const int rem = T - J - 1;
+    const int npairs = rem * (rem + 1) / 2;
+    for (int p = wave; p < ((skip & 8) ? 0 : npairs); p += nw) {
+      int I = 0, q = p;
+      while (q > I) {
+        q -= I + 1;
+        ++I;
+      }
+      const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
+      double4_t acc;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = A[(long)(i0 + (lane >> 4) + 4 * i) * ld + k0 + (lane & 15)];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int col = j0 + 4 * s + (lane >> 4);
+        const double av = -A[(long)(i0 + (lane & 15)) * ld + col];
+        const double bv = A[(long)(k0 + (lane & 15)) * ld + col];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) A[(long)(i0 + (lane >> 4) + 4 * i) * ld + k0 + (lane & 15)] = acc[i];
+    }
+    __syncthreads();
+    SOLVE_STAMP(3);
+    if (J + 1 < T) SOLVE_START(1);
   }
+  SOLVE_START(4);
   if (sfail) {
     if (tid == 0) st->fail = 1;
     return;
   }
-  // forward: L u = -b ; backward: L^T y = u
-  for (int i = 0; i < n; ++i) {
-    if (tid == 0) b.yc[i] /= A[(long)i * n + i];
+  // L_JJ^-1 of every diagonal block: one thread per (block, column)
+  for (int q = tid; q < ((skip & 16) ? 0 : N); q += nt) {
+    const int J = q >> 4, c = q & 15, j0 = 16 * J;
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      double s = (r == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int m = 0; m < r; ++m) s -= A[(long)(j0 + r) * ld + j0 + m] * x[m];
+      x[r] = r < c ? 0.0 : s * invd[j0 + r];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Linv[256 * J + r * 16 + c] = x[r];
+  }
+  __syncthreads();
+  SOLVE_STAMP(4);
+  SOLVE_START(5);
+  // forward: L u = -b, block by block
+  for (int J = 0; J < ((skip & 32) ? 0 : T); ++J) {
+    const int j0 = 16 * J;
+    double uj = 0;
+    if (tid < 16) {
+      for (int m = 0; m <= tid; ++m) uj += Linv[256 * J + tid * 16 + m] * u[j0 + m];
+    }
     __syncthreads();
-    const double ui = b.yc[i];
-    for (int r = i + 1 + tid; r < n; r += nt) b.yc[r] -= A[(long)r * n + i] * ui;
+    if (tid < 16) u[j0 + tid] = uj;
+    __syncthreads();
+    for (int rr = j0 + 16 + tid; rr < N; rr += nt) {
+      double s = 0;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s += A[(long)rr * ld + j0 + m] * u[j0 + m];
+      u[rr] -= s;
+    }
     __syncthreads();
   }
-  for (int i = n - 1; i >= 0; --i) {
-    if (tid == 0) b.yc[i] /= A[(long)i * n + i];
+  // backward: L^T y = u
+  for (int J = ((skip & 64) ? -1 : T - 1); J >= 0; --J) {
+    const int j0 = 16 * J;
+    double yj = 0;
+    if (tid < 16) {
+      for (int r = tid; r < 16; ++r) yj += Linv[256 * J + r * 16 + tid] * u[j0 + r];
+    }
     __syncthreads();
-    const double yi = b.yc[i];
-    for (int r = tid; r < i; r += nt) b.yc[r] -= A[(long)i * n + r] * yi;
+    if (tid < 16) u[j0 + tid] = yj;
+    __syncthreads();
+    for (int cc = tid; cc < j0; cc += nt) {
+      double s = 0;
+#pragma unroll
+      for (int m = 0; m < 16; ++m) s += A[(long)(j0 + m) * ld + cc] * u[j0 + m];
+      u[cc] -= s;
+    }
     __syncthreads();
   }
+  SOLVE_STAMP(5);
+  for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
   // candidate cameras
   const int cur = st->cur;
   const double* x = b.cams[cur];
@@ -614,7 +786,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       xc[i] = x[i];
       continue;
     }
-    const double d = b.yc[i - 6 * g.nf] * b.csc[i - 6 * g.nf];
+    const double d = u[i - 6 * g.nf] * b.csc[i - 6 * g.nf];
     b.dc[i - 6 * g.nf] = d;
     const double v = x[i] + d;
     xc[i] = v;
@@ -630,23 +802,46 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   }
 }
 
-__global__ __launch_bounds__(kBlock) void pt_backsub_kernel(Geo g, Bufs b) {
+// Per CSR slot: t_q = W_q^T (Dc y_c) of the point back-substitution (3 doubles),
+// so the per-point kernel sums contiguous values instead of chasing
+// camera indices observation by observation.
+__global__ __launch_bounds__(kBlock) void obs_backsub_kernel(Geo g, Bufs b) {
+  const State* st = b.st;
+  if (st->done || st->fail) return;
+  const int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= g.no) return;
+  const int ci = b.p_cam[q];
+  double* t = b.tq + 3 * (long)q;
+  if (ci < 0) {
+    t[0] = t[1] = t[2] = 0.0;
+    return;
+  }
+  const double* W = b.Wo + 18 * (long)q;
+  const double* y = b.yc + 6 * ci;
+  const double* cs = b.csc + 6 * ci;
+  double ys[6];
+  for (int a = 0; a < 6; ++a) ys[a] = cs[a] * y[a];
+  for (int c = 0; c < 3; ++c) {
+    double s = 0;
+    for (int a = 0; a < 6; ++a) s += W[a * 3 + c] * ys[a];
+    t[c] = s;
+  }
+}
+
+
+__global__ __launch_bounds__(kPtBlock) void pt_backsub_kernel(Geo g, Bufs b) {
   __shared__ double lds[8];
   const State* st = b.st;
   if (st->done) return;
-  const int j = blockIdx.x * kBlock + threadIdx.x;
+  const int j = blockIdx.x * kPtBlock + threadIdx.x;
   double s2 = 0, xn2 = 0;
   if (j < g.np && !st->fail) {
+    const double* ps = b.psc + 3 * (long)j;
     double rhs[3] = {-b.gps[3 * (long)j], -b.gps[3 * (long)j + 1], -b.gps[3 * (long)j + 2]};
-    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
-      const int ob = b.p_obs[q];
-      const int ci = b.cam_idx[ob] - g.nf;
-      if (ci < 0) continue;
-      const double* W = b.Wo + 18 * (long)ob;
-      const double* y = b.yc + 6 * ci;
-      for (int c = 0; c < 3; ++c)
-        rhs[c] -= W[c] * y[0] + W[3 + c] * y[1] + W[6 + c] * y[2] + W[9 + c] * y[3] + W[12 + c] * y[4] + W[15 + c] * y[5];
-    }
+    double tsum[3] = {0, 0, 0};
+    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q)
+      for (int c = 0; c < 3; ++c) tsum[c] += b.tq[3 * (long)q + c];
+    for (int c = 0; c < 3; ++c) rhs[c] -= tsum[c] * ps[c];
     const double* L = b.Lp + 9 * (long)j;
     double u[3], yp[3];
     fwd3(L, rhs, u);
@@ -655,7 +850,7 @@ __global__ __launch_bounds__(kBlock) void pt_backsub_kernel(Geo g, Bufs b) {
     const double* x = b.pts[cur] + 3 * (long)j;
     double* xc = b.pts[1 - cur] + 3 * (long)j;
     for (int a = 0; a < 3; ++a) {
-      const double d = yp[a] * b.psc[3 * (long)j + a];
+      const double d = yp[a] * ps[a];
       b.dp[3 * (long)j + a] = d;
       double v = x[a] + d;
       v = fmin(fmax(v, g.lo[a]), g.hi[a]);
@@ -708,35 +903,11 @@ __global__ __launch_bounds__(kBlock) void obs_step_kernel(Geo g, Bufs b) {
   }
 }
 
-__global__ __launch_bounds__(1024) void step_reduce_kernel(Geo g, Bufs b) {
-  __shared__ double lds[64];
-  const State* st = b.st;
-  if (st->done) return;
-  double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_obs; i += 1024) {
-    v[0] += b.part[R_MODEL * g.pstride + i];
-    v[1] += b.part[R_CAND * g.pstride + i];
-  }
-  for (int i = threadIdx.x; i < g.nblk_pts; i += 1024) {
-    v[2] += b.part[R_STEP2 * g.pstride + i];
-    v[3] += b.part[R_XN2 * g.pstride + i];
-  }
-  double out[4];
-  block_sum<4>(v, out, lds);
-  if (threadIdx.x == 0) {
-    b.scal[R_MODEL] = out[0];
-    b.scal[R_CAND] = out[1];
-    b.scal[R_STEP2] = out[2];
-    b.scal[R_XN2] = out[3];
-    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
-  }
-}
-
-// TrustRegionMinimizer step handling + LevenbergMarquardtStrategy radius update
-__global__ void decide_kernel(Geo g, Bufs b, Opts o) {
-  if (threadIdx.x != 0) return;
+// Step partials -> scal (fixed order).  In single-GPU mode the same workgroup
+// then runs the Ceres step handling (decide); in sharded mode the host
+// all-reduces scal between step_partials and a decide-only launch.
+__device__ void decide(Bufs& b, const Opts& o) {
   State* st = b.st;
-  if (st->done) return;
   st->accepted = 0;
   const double model_change = b.scal[R_MODEL];
   const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
@@ -785,6 +956,37 @@ __global__ void decide_kernel(Geo g, Bufs b, Opts o) {
   }
 }
 
+__global__ __launch_bounds__(kFinBlock) void step_finalize_kernel(Geo g, Bufs b, Opts o, int do_decide) {
+  __shared__ double lds[32];
+  State* st = b.st;
+  if (st->done) return;
+  double v[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) {
+    v[0] += b.part[R_MODEL * g.pstride + i];
+    v[1] += b.part[R_CAND * g.pstride + i];
+  }
+  for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) {
+    v[2] += b.part[R_STEP2 * g.pstride + i];
+    v[3] += b.part[R_XN2 * g.pstride + i];
+  }
+  double out[4];
+  block_sum<4>(v, out, lds);
+  if (threadIdx.x == 0) {
+    b.scal[R_MODEL] = out[0];
+    b.scal[R_CAND] = out[1];
+    b.scal[R_STEP2] = out[2];
+    b.scal[R_XN2] = out[3];
+    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
+    if (do_decide) decide(b, o);
+  }
+}
+
+__global__ void decide_kernel(Geo g, Bufs b, Opts o) {
+  if (threadIdx.x != 0) return;
+  if (b.st->done) return;
+  decide(b, o);
+}
+
 __global__ __launch_bounds__(kBlock) void cost_kernel(Geo g, Bufs b, int which, double* part) {
   __shared__ double lds[4];
   const int o = blockIdx.x * kBlock + threadIdx.x;
@@ -823,9 +1025,12 @@ struct Plan {
   Opts o;
   double* colnorm = nullptr;
   double* gc_raw = nullptr;
+  double* gc_glob = nullptr;
+  double* Uraw = nullptr;
   double* host = nullptr;  // pinned State copy
   size_t solve_lds = 0;
   int use_lds = 0;
+  int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
 };
 
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
@@ -838,6 +1043,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
              "BA: observation %d indexes outside the window", i);
   }
   P.c = c;
+  if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
   Geo& g = P.g;
   g.nc = p->n_cams;
   g.np = p->n_pts;
@@ -852,7 +1058,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.Kpad = (int)rup(std::max(g.K3, 1), 16L * g.ksplit);
   g.npairs = g.T * (g.T + 1) / 2 + g.T;
   g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
-  g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kBlock) / kBlock);
+  g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kPtBlock) / kPtBlock);
+  g.jacobi = opt->jacobi_scaling ? 1 : 0;
   g.pstride = std::max(g.nblk_obs, g.nblk_pts);
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
@@ -899,6 +1106,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       std::stable_sort(p_obs.begin() + p_off[j], p_obs.begin() + p_off[j + 1],
                        [&](int a, int bb) { return p->cam_idx[a] < p->cam_idx[bb]; });
   }
+  // observations sharing (point, camera) with another one accumulate atomically in Y
+  std::vector<uint8_t> dup(std::max(g.no, 1), 0);
+  for (int j = 0; j < g.np; ++j)
+    for (int q = p_off[j] + 1; q < p_off[j + 1]; ++q)
+      if (p->cam_idx[p_obs[q]] == p->cam_idx[p_obs[q - 1]]) dup[p_obs[q]] = dup[p_obs[q - 1]] = 1;
   // one arena
   const long nb = std::max(g.nblk_obs, g.nblk_pts);
   struct Item { size_t bytes; void** dst; };
@@ -914,9 +1126,15 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(4 * (size_t)g.no, &b.pt_idx);
   add(4 * (size_t)(g.np + 1), &b.p_off);
   add(4 * (size_t)g.no, &b.p_obs);
+  add(4 * (size_t)g.no, &b.pos);
+  add(4 * (size_t)g.no, &b.p_cam);
   add(4 * (size_t)(g.m + 1), &b.c_off);
   add(4 * (size_t)g.no, &b.c_obs);
   add(8 * kLinStride * (size_t)g.no, &b.lin);
+  add(8 * kObsxStride * (size_t)g.no, &b.obsx);
+  add((size_t)g.no, &b.dup);
+  add(8 * ((size_t)(16 * g.T) * (((16 * g.T + 31) / 32) * 32 + 2) + 256 * (size_t)g.T + 32 * (size_t)g.T), &b.Abuf);
+  add(8 * 3 * (size_t)g.no, &b.tq);
   add(8 * 18 * (size_t)g.no, &b.Wo);
   add(8 * (size_t)g.n6, &b.csc);
   add(8 * 3 * (size_t)g.np, &b.psc);
@@ -938,6 +1156,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(sizeof(State), &b.st);
   add(8 * (size_t)g.n6, &P.colnorm);
   add(8 * (size_t)g.n6, &P.gc_raw);
+  add(8 * (size_t)g.n6, &P.gc_glob);
+  add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   size_t total = 0;
   for (auto& it : items) total += it.first;
   void* arena;
@@ -958,7 +1178,16 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     ME_HIP(c, hipMemcpyAsync((void*)b.cam_idx, p->cam_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
     ME_HIP(c, hipMemcpyAsync((void*)b.pt_idx, p->pt_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
     ME_HIP(c, hipMemcpyAsync((void*)b.p_obs, p_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    std::vector<int> pos(g.no), p_cam(g.no);
+    for (int q = 0; q < g.no; ++q) {
+      pos[p_obs[q]] = q;
+      p_cam[q] = p->cam_idx[p_obs[q]] - g.nf;
+    }
+    ME_HIP(c, hipMemcpyAsync((void*)b.pos, pos.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.p_cam, p_cam.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipStreamSynchronize(s));  // host vectors above go out of scope
     ME_HIP(c, hipMemcpyAsync((void*)b.c_obs, c_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
+    ME_HIP(c, hipMemcpyAsync((void*)b.dup, dup.data(), (size_t)g.no, hipMemcpyHostToDevice, s));
   }
   ME_HIP(c, hipMemcpyAsync((void*)b.p_off, p_off.data(), 4 * (size_t)(g.np + 1), hipMemcpyHostToDevice, s));
   ME_HIP(c, hipMemcpyAsync((void*)b.c_off, c_off.data(), 4 * (size_t)(g.m + 1), hipMemcpyHostToDevice, s));
@@ -977,11 +1206,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   ME_HIP(c, hipMemsetAsync(b.csc, 0, 8 * (size_t)std::max(g.n6, 1), s));
   ME_HIP(c, hipMemsetAsync(P.gc_raw, 0, 8 * (size_t)std::max(g.n6, 1), s));
   ME_HIP(c, hipMemsetAsync(b.dc, 0, 8 * (size_t)std::max(g.n6, 1), s));
-  if (!opt->jacobi_scaling) {
-    std::vector<double> ones(std::max(g.n6, 1), 1.0);
-    ME_HIP(c, hipMemcpyAsync(b.csc, ones.data(), 8 * ones.size(), hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipStreamSynchronize(s));
-  }
   // feasibility (Ceres Problem::IsFeasible): host-side, before any launch
   for (int j = 0; j < g.np; ++j)
     for (int a = 0; a < 3; ++a) {
@@ -989,7 +1213,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       if (x < g.lo[a] || x > g.hi[a]) return 1;  // infeasible
     }
   // LDS for the camera solve
-  P.solve_lds = 8 * (size_t)g.n6 * g.n6;
+  P.solve_lds = 8 * ((size_t)(16 * g.T) * (((16 * g.T + 31) / 32) * 32 + 2) + 256 * (size_t)g.T + 32 * (size_t)g.T);
   P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
   if (!P.use_lds) P.solve_lds = 0;
   else
@@ -998,10 +1222,16 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   return ME_OK;
 }
 
+
 int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 
-// Linearisation part of an iteration (skipped on device when need_lin == 0)
-int enqueue_linearize(Plan& P, int jacobi, me_allreduce_fn ar, void* user) {
+#define ME_AR(ptr, n)                                                                         \
+  do {                                                                                        \
+    if (ar((ptr), (n), user) != 0) return me_set_error(c, ME_ERR_HIP, "allreduce callback failed"); \
+  } while (0)
+
+// Linearisation stage (device-skipped when need_lin == 0)
+int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
@@ -1010,65 +1240,83 @@ int enqueue_linearize(Plan& P, int jacobi, me_allreduce_fn ar, void* user) {
     hipLaunchKernelGGL(linearize_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
   if (g.m > 0) {
-    if (jacobi) {
-      hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, 0, P.colnorm, P.gc_raw);
-      if (ar) ME_TRY(ar(P.colnorm, g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-      hipLaunchKernelGGL(cam_scaling_kernel, dim3(blocks(g.n6, 256)), dim3(256), 0, s, g, P.b,
-                         (const double*)P.colnorm);
+    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, ar ? 1 : 0, P.colnorm, P.gc_raw,
+                       P.Uraw);
+    if (ar) {
+      ME_AR(P.colnorm, g.n6);
+      hipLaunchKernelGGL(cam_finish_kernel, dim3(blocks(g.m, 64)), dim3(64), 0, s, g, P.b, (const double*)P.colnorm,
+                         (const double*)P.gc_raw, (const double*)P.Uraw);
+      ME_HIP(c, hipMemcpyAsync(P.gc_glob, P.gc_raw, 8 * (size_t)g.n6, hipMemcpyDeviceToDevice, s));
+      ME_AR(P.gc_glob, g.n6);
     }
-    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, 1, P.colnorm, P.gc_raw);
   }
   {
     me_ktimer t(c, ME_KT_BA_POINTS);
-    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b, jacobi);
+    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b);
   }
-  hipLaunchKernelGGL(lin_reduce_kernel, dim3(1), dim3(1024), 0, s, g, P.b);
+  if (ar) {
+    hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
+    ME_AR(P.b.scal + R_COST, 1);
+    ME_AR(P.b.scal + R_GMAX_PT, -1);
+  }
+  hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o,
+                     (const double*)(ar ? P.gc_glob : P.gc_raw), ar ? 1 : 0);
   return me_check_launch(c, "BA linearize");
 }
 
-int enqueue_iteration(Plan& P, int jacobi, me_allreduce_fn ar, void* user) {
+// Schur stage: point blocks, dense Y, S partial tiles on the FP64 MFMA
+int enqueue_schur(Plan& P) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
-  ME_TRY(enqueue_linearize(P, jacobi, ar, user));
-  if (ar) {
-    // sum the cost / unscaled camera gradient, max of the point gradient
-    // (gradient max is a max: the callback gets n < 0 to request MAX)
-    ME_TRY(ar(P.b.scal + R_COST, 1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-    ME_TRY(ar(P.b.scal + R_GMAX_PT, -1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-    ME_TRY(ar(P.gc_raw, g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-  }
-  hipLaunchKernelGGL(lin_check_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o, (const double*)P.gc_raw);
   {
     me_ktimer t(c, ME_KT_BA_POINTS);
-    hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b, P.o);
+    hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b, P.o);
   }
   if (g.m > 0) {
     me_ktimer t(c, ME_KT_BA_SCHUR);
-    hipLaunchKernelGGL(y_scatter_kernel, dim3(blocks((long)g.Kpad * g.Rpad, kBlock)), dim3(kBlock), 0, s, g, P.b);
+    ME_HIP(c, hipMemsetAsync(P.b.Y, 0, 8 * (size_t)g.Kpad * g.Rpad, s));
+    hipLaunchKernelGGL(y_obs_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
     hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, s, g, P.b);
   }
+  return me_check_launch(c, "BA schur");
+}
+
+int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
+  me_ctx* c = P.c;
+  const Geo& g = P.g;
+  hipStream_t s = c->stream;
+  ME_TRY(enqueue_linearize(P, ar, user));
+  ME_TRY(enqueue_schur(P));
+  // S = U - sum of split-K partials is assembled by a wide kernel (coalesced,
+  // all CUs) rather than inside the one-workgroup solve, whose dependent
+  // cross-XCD loads would otherwise dominate the iteration.
   if (g.m > 0) {
-    int mode = 0;
+    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0, s, g,
+                       P.b);
     if (ar) {
-      hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0, s,
-                         g, P.b);
-      // S | b | diagU are contiguous; the failure flag lives in scal[R_COUNT]
-      ME_TRY(ar(P.b.S, g.n6 * g.n6 + 2 * g.n6, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-      ME_TRY(ar(P.b.scal + R_COUNT, 1, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-      mode = 1;
+      ME_AR(P.b.S, g.n6 * g.n6 + 2 * g.n6);  // S | b | diag(U) are contiguous
+      ME_AR(P.b.scal + R_COUNT, 1);          // linear-solver failure flag
     }
+  } else {
+    ME_HIP(c, hipMemsetAsync(P.b.scal + R_COUNT, 0, 8, s));
+  }
+  {
     me_ktimer t(c, ME_KT_BA_SOLVE);
-    hipLaunchKernelGGL(cam_solve_kernel, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, mode, P.use_lds);
+    hipLaunchKernelGGL(cam_solve_kernel, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
+                       P.use_lds);
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
-    hipLaunchKernelGGL(pt_backsub_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(obs_backsub_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(pt_backsub_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b);
     hipLaunchKernelGGL(obs_step_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
-  hipLaunchKernelGGL(step_reduce_kernel, dim3(1), dim3(1024), 0, s, g, P.b);
-  if (ar) ME_TRY(ar(P.b.scal + R_MODEL, 5, user) == 0 ? ME_OK : me_set_error(c, ME_ERR_HIP, "allreduce failed"));
-  hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o);
+  hipLaunchKernelGGL(step_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
+  if (ar) {
+    ME_AR(P.b.scal + R_MODEL, 5);  // model change, candidate cost, step^2, |x|^2, failure flag
+    hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o);
+  }
   return me_check_launch(c, "BA iteration");
 }
 
@@ -1077,6 +1325,7 @@ int read_state(Plan& P, State* st) {
   ME_HIP(c, hipMemcpyAsync(P.host, P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
   std::memcpy(st, P.host, sizeof(State));
+  std::memcpy(P.c->dbg, st->stamps, sizeof(st->stamps));
   return ME_OK;
 }
 
@@ -1116,11 +1365,10 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
     }
     return ME_OK;
   }
-  const int jacobi = opt->jacobi_scaling ? 1 : 0;
   // enqueue the whole solve; poll the device state every `chunk` iterations
   const int chunk = 4;
   for (int it = 0; it <= opt->max_num_iterations; it += chunk) {
-    for (int k = 0; k < chunk && it + k <= opt->max_num_iterations; ++k) ME_TRY(enqueue_iteration(P, jacobi, ar, user));
+    for (int k = 0; k < chunk && it + k <= opt->max_num_iterations; ++k) ME_TRY(enqueue_iteration(P, ar, user));
     State st;
     ME_TRY(read_state(P, &st));
     if (st.done) break;
@@ -1207,13 +1455,9 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
   const Geo& g = P.g;
-  ME_TRY(enqueue_linearize(P, 1, nullptr, nullptr));
-  hipLaunchKernelGGL(lin_check_kernel, dim3(1), dim3(64), 0, c->stream, g, P.b, P.o, (const double*)P.gc_raw);
-  hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kBlock), 0, c->stream, g, P.b, P.o);
+  ME_TRY(enqueue_linearize(P, nullptr, nullptr));
+  ME_TRY(enqueue_schur(P));
   if (g.m > 0) {
-    hipLaunchKernelGGL(y_scatter_kernel, dim3(blocks((long)g.Kpad * g.Rpad, kBlock)), dim3(kBlock), 0, c->stream, g,
-                       P.b);
-    hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, c->stream, g, P.b);
     hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0,
                        c->stream, g, P.b);
   }
@@ -1230,5 +1474,11 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
       S[(size_t)i * n + j] = v;
     }
   for (int i = 0; i < n; ++i) bout[i] = Sh[(size_t)n * n + i];
+  return ME_OK;
+}
+
+extern "C" int me_debug_read(me_ctx* c, long long* out, int n) {
+  if (!c || n < 0 || n > 16) return ME_ERR_INVALID;
+  std::memcpy(out, c->dbg, 8 * (size_t)n);
   return ME_OK;
 }

@@ -29,6 +29,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
 constexpr int kLinStride = 40;   // r[4], Jc[24], Jp[12] per observation (corrected, unscaled)
+constexpr int kObsxStride = 9;   // V_o (6 unique) + g_o (3), unscaled
 
 struct Opts {
   int max_num_iterations;
@@ -51,13 +52,14 @@ struct State {
   double x_cost, cand_cost, model_change, initial_cost;
   double cam_step2, cam_xn2, cam_gmax;
   double last_q;
+  long long stamps[16];  // s_memtime at cam_solve phase ends (ME_SOLVE_SKIP & 256)
 };
 
 // Scalars reduced from block partials (one slot per quantity).
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride;
+  int nc, np, no, nf, m, n6, Rpad, T, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi;
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -71,10 +73,15 @@ struct Bufs {
   const int* pt_idx;
   const int* p_off;   // CSR by point (obs sorted by cam inside a point)
   const int* p_obs;
+  const int* pos;     // obs -> CSR slot
+  const int* p_cam;   // CSR slot -> variable camera index (-1 fixed)
   const int* c_off;   // CSR by variable camera
   const int* c_obs;
   double* lin;        // no * 40
-  double* Wo;         // no * 18 (scaled Jc^T Jp, row-major 6x3)
+  double* obsx;       // no * 9  (V_o, g_o unscaled)
+  const uint8_t* dup; // obs shares (point, camera) with another obs
+  double* Abuf;       // n6 * (n6|1) factorisation workspace (when S does not fit LDS)
+  double* Wo;         // no * 18 (unscaled Jc^T Jp, row-major 6x3)
   double* csc;        // 6m jacobi scaling (cameras)
   double* psc;        // 3np (points)
   double* U;          // m * 36 scaled Jc^T Jc
@@ -92,6 +99,7 @@ struct Bufs {
   double* yc;         // n6
   double* dc;         // n6 camera step (unscaled)
   double* dp;         // 3np point step (unscaled)
+  double* tq;         // 3 per CSR slot: W_q^T Dc y_c
   double* part;       // R_COUNT * max(nblk_obs, nblk_pts)
   double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
   State* st;

@@ -111,6 +111,90 @@ struct LaneHist {
 };
 
 // ---------------------------------------------------------------------
+// Group MI: G consecutive lanes of one wavefront cooperate on one patch pair
+// (latency-bound batches: a few thousand pairs cannot fill 256 CUs at one
+// pair per lane).  The histogram is shared by the group (LDS atomics), the
+// expensive terms of the non-empty joint bins are computed in parallel (lane
+// l of the group owns bitmap word l) and stored in row-major order, and the
+// group's lane 0 adds them sequentially -- the reference's float summation
+// order is preserved bit for bit.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr int kGroupTerms = 256;  // >= max non-empty joint bins (<= pixels <= 255)
+constexpr int kGroupWords = kHistWords + kGroupTerms;
+
+template <int G>
+struct GroupHist {
+  static_assert(G == 16, "group MI is written for 16-lane groups (13 bitmap words)");
+  uint32_t* h;  // kGroupWords words of this group: histogram then float terms
+  int gl;       // lane within the group
+  __device__ __forceinline__ void clear() {
+    for (int i = gl; i < kHistWords; i += G) h[i] = 0u;
+    wave_sync();
+  }
+  __device__ __forceinline__ void add(int vl, int vr) {
+    int bl = bin20(vl), br = bin20(vr);
+    int code = bl * 20 + br;
+    atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
+    atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
+    atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
+    atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
+  }
+  // Returns the MI in lane gl == 0 of the group (other lanes: unspecified).
+  __device__ __forceinline__ float mi(float invN) {
+    wave_sync();
+    float* terms = reinterpret_cast<float*>(h + kHistWords);
+    uint32_t bits = gl < 13 ? h[110 + gl] : 0u;
+    const int cnt = __builtin_popcount(bits);
+    int pre = cnt;
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+      const int t = __shfl_up(pre, off, G);
+      if (gl >= off) pre += t;
+    }
+    const int total = __shfl(pre, G - 1, G);
+    int idx = pre - cnt;
+    while (bits) {
+      const int b = __builtin_ctz(bits);
+      bits &= bits - 1u;
+      const int code = gl * 32 + b;
+      const int i = code / 20, j = code - i * 20;
+      const int cJ = (h[code >> 2] >> ((code & 3) * 8)) & 0xff;
+      const int cL = (h[100 + (i >> 2)] >> ((i & 3) * 8)) & 0xff;
+      const int cR = (h[105 + (j >> 2)] >> ((j & 3) * 8)) & 0xff;
+      terms[idx++] = mi_term(cJ, cL, cR, invN);
+    }
+    wave_sync();
+    float MI = 0.0f;
+    if (gl == 0)
+      for (int t = 0; t < total; ++t) MI += terms[t];
+    return MI;
+  }
+};
+
+// Patch pair MI by a 16-lane group; pixels strided over the group.
+template <bool BIN>
+__device__ __forceinline__ float group_mi(GroupHist<16>& h, const uint8_t* A, long astride, const uint8_t* B,
+                                          long bstride, int pw, int ph, float invN) {
+  h.clear();
+  const int npx = pw * ph;
+  for (int p = h.gl; p < npx; p += 16) {
+    const int y = p / pw, x = p - y * pw;
+    int va = A[y * astride + x], vb = B[y * bstride + x];
+    if (BIN) {
+      va = va ? 255 : 0;
+      vb = vb ? 255 : 0;
+    }
+    h.add(va, vb);
+  }
+  return h.mi(invN);
+}
+
+// ---------------------------------------------------------------------
 // Pose / projection math for the ScaleState residuals, restating the
 // OpenCV Matx evaluation order of optimisation.cpp:172-215 (s = 0; s += ...).
 struct Pose44 { double T[16]; };

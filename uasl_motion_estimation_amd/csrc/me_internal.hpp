@@ -30,6 +30,7 @@ struct me_ctx {
   std::vector<hipEvent_t> event_pool;
   long launches[ME_KT_COUNT] = {0};
   double total_ms[ME_KT_COUNT] = {0};
+  long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
 };
 
 int me_set_error(me_ctx* ctx, int code, const char* fmt, ...);

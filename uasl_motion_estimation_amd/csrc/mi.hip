@@ -18,6 +18,8 @@ using namespace me_dev;
 namespace {
 
 constexpr int kMiBlock = 256;
+// below this many pairs the batch cannot fill 256 CUs one pair per lane
+constexpr int kGroupThreshold = 65536;
 
 __global__ __launch_bounds__(kMiBlock) void mi_pairs_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                             const uint8_t* __restrict__ imgR, int strideR,
@@ -38,6 +40,25 @@ __global__ __launch_bounds__(kMiBlock) void mi_pairs_kernel(const uint8_t* __res
       pr += strideR;
     }
     out[k] = h.mi(invN);
+  }
+}
+
+// Latency-bound batches: 16 lanes per pair (me_device.hpp GroupHist).
+constexpr int kGroupBlock = 256;
+__global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8_t* __restrict__ imgL, int strideL,
+                                                                     const uint8_t* __restrict__ imgR, int strideR,
+                                                                     const int32_t* __restrict__ xyL,
+                                                                     const int32_t* __restrict__ xyR, int n, int pw,
+                                                                     int ph, float invN, float* __restrict__ out) {
+  __shared__ uint32_t lds[(kGroupBlock / 16) * kGroupWords];
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  for (int k = blockIdx.x * (kGroupBlock / 16) + grp; k < n; k += gridDim.x * (kGroupBlock / 16)) {
+    const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
+    const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
+    const float mi = group_mi<false>(h, imgL + (long)cl.y * strideL + cl.x, strideL,
+                                     imgR + (long)cr.y * strideR + cr.x, strideR, pw, ph, invN);
+    if (h.gl == 0) out[k] = mi;
   }
 }
 
@@ -103,9 +124,17 @@ inline float inv_count(long n) { return (float)(1.0 / (double)n); }
 int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, const int32_t* dxyL,
                        const int32_t* dxyR, int n, int pw, int ph, float* dout) {
   if (n <= 0) return ME_OK;
+  me_ktimer t(c, ME_KT_MI);
+  if (n < kGroupThreshold) {
+    // fewer pairs than lanes to fill the chip: 16 lanes per pair
+    const int per = kGroupBlock / 16;
+    int blocks = (n + per - 1) / per;
+    hipLaunchKernelGGL(mi_pairs_group_kernel, dim3(blocks), dim3(kGroupBlock), 0, c->stream, dL, sL, dR, sR, dxyL,
+                       dxyR, n, pw, ph, inv_count((long)pw * ph), dout);
+    return me_check_launch(c, "mi_pairs_group_kernel");
+  }
   int blocks = (n + kMiBlock - 1) / kMiBlock;
   if (blocks > 8192) blocks = 8192;
-  me_ktimer t(c, ME_KT_MI);
   hipLaunchKernelGGL(mi_pairs_kernel, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, dxyL, dxyR, n, pw,
                      ph, inv_count((long)pw * ph), dout);
   return me_check_launch(c, "mi_pairs_kernel");

@@ -190,13 +190,27 @@ __device__ __forceinline__ bool roi_in(const ScaleArgs& a, int x0, int y0, int P
   return x0 >= 0 && y0 >= 0 && x0 + P <= a.cols && y0 + P <= a.rows;
 }
 
+// 16 lanes per track (GroupHist): a window has a few thousand tracks, far
+// fewer than the lanes of 256 CUs; the reprojection is computed redundantly
+// by the 16 lanes (identical doubles), the MI histogram/terms are shared.
+constexpr int kTracksPerBlock = kScBlock / 16;
+#define SCALE_GROUP_SETUP()                                                 \
+  __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];                   \
+  const int grp_ = threadIdx.x >> 4;                                        \
+  GroupHist<16> h{&lds[grp_ * kGroupWords], (int)(threadIdx.x & 15)};       \
+  const int t = blockIdx.x * kTracksPerBlock + grp_;                        \
+  if (t >= a.nL + a.nR) return;
+
+template <bool BIN>
+__device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int ax, int ay, const uint8_t* B, int bx,
+                                        int by, int stride, int P, float invN) {
+  return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN);
+}
+
 // A4: compute_residuals
 __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
                                                                   int* __restrict__ err) {
-  __shared__ uint32_t lds[kHistWords * kScBlock];
-  LaneHist<kScBlock> h{&lds[threadIdx.x]};
-  const int t = blockIdx.x * kScBlock + threadIdx.x;
-  if (t >= a.nL + a.nR) return;
+  SCALE_GROUP_SETUP();
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
   if (row < 0 || !(fl & 2)) return;
@@ -213,24 +227,23 @@ __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, T
   float mi;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, lx, ly, P);
-    mi = lane_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN);
+    mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN);
   } else {
     if (a.weighting) wv = sobel_weight(a.imgR, a.stride, a.cols, a.rows, rx, ry, P);
-    mi = lane_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN);
+    mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN);
   }
-  res[row] = (double)mi * wv;
+  if (h.gl == 0) res[row] = (double)mi * wv;
 }
 
 // A5: compute_normal_equations — per track J^2*w and J*r_k
 __global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackDev td, const double* __restrict__ res,
                                                              double* __restrict__ jj, double* __restrict__ je,
                                                              int* __restrict__ err) {
-  __shared__ uint32_t lds[kHistWords * kScBlock];
-  LaneHist<kScBlock> h{&lds[threadIdx.x]};
-  const int t = blockIdx.x * kScBlock + threadIdx.x;
-  if (t >= a.nL + a.nR) return;
-  jj[t] = 0.0;
-  je[t] = 0.0;
+  SCALE_GROUP_SETUP();
+  if (h.gl == 0) {
+    jj[t] = 0.0;
+    je[t] = 0.0;
+  }
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
   if (row < 0 || !(fl & 2)) return;
@@ -261,22 +274,21 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackD
   const uint8_t* I0 = left ? a.imgL : a.imgR;
   const uint8_t* I1 = left ? a.imgR : a.imgL;
   double wv = a.weighting ? sobel_weight(I0, a.stride, a.cols, a.rows, x0x, x0y, P) : 1.0;
-  double MIp = lane_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN);
-  double MIm = lane_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN);
+  double MIp = grp_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN);
+  double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN);
   double J = (MIp - MIm) / 1.0 * duds;
-  jj[t] = J * J * wv;
-  je[t] = J * res[row];
+  if (h.gl == 0) {
+    jj[t] = J * J * wv;
+    je[t] = J * res[row];
+  }
 }
 
 // A6: compute_jacobian — JJ only; right tracks use poses.first / K.first and
 // binarised ROIs (optimisation.cpp:592-632)
 __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackDev td, double* __restrict__ jj,
                                                              int* __restrict__ err) {
-  __shared__ uint32_t lds[kHistWords * kScBlock];
-  LaneHist<kScBlock> h{&lds[threadIdx.x]};
-  const int t = blockIdx.x * kScBlock + threadIdx.x;
-  if (t >= a.nL + a.nR) return;
-  jj[t] = 0.0;
+  SCALE_GROUP_SETUP();
+  if (h.gl == 0) jj[t] = 0.0;
   const uint8_t fl = td.flags[t];
   // bit2: unmasked under compute_jacobian's mask indexing (first.size()+i)
   if (!(fl & 4) || !(fl & 8) || !(fl & 2)) return;
@@ -307,15 +319,15 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
   double MIp, MIm, wv = 1.0;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, x0x, x0y, P);
-    MIp = lane_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN);
-    MIm = lane_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN);
+    MIp = grp_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN);
+    MIm = grp_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN);
   } else {
     if (a.weighting) wv = sobel_weight_bin(a.imgR, a.stride, x0x, x0y, P);
-    MIp = lane_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN);
-    MIm = lane_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN);
+    MIp = grp_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN);
+    MIm = grp_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN);
   }
   double J = (MIp - MIm) / 1.0 * duds;
-  jj[t] = J * J * wv;
+  if (h.gl == 0) jj[t] = J * J * wv;
 }
 
 // Fixed-order reductions: out[0] = sum(x^2) (mode 0) or sum(x) (mode 1) over
@@ -482,7 +494,7 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   return ME_OK;
 }
 
-int blocks_for(int n) { return n > 0 ? (n + kScBlock - 1) / kScBlock : 1; }
+int blocks_for(int n) { return n > 0 ? (n + kTracksPerBlock - 1) / kTracksPerBlock : 1; }
 
 int check_err(ScaleProblem& P) {
   // err flag is read back with the scalars
