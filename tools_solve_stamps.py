@@ -16,5 +16,10 @@ for cfg in (2, 3, 4):
     ctx.lib.me_debug_read(ctx.h, buf, 16)
     calls = max(buf[15], 1)
     names = ["load", "diag", "panel", "trail", "Linv", "solves"]
+    os.environ["ME_SOLVE_SKIP"] = "0"
+    ctx.timing(True); ctx.timing_reset()
+    ba_solve(bp, SolverOptions.fixed_iterations(10), ctx=ctx)
+    ns, ms = ctx.timing_read("BA_SOLVE"); ctx.timing(False)
+    print(cfg, "solve kernel us", round(1000 * ms / max(ns, 1), 1), "ticks/us", round(sum(buf[:6]) / calls / (1000 * ms / max(ns, 1)), 0))
     print(cfg, "calls", calls, {nm: round(buf[i] / calls / 100.0, 1) for i, nm in enumerate(names)},
           "(us, s_memtime ticks/100 assuming 100 MHz)", flush=True)

@@ -564,215 +564,254 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b) {
 }
 
 // One workgroup: S (assembled by s_assemble_kernel, all-reduced in sharded
-// mode) + LM diagonal, blocked right-looking Cholesky with 16x16 blocks and
-// block-inverse triangular solves.  Every sequential chain is O(T = n/16):
-//  * diagonal block: 16 lanes, one row per lane in registers, shuffles;
-//  * panel: one lane per row, reciprocal pivots;
-//  * trailing update A_IK -= L_IJ L_KJ^T on v_mfma_f64_16x16x4f64;
-//  * solves: L_JJ^-1 of all diagonal blocks in parallel, then T block steps of
-//    16-term dot products forward and backward.
-// S is padded to N = 16T with an identity block.
-constexpr int kSolveBlock = 256;
+// mode) + LM diagonal, blocked right-looking Cholesky with 16x16 blocks.
+// The right-hand side rides along as an extra row [-b^T | 1] below S, so the
+// factorisation also yields z = L^-1 (-b) (no separate forward solve).
+// Per block column J:
+//  * diagonal block (wave 0): L_JJ and X_J = L_JJ^-1 together, lane = (row,
+//    4-column group), pivots by readlane, row broadcast by quad DPP;
+//  * panel L_IJ = A_IJ X_J^T on v_mfma_f64_16x16x4f64, one wave per block row;
+//  * trailing update A_IK -= L_IJ L_KJ^T on the matrix cores.
+// Then the backward solve L^T y = z in wave 0 with the block inverses.
+// The matrix is padded to N = 16 Ts >= n + 1 with an identity block.
+constexpr int kSolveBlock = 1024;
 constexpr int kLoadBatch = 16;
-#define SOLVE_STAMP(i)                                                        \
-  do {                                                                        \
+#define SOLVE_STAMP(i)                                                                      \
+  do {                                                                                      \
     if ((skip & 256) && tid == 0) st->stamps[(i)] += (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
-#define SOLVE_START(i)                                                        \
-  do {                                                                        \
+#define SOLVE_START(i)                                                                      \
+  do {                                                                                      \
     if ((skip & 256) && tid == 0) st->stamps[(i)] -= (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
-__device__ __forceinline__ int solve_ld(int T) { return ((16 * T + 31) / 32) * 32 + 2; }  // == 2 mod 32
+__host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
+// dynamic LDS: X (Ts x 256) | z/y (N) | column scratch (16) | A (N x ld, when it fits)
+__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 16; }
+__host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
 
-__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int use_lds) {
+// wave-local ordering of LDS (and, for the global fallback, L1) traffic
+__device__ __forceinline__ void solve_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+template <int S>
+__device__ __forceinline__ double quad_bcast(double x) {
+  constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// One elimination step of the 16x16 diagonal block held by one wave:
+// lane = 4 i + g holds a[q] = A[i][4g+q] and y[q] = Y[i][4g+q] (Y -> L^-1).
+// The trailing block stays symmetric, so column K of L is read from row K
+// (lane 4K + g) by ds_bpermute issued at the start of the step, in parallel
+// with the pivot chain; no LDS round trip sits on the critical path.
+// 1/sqrt(pivot) by v_rsq_f64 + two Newton steps (the correctly rounded
+// sqrt-then-divide sequence is ~30 dependent FP64 ops).
+template <int K>
+__device__ __forceinline__ void chol16_step(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
+                                            double* Ablk, int ld, double* X) {
+  double ca[4], cy[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    ca[q] = __shfl(a[q], 4 * K + g, 64);
+    cy[q] = __shfl(y[q], 4 * K + g, 64);
+  }
+  double piv = readlane_f64(a[K & 3], 4 * K + (K >> 2));
+  const bool pad = K >= nreal;  // padding / right-hand-side row: never a failure
+  ok = ok && (pad || piv > 0);
+  piv = (pad && !(piv > 0)) ? 1.0 : piv;
+  double r = __builtin_amdgcn_rsq(piv);
+  r = r * fma(-0.5 * piv * r, r, 1.5);
+  r = r * fma(-0.5 * piv * r, r, 1.5);
+  const double inv = r, d = piv * r;
+  const double aik = quad_bcast<(K >> 2)>(a[K & 3]);
+  const double lik = i > K ? aik * inv : (i == K ? d : 0.0);
+  const double la = i > K ? lik : 0.0;
+  if (g == (K >> 2) && i >= K) Ablk[i * ld + K] = lik;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const double xk = cy[q] * inv;
+    if (i == K) X[K * 16 + 4 * g + q] = xk;
+    a[q] = fma(-lik, (4 * g + q > K) ? ca[q] * inv : 0.0, a[q]);
+    y[q] = fma(-la, xk, y[q]);
+  }
+}
+template <int K>
+__device__ __forceinline__ void chol16_steps(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
+                                             double* Ablk, int ld, double* X) {
+  if constexpr (K < 16) {
+    chol16_step<K>(a, y, i, g, nreal, ok, Ablk, ld, X);
+    chol16_steps<K + 1>(a, y, i, g, nreal, ok, Ablk, ld, X);
+  }
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip) {
   extern __shared__ double smem[];
   __shared__ double red[64];
   __shared__ int sfail;
   State* st = b.st;
-  if (st->done) return;
-  const int n = g.n6, T = g.T, N = 16 * T;
-  const int ld = solve_ld(T);
+  const int n = g.n6, Ts = g.Ts, N = 16 * Ts;
+  const int ld = solve_ld(Ts);
   const int tid = threadIdx.x, nt = blockDim.x;
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
-  // workspace: A (N x ld) | Linv (T x 256) | invd (N) | u (N)
-  double* A = use_lds ? smem : b.Abuf;
-  double* Linv = A + (long)N * ld;
-  double* invd = Linv + 256 * (long)T;
-  double* u = invd + N;
+  double* X = smem;
+  double* u = X + 256 * (size_t)Ts;
+  double* col = u + N;
+  double* A = kLds ? col + 16 : b.Abuf;
+  // flags, radius and the whole lower block triangle of [S; -b^T] are
+  // requested together: one round of global latency instead of a chain
+  const int done = st->done;
+  const int fail_in = st->fail || b.scal[R_COUNT] != 0.0;
   const double radius = st->radius;
-  if (tid == 0) sfail = st->fail || b.scal[R_COUNT] != 0.0;
+  const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
+  for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
+    double v[kLoadBatch];
+#pragma unroll
+    for (int k = 0; k < kLoadBatch; ++k) {
+      const int q = q0 + k, t = q / CC, uu = q - t * CC;
+      const int r = wave + nw * t, c = lane + 64 * uu;
+      v[k] = 0.0;
+      if (q < NQ && r < N && c < n && (c >> 4) <= (r >> 4)) {
+        if (r < n) v[k] = b.S[r * n + c];
+        else if (r == n) v[k] = -b.bvec[c];
+      } else if (q < NQ && c == n && r < n && (r >> 4) == (n >> 4)) {
+        v[k] = -b.bvec[r];  // the diagonal block must stay symmetric
+      }
+    }
+    if (done) return;
+#pragma unroll
+    for (int k = 0; k < kLoadBatch; ++k) {
+      const int q = q0 + k, t = q / CC, uu = q - t * CC;
+      const int r = wave + nw * t, c = lane + 64 * uu;
+      if (q < NQ && r < N && c < N && (c >> 4) <= (r >> 4)) A[r * ld + c] = (r == c && r >= n) ? 1.0 : v[k];
+    }
+  }
+  if (done) return;
+  if (tid == 0) sfail = fail_in;
+  if ((skip & 256) && tid == 0) st->stamps[15] += 1;
+  SOLVE_START(0);
   __syncthreads();
   if (sfail) {
     if (tid == 0) st->fail = 1;
     return;
   }
-  if ((skip & 256) && tid == 0) st->stamps[15] += 1;
-  SOLVE_START(0);
-  // S -> A with kLoadBatch independent (coalesced) loads in flight per thread
-  // (32-bit index math: a 64-bit division per element costs more than the load)
-  const int NN = N * N;
-  for (int base = tid; base < ((skip & 1) ? 0 : NN); base += nt * kLoadBatch) {
-    double v[kLoadBatch];
-    int rr[kLoadBatch], cc[kLoadBatch];
-#pragma unroll
-    for (int k = 0; k < kLoadBatch; ++k) {
-      const int idx = base + k * nt;
-      rr[k] = idx / N;
-      cc[k] = idx - rr[k] * N;
-      v[k] = (idx < NN && rr[k] < n && cc[k] < n) ? b.S[rr[k] * n + cc[k]] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < kLoadBatch; ++k) {
-      if (base + k * nt < NN) {
-        const int r = rr[k], c = cc[k];
-        double x = v[k];
-        if (r == c) x = r < n ? x + fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius : 1.0;
-        A[r * ld + c] = x;
-      }
-    }
-  }
-  for (int r = tid; r < N; r += nt) u[r] = r < n ? -b.bvec[r] : 0.0;
+  for (int r = tid; r < n; r += nt) A[r * ld + r] += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
   __syncthreads();
   SOLVE_STAMP(0);
-  SOLVE_START(1);
-  for (int J = 0; J < T; ++J) {
+  for (int J = 0; J < Ts; ++J) {
     const int j0 = 16 * J;
-    // (a) diagonal block: lane i (< 16) of wave 0 holds row i in registers
-    if (wave == 0 && !(skip & 2)) {
-      const int i = lane & 15;
-      double r[16];
+    SOLVE_START(1);
+    // (a) diagonal block + its inverse
+    if (wave == 0) {
+      const int i = lane >> 2, gq = lane & 3;
+      double* Ablk = A + (long)j0 * ld + j0;
+      double a[4], y[4];
 #pragma unroll
-      for (int m = 0; m < 16; ++m) r[m] = A[(long)(j0 + i) * ld + j0 + m];
+      for (int q = 0; q < 4; ++q) {
+        a[q] = Ablk[i * ld + 4 * gq + q];
+        y[q] = (4 * gq + q == i) ? 1.0 : 0.0;
+      }
       bool ok = true;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const double piv = __shfl(r[k], k, 16);
-        ok = ok && (piv > 0);
-        const double d = sqrt(piv), inv = 1.0 / d;
-        if (i > k) r[k] *= inv;
-        else if (i == k) r[k] = d;
-#pragma unroll
-        for (int m = k + 1; m < 16; ++m) {
-          const double lmk = __shfl(r[k], m, 16);
-          if (i >= m) r[m] -= r[k] * lmk;
-        }
-      }
-      if (!ok && lane == 0) sfail = 1;
-      if (lane < 16) {
-#pragma unroll
-        for (int m = 0; m < 16; ++m)
-          if (m <= i) A[(long)(j0 + i) * ld + j0 + m] = r[m];
-        invd[j0 + i] = 1.0 / r[i];
-      }
+      chol16_steps<0>(a, y, i, gq, n - j0, ok, Ablk, ld, X + 256 * J);
+      if (!ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
     SOLVE_STAMP(1);
-    SOLVE_START(2);
     if (sfail) break;
-    // (b) panel: L_IJ = A_IJ L_JJ^-T, one thread per row below the block
-    for (int rr = j0 + 16 + tid; rr < ((skip & 4) ? 0 : N); rr += nt) {
-      double x[16];
+    SOLVE_START(2);
+    // (b) panel on the matrix cores: L_IJ = A_IJ X_J^T
+    {
+      const double* XJ = X + 256 * J;
+      for (int I = J + 1 + wave; I < Ts; I += nw) {
+        const int i0 = 16 * I;
+        double av[4], bv[4];
 #pragma unroll
-      for (int k = 0; k < 16; ++k) x[k] = A[(long)rr * ld + j0 + k];
+        for (int s = 0; s < 4; ++s) {
+          av[s] = A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s + (lane >> 4)];
+          bv[s] = XJ[(lane & 15) * 16 + 4 * s + (lane >> 4)];
+        }
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        double s = x[k];
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
-        for (int m = 0; m < k; ++m) s -= x[m] * A[(long)(j0 + k) * ld + j0 + m];
-        x[k] = s * invd[j0 + k];
+        for (int q = 0; q < 4; ++q) A[(long)(i0 + (lane >> 4) + 4 * q) * ld + j0 + (lane & 15)] = acc[q];
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) A[(long)rr * ld + j0 + k] = x[k];
     }
     __syncthreads();
     SOLVE_STAMP(2);
     SOLVE_START(3);
     // (c) trailing update on the matrix cores: A_IK -= L_IJ L_KJ^T, J < K <= I
-    const int rem = T - J - 1;
+    const int rem = Ts - J - 1;
     const int npairs = rem * (rem + 1) / 2;
-    for (int p = wave; p < ((skip & 8) ? 0 : npairs); p += nw) {
+    for (int p = wave; p < npairs; p += nw) {
       int I = 0, q = p;
       while (q > I) {
         q -= I + 1;
         ++I;
       }
       const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
+      double av[4], bv[4];
       double4_t acc;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i] = A[(long)(i0 + (lane >> 4) + 4 * i) * ld + k0 + (lane & 15)];
-#pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int col = j0 + 4 * s + (lane >> 4);
-        const double av = -A[(long)(i0 + (lane & 15)) * ld + col];
-        const double bv = A[(long)(k0 + (lane & 15)) * ld + col];
-        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+        const int cc = j0 + 4 * s + (lane >> 4);
+        av[s] = -A[(long)(i0 + (lane & 15)) * ld + cc];
+        bv[s] = A[(long)(k0 + (lane & 15)) * ld + cc];
+        acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)];
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) A[(long)(i0 + (lane >> 4) + 4 * i) * ld + k0 + (lane & 15)] = acc[i];
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)] = acc[s];
     }
     __syncthreads();
     SOLVE_STAMP(3);
-    if (J + 1 < T) SOLVE_START(1);
   }
-  SOLVE_START(4);
   if (sfail) {
     if (tid == 0) st->fail = 1;
     return;
   }
-  // L_JJ^-1 of every diagonal block: one thread per (block, column)
-  for (int q = tid; q < ((skip & 16) ? 0 : N); q += nt) {
-    const int J = q >> 4, c = q & 15, j0 = 16 * J;
-    double x[16];
+  SOLVE_START(5);
+  // backward solve L^T y = z (z = row n of L), wave 0, block by block
+  if (wave == 0) {
+    for (int c = lane; c < N; c += 64) u[c] = c < n ? A[(long)n * ld + c] : 0.0;
+    solve_wave_sync();
+    for (int J = (n - 1) >> 4; J >= 0; --J) {
+      const int j0 = 16 * J;
+      const double* XJ = X + 256 * J;
+      // y_J = X_J^T z_J: 4 lanes per component, 4 terms each, quad reduce
+      const int t = lane >> 2, gq = lane & 3;
+      double s = 0.0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      double s = (r == c) ? 1.0 : 0.0;
+      for (int m = 0; m < 4; ++m) s += XJ[(4 * gq + m) * 16 + t] * u[j0 + 4 * gq + m];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      solve_wave_sync();
+      if (gq == 0) u[j0 + t] = j0 + t < n ? s : 0.0;
+      solve_wave_sync();
+      double yj[16];
 #pragma unroll
-      for (int m = 0; m < r; ++m) s -= A[(long)(j0 + r) * ld + j0 + m] * x[m];
-      x[r] = r < c ? 0.0 : s * invd[j0 + r];
+      for (int m = 0; m < 16; ++m) yj[m] = u[j0 + m];
+      for (int cc = lane; cc < j0; cc += 64) {
+        double acc = 0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc += A[(long)(j0 + m) * ld + cc] * yj[m];
+        u[cc] -= acc;
+      }
+      solve_wave_sync();
     }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) Linv[256 * J + r * 16 + c] = x[r];
   }
   __syncthreads();
-  SOLVE_STAMP(4);
-  SOLVE_START(5);
-  // forward: L u = -b, block by block
-  for (int J = 0; J < ((skip & 32) ? 0 : T); ++J) {
-    const int j0 = 16 * J;
-    double uj = 0;
-    if (tid < 16) {
-      for (int m = 0; m <= tid; ++m) uj += Linv[256 * J + tid * 16 + m] * u[j0 + m];
-    }
-    __syncthreads();
-    if (tid < 16) u[j0 + tid] = uj;
-    __syncthreads();
-    for (int rr = j0 + 16 + tid; rr < N; rr += nt) {
-      double s = 0;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) s += A[(long)rr * ld + j0 + m] * u[j0 + m];
-      u[rr] -= s;
-    }
-    __syncthreads();
-  }
-  // backward: L^T y = u
-  for (int J = ((skip & 64) ? -1 : T - 1); J >= 0; --J) {
-    const int j0 = 16 * J;
-    double yj = 0;
-    if (tid < 16) {
-      for (int r = tid; r < 16; ++r) yj += Linv[256 * J + r * 16 + tid] * u[j0 + r];
-    }
-    __syncthreads();
-    if (tid < 16) u[j0 + tid] = yj;
-    __syncthreads();
-    for (int cc = tid; cc < j0; cc += nt) {
-      double s = 0;
-#pragma unroll
-      for (int m = 0; m < 16; ++m) s += A[(long)(j0 + m) * ld + cc] * u[j0 + m];
-      u[cc] -= s;
-    }
-    __syncthreads();
-  }
   SOLVE_STAMP(5);
   for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
   // candidate cameras
@@ -1053,6 +1092,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.n6 = 6 * g.m;
   g.Rpad = (int)rup(std::max(g.n6, 1), 16);
   g.T = g.Rpad / 16;
+  g.Ts = (g.n6 + 1 + 15) / 16;
   g.K3 = 3 * g.np;
   g.ksplit = (int)std::max(1L, std::min(64L, rup(std::max(g.K3, 1), 512) / 512));
   g.Kpad = (int)rup(std::max(g.K3, 1), 16L * g.ksplit);
@@ -1133,7 +1173,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * kLinStride * (size_t)g.no, &b.lin);
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);
   add((size_t)g.no, &b.dup);
-  add(8 * ((size_t)(16 * g.T) * (((16 * g.T + 31) / 32) * 32 + 2) + 256 * (size_t)g.T + 32 * (size_t)g.T), &b.Abuf);
+  add(8 * solve_a_doubles(g.Ts), &b.Abuf);
   add(8 * 3 * (size_t)g.no, &b.tq);
   add(8 * 18 * (size_t)g.no, &b.Wo);
   add(8 * (size_t)g.n6, &b.csc);
@@ -1213,12 +1253,12 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       if (x < g.lo[a] || x > g.hi[a]) return 1;  // infeasible
     }
   // LDS for the camera solve
-  P.solve_lds = 8 * ((size_t)(16 * g.T) * (((16 * g.T + 31) / 32) * 32 + 2) + 256 * (size_t)g.T + 32 * (size_t)g.T);
+  P.solve_lds = 8 * (solve_small_doubles(g.Ts) + solve_a_doubles(g.Ts));
   P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
-  if (!P.use_lds) P.solve_lds = 0;
-  else
-    ME_HIP(c, hipFuncSetAttribute((const void*)cam_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)P.solve_lds));
+  if (!P.use_lds) P.solve_lds = 8 * solve_small_doubles(g.Ts);
+  ME_CHECK(c, P.solve_lds <= 150 * 1024, "BA: %d variable cameras exceed the camera-solve workspace", g.m);
+  ME_HIP(c, hipFuncSetAttribute(P.use_lds ? (const void*)cam_solve_kernel<true> : (const void*)cam_solve_kernel<false>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   return ME_OK;
 }
 
@@ -1303,8 +1343,10 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_SOLVE);
-    hipLaunchKernelGGL(cam_solve_kernel, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
-                       P.use_lds);
+    if (P.use_lds)
+      hipLaunchKernelGGL(cam_solve_kernel<true>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip);
+    else
+      hipLaunchKernelGGL(cam_solve_kernel<false>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip);
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);

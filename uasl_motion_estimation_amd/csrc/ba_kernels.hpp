@@ -59,7 +59,7 @@ struct State {
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi;
+  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi;
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
