@@ -312,6 +312,23 @@ static void compute_scaling(Solver& S, const Linearisation& L, bool jacobi) {
   for (double& c : S.psc) c = jacobi ? 1.0 / (1.0 + std::sqrt(c)) : 1.0;
 }
 
+// Reduced camera system S = U - W V^-1 W^T, b of the first LM step
+// (Ceres SPARSE_SCHUR, BundleAdjuster.h:463).  `jacobi` = 0 leaves the
+// columns unscaled, which makes S and b additive over landmark shards (the
+// exchange of the multi-GPU solve).
+extern "C" int oracle_ba_reduced_system_ex(const oracle_ba_problem* p, double radius, int jacobi, double* Sout,
+                                           double* bout) {
+  Solver S = make_solver(p);
+  Linearisation L;
+  linearise(p, p->cams, p->pts, L);
+  compute_scaling(S, L, jacobi != 0);
+  std::vector<double> yc, yp, Sm, bm;
+  bool ok = solve_lm(S, L, radius, yc, yp, &Sm, &bm);
+  std::memcpy(Sout, Sm.data(), Sm.size() * 8);
+  std::memcpy(bout, bm.data(), bm.size() * 8);
+  return ok ? 0 : -1;
+}
+
 extern "C" int oracle_ba_reduced_system(const oracle_ba_problem* p, double radius, double* Sout, double* bout) {
   Solver S = make_solver(p);
   Linearisation L;

@@ -112,6 +112,7 @@ int oracle_ba_solve(oracle_ba_problem* p, const oracle_ba_options* o, oracle_ba_
 /* one linearisation at the given params: reduced camera system of the first
    LM step (scaled coordinates, radius r).  S is (6m)x(6m), b 6m, m = non-fixed cams. */
 int oracle_ba_reduced_system(const oracle_ba_problem* p, double radius, double* S, double* b);
+int oracle_ba_reduced_system_ex(const oracle_ba_problem* p, double radius, int jacobi, double* S, double* b);
 
 /* ---- A11: nonMaxSupScanline3x3 (src/core/feature_types.cpp:253-351) ---- */
 int oracle_nms_scanline3x3(const double* resp, int w, int h, uint8_t* mask, double* maxima, int cap);

@@ -120,6 +120,7 @@ def lib():
         L.oracle_ba_cost.argtypes = [P(OBAProblem)]
         L.oracle_ba_solve.argtypes = [P(OBAProblem), P(OBAOptions), P(OBASummary), P(c_double), c_int]
         L.oracle_ba_reduced_system.argtypes = [P(OBAProblem), c_double, P(c_double), P(c_double)]
+        L.oracle_ba_reduced_system_ex.argtypes = [P(OBAProblem), c_double, c_int, P(c_double), P(c_double)]
         L.oracle_nms_scanline3x3.argtypes = [P(c_double), c_int, c_int, P(c_uint8), P(c_double), c_int]
         L.oracle_klt_track.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, P(c_float), P(c_float), P(c_uint8),
                                        c_int, P(OKLTParams)]
@@ -344,6 +345,17 @@ def ba_reduced_system(bp, radius=1e4):
     S = np.zeros(n * n)
     b = np.zeros(n)
     rc = lib().oracle_ba_reduced_system(ctypes.byref(p), radius, _p(S), _p(b))
+    return S.reshape(n, n), b, rc
+
+
+def ba_reduced_system_unscaled(bp, radius=1e300):
+    """S, b without Jacobi scaling (additive over landmark shards)."""
+    p, keep, _, _ = ba_struct(bp)
+    m = len(bp.cams) - min(max(bp.fixed_frames, 0), len(bp.cams))
+    n = 6 * m
+    S = np.zeros(n * n)
+    b = np.zeros(n)
+    rc = lib().oracle_ba_reduced_system_ex(ctypes.byref(p), radius, 0, _p(S), _p(b))
     return S.reshape(n, n), b, rc
 
 

@@ -1,0 +1,135 @@
+"""Multi-rank BA: landmark shards, one all-reduce of the reduced
+camera system per LM iteration.
+
+CPU (gloo, world size 2): the shard partition and the exchange itself —
+S and b of the shards, summed by torch.distributed, equal the full system.
+GPU: me_ba_solve_sharded on two contexts of one device with a host-side
+all-reduce reproduces the single-device solve.
+"""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from uasl_motion_estimation_amd import synthetic as S
+from uasl_motion_estimation_amd.optimisation import shard_landmarks
+
+
+def _problem():
+    return S.ba_problem(20261019, 300, 8, 640, 480)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_partition_covers_every_landmark_once(world):
+    bp = _problem()
+    seen_pts, seen_obs, sizes = 0, 0, []
+    for r in range(world):
+        local, (lo, hi) = shard_landmarks(bp, r, world)
+        assert lo == seen_pts  # contiguous, in order
+        seen_pts = hi
+        np.testing.assert_array_equal(local.pts, bp.pts[lo:hi])
+        assert local.pt_idx.min(initial=0) >= 0 and local.pt_idx.max(initial=-1) < hi - lo
+        np.testing.assert_array_equal(local.cams, bp.cams)
+        seen_obs += len(local.obs)
+        sizes.append(len(local.obs))
+    assert seen_pts == len(bp.pts) and seen_obs == len(bp.obs)
+    assert max(sizes) - min(sizes) <= 2 * S.CONFIGS[2]["window"]  # balanced to within a track or two
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_rank(rank, world, port, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bp = _problem()
+    local, _ = shard_landmarks(bp, rank, world)
+    Sg, bg, rc = O.ba_reduced_system_unscaled(local)
+    t = torch.from_numpy(np.concatenate([Sg.ravel(), bg]))
+    dist.all_reduce(t)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "sum.npy"), t.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_exchange_sums_to_full_reduced_system(tmp_path, oracle):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_gloo_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    got = np.load(tmp_path / "sum.npy")
+    bp = _problem()
+    Sf, bf, rc = oracle.ba_reduced_system_unscaled(bp)
+    assert rc == 0
+    n = len(bf)
+    np.testing.assert_allclose(got[:n * n].reshape(n, n), Sf, rtol=1e-10, atol=1e-10 * np.abs(Sf).max())
+    np.testing.assert_allclose(got[n * n:], bf, rtol=1e-10, atol=1e-10 * np.abs(bf).max())
+
+
+# ------------------------------------------------------------------ GPU
+class _HostAllReduce:
+    """All-reduce of device buffers between threads (stands in for RCCL)."""
+
+    def __init__(self, world):
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.bufs = [None] * world
+
+    def callback(self, rank, ctx):
+        def _ar(ptr, n):
+            ctx.synchronize()
+            a = np.zeros(abs(n))
+            ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, a.ctypes.data, ptr, 8 * abs(n)))
+            self.bufs[rank] = a
+            self.barrier.wait()
+            tot = np.max(self.bufs, axis=0) if n < 0 else np.sum(self.bufs, axis=0)
+            self.barrier.wait()
+            ctx.check(ctx.lib.me_memcpy_h2d(ctx.h, ptr, np.ascontiguousarray(tot).ctypes.data, 8 * abs(n)))
+            ctx.synchronize()
+
+        return _ar
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jacobi", [True, False])
+def test_gpu_sharded_solve_matches_single_device(ctx, jacobi):
+    from uasl_motion_estimation_amd._lib import Context
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve, ba_solve_sharded
+
+    bp = _problem()
+    opts = SolverOptions.fixed_iterations(8)
+    opts.jacobi_scaling = jacobi
+    ref_c, ref_p, ref_s = ba_solve(bp.copy(), opts, ctx=ctx)
+    world = 2
+    ar = _HostAllReduce(world)
+    ctxs = [Context(0) for _ in range(world)]
+    res = [None] * world
+
+    def run(r):
+        local, rng = shard_landmarks(bp, r, world)
+        res[r] = (ba_solve_sharded(local, ar.callback(r, ctxs[r]), opts, ctx=ctxs[r]), rng)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    pts = np.zeros_like(ref_p)
+    for r in range(world):
+        (cams, p, s), (lo, hi) = res[r]
+        np.testing.assert_allclose(cams, ref_c, rtol=1e-6, atol=1e-9)
+        assert s["iterations"] == ref_s["iterations"]
+        pts[lo:hi] = p
+    np.testing.assert_allclose(pts, ref_p, rtol=1e-6, atol=1e-9)

@@ -11,6 +11,8 @@
 """
 from __future__ import annotations
 
+import copy
+
 import ctypes
 from ctypes import POINTER, byref, c_double, c_int, c_int32, c_long, c_uint8, c_uint32
 from dataclasses import dataclass, field
@@ -353,6 +355,66 @@ def ba_solve_sharded(bp_local, allreduce, options: SolverOptions | None = None, 
     keep.append(cb)
     ctx.check(ctx.lib.me_ba_solve_sharded(ctx.h, byref(p), byref(o), cb, None, byref(s)), "me_ba_solve_sharded")
     return cams, pts, _summary(s)
+
+
+def shard_landmarks(bp, rank: int, world: int):
+    """Contiguous landmark range of `rank`, balanced by observation count
+    (SURVEY §8e).  Returns (local problem, (first, last+1) landmark range).
+    Cameras are replicated; observations follow their landmark."""
+    npt = len(bp.pts)
+    pidx = np.asarray(bp.pt_idx)
+    cum = np.concatenate([[0], np.cumsum(np.bincount(pidx, minlength=npt))])
+    total = cum[-1]
+    cuts = [0] + [int(np.searchsorted(cum, total * k / world, side="left")) for k in range(1, world)] + [npt]
+    cuts = np.maximum.accumulate(np.clip(cuts, 0, npt))
+    lo, hi = int(cuts[rank]), int(cuts[rank + 1])
+    sel = (pidx >= lo) & (pidx < hi)
+    local = copy.copy(bp)
+    local.cams = np.array(bp.cams, np.float64, copy=True)
+    local.pts = np.array(bp.pts[lo:hi], np.float64, copy=True)
+    local.obs = np.ascontiguousarray(np.asarray(bp.obs)[sel])
+    local.cam_idx = np.ascontiguousarray(np.asarray(bp.cam_idx)[sel], dtype=np.int32)
+    local.pt_idx = np.ascontiguousarray(pidx[sel] - lo, dtype=np.int32)
+    return local, (lo, hi)
+
+
+class _DeviceDoubles:
+    """Zero-copy view of a device buffer for torch.as_tensor (CUDA array interface)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+def torch_allreduce(group=None):
+    """all-reduce callback over torch.distributed (RCCL on MI355X, gloo on CPU
+    tests): sums n doubles in place, or takes the max for n < 0."""
+    import torch
+    import torch.distributed as dist
+
+    def _ar(ptr: int, n: int):
+        t = torch.as_tensor(_DeviceDoubles(ptr, abs(n)), device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.SUM if n > 0 else dist.ReduceOp.MAX, group=group)
+
+    return _ar
+
+
+def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context | None = None, group=None):
+    """Landmark-sharded BA over torch.distributed: each rank solves the same
+    camera system from the all-reduced S, b (one exchange per LM iteration)
+    and updates its own landmarks.  Returns (cams, local pts, (lo, hi), summary)."""
+    import torch
+    import torch.distributed as dist
+
+    ctx = ctx or default_context()
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    local, rng = shard_landmarks(bp, rank, world)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)  # order kernels and RCCL on one stream
+    try:
+        cams, pts, summ = ba_solve_sharded(local, torch_allreduce(group), options, ctx)
+    finally:
+        ctx.set_stream(None)
+    return cams, pts, rng, summ
 
 
 def ba_cost(bp, ctx: Context | None = None) -> float:
