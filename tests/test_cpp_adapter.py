@@ -1,0 +1,85 @@
+"""The C++ mirror of the reference API (include/MotionEstimationAMD) driven by a
+compiled C++ caller (tests/cpp/adapter_cli) — the binding a maintainer adds
+under the reference's src/ (INTEGRATION.md)."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from uasl_motion_estimation_amd import synthetic as S
+
+CLI = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "adapter_cli")
+
+
+def _run(mode, payload, tmp_path, check=True):
+    i, o = tmp_path / f"{mode}.in", tmp_path / f"{mode}.out"
+    i.write_bytes(payload)
+    p = subprocess.run([CLI, mode, str(i), str(o)], capture_output=True, text=True, timeout=300)
+    if check:
+        assert p.returncode == 0, p.stderr
+    return p, (o.read_bytes() if o.exists() else b"")
+
+
+def _mi_payload(L, R):
+    return struct.pack("<ii", *L.shape) + L.tobytes() + R.tobytes()
+
+
+def test_cli_is_built_and_fails_loudly_without_a_device(tmp_path):
+    assert os.path.exists(CLI), "build() compiles tests/cpp/adapter_cli"
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            pytest.skip("device present")
+    except ImportError:
+        pass
+    L = np.zeros((11, 11), np.uint8)
+    p, _ = _run("mi", _mi_payload(L, L), tmp_path, check=False)
+    assert p.returncode == 1 and "me_create" in p.stderr  # no silent CPU fallback
+
+
+@pytest.mark.gpu
+def test_cpp_mi_and_entropy_bit_exact(tmp_path, oracle):
+    rng = np.random.default_rng(7)
+    L = rng.integers(0, 256, (11, 11), dtype=np.uint8)
+    R = np.clip(L.astype(int) + rng.integers(-30, 30, L.shape), 0, 255).astype(np.uint8)
+    _, out = _run("mi", _mi_payload(L, R), tmp_path)
+    mi, h, threw = struct.unpack("<ffi", out)
+    assert np.float32(mi) == np.float32(oracle.mutual_information(L, R))
+    assert np.float32(h) == np.float32(oracle.entropy(L))
+    assert threw == 1
+
+
+@pytest.mark.gpu
+def test_cpp_nms_bit_exact(tmp_path, oracle):
+    rng = np.random.default_rng(8)
+    r = np.round(rng.random((40, 50)) * 6) / 6
+    _, out = _run("nms", struct.pack("<ii", *r.shape) + r.tobytes(), tmp_path)
+    n = struct.unpack_from("<i", out)[0]
+    mx = np.frombuffer(out, np.float64, 2 * n, 4).reshape(n, 2)
+    mask = np.frombuffer(out, np.uint8, r.size, 4 + 16 * n).reshape(r.shape)
+    rmx, rmask = oracle.nms(r)
+    assert np.array_equal(mx, rmx) and np.array_equal(mask, rmask)
+
+
+@pytest.mark.gpu
+def test_cpp_bundle_adjuster_matches_oracle(tmp_path, oracle):
+    bp = S.ba_problem(20261020, 150, 6, 640, 480)
+    payload = struct.pack("<iiii", len(bp.cams), len(bp.pts), len(bp.obs), bp.fixed_frames)
+    payload += np.asarray(bp.K0, np.float64).tobytes() + np.asarray(bp.K1, np.float64).tobytes()
+    payload += struct.pack("<dd", bp.baseline, bp.feat_var)
+    payload += np.ascontiguousarray(bp.cams, np.float64).tobytes() + np.ascontiguousarray(bp.pts).tobytes()
+    payload += np.ascontiguousarray(bp.obs, np.float64).tobytes()
+    payload += np.ascontiguousarray(bp.cam_idx, np.int32).tobytes() + np.ascontiguousarray(bp.pt_idx).tobytes()
+    _, out = _run("ba", payload, tmp_path)
+    status, iters, cost = struct.unpack_from("<iid", out)
+    off = 16
+    cams = np.frombuffer(out, np.float64, 6 * len(bp.cams), off).reshape(-1, 6)
+    pts = np.frombuffer(out, np.float64, 3 * len(bp.pts), off + 48 * len(bp.cams)).reshape(-1, 3)
+    rc, rp, rs = oracle.ba_solve(bp)
+    assert status == 2 and iters == rs["iterations"]  # Status::SUCCESSFUL
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(cost, rs["final_cost"], rtol=1e-8)
