@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--frames", type=int, default=4, help="distinct synthetic frames cycled per rank")
     ap.add_argument("--ba-iters", type=int, default=10)
-    ap.add_argument("--cpu-frames", type=int, default=2, help="frames of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
 
@@ -67,7 +67,10 @@ def make_frames(cfg: dict, seed: int, n_frames: int):
 
 
 def upload_images(ctx, frames):
-    """Device copies of every image (inputs resident in HBM before timing)."""
+    """Device copies of every image, KLT point list and BA window (inputs
+    resident in HBM before timing)."""
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, DeviceScaleTracks
+
     keep = []
     for fd in frames:
         for name, img in (("d_prev", fd.prev), ("d_curL", fd.cur.left), ("d_curR", fd.cur.right)):
@@ -83,21 +86,24 @@ def upload_images(ctx, frames):
             ctx.check(ctx.lib.me_malloc(ctx.h, ctypes.byref(p), max(nbytes, 16)))
             setattr(fd, name, p.value)
         ctx.check(ctx.lib.me_memcpy_h2d(ctx.h, ctypes.c_void_p(fd.d_pts_in), fd.klt_pts.ctypes.data, 8 * n))
+        fd.dba = DeviceBAProblem(fd.ba, ctx)  # BA window resident in HBM
+        fd.dscale = DeviceScaleTracks(fd.scale, ctx)  # scale-state tracks resident in HBM
     return keep
 
 
 def gpu_step(ctx, fd, kp, ba_opts, stats):
     from uasl_motion_estimation_amd._lib import ME_DEVICE
-    from uasl_motion_estimation_amd.optimisation import ba_solve, scale_optimise
+    from uasl_motion_estimation_amd.optimisation import scale_optimise
 
     H, W = fd.prev.shape
     n = len(fd.klt_pts)
     ctx.check(ctx.lib.me_klt_track(ctx.h, ME_DEVICE, ctypes.c_void_p(fd.d_prev), ctypes.c_void_p(fd.d_curL), W, H, W,
                                    ctypes.c_void_p(fd.d_pts_in), ctypes.c_void_p(fd.d_pts_out),
                                    ctypes.c_void_p(fd.d_status), n, ctypes.byref(kp)), "klt")
-    r = scale_optimise(fd.scale, ctx=ctx, img_mem=ME_DEVICE, dev_imgs=(fd.d_curL, fd.d_curR))
+    r = scale_optimise(fd.scale, ctx=ctx, img_mem=ME_DEVICE, dev_imgs=(fd.d_curL, fd.d_curR), dev_tracks=fd.dscale.d)
     stats["scale_iters"] += r["iterations"]
-    cams, pts, s = ba_solve(fd.ba, ba_opts, ctx=ctx)
+    fd.dba.reset()  # same starting point every time the frame is replayed (device copy)
+    s = fd.dba.solve(ba_opts)
     stats["ba_iters"] += s["iterations"]
     stats["frames"] += 1
 

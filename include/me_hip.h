@@ -115,6 +115,7 @@ typedef struct {
   const uint8_t* mask;       /* optional Eigen::VectorXi mask as 0/1 bytes (host) */
   int mask_len;
   me_mem img_mem;
+  me_mem tracks_mem;         /* X_*, tri_*, last_* in host (ME_HOST) or device memory; mask is always host */
 } me_scale_state;
 
 typedef struct {
@@ -161,6 +162,9 @@ typedef struct {
   double K0[9], K1[9];       /* CalibrationParameters::K[0], K[1] */
   double baseline, feat_var;
   int fixed_frames;          /* optimise(fixedFrames) */
+  me_mem mem;                /* ME_HOST: the arrays above are host memory (copied in/out);
+                                ME_DEVICE: device memory on the ctx device, cams/pts updated in
+                                place on the device (me_ba_solve / me_ba_solve_sharded only) */
 } me_ba_problem;
 
 typedef struct {

@@ -258,3 +258,57 @@ def test_klt_bit_exact(ctx, oracle):
     assert np.array_equal(gst, rst)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst.mean() > 0.8
+
+
+# ------------------------------------------------------------------ device-resident BA windows
+def test_ba_device_resident_matches_host_bit_exact(ctx):
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions, ba_solve
+
+    bp = S.ba_problem(31, 400, 10, 640, 480)
+    hc, hp, hs = ba_solve(bp.copy(), SolverOptions.fixed_iterations(6), ctx=ctx)
+    d = DeviceBAProblem(bp, ctx)
+    ds = d.solve(SolverOptions.fixed_iterations(6))
+    dc, dp = d.download()
+    assert ds == hs
+    assert np.array_equal(dc, hc) and np.array_equal(dp, hp)
+    d.reset()
+    ds2 = d.solve(SolverOptions.fixed_iterations(6))
+    assert ds2 == hs and np.array_equal(d.download()[0], hc)
+    d.close()
+
+
+def test_ba_device_resident_bad_index_and_infeasible(ctx):
+    from uasl_motion_estimation_amd._lib import MEError
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem
+
+    bp = S.ba_problem(32, 50, 5, 640, 480)
+    bad = bp.copy()
+    bad.pt_idx = bp.pt_idx.copy()
+    bad.pt_idx[3] = len(bp.pts) + 7
+    d = DeviceBAProblem(bad, ctx)
+    with pytest.raises(MEError):
+        d.solve()
+    d.close()
+    inf = bp.copy()
+    inf.pts[0, 2] = -5.0  # behind the camera: outside the Z box (BundleAdjuster.h:455-460)
+    d = DeviceBAProblem(inf, ctx)
+    s = d.solve()
+    assert s["status"] == 3 and s["iterations"] == 0 and np.isnan(s["final_cost"])
+    assert np.array_equal(d.download()[1], inf.pts)  # parameters untouched
+    d.close()
+
+
+def test_scale_device_resident_tracks_match_host(ctx, oracle):
+    from uasl_motion_estimation_amd.optimisation import DeviceScaleTracks, scale_optimise
+
+    sp = S.scale_problem(33, 320, 240, 300, window=5, w=5)
+    ref = oracle.scale_optimise(sp)
+    host = scale_optimise(sp, ctx=ctx)
+    d = DeviceScaleTracks(sp, ctx)
+    dev = scale_optimise(sp, ctx=ctx, dev_tracks=d.d)
+    d.close()
+    assert int(host["stop"]) == int(dev["stop"]) == int(ref["stop"])
+    assert host["iterations"] == dev["iterations"] == ref["iterations"]
+    assert host["scale"] == dev["scale"]
+    np.testing.assert_allclose(dev["scale"], ref["scale"], rtol=1e-9)
+    np.testing.assert_allclose(dev["trace"], ref["trace"], rtol=1e-9)

@@ -62,7 +62,7 @@ class ScaleStateC(ctypes.Structure):
         ("stride", c_int), ("cols", c_int), ("rows", c_int),
         ("bb_cols", c_int), ("bb_rows", c_int),
         ("mask", POINTER(c_uint8)), ("mask_len", c_int),
-        ("img_mem", c_int),
+        ("img_mem", c_int), ("tracks_mem", c_int),
     ]
 
 
@@ -82,7 +82,7 @@ class BAProblemC(ctypes.Structure):
         ("cam_idx", POINTER(c_int32)), ("pt_idx", POINTER(c_int32)),
         ("K0", c_double * 9), ("K1", c_double * 9),
         ("baseline", c_double), ("feat_var", c_double),
-        ("fixed_frames", c_int),
+        ("fixed_frames", c_int), ("mem", c_int),
     ]
 
 
@@ -247,6 +247,26 @@ class Context:
 
     def synchronize(self):
         self.check(self.lib.me_synchronize(self.h), "me_synchronize")
+
+    # --- device memory on the ctx device (ctx stream) ---
+    def malloc(self, nbytes: int) -> int:
+        p = c_void_p()
+        self.check(self.lib.me_malloc(self.h, ctypes.byref(p), int(nbytes)), "me_malloc")
+        return p.value
+
+    def free(self, ptr: int):
+        self.check(self.lib.me_free(self.h, c_void_p(ptr)), "me_free")
+
+    def h2d(self, dst: int, src: np.ndarray):
+        src = np.ascontiguousarray(src)
+        self.check(self.lib.me_memcpy_h2d(self.h, c_void_p(dst), src.ctypes.data, src.nbytes), "me_memcpy_h2d")
+
+    def d2h(self, dst: np.ndarray, src: int):
+        assert dst.flags.c_contiguous
+        self.check(self.lib.me_memcpy_d2h(self.h, dst.ctypes.data, c_void_p(src), dst.nbytes), "me_memcpy_d2h")
+
+    def d2d(self, dst: int, src: int, nbytes: int):
+        self.check(self.lib.me_memcpy_d2d(self.h, c_void_p(dst), c_void_p(src), int(nbytes)), "me_memcpy_d2d")
 
     # --- kernel timing (HIP events on the ctx stream) ---
     def timing(self, on: bool = True):

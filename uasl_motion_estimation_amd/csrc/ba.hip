@@ -193,6 +193,16 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
     X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
     X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
     for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
+    const int cs = b.cpos[o];
+    if (cs >= 0) {  // camera normal-equation pieces, component-major by camera slot
+      double* C = b.cvec + cs;
+      int u = 0;
+      for (int a = 0; a < 6; ++a)
+        for (int c = a; c < 6; ++c, ++u)
+          C[(long)u * g.no] = Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c] + Jc[12 + a] * Jc[12 + c] + Jc[18 + a] * Jc[18 + c];
+      for (int a = 0; a < 6; ++a)
+        C[(long)(21 + a) * g.no] = Jc[a] * r[0] + Jc[6 + a] * r[1] + Jc[12 + a] * r[2] + Jc[18 + a] * r[3];
+    }
     if (ci - g.nf >= 0) {
       double* W = b.Wo + 18 * slot;
       for (int a = 0; a < 6; ++a)
@@ -206,51 +216,71 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
   if (threadIdx.x == 0) b.part[R_COST * g.pstride + blockIdx.x] = out[0];
 }
 
-// One workgroup per variable camera: unscaled U = Jc^T Jc and g = Jc^T r over
-// its observations (fixed order), then (unless sharded) the Jacobi scaling at
-// iteration 0 from diag(U) = squared column norms, and the scaled blocks.
-__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, int sharded, double* colnorm,
-                                                              double* gc_raw, double* Uraw) {
+// Unscaled U = Jc^T Jc (21 unique) and g = Jc^T r per variable camera, in
+// two deterministic stages over the per-observation pieces linearize wrote
+// contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
+// k + ck, ... of 256 slots of camera c into a partial; cam_reduce adds the ck
+// partials in order.
+__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart) {
   __shared__ double lds[4 * 27];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
-  const int ci = blockIdx.x;
+  const int ci = blockIdx.x, k = blockIdx.y;
   const int beg = b.c_off[ci], end = b.c_off[ci + 1];
   double v[27];
   for (int i = 0; i < 27; ++i) v[i] = 0;
-  for (int q = beg + threadIdx.x; q < end; q += kBlock) {
-    const double* L = b.lin + (long)b.c_obs[q] * kLinStride;
-    int u = 0;
-    for (int a = 0; a < 6; ++a)
-      for (int c = a; c < 6; ++c, ++u)
-        v[u] += L[4 + a] * L[4 + c] + L[10 + a] * L[10 + c] + L[16 + a] * L[16 + c] + L[22 + a] * L[22 + c];
-    for (int a = 0; a < 6; ++a) v[21 + a] += L[4 + a] * L[0] + L[10 + a] * L[1] + L[16 + a] * L[2] + L[22 + a] * L[3];
-  }
+  for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock)
+    for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
   double out[27];
   block_sum<27>(v, out, lds);
   if (threadIdx.x == 0) {
-    double* Ur = Uraw + 21 * (long)ci;
-    for (int u = 0; u < 21; ++u) Ur[u] = out[u];
-    int u = 0;
-    for (int a = 0; a < 6; ++a) {
-      colnorm[6 * ci + a] = out[u];  // diagonal entry (a, a)
-      u += 6 - a;
-      gc_raw[6 * ci + a] = out[21 + a];
-    }
+    double* P = cpart + 27 * ((long)ci * g.ck + k);
+    for (int u = 0; u < 27; ++u) P[u] = out[u];
+  }
+}
+
+// One wavefront per variable camera: lane u < 27 sums component u of the
+// partials (fixed order) -> raw U, column norms, raw gradient; unless
+// sharded, the Jacobi scaling (iteration 0) and the scaled blocks.
+__global__ __launch_bounds__(64) void cam_reduce_kernel(Geo g, Bufs b, int sharded, const double* cpart,
+                                                        double* colnorm, double* gc_raw, double* Uraw) {
+  __shared__ double tot[27];
+  __shared__ double csl[6];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  const int ci = blockIdx.x, u = threadIdx.x;
+  if (u < 27) {
+    double sum = 0.0;
+    for (int k = 0; k < g.ck; ++k) sum += cpart[27 * ((long)ci * g.ck + k) + u];
+    tot[u] = sum;
+    if (u < 21) Uraw[21 * (long)ci + u] = sum;
+    else gc_raw[6 * ci + u - 21] = sum;
+  }
+  __syncthreads();
+  if (u < 6) {
+    const int d = u * 6 - u * (u - 1) / 2;  // index of (u, u) in the packed upper triangle
+    colnorm[6 * ci + u] = tot[d];
     if (!sharded) {
       double* cs = b.csc + 6 * ci;
-      if (!st->scaled)
-        for (int a = 0; a < 6; ++a) cs[a] = g.jacobi ? 1.0 / (1.0 + sqrt(colnorm[6 * ci + a])) : 1.0;
-      double* U = b.U + 36 * (long)ci;
-      u = 0;
-      for (int a = 0; a < 6; ++a)
-        for (int c = a; c < 6; ++c, ++u) {
-          const double x = out[u] * cs[a] * cs[c];
-          U[a * 6 + c] = x;
-          U[c * 6 + a] = x;
-        }
-      for (int a = 0; a < 6; ++a) b.gcs[6 * ci + a] = out[21 + a] * cs[a];
+      if (!st->scaled) cs[u] = g.jacobi ? 1.0 / (1.0 + sqrt(tot[d])) : 1.0;
+      csl[u] = cs[u];
     }
+  }
+  if (sharded) return;
+  __syncthreads();
+  if (u < 21) {
+    int a = 0, r = u;
+    while (r >= 6 - a) {
+      r -= 6 - a;
+      ++a;
+    }
+    const int c = a + r;
+    const double x = tot[u] * csl[a] * csl[c];
+    double* U = b.U + 36 * (long)ci;
+    U[a * 6 + c] = x;
+    U[c * 6 + a] = x;
+  } else if (u < 27) {
+    b.gcs[6 * ci + u - 21] = tot[u] * csl[u - 21];
   }
 }
 
@@ -276,43 +306,91 @@ __global__ void cam_finish_kernel(Geo g, Bufs b, const double* colnorm, const do
   for (int a = 0; a < 6; ++a) b.gcs[6 * ci + a] = gc_raw[6 * ci + a] * cs[a];
 }
 
-// One lane per point: sum V_o, g_o; point Jacobi scaling at iteration 0
-// (diag V = squared column norms); projected-gradient max-norm contribution.
-__global__ __launch_bounds__(kPtBlock) void pt_assemble_kernel(Geo g, Bufs b) {
+__device__ __forceinline__ bool chol3(const double* A, double* L) {
+  double d0 = A[0];
+  if (!(d0 > 0)) return false;
+  d0 = sqrt(d0);
+  const double l10 = A[3] / d0, l20 = A[6] / d0;
+  double d1 = A[4] - l10 * l10;
+  if (!(d1 > 0)) return false;
+  d1 = sqrt(d1);
+  const double l21 = (A[7] - l20 * l10) / d1;
+  double d2 = A[8] - l20 * l20 - l21 * l21;
+  if (!(d2 > 0)) return false;
+  d2 = sqrt(d2);
+  L[0] = d0; L[1] = 0; L[2] = 0;
+  L[3] = l10; L[4] = d1; L[5] = 0;
+  L[6] = l20; L[7] = l21; L[8] = d2;
+  return true;
+}
+__device__ __forceinline__ void fwd3(const double* L, const double* b, double* y) {
+  y[0] = b[0] / L[0];
+  y[1] = (b[1] - L[3] * y[0]) / L[4];
+  y[2] = (b[2] - L[6] * y[0] - L[7] * y[1]) / L[8];
+}
+__device__ __forceinline__ void bwd3(const double* L, const double* y, double* x) {
+  x[2] = y[2] / L[8];
+  x[1] = (y[1] - L[7] * x[2]) / L[4];
+  x[0] = (y[0] - L[3] * x[1] - L[6] * x[2]) / L[0];
+}
+
+// One lane per point.  After a linearisation: sum V_o, g_o over the point's
+// CSR range, Jacobi scaling at iteration 0 (diag V = squared column norms),
+// projected-gradient max-norm contribution.  Every iteration: V + D/radius ->
+// Cholesky L_p and z_p = L_p^-1 g_p (the point half of the Schur step).
+__global__ __launch_bounds__(kPtBlock) void pt_assemble_kernel(Geo g, Bufs b, Opts o) {
   __shared__ double lds[4];
-  const State* st = b.st;
-  if (st->done || !st->need_lin) return;
+  State* st = b.st;
+  if (st->done) return;
+  const int need_lin = st->need_lin;
   const int j = blockIdx.x * kPtBlock + threadIdx.x;
   double gm = 0;
+  double Vs[9], gs[3];
   if (j < g.np) {
-    double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
-    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
-      const double* X = b.obsx + (long)q * kObsxStride;
-      for (int i = 0; i < 6; ++i) V[i] += X[i];
-      for (int a = 0; a < 3; ++a) gr[a] += X[6 + a];
+    if (need_lin) {
+      double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
+      for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
+        const double* X = b.obsx + (long)q * kObsxStride;
+        for (int i = 0; i < 6; ++i) V[i] += X[i];
+        for (int a = 0; a < 3; ++a) gr[a] += X[6 + a];
+      }
+      double* ps = b.psc + 3 * (long)j;
+      if (!st->scaled) {
+        ps[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
+        ps[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
+        ps[2] = g.jacobi ? 1.0 / (1.0 + sqrt(V[5])) : 1.0;
+      }
+      const double p0 = ps[0], p1 = ps[1], p2 = ps[2];
+      Vs[0] = V[0] * p0 * p0; Vs[1] = V[1] * p0 * p1; Vs[2] = V[2] * p0 * p2;
+      Vs[3] = Vs[1];          Vs[4] = V[3] * p1 * p1; Vs[5] = V[4] * p1 * p2;
+      Vs[6] = Vs[2];          Vs[7] = Vs[5];          Vs[8] = V[5] * p2 * p2;
+      gs[0] = gr[0] * p0;
+      gs[1] = gr[1] * p1;
+      gs[2] = gr[2] * p2;
+      double* Vo = b.V + 9 * (long)j;
+      for (int i = 0; i < 9; ++i) Vo[i] = Vs[i];
+      for (int a = 0; a < 3; ++a) b.gps[3 * (long)j + a] = gs[a];
+      const double* x = b.pts[st->cur] + 3 * (long)j;
+      for (int a = 0; a < 3; ++a) {
+        const double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
+        gm = fmax(gm, fabs(x[a] - xp));
+      }
+    } else {
+      for (int i = 0; i < 9; ++i) Vs[i] = b.V[9 * (long)j + i];
+      for (int a = 0; a < 3; ++a) gs[a] = b.gps[3 * (long)j + a];
     }
-    double* ps = b.psc + 3 * (long)j;
-    if (!st->scaled) {
-      ps[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
-      ps[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
-      ps[2] = g.jacobi ? 1.0 / (1.0 + sqrt(V[5])) : 1.0;
-    }
-    const double p0 = ps[0], p1 = ps[1], p2 = ps[2];
-    double* Vo = b.V + 9 * (long)j;
-    Vo[0] = V[0] * p0 * p0; Vo[1] = V[1] * p0 * p1; Vo[2] = V[2] * p0 * p2;
-    Vo[3] = Vo[1];          Vo[4] = V[3] * p1 * p1; Vo[5] = V[4] * p1 * p2;
-    Vo[6] = Vo[2];          Vo[7] = Vo[5];          Vo[8] = V[5] * p2 * p2;
-    b.gps[3 * (long)j + 0] = gr[0] * p0;
-    b.gps[3 * (long)j + 1] = gr[1] * p1;
-    b.gps[3 * (long)j + 2] = gr[2] * p2;
-    const double* x = b.pts[st->cur] + 3 * (long)j;
-    for (int a = 0; a < 3; ++a) {
-      const double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
-      gm = fmax(gm, fabs(x[a] - xp));
-    }
+    const double radius = st->radius;
+    double A[9];
+    for (int i = 0; i < 9; ++i) A[i] = Vs[i];
+    for (int a = 0; a < 3; ++a) A[4 * a] += fmin(fmax(Vs[4 * a], o.min_diag), o.max_diag) / radius;
+    double* L = b.Lp + 9 * (long)j;
+    if (!chol3(A, L)) st->fail = 1;
+    else fwd3(L, gs, b.zp + 3 * (long)j);
   }
-  const double r = block_max(gm, lds);
-  if (threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+  if (need_lin) {
+    const double r = block_max(gm, lds);
+    if (threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+  }
 }
 
 // Linearisation bookkeeping + iteration start: reduce the cost / gradient
@@ -361,7 +439,6 @@ __global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, 
     return;
   }
   st->iterations += 1;
-  st->fail = 0;
 }
 
 // Sharded mode: local partial sums into scal (all-reduced by the host callback)
@@ -383,79 +460,39 @@ __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) 
   }
 }
 
-__device__ __forceinline__ bool chol3(const double* A, double* L) {
-  double d0 = A[0];
-  if (!(d0 > 0)) return false;
-  d0 = sqrt(d0);
-  const double l10 = A[3] / d0, l20 = A[6] / d0;
-  double d1 = A[4] - l10 * l10;
-  if (!(d1 > 0)) return false;
-  d1 = sqrt(d1);
-  const double l21 = (A[7] - l20 * l10) / d1;
-  double d2 = A[8] - l20 * l20 - l21 * l21;
-  if (!(d2 > 0)) return false;
-  d2 = sqrt(d2);
-  L[0] = d0; L[1] = 0; L[2] = 0;
-  L[3] = l10; L[4] = d1; L[5] = 0;
-  L[6] = l20; L[7] = l21; L[8] = d2;
-  return true;
-}
-__device__ __forceinline__ void fwd3(const double* L, const double* b, double* y) {
-  y[0] = b[0] / L[0];
-  y[1] = (b[1] - L[3] * y[0]) / L[4];
-  y[2] = (b[2] - L[6] * y[0] - L[7] * y[1]) / L[8];
-}
-__device__ __forceinline__ void bwd3(const double* L, const double* y, double* x) {
-  x[2] = y[2] / L[8];
-  x[1] = (y[1] - L[7] * x[2]) / L[4];
-  x[0] = (y[0] - L[3] * x[1] - L[6] * x[2]) / L[0];
-}
-
-// One lane per point: V + D/radius -> Cholesky L_p, z_p = L_p^-1 g_p
-__global__ __launch_bounds__(kPtBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
-  State* st = b.st;
-  if (st->done) return;
-  const int j = blockIdx.x * kPtBlock + threadIdx.x;
-  if (j >= g.np) return;
-  const double radius = st->radius;
-  double A[9];
-  const double* V = b.V + 9 * (long)j;
-  for (int i = 0; i < 9; ++i) A[i] = V[i];
-  for (int a = 0; a < 3; ++a) A[4 * a] += fmin(fmax(V[4 * a], o.min_diag), o.max_diag) / radius;
-  double* L = b.Lp + 9 * (long)j;
-  if (!chol3(A, L)) {
-    st->fail = 1;
-    return;
-  }
-  fwd3(L, b.gps + 3 * (long)j, b.zp + 3 * (long)j);
-}
-
-// One lane per observation with a variable camera: Y_o = (Dc W_o Dp) L_p^-T
-// written straight into the dense K-major Y (pre-zeroed).  A point seen twice
-// by one camera (duplicate residual blocks) accumulates with an FP64 atomic.
-__global__ __launch_bounds__(kBlock) void y_obs_kernel(Geo g, Bufs b) {
+// One lane per (point, column of a variable camera): column col = 6 c + a of
+// the point's 3 rows of the dense K-major Y = (Dc W Dp) L_p^-T, with W summed
+// over the point's observations by camera c (duplicate residual blocks add in
+// CSR order, no atomics) and zeros where c does not see the point.  Every
+// entry of Y's live region is rewritten each iteration (no memset; the
+// padding is zeroed once per solve); consecutive lanes store consecutive
+// columns.
+__global__ __launch_bounds__(kBlock) void y_block_kernel(Geo g, Bufs b) {
   const State* st = b.st;
   if (st->done || st->fail) return;
-  const int o = blockIdx.x * kBlock + threadIdx.x;
-  if (o >= g.no) return;
-  const int ci = b.cam_idx[o] - g.nf;
-  if (ci < 0) return;
-  const int j = b.pt_idx[o];
-  const double* W = b.Wo + 18 * (long)b.pos[o];
-  const double* L = b.Lp + 9 * (long)j;
-  const double* cs = b.csc + 6 * ci;
-  const double* ps = b.psc + 3 * (long)j;
-  const bool dup = b.dup[o] != 0;
-  for (int a = 0; a < 6; ++a) {
-    const double w[3] = {W[a * 3 + 0] * cs[a] * ps[0], W[a * 3 + 1] * cs[a] * ps[1], W[a * 3 + 2] * cs[a] * ps[2]};
-    double y[3];
-    fwd3(L, w, y);
-    for (int c = 0; c < 3; ++c) {
-      double* dst = b.Y + (long)(3 * j + c) * g.Rpad + 6 * ci + a;
-      if (dup) atomicAdd(dst, y[c]);
-      else *dst = y[c];
-    }
+  const long gid = (long)blockIdx.x * kBlock + threadIdx.x;
+  if (gid >= (long)g.np * g.n6) return;
+  const int j = (int)(gid / g.n6), col = (int)(gid - (long)j * g.n6);
+  const int ci = col / 6, a = col - 6 * ci;
+  double w[3] = {0.0, 0.0, 0.0};
+  const int beg = b.p_off[j], end = b.p_off[j + 1];
+  for (int q = beg; q < end; ++q) {
+    if (b.p_cam[q] != ci) continue;
+    const double* W = b.Wo + 18 * (long)q + 3 * a;
+    w[0] += W[0];
+    w[1] += W[1];
+    w[2] += W[2];
   }
+  const double* L = b.Lp + 9 * (long)j;
+  const double* ps = b.psc + 3 * (long)j;
+  const double cs = b.csc[col];
+  const double wa[3] = {w[0] * cs * ps[0], w[1] * cs * ps[1], w[2] * cs * ps[2]};
+  double y[3];
+  fwd3(L, wa, y);
+  double* dst = b.Y + (long)(3 * j) * g.Rpad + col;
+  dst[0] = y[0];
+  dst[g.Rpad] = y[1];
+  dst[2 * (long)g.Rpad] = y[2];
 }
 
 // S partial tiles on the FP64 matrix cores: D(16x16) += A(16x4) B(4x16) with
@@ -574,8 +611,8 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b) {
 //  * trailing update A_IK -= L_IJ L_KJ^T on the matrix cores.
 // Then the backward solve L^T y = z in wave 0 with the block inverses.
 // The matrix is padded to N = 16 Ts >= n + 1 with an identity block.
-constexpr int kSolveBlock = 1024;
-constexpr int kLoadBatch = 16;
+constexpr int kSolveBlock = 512;
+constexpr int kLoadBatch = 32;
 #define SOLVE_STAMP(i)                                                                      \
   do {                                                                                      \
     if ((skip & 256) && tid == 0) st->stamps[(i)] += (long long)__builtin_amdgcn_s_memtime(); \
@@ -586,8 +623,8 @@ constexpr int kLoadBatch = 16;
   } while (0)
 
 __host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
-// dynamic LDS: X (Ts x 256) | z/y (N) | column scratch (16) | A (N x ld, when it fits)
-__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 16; }
+// dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
+__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 256; }
 __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
 
 // wave-local ordering of LDS (and, for the global fallback, L1) traffic
@@ -609,48 +646,128 @@ __device__ __forceinline__ double quad_bcast(double x) {
   return __hiloint2double(hi, lo);
 }
 
-// One elimination step of the 16x16 diagonal block held by one wave:
-// lane = 4 i + g holds a[q] = A[i][4g+q] and y[q] = Y[i][4g+q] (Y -> L^-1).
-// The trailing block stays symmetric, so column K of L is read from row K
-// (lane 4K + g) by ds_bpermute issued at the start of the step, in parallel
-// with the pivot chain; no LDS round trip sits on the critical path.
-// 1/sqrt(pivot) by v_rsq_f64 + two Newton steps (the correctly rounded
-// sqrt-then-divide sequence is ~30 dependent FP64 ops).
-template <int K>
-__device__ __forceinline__ void chol16_step(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
-                                            double* Ablk, int ld, double* X) {
-  double ca[4], cy[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    ca[q] = __shfl(a[q], 4 * K + g, 64);
-    cy[q] = __shfl(y[q], 4 * K + g, 64);
-  }
-  double piv = readlane_f64(a[K & 3], 4 * K + (K >> 2));
-  const bool pad = K >= nreal;  // padding / right-hand-side row: never a failure
-  ok = ok && (pad || piv > 0);
-  piv = (pad && !(piv > 0)) ? 1.0 : piv;
-  double r = __builtin_amdgcn_rsq(piv);
-  r = r * fma(-0.5 * piv * r, r, 1.5);
-  r = r * fma(-0.5 * piv * r, r, 1.5);
-  const double inv = r, d = piv * r;
-  const double aik = quad_bcast<(K >> 2)>(a[K & 3]);
-  const double lik = i > K ? aik * inv : (i == K ? d : 0.0);
-  const double la = i > K ? lik : 0.0;
-  if (g == (K >> 2) && i >= K) Ablk[i * ld + K] = lik;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const double xk = cy[q] * inv;
-    if (i == K) X[K * 16 + 4 * g + q] = xk;
-    a[q] = fma(-lik, (4 * g + q > K) ? ca[q] * inv : 0.0, a[q]);
-    y[q] = fma(-la, xk, y[q]);
-  }
+// Diagonal block of the blocked Cholesky, held by one wave: lane = 4 i + g
+// holds a[q] = A[i][4g+q] and y[q] = Y[i][4g+q] (Y -> X = L^-1).  Four
+// rounds of 4 pivots: the 4x4 pivot block is read with v_readlane and
+// factored + inverted redundantly by every lane (uniform values), the four
+// pivot rows travel through LDS once (xch) in parallel with that, and a
+// rank-4 update finishes the round.  1/sqrt by v_rsq_f64 + two Newton steps.
+__device__ __forceinline__ double rsqrt_nr(double p) {
+  double r = __builtin_amdgcn_rsq(p);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  r = r * fma(-0.5 * p * r, r, 1.5);
+  return r;
 }
-template <int K>
-__device__ __forceinline__ void chol16_steps(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
-                                             double* Ablk, int ld, double* X) {
-  if constexpr (K < 16) {
-    chol16_step<K>(a, y, i, g, nreal, ok, Ablk, ld, X);
-    chol16_steps<K + 1>(a, y, i, g, nreal, ok, Ablk, ld, X);
+template <int R>
+__device__ __forceinline__ void chol4_round(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
+                                            double* Ablk, int ld, double* X, double* xch) {
+  double* xb = xch + 128 * (R & 1);
+  if ((i >> 2) == R) {  // pivot rows 4R..4R+3 publish A and Y (their group-g columns)
+    double* d = xb + 8 * (4 * (i - 4 * R) + g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      d[q] = a[q];
+      d[4 + q] = y[q];
+    }
+  }
+  // pivot block P[t][u] = A[4R+t][4R+u] (u <= t): lane 4(4R+t) + R, register u
+  double P[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u <= t; ++u) P[t][u] = readlane_f64(a[u], 4 * (4 * R + t) + R);
+  // uniform 4x4 Cholesky and its inverse M = L44^-1 (lower)
+  double Lq[4][4], rinv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    double piv = P[t][t];
+#pragma unroll
+    for (int u = 0; u < t; ++u) piv = fma(-Lq[t][u], Lq[t][u], piv);
+    const bool pad = 4 * R + t >= nreal;  // padding / right-hand-side row: never a failure
+    ok = ok && (pad || piv > 0);
+    piv = (pad && !(piv > 0)) ? 1.0 : piv;
+    const double r = rsqrt_nr(piv);
+    rinv[t] = r;
+    Lq[t][t] = piv * r;
+#pragma unroll
+    for (int v = t + 1; v < 4; ++v) {
+      double x = P[v][t];
+#pragma unroll
+      for (int u = 0; u < t; ++u) x = fma(-Lq[v][u], Lq[t][u], x);
+      Lq[v][t] = x * r;
+    }
+  }
+  double M[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    M[t][t] = rinv[t];
+#pragma unroll
+    for (int u = t - 1; u >= 0; --u) {
+      double x = 0.0;
+#pragma unroll
+      for (int v = u; v < t; ++v) x = fma(Lq[t][v], M[v][u], x);
+      M[t][u] = -x * rinv[t];
+    }
+  }
+  // own row: A[i][4R+u] from lane 4i + R (quad broadcast)
+  double ar[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) ar[u] = quad_bcast<R>(a[u]);
+  solve_wave_sync();
+  double xa[4][4], xy[4][4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const double* d = xb + 8 * (4 * u + g);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xa[u][q] = d[q];      // A[4R+u][4g+q] = A[4g+q][4R+u]
+      xy[u][q] = d[4 + q];  // Y[4R+u][4g+q]
+    }
+  }
+  // L[i][4R+t], L[4g+q][4R+t], X[4R+t][4g+q]
+  double Lr[4], Lc[4][4], Xg[4][4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u <= t; ++u) s = fma(ar[u], M[t][u], s);
+    Lr[t] = s;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double c = 0.0, x = 0.0;
+#pragma unroll
+      for (int u = 0; u <= t; ++u) {
+        c = fma(xa[u][q], M[t][u], c);
+        x = fma(M[t][u], xy[u][q], x);
+      }
+      Lc[q][t] = c;
+      Xg[t][q] = x;
+    }
+  }
+  if (g == R && i >= 4 * R) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (4 * R + t <= i) Ablk[i * ld + 4 * R + t] = (4 * R + t == i) ? Lq[t][t] : Lr[t];
+  }
+  if ((i >> 2) == R) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (4 * R + t == i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) X[i * 16 + 4 * g + q] = Xg[t][q];
+  }
+  if (i > 4 * R + 3) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double av = a[q], yv = y[q];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        av = fma(-Lr[t], Lc[q][t], av);
+        yv = fma(-Lr[t], Xg[t][q], yv);
+      }
+      a[q] = av;
+      y[q] = yv;
+    }
   }
 }
 
@@ -666,8 +783,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   double* X = smem;
   double* u = X + 256 * (size_t)Ts;
-  double* col = u + N;
-  double* A = kLds ? col + 16 : b.Abuf;
+  double* xch = u + N;  // diagonal-block row exchange (2 x 128)
+  double* A = kLds ? xch + 256 : b.Abuf;
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
@@ -722,7 +839,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         y[q] = (4 * gq + q == i) ? 1.0 : 0.0;
       }
       bool ok = true;
-      chol16_steps<0>(a, y, i, gq, n - j0, ok, Ablk, ld, X + 256 * J);
+      double* XJw = X + 256 * J;
+      chol4_round<0>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4_round<1>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4_round<2>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4_round<3>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
       if (!ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
@@ -950,6 +1071,7 @@ __device__ void decide(Bufs& b, const Opts& o) {
   st->accepted = 0;
   const double model_change = b.scal[R_MODEL];
   const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
+  st->fail = 0;  // consumed: the next iteration starts clean
   if (fail || !(model_change > 0.0)) {
     st->invalid_count += 1;
     if (st->invalid_count >= o.max_invalid) {
@@ -1056,6 +1178,249 @@ __global__ __launch_bounds__(kBlock) void eval_kernel(Geo g, Bufs b, double* res
     for (int k = 0; k < 12; ++k) Jp[12 * (long)o + k] = jp[k];
 }
 
+// ---------------------------------------------------------------- device plan
+// The observation layout is built on the device from the raw inputs, so a
+// problem already resident in HBM (me_ba_problem.mem == ME_DEVICE) never
+// crosses PCIe and no host sort sits on the frame's critical path.
+//   plan_count   per obs: point histogram (atomics), per-(block, camera)
+//                counts (LDS), index validation; per point: box feasibility;
+//                copies the starting parameters into the solver buffers.
+//   plan_scan    one workgroup: CSR offsets by point, per-camera block offsets,
+//                State initialisation.
+//   plan_scatter per obs: point slot (atomic), camera slot = block offset +
+//                stable rank inside the block (original order kept).
+//   plan_segsort per point: its slots sorted by (camera, obs index), exactly
+//                the host stable_sort by camera; pos / p_cam / dup.
+enum { F_BAD = 0, F_INFEASIBLE = 1 };
+struct PlanWork {
+  int* cnt_p;
+  int* fill_p;
+  int* blk_cam;
+  int* flags;
+};
+__device__ __forceinline__ PlanWork plan_work(const Geo& g, int* w) {
+  PlanWork pw;
+  pw.cnt_p = w;
+  pw.fill_p = w + g.np;
+  pw.blk_cam = w + 2 * (long)g.np;
+  pw.flags = pw.blk_cam + (long)g.nblk_obs * g.nc;
+  return pw;
+}
+
+__global__ __launch_bounds__(kBlock) void plan_count_kernel(Geo g, Bufs b, const double* cams_in,
+                                                            const double* pts_in) {
+  extern __shared__ int lcnt[];  // nc
+  const PlanWork w = plan_work(g, b.work);
+  const int t = threadIdx.x, blk = blockIdx.x;
+  const long gid = (long)blk * kBlock + t;
+  for (int c = t; c < g.nc; c += kBlock) lcnt[c] = 0;
+  __syncthreads();
+  if (blk < g.nblk_obs && gid < g.no) {
+    const int ci = b.cam_idx[gid], pi = b.pt_idx[gid];
+    if (ci < 0 || ci >= g.nc || pi < 0 || pi >= g.np) {
+      atomicOr(&w.flags[F_BAD], 1);
+    } else {
+      atomicAdd(&w.cnt_p[pi], 1);
+      atomicAdd(&lcnt[ci], 1);
+    }
+  }
+  if (gid < g.np) {
+    for (int a = 0; a < 3; ++a) {
+      const double x = pts_in[3 * gid + a];
+      if (!(x >= g.lo[a] && x <= g.hi[a])) atomicOr(&w.flags[F_INFEASIBLE], 1);
+    }
+  }
+  if (cams_in != b.cams[0] && gid < 6 * (long)g.nc) b.cams[0][gid] = cams_in[gid];
+  if (pts_in != b.pts[0] && gid < 3 * (long)g.np) b.pts[0][gid] = pts_in[gid];
+  __syncthreads();
+  if (blk < g.nblk_obs)
+    for (int c = t; c < g.nc; c += kBlock) w.blk_cam[(long)blk * g.nc + c] = lcnt[c];
+}
+
+constexpr int kScanBlock = 1024;
+constexpr int kMaxScanCams = 4096;
+__global__ __launch_bounds__(kScanBlock) void plan_scan_kernel(Geo g, Bufs b, Opts o) {
+  __shared__ int wsum[kScanBlock / 64];
+  __shared__ int total;
+  const PlanWork w = plan_work(g, b.work);
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  // exclusive scan of the point counts: contiguous chunk per thread
+  const int chunk = (g.np + kScanBlock - 1) / kScanBlock;
+  const int beg = min(g.np, t * chunk), end = min(g.np, beg + chunk);
+  int s = 0;
+  for (int j = beg; j < end; ++j) s += w.cnt_p[j];
+  int x = s;  // inclusive wave scan
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < kScanBlock / 64; ++k) {
+      const int v = wsum[k];
+      wsum[k] = acc;
+      acc += v;
+    }
+    total = acc;
+  }
+  __syncthreads();
+  int run = wsum[wv] + x - s;
+  for (int j = beg; j < end; ++j) {
+    b.p_off[j] = run;
+    run += w.cnt_p[j];
+  }
+  if (t == 0) b.p_off[g.np] = total;
+  // per-camera offsets of every observation block (variable cameras only):
+  // one wave per camera scans its column of block counts, then the camera
+  // totals are scanned and added
+  __shared__ int ctot[kMaxScanCams];
+  const int bchunk = (g.nblk_obs + 63) / 64;
+  for (int c = wv; c < g.m; c += kScanBlock / 64) {
+    const int k0 = min(g.nblk_obs, lane * bchunk), k1 = min(g.nblk_obs, k0 + bchunk);
+    int cs = 0;
+    for (int k = k0; k < k1; ++k) cs += w.blk_cam[(long)k * g.nc + g.nf + c];
+    int cx = cs;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(cx, off, 64);
+      if (lane >= off) cx += y;
+    }
+    int r = cx - cs;
+    for (int k = k0; k < k1; ++k) {
+      int* e = &w.blk_cam[(long)k * g.nc + g.nf + c];
+      const int v = *e;
+      *e = r;
+      r += v;
+    }
+    if (lane == 63) ctot[c] = cx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int c = 0; c < g.m; ++c) {
+      b.c_off[c] = acc;
+      const int v = ctot[c];
+      ctot[c] = acc;
+      acc += v;
+    }
+    b.c_off[g.m] = acc;
+  }
+  __syncthreads();
+  for (int c = wv; c < g.m; c += kScanBlock / 64) {
+    const int k0 = min(g.nblk_obs, lane * bchunk), k1 = min(g.nblk_obs, k0 + bchunk);
+    for (int k = k0; k < k1; ++k) w.blk_cam[(long)k * g.nc + g.nf + c] += ctot[c];
+  }
+  for (int i = t; i < g.n6; i += kScanBlock) {
+    b.csc[i] = 0.0;
+    b.dc[i] = 0.0;
+  }
+  if (t == 0) {
+    State* st = b.st;
+    st->cur = 0;
+    st->need_lin = 1;
+    st->done = 0;
+    st->termination = 1;
+    st->iterations = st->successful = st->invalid_count = 0;
+    st->fail = st->scaled = st->accepted = 0;
+    st->bad_input = w.flags[F_BAD];
+    st->infeasible = w.flags[F_INFEASIBLE];
+    st->radius = o.initial_radius;
+    st->decrease = 2.0;
+    st->x_cost = st->cand_cost = st->model_change = st->initial_cost = 0.0;
+    st->cam_step2 = st->cam_xn2 = st->cam_gmax = st->last_q = 0.0;
+    for (int k = 0; k < 16; ++k) st->stamps[k] = 0;
+    if (st->bad_input || st->infeasible) {
+      st->done = 1;
+      st->termination = 2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void plan_scatter_kernel(Geo g, Bufs b) {
+  __shared__ int scam[kBlock];
+  const PlanWork w = plan_work(g, b.work);
+  if (w.flags[F_BAD]) return;
+  const int t = threadIdx.x, blk = blockIdx.x;
+  const int o = blk * kBlock + t;
+  const int ci = o < g.no ? b.cam_idx[o] : -1;
+  scam[t] = ci;
+  if (o < g.no) {
+    const int pi = b.pt_idx[o];
+    b.tmp_obs[b.p_off[pi] + atomicAdd(&w.fill_p[pi], 1)] = o;
+  }
+  __syncthreads();
+  if (o < g.no) {
+    int slot = -1;
+    if (ci >= g.nf) {
+      int rank = 0;
+      for (int k = 0; k < t; ++k) rank += scam[k] == ci;
+      slot = w.blk_cam[(long)blk * g.nc + ci] + rank;
+      b.c_obs[slot] = o;
+    }
+    b.cpos[o] = slot;
+  }
+}
+
+// One wave per point: rank of each slot by (camera, observation index) --
+// the order of the host stable_sort by camera -- then p_obs / pos / p_cam /
+// dup.  Segments of <= 64 observations rank with shuffles; longer ones with a
+// loop over the (cached) segment.
+constexpr int kSortBlock = 256;
+__global__ __launch_bounds__(kSortBlock) void plan_segsort_kernel(Geo g, Bufs b) {
+  const PlanWork w = plan_work(g, b.work);
+  if (w.flags[F_BAD]) return;
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * (kSortBlock / 64) + (threadIdx.x >> 6);
+  if (j >= g.np) return;
+  const int beg = b.p_off[j], k = b.p_off[j + 1] - beg;
+  auto key_of = [&](int o) { return ((unsigned long long)(unsigned)b.cam_idx[o] << 32) | (unsigned)o; };
+  if (k <= 64) {
+    const int o = lane < k ? b.tmp_obs[beg + lane] : 0;
+    const unsigned long long key = lane < k ? key_of(o) : ~0ull;
+    int rank = 0, same = 0;
+    for (int l = 0; l < k; ++l) {
+      const unsigned long long kl = __shfl(key, l, 64);
+      rank += kl < key;
+      same += (kl >> 32) == (key >> 32);
+    }
+    if (lane < k) {
+      const int q = beg + rank;
+      b.p_obs[q] = o;
+      b.pos[o] = q;
+      b.p_cam[q] = (int)(key >> 32) - g.nf;
+      b.dup[o] = same > 1 ? 1 : 0;
+    }
+    return;
+  }
+  for (int e = lane; e < k; e += 64) {
+    const int o = b.tmp_obs[beg + e];
+    const unsigned long long key = key_of(o);
+    int rank = 0, same = 0;
+    for (int l = 0; l < k; ++l) {
+      const unsigned long long kl = key_of(b.tmp_obs[beg + l]);
+      rank += kl < key;
+      same += (kl >> 32) == (key >> 32);
+    }
+    const int q = beg + rank;
+    b.p_obs[q] = o;
+    b.pos[o] = q;
+    b.p_cam[q] = (int)(key >> 32) - g.nf;
+    b.dup[o] = same > 1 ? 1 : 0;
+  }
+}
+
+// State | cams[cur] | pts[cur] -> one contiguous read-back (or straight into
+// the caller's device arrays for a device-resident problem)
+__global__ __launch_bounds__(kBlock) void output_kernel(Geo g, Bufs b, double* cams_dst, double* pts_dst) {
+  const int cur = b.st->cur;
+  const long gid = (long)blockIdx.x * kBlock + threadIdx.x;
+  constexpr int kStateWords = (int)(sizeof(State) / 8);
+  if (gid < kStateWords) b.out[gid] = ((const double*)b.st)[gid];
+  if (gid < 6 * (long)g.nc) cams_dst[gid] = b.cams[cur][gid];
+  if (gid < 3 * (long)g.np) pts_dst[gid] = b.pts[cur][gid];
+}
+
 // ---------------------------------------------------------------- host plan
 struct Plan {
   me_ctx* c = nullptr;
@@ -1066,20 +1431,27 @@ struct Plan {
   double* gc_raw = nullptr;
   double* gc_glob = nullptr;
   double* Uraw = nullptr;
-  double* host = nullptr;  // pinned State copy
+  double* cpart = nullptr;  // camera assembly partials (m x ck x 27)
+  double* host = nullptr;  // pinned staging (inputs in, State / results out)
+  bool dev = false;        // problem arrays are device-resident
   size_t solve_lds = 0;
   int use_lds = 0;
   int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
 };
 
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
+int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 
 int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base) {
   ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
+  ME_CHECK(c, p->n_cams <= kMaxScanCams, "BA: at most %d cameras per window", kMaxScanCams);
   ME_CHECK(c, p->feat_var > 0 && p->baseline != 0.0, "BA: wrong calibration parameters (BundleAdjuster.h:147)");
-  for (int i = 0; i < p->n_obs; ++i) {
-    ME_CHECK(c, p->cam_idx[i] >= 0 && p->cam_idx[i] < p->n_cams && p->pt_idx[i] >= 0 && p->pt_idx[i] < p->n_pts,
-             "BA: observation %d indexes outside the window", i);
+  ME_CHECK(c, p->mem == ME_HOST || p->mem == ME_DEVICE, "BA: bad memory kind");
+  if (p->mem == ME_HOST) {  // device-resident input is validated on the device (State::bad_input)
+    for (int i = 0; i < p->n_obs; ++i) {
+      ME_CHECK(c, p->cam_idx[i] >= 0 && p->cam_idx[i] < p->n_cams && p->pt_idx[i] >= 0 && p->pt_idx[i] < p->n_pts,
+               "BA: observation %d indexes outside the window", i);
+    }
   }
   P.c = c;
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
@@ -1100,6 +1472,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
   g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kPtBlock) / kPtBlock);
   g.jacobi = opt->jacobi_scaling ? 1 : 0;
+  g.ck = (int)std::min(64L, std::max(1L, rup(std::max(g.no, 1), (long)std::max(g.m, 1) * kBlock) /
+                                             ((long)std::max(g.m, 1) * kBlock)));
   g.pstride = std::max(g.nblk_obs, g.nblk_pts);
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
@@ -1125,51 +1499,29 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   o.max_diag = opt->max_lm_diagonal;
   o.min_rel_decrease = opt->min_relative_decrease;
   o.max_invalid = opt->max_num_consecutive_invalid_steps;
-  // CSR by point (obs ordered by camera inside each point), CSR by variable camera
-  std::vector<int> p_off(g.np + 1, 0), c_off(g.m + 1, 0);
-  for (int i = 0; i < g.no; ++i) {
-    p_off[p->pt_idx[i] + 1]++;
-    int ci = p->cam_idx[i] - g.nf;
-    if (ci >= 0) c_off[ci + 1]++;
-  }
-  for (int j = 0; j < g.np; ++j) p_off[j + 1] += p_off[j];
-  for (int j = 0; j < g.m; ++j) c_off[j + 1] += c_off[j];
-  std::vector<int> p_obs(std::max(g.no, 1)), c_obs(std::max(g.no, 1));
-  {
-    std::vector<int> fp(p_off.begin(), p_off.end() - 1), fc(c_off.begin(), c_off.end() - 1);
-    for (int i = 0; i < g.no; ++i) {
-      p_obs[fp[p->pt_idx[i]]++] = i;
-      int ci = p->cam_idx[i] - g.nf;
-      if (ci >= 0) c_obs[fc[ci]++] = i;
-    }
-    for (int j = 0; j < g.np; ++j)
-      std::stable_sort(p_obs.begin() + p_off[j], p_obs.begin() + p_off[j + 1],
-                       [&](int a, int bb) { return p->cam_idx[a] < p->cam_idx[bb]; });
-  }
-  // observations sharing (point, camera) with another one accumulate atomically in Y
-  std::vector<uint8_t> dup(std::max(g.no, 1), 0);
-  for (int j = 0; j < g.np; ++j)
-    for (int q = p_off[j] + 1; q < p_off[j + 1]; ++q)
-      if (p->cam_idx[p_obs[q]] == p->cam_idx[p_obs[q - 1]]) dup[p_obs[q]] = dup[p_obs[q - 1]] = 1;
-  // one arena
+  const bool dev = p->mem == ME_DEVICE;
+  // one arena; the five inputs first and contiguous (one H2D for host input)
   const long nb = std::max(g.nblk_obs, g.nblk_pts);
-  struct Item { size_t bytes; void** dst; };
   Bufs& b = P.b;
   std::vector<std::pair<size_t, void**>> items;
   auto add = [&](size_t bytes, void* dst) { items.push_back({rup((long)std::max<size_t>(bytes, 8), 256), (void**)dst}); };
   add(8 * 6 * (size_t)g.nc, &b.cams[0]);
-  add(8 * 6 * (size_t)g.nc, &b.cams[1]);
   add(8 * 3 * (size_t)g.np, &b.pts[0]);
-  add(8 * 3 * (size_t)g.np, &b.pts[1]);
   add(8 * 4 * (size_t)g.no, &b.obs);
   add(4 * (size_t)g.no, &b.cam_idx);
   add(4 * (size_t)g.no, &b.pt_idx);
+  const size_t n_inputs = items.size();
+  add(8 * 6 * (size_t)g.nc, &b.cams[1]);
+  add(8 * 3 * (size_t)g.np, &b.pts[1]);
   add(4 * (size_t)(g.np + 1), &b.p_off);
   add(4 * (size_t)g.no, &b.p_obs);
   add(4 * (size_t)g.no, &b.pos);
   add(4 * (size_t)g.no, &b.p_cam);
   add(4 * (size_t)(g.m + 1), &b.c_off);
   add(4 * (size_t)g.no, &b.c_obs);
+  add(4 * (size_t)g.no, &b.tmp_obs);
+  add(4 * (size_t)g.no, &b.cpos);
+  add(8 * 27 * (size_t)g.no, &b.cvec);
   add(8 * kLinStride * (size_t)g.no, &b.lin);
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);
   add((size_t)g.no, &b.dup);
@@ -1184,7 +1536,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * 3 * (size_t)g.np, &b.gps);
   add(8 * 9 * (size_t)g.np, &b.Lp);
   add(8 * 3 * (size_t)g.np, &b.zp);
-  add(8 * 18 * (size_t)g.no, &b.Yo);
   add(8 * (size_t)g.Kpad * g.Rpad, &b.Y);
   add(8 * 256 * (size_t)g.ksplit * g.npairs, &b.Spart);
   add(8 * (size_t)g.n6 * g.n6 + 8 * (size_t)(2 * g.n6 + 2), &b.S);  // S | b | diagU | fail (contiguous for all-reduce)
@@ -1198,8 +1549,16 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * (size_t)g.n6, &P.gc_raw);
   add(8 * (size_t)g.n6, &P.gc_glob);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
-  size_t total = 0;
-  for (auto& it : items) total += it.first;
+  add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
+  const size_t work_bytes = 4 * (2 * (size_t)g.np + (size_t)g.nblk_obs * g.nc + 4);
+  add(work_bytes, &b.work);
+  const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
+  add(8 * out_doubles, &b.out);
+  size_t total = 0, input_span = 0;
+  for (size_t k = 0; k < items.size(); ++k) {
+    total += items[k].first;
+    if (k < n_inputs) input_span += items[k].first;
+  }
   void* arena;
   ME_TRY(me_scratch(c, SLOT_COUNT + slot_base, total, &arena));
   char* ptr = (char*)arena;
@@ -1209,49 +1568,40 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   b.bvec = b.S + (size_t)g.n6 * g.n6;
   b.diagU = b.bvec + g.n6;
-  // uploads
-  hipStream_t s = c->stream;
-  ME_HIP(c, hipMemcpyAsync(b.cams[0], p->cams, 8 * 6 * (size_t)g.nc, hipMemcpyHostToDevice, s));
-  if (g.np) ME_HIP(c, hipMemcpyAsync(b.pts[0], p->pts, 8 * 3 * (size_t)g.np, hipMemcpyHostToDevice, s));
-  if (g.no) {
-    ME_HIP(c, hipMemcpyAsync((void*)b.obs, p->obs, 8 * 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipMemcpyAsync((void*)b.cam_idx, p->cam_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipMemcpyAsync((void*)b.pt_idx, p->pt_idx, 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipMemcpyAsync((void*)b.p_obs, p_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    std::vector<int> pos(g.no), p_cam(g.no);
-    for (int q = 0; q < g.no; ++q) {
-      pos[p_obs[q]] = q;
-      p_cam[q] = p->cam_idx[p_obs[q]] - g.nf;
-    }
-    ME_HIP(c, hipMemcpyAsync((void*)b.pos, pos.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipMemcpyAsync((void*)b.p_cam, p_cam.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipStreamSynchronize(s));  // host vectors above go out of scope
-    ME_HIP(c, hipMemcpyAsync((void*)b.c_obs, c_obs.data(), 4 * (size_t)g.no, hipMemcpyHostToDevice, s));
-    ME_HIP(c, hipMemcpyAsync((void*)b.dup, dup.data(), (size_t)g.no, hipMemcpyHostToDevice, s));
-  }
-  ME_HIP(c, hipMemcpyAsync((void*)b.p_off, p_off.data(), 4 * (size_t)(g.np + 1), hipMemcpyHostToDevice, s));
-  ME_HIP(c, hipMemcpyAsync((void*)b.c_off, c_off.data(), 4 * (size_t)(g.m + 1), hipMemcpyHostToDevice, s));
-  State st0;
-  std::memset(&st0, 0, sizeof(st0));
-  st0.cur = 0;
-  st0.need_lin = 1;
-  st0.termination = 1;
-  st0.radius = o.initial_radius;
-  st0.decrease = 2.0;
   void* hp;
-  ME_TRY(me_pinned(c, sizeof(State) + 64, &hp));
+  ME_TRY(me_pinned(c, std::max(8 * out_doubles, dev ? (size_t)0 : input_span) + 64, &hp));
   P.host = (double*)hp;
-  std::memcpy(hp, &st0, sizeof(st0));
-  ME_HIP(c, hipMemcpyAsync(b.st, hp, sizeof(State), hipMemcpyHostToDevice, s));
-  ME_HIP(c, hipMemsetAsync(b.csc, 0, 8 * (size_t)std::max(g.n6, 1), s));
-  ME_HIP(c, hipMemsetAsync(P.gc_raw, 0, 8 * (size_t)std::max(g.n6, 1), s));
-  ME_HIP(c, hipMemsetAsync(b.dc, 0, 8 * (size_t)std::max(g.n6, 1), s));
-  // feasibility (Ceres Problem::IsFeasible): host-side, before any launch
-  for (int j = 0; j < g.np; ++j)
-    for (int a = 0; a < 3; ++a) {
-      double x = p->pts[3 * j + a];
-      if (x < g.lo[a] || x > g.hi[a]) return 1;  // infeasible
+  P.dev = dev;
+  hipStream_t s = c->stream;
+  if (!dev) {
+    // pack the inputs at their arena offsets in pinned memory: one H2D copy
+    char* h = (char*)hp;
+    const void* src[5] = {p->cams, p->pts, p->obs, p->cam_idx, p->pt_idx};
+    const size_t len[5] = {8 * 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np, 8 * 4 * (size_t)g.no, 4 * (size_t)g.no,
+                           4 * (size_t)g.no};
+    size_t off = 0;
+    for (int k = 0; k < 5; ++k) {
+      if (len[k]) std::memcpy(h + off, src[k], len[k]);
+      off += items[k].first;
     }
+    ME_HIP(c, hipMemcpyAsync(b.cams[0], hp, input_span, hipMemcpyHostToDevice, s));
+  } else {
+    b.obs = p->obs;
+    b.cam_idx = p->cam_idx;
+    b.pt_idx = p->pt_idx;
+  }
+  ME_HIP(c, hipMemsetAsync(b.work, 0, work_bytes, s));
+  ME_HIP(c, hipMemsetAsync(b.Y, 0, 8 * (size_t)g.Kpad * g.Rpad, s));  // padding rows/columns stay zero
+  const double* cams_in = dev ? p->cams : b.cams[0];
+  const double* pts_in = dev ? p->pts : b.pts[0];
+  const long nthr = std::max({(long)g.nblk_obs * kBlock, (long)g.np, 6L * g.nc, 3L * g.np});
+  hipLaunchKernelGGL(plan_count_kernel, dim3(blocks(nthr, kBlock)), dim3(kBlock), 4 * (size_t)g.nc, s, g, b, cams_in,
+                     pts_in);
+  hipLaunchKernelGGL(plan_scan_kernel, dim3(1), dim3(kScanBlock), 0, s, g, b, o);
+  hipLaunchKernelGGL(plan_scatter_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, b);
+  hipLaunchKernelGGL(plan_segsort_kernel, dim3(blocks(std::max(g.np, 1), kSortBlock / 64)), dim3(kSortBlock), 0, s, g,
+                     b);
+  ME_TRY(me_check_launch(c, "BA plan"));
   // LDS for the camera solve
   P.solve_lds = 8 * (solve_small_doubles(g.Ts) + solve_a_doubles(g.Ts));
   P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
@@ -1263,7 +1613,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
 }
 
 
-int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 
 #define ME_AR(ptr, n)                                                                         \
   do {                                                                                        \
@@ -1280,8 +1629,9 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     hipLaunchKernelGGL(linearize_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
   if (g.m > 0) {
-    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m), dim3(kBlock), 0, s, g, P.b, ar ? 1 : 0, P.colnorm, P.gc_raw,
-                       P.Uraw);
+    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart);
+    hipLaunchKernelGGL(cam_reduce_kernel, dim3(g.m), dim3(64), 0, s, g, P.b, ar ? 1 : 0,
+                       (const double*)P.cpart, P.colnorm, P.gc_raw, P.Uraw);
     if (ar) {
       ME_AR(P.colnorm, g.n6);
       hipLaunchKernelGGL(cam_finish_kernel, dim3(blocks(g.m, 64)), dim3(64), 0, s, g, P.b, (const double*)P.colnorm,
@@ -1292,7 +1642,7 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_POINTS);
-    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b, P.o);
   }
   if (ar) {
     hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
@@ -1309,14 +1659,9 @@ int enqueue_schur(Plan& P) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
-  {
-    me_ktimer t(c, ME_KT_BA_POINTS);
-    hipLaunchKernelGGL(pt_schur_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b, P.o);
-  }
   if (g.m > 0) {
     me_ktimer t(c, ME_KT_BA_SCHUR);
-    ME_HIP(c, hipMemsetAsync(P.b.Y, 0, 8 * (size_t)g.Kpad * g.Rpad, s));
-    hipLaunchKernelGGL(y_obs_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(y_block_kernel, dim3(blocks((long)g.np * g.n6, kBlock)), dim3(kBlock), 0, s, g, P.b);
     hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, s, g, P.b);
   }
   return me_check_launch(c, "BA schur");
@@ -1373,12 +1718,25 @@ int read_state(Plan& P, State* st) {
 
 int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
   me_ctx* c = P.c;
-  State st;
-  ME_TRY(read_state(P, &st));
-  ME_HIP(c, hipMemcpyAsync(p->cams, P.b.cams[st.cur], 8 * 6 * (size_t)P.g.nc, hipMemcpyDeviceToHost, c->stream));
-  if (P.g.np)
-    ME_HIP(c, hipMemcpyAsync(p->pts, P.b.pts[st.cur], 8 * 3 * (size_t)P.g.np, hipMemcpyDeviceToHost, c->stream));
+  const Geo& g = P.g;
+  constexpr size_t nst = sizeof(State) / 8;
+  static_assert(sizeof(State) % 8 == 0, "State is read back as doubles");
+  double* cams_dst = P.dev ? p->cams : P.b.out + nst;
+  double* pts_dst = P.dev ? p->pts : P.b.out + nst + 6 * (size_t)g.nc;
+  const long n = std::max({(long)nst, 6L * g.nc, 3L * g.np});
+  hipLaunchKernelGGL(output_kernel, dim3(blocks(n, kBlock)), dim3(kBlock), 0, c->stream, g, P.b, cams_dst, pts_dst);
+  ME_TRY(me_check_launch(c, "BA output"));
+  const size_t bytes = 8 * (P.dev ? nst : nst + 6 * (size_t)g.nc + 3 * (size_t)g.np);
+  ME_HIP(c, hipMemcpyAsync(P.host, P.b.out, bytes, hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
+  State st;
+  std::memcpy(&st, P.host, sizeof(State));
+  std::memcpy(P.c->dbg, st.stamps, sizeof(st.stamps));
+  if (!P.dev) {
+    std::memcpy(p->cams, P.host + nst, 8 * 6 * (size_t)g.nc);
+    if (g.np) std::memcpy(p->pts, P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
+  }
+  if (st.bad_input) return me_set_error(c, ME_ERR_INVALID, "BA: an observation indexes outside the window");
   if (sum) {
     sum->termination = st.termination;
     sum->iterations = st.iterations;
@@ -1386,6 +1744,11 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
     sum->initial_cost = st.initial_cost;
     sum->final_cost = st.x_cost;
     sum->status = st.termination == 2 ? 3 : 2;
+    if (st.infeasible) {  // Ceres: infeasible start -> FAILURE, parameters untouched
+      sum->iterations = 0;
+      sum->successful_steps = 0;
+      sum->initial_cost = sum->final_cost = NAN;
+    }
   }
   return ME_OK;
 }
@@ -1395,18 +1758,7 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   Plan P;
-  int rc = plan_build(c, p, opt, P, 0);
-  if (rc < 0) return rc;
-  if (rc == 1) {  // infeasible start -> Ceres FAILURE, parameters untouched
-    if (sum) {
-      sum->status = 3;
-      sum->termination = 2;
-      sum->iterations = 0;
-      sum->successful_steps = 0;
-      sum->initial_cost = sum->final_cost = NAN;
-    }
-    return ME_OK;
-  }
+  ME_TRY(plan_build(c, p, opt, P, 0));
   // enqueue the whole solve; poll the device state every `chunk` iterations
   const int chunk = 4;
   for (int it = 0; it <= opt->max_num_iterations; it += chunk) {
@@ -1451,6 +1803,7 @@ extern "C" int me_ba_cost(me_ctx* c, const me_ba_problem* p, double* cost) {
   me_ba_options o;
   me_ba_default_options(&o);
   Plan P;
+  ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
   std::vector<double> part(P.g.nblk_obs);
@@ -1470,6 +1823,7 @@ extern "C" int me_ba_evaluate(me_ctx* c, const me_ba_problem* p, double* res, do
   me_ba_options o;
   me_ba_default_options(&o);
   Plan P;
+  ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
   const int no = P.g.no;
@@ -1494,6 +1848,7 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
   me_ba_default_options(&o);
   o.initial_trust_region_radius = radius;
   Plan P;
+  ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
   const Geo& g = P.g;

@@ -47,7 +47,9 @@ struct State {
   int fail;           // linear solver failure in this iteration
   int scaled;         // jacobi scaling computed
   int accepted;
-  int pad[6];
+  int bad_input;      // device-resident input: an observation indexes outside the window
+  int infeasible;     // a starting point violates the box bounds (Ceres IsFeasible -> FAILURE)
+  int pad[4];
   double radius, decrease;
   double x_cost, cand_cost, model_change, initial_cost;
   double cam_step2, cam_xn2, cam_gmax;
@@ -59,7 +61,7 @@ struct State {
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi;
+  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi, ck;
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -71,15 +73,18 @@ struct Bufs {
   const double* obs;
   const int* cam_idx;
   const int* pt_idx;
-  const int* p_off;   // CSR by point (obs sorted by cam inside a point)
-  const int* p_obs;
-  const int* pos;     // obs -> CSR slot
-  const int* p_cam;   // CSR slot -> variable camera index (-1 fixed)
-  const int* c_off;   // CSR by variable camera
-  const int* c_obs;
+  int* p_off;         // CSR by point (obs sorted by cam inside a point)
+  int* p_obs;
+  int* pos;           // obs -> CSR slot
+  int* p_cam;         // CSR slot -> variable camera index (-1 fixed)
+  int* c_off;         // CSR by variable camera (original observation order inside a camera)
+  int* c_obs;
+  int* tmp_obs;       // plan: unsorted CSR-by-point slots
+  int* cpos;          // obs -> slot in c_obs (-1: fixed camera)
+  double* cvec;       // 27 x no (component-major by c_obs slot): Jc'Jc (21) + Jc'r (6) per observation
   double* lin;        // no * 40
   double* obsx;       // no * 9  (V_o, g_o unscaled)
-  const uint8_t* dup; // obs shares (point, camera) with another obs
+  uint8_t* dup;       // obs shares (point, camera) with another obs
   double* Abuf;       // n6 * (n6|1) factorisation workspace (when S does not fit LDS)
   double* Wo;         // no * 18 (unscaled Jc^T Jp, row-major 6x3)
   double* csc;        // 6m jacobi scaling (cameras)
@@ -103,6 +108,8 @@ struct Bufs {
   double* part;       // R_COUNT * max(nblk_obs, nblk_pts)
   double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
   State* st;
+  int* work;          // plan build: cnt_p[np] | fill_p[np] | blk_cam[nblk_obs*nc] | flags[4] (zeroed)
+  double* out;        // State | cams[cur] | pts[cur] for the single read-back
 };
 
 }  // namespace ba

@@ -6,9 +6,12 @@
 // applies the reference's ROI rounding rules, builds the lane-private MI
 // histograms of its patch pair(s) in LDS and writes its residual / Jacobian
 // contribution; a single-workgroup kernel then reduces in a fixed order.  The
-// scalar LM control (run_LM_step) stays on the host exactly as in the
-// reference, with one 16-byte read-back per evaluation.
+// scalar LM control (optimise / run_GN_step / run_LM_step) runs on the device
+// as a small state machine (ScaleLM) between the evaluations, so an
+// optimisation needs no host round trip per evaluation: the host enqueues
+// phase-predicated blocks of launches and polls the state every few blocks.
 #include <cmath>
+#include <cstddef>
 #include <cstring>
 #include <vector>
 #include <algorithm>
@@ -32,14 +35,41 @@ struct ScaleArgs {
   int bb_cols, bb_rows;
   int weighting;
   float invN;          // 1/(P*P)
+  int nrows;           // residual rows (rows >= nrows are never written: the prep kernel flags them)
 };
 
 // flags per track: bit0 = triangulated & unmasked (owns a row), bit1 = seen in lframe
 struct TrackDev {
-  const double* X;     // 4 per track, left tracks then right tracks
+  const double* XL;    // 4 per left track
+  const double* XR;    // 4 per right track
   const uint8_t* flags;
   const int* row;      // residual row of the track or -1
 };
+
+// Device-side state of Optimiser::optimise (optimisation.cpp:29-147).
+// Phases of one outer iteration: A residuals at s -> e1; B normal equations
+// -> JJ, e and the GN / first LM step; C residuals at the LM candidate (LM
+// retries loop here); D residuals at the accepted s, stop tests, next k.
+enum { PH_A = 0, PH_B, PH_C, PH_D, PH_DONE };
+enum { NO_STOP = 0, SMALL_GRADIENT, SMALL_INCREMENT, MAX_ITERATIONS, SMALL_DECREASE_FUNCTION, SMALL_REPROJ_ERROR,
+       NO_CONVERGENCE };  // StopCondition (rotation_utils.h:20)
+constexpr int kTraceCap = 512;
+struct ScaleLM {
+  double scale, tmp_scale, mu, v, e1, JJ, e, dX;
+  long nevals;
+  int phase, k, stop, ntrace, err;
+  int pad;
+  double trace[2 * kTraceCap];
+};
+
+__device__ __forceinline__ bool lm_skip(const ScaleLM* lm, int phase) { return lm && lm->phase != phase; }
+__device__ __forceinline__ void lm_scale(ScaleArgs& a, const ScaleLM* lm, int use_tmp) {
+  if (lm) a.scale = use_tmp ? lm->tmp_scale : lm->scale;
+}
+
+__device__ __forceinline__ const double* track_X(const TrackDev& td, const ScaleArgs& a, int t) {
+  return t < a.nL ? td.XL + 4 * (long)t : td.XR + 4 * (long)(t - a.nL);
+}
 
 __device__ __forceinline__ int refl101(int i, int n) {
   if (n == 1) return 0;
@@ -209,20 +239,34 @@ __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int 
 
 // A4: compute_residuals
 __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
-                                                                  int* __restrict__ err) {
+                                                                  int* __restrict__ err, const ScaleLM* lm, int phase,
+                                                                  int use_tmp) {
+  if (lm_skip(lm, phase)) return;
+  lm_scale(a, lm, use_tmp);
   SCALE_GROUP_SETUP();
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
-  if (row < 0 || !(fl & 2)) return;
+  if (row < 0 || row >= a.nrows) return;
+  if (!(fl & 2)) {  // an owned row stays 0 (the reference leaves it untouched)
+    if (h.gl == 0) res[row] = 0.0;
+    return;
+  }
   const bool left = t < a.nL;
   const int w = a.w, P = 2 * w + 1;
   const int bx = w, by = w, bw = a.bb_cols - 2 * w - 1, bh = a.bb_rows - 2 * w - 1;
   Proj p;
-  if (left) project_left(a, td.X + 4 * (long)t, p);
-  else project_right<false, false>(a, td.X + 4 * (long)t, p, nullptr);
-  if (!(rect_contains(bx, by, bw, bh, p.lx, p.ly) && rect_contains(bx, by, bw, bh, p.rx, p.ry))) return;
+  if (left) project_left(a, track_X(td, a, t), p);
+  else project_right<false, false>(a, track_X(td, a, t), p, nullptr);
+  if (!(rect_contains(bx, by, bw, bh, p.lx, p.ly) && rect_contains(bx, by, bw, bh, p.rx, p.ry))) {
+    if (h.gl == 0) res[row] = 0.0;
+    return;
+  }
   int lx = roi_corner(p.lx, w), ly = roi_corner(p.ly, w), rx = roi_corner(p.rx, w), ry = roi_corner(p.ry, w);
-  if (!roi_in(a, lx, ly, P) || !roi_in(a, rx, ry, P)) { atomicOr(err, 1); return; }
+  if (!roi_in(a, lx, ly, P) || !roi_in(a, rx, ry, P)) {
+    if (h.gl == 0) res[row] = 0.0;
+    atomicOr(err, 1);
+    return;
+  }
   double wv = 1.0;
   float mi;
   if (left) {
@@ -238,7 +282,9 @@ __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, T
 // A5: compute_normal_equations — per track J^2*w and J*r_k
 __global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackDev td, const double* __restrict__ res,
                                                              double* __restrict__ jj, double* __restrict__ je,
-                                                             int* __restrict__ err) {
+                                                             int* __restrict__ err, const ScaleLM* lm) {
+  if (lm_skip(lm, PH_B)) return;
+  lm_scale(a, lm, 0);
   SCALE_GROUP_SETUP();
   if (h.gl == 0) {
     jj[t] = 0.0;
@@ -246,11 +292,11 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackD
   }
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
-  if (row < 0 || !(fl & 2)) return;
+  if (row < 0 || row >= a.nrows || !(fl & 2)) return;
   const bool left = t < a.nL;
   const int w = a.w, P = 2 * w;
   const int bx = w, by = w, bw = a.bb_cols - 2 * w - 1, bh = a.bb_rows - 2 * w - 1;
-  const double* X = td.X + 4 * (long)t;
+  const double* X = track_X(td, a, t);
   Proj p;
   double duds;
   if (left) {
@@ -295,7 +341,7 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
   const bool left = t < a.nL;
   const int w = a.w, P = 2 * w;
   const int bx = 2 * w, by = 2 * w, bw = a.bb_cols - 4 * w - 2, bh = a.bb_rows - 4 * w - 2;
-  const double* X = td.X + 4 * (long)t;
+  const double* X = track_X(td, a, t);
   Proj p;
   double duds;
   if (left) {
@@ -330,11 +376,11 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
   if (h.gl == 0) jj[t] = J * J * wv;
 }
 
-// Fixed-order reductions: out[0] = sum(x^2) (mode 0) or sum(x) (mode 1) over
-// n entries; a second array y (if non-null) is summed into out[1].
+// Fixed-order reduction of one workgroup: sum(x^2) (square) or sum(x) over n
+// entries into *ox, and sum(y) into *oy (y may be null).
 constexpr int kRedBlock = 1024;
-__global__ __launch_bounds__(kRedBlock) void reduce_kernel(const double* __restrict__ x, const double* __restrict__ y,
-                                                           int n, int square, double* __restrict__ out) {
+__device__ __forceinline__ void block_reduce2(const double* __restrict__ x, const double* __restrict__ y, int n,
+                                              int square, double* ox, double* oy) {
   __shared__ double sx[kRedBlock], sy[kRedBlock];
   double ax = 0, ay = 0;
   for (int i = threadIdx.x; i < n; i += kRedBlock) {
@@ -352,14 +398,204 @@ __global__ __launch_bounds__(kRedBlock) void reduce_kernel(const double* __restr
     }
     __syncthreads();
   }
+  *ox = sx[0];
+  *oy = sy[0];
+}
+
+__global__ __launch_bounds__(kRedBlock) void reduce_kernel(const double* __restrict__ x, const double* __restrict__ y,
+                                                           int n, int square, double* __restrict__ out) {
+  double ox, oy;
+  block_reduce2(x, y, n, square, &ox, &oy);
   if (threadIdx.x == 0) {
-    out[0] = sx[0];
-    out[1] = sy[0];
+    out[0] = ox;
+    out[1] = oy;
+  }
+}
+
+struct LMParams {
+  int type, minim, max_nb_iter, test;
+  double abs_tol, grad_tol, incr_tol, rel_tol, alpha;
+  int rows, n;
+};
+
+__device__ __forceinline__ double ldlt1(double JJ, double e) { return fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
+
+// LM (or GN) step from the current JJ, e, mu (run_LM_step head,
+// optimisation.cpp:688-698): the candidate is evaluated in phase C.
+__device__ void lm_propose(ScaleLM* lm, const LMParams& p) {
+  lm->JJ += lm->mu;
+  lm->dX = ldlt1(lm->JJ, lm->e);
+  if (sqrt(lm->dX * lm->dX) <= p.incr_tol) {
+    lm->stop = SMALL_INCREMENT;
+    lm->phase = PH_D;
+  } else {
+    lm->tmp_scale = lm->scale + p.alpha * lm->dX;
+    lm->phase = PH_C;
+  }
+}
+
+// One workgroup: reduce the evaluation of `phase`, then thread 0 runs the
+// reference's scalar control for that phase (optimisation.cpp:29-147,
+// run_GN_step :674-683, run_LM_step :685-730).
+__global__ __launch_bounds__(kRedBlock) void scale_ctrl_kernel(ScaleLM* lm, LMParams p, int phase,
+                                                               const double* __restrict__ x,
+                                                               const double* __restrict__ y, const int* err) {
+  if (lm->phase != phase) return;
+  double sx = 0, sy = 0;
+  if (phase == PH_B) {
+    if (!p.test) block_reduce2(x, y, p.n, 0, &sx, &sy);
+  } else {
+    block_reduce2(x, nullptr, p.rows, 1, &sx, &sy);
+  }
+  if (threadIdx.x != 0) return;
+  if (*err) {  // ROI outside the image (the reference throws cv::Exception) / bad mask
+    lm->err = *err;
+    lm->phase = PH_DONE;
+    return;
+  }
+  switch (phase) {
+    case PH_A: {
+      lm->e1 = sx;
+      lm->nevals += p.n;
+      const double mre = sx / (double)(p.rows * 1);
+      if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
+      lm->phase = PH_B;
+      break;
+    }
+    case PH_B: {
+      double JJ = 75, e = 1;  // test mode (optimisation.cpp:60-63)
+      if (!p.test) {
+        JJ = sx;
+        e = sy;
+        lm->nevals += 2 * (long)p.n;
+      }
+      if (lm->k == 0) lm->mu = JJ;
+      if (sqrt(e * e) < p.grad_tol) lm->stop = SMALL_GRADIENT;
+      lm->JJ = JJ;
+      lm->e = e;
+      if (p.type == 0) {  // run_GN_step
+        lm->JJ += lm->mu;
+        lm->dX = ldlt1(lm->JJ, e);
+        lm->scale += p.alpha * lm->dX;
+        lm->phase = PH_D;
+      } else {
+        lm_propose(lm, p);
+      }
+      break;
+    }
+    case PH_C: {
+      const double e1 = lm->e1, e2 = sx;
+      lm->nevals += p.n;
+      const double rho = (p.minim ? -1.0 : 1.0) * (e2 - e1);
+      if (rho > 0) {
+        lm->mu *= fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
+        lm->v = 2;
+        const double dd = sqrt(e1) - sqrt(e2);
+        if (dd * dd < p.rel_tol * sqrt(e1)) lm->stop = SMALL_DECREASE_FUNCTION;
+        lm->scale = lm->tmp_scale;
+        lm->phase = PH_D;
+      } else {
+        lm->mu *= lm->v;
+        const double v2 = 2 * lm->v;
+        if (v2 <= lm->v) {
+          lm->stop = NO_CONVERGENCE;
+          lm->phase = PH_D;
+        } else {
+          lm->v = v2;
+          lm_propose(lm, p);
+        }
+      }
+      break;
+    }
+    case PH_D: {
+      // (the SMALL_INCREMENT test precedes this evaluation in the reference;
+      // it only reads dX, so it is applied here with the same result)
+      if (!lm->stop && sqrt(lm->dX * lm->dX) <= p.incr_tol) lm->stop = SMALL_INCREMENT;
+      const double e2 = sx;
+      lm->nevals += p.n;
+      if (p.type == 0 && (e2 - lm->e1) * (e2 - lm->e1) < p.rel_tol) lm->stop = SMALL_DECREASE_FUNCTION;
+      if (lm->ntrace < kTraceCap) {
+        lm->trace[2 * lm->ntrace] = lm->e1;
+        lm->trace[2 * lm->ntrace + 1] = lm->scale;
+      }
+      lm->ntrace++;
+      // while (!stop && k++ < max_nb_iter)
+      bool more = false;
+      if (!lm->stop) {
+        more = lm->k < p.max_nb_iter;
+        lm->k++;
+      }
+      if (more) {
+        lm->phase = PH_A;
+      } else {
+        if (lm->k == p.max_nb_iter) lm->stop = MAX_ITERATIONS;
+        lm->phase = PH_DONE;
+      }
+      break;
+    }
+  }
+}
+
+// Track flags / residual rows (optimisation.cpp:157-194) from the raw track
+// arrays: bit0 = owns a residual row (triangulated and unmasked; the right
+// loop tests mask(pts.second.size()+i), SURVEY A-6), bit1 = seen in the last
+// keyframe, bit2 = unmasked under compute_jacobian's indexing
+// (mask(pts.first.size()+i)), bit3 = triangulated.  Rows are the running
+// count of bit0 in track order (one workgroup scan).
+struct PrepArgs {
+  const uint8_t* tri_l;
+  const uint8_t* tri_r;
+  const uint32_t* last_l;
+  const uint32_t* last_r;
+  const uint8_t* mask;  // device copy or null
+  int mask_len, nL, nR, tot;
+  uint32_t lframe;
+};
+constexpr int kPrepBlock = 1024;
+__global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uint8_t* flags, int* row, int* err) {
+  __shared__ int wsum[kPrepBlock / 64];
+  const int n = pa.nL + pa.nR, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  auto mask_at = [&](int idx) { return !pa.mask || (idx < pa.mask_len && pa.mask[idx]); };
+  const int chunk = (n + kPrepBlock - 1) / kPrepBlock;
+  const int beg = min(n, t * chunk), end = min(n, beg + chunk);
+  int cnt = 0;
+  for (int i = beg; i < end; ++i) {
+    const bool left = i < pa.nL;
+    const int r = left ? i : i - pa.nL;
+    const bool tri = (left ? pa.tri_l[r] : pa.tri_r[r]) != 0;
+    const uint32_t last = left ? pa.last_l[r] : pa.last_r[r];
+    uint8_t f = 0;
+    if (last == pa.lframe) f |= 2;
+    if (mask_at(i)) f |= 4;
+    if (tri) f |= 8;
+    if (tri && mask_at(left ? i : pa.nR + r)) f |= 1;
+    flags[i] = f;
+    cnt += f & 1;
+  }
+  int x = cnt;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int yv = __shfl_up(x, off, 64);
+    if (lane >= off) x += yv;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < wv; ++k) base += wsum[k];
+  int r = base + x - cnt;
+  for (int i = beg; i < end; ++i) {
+    if (flags[i] & 1) {
+      row[i] = r;
+      // rows beyond tot_nb_elements would write outside the reference's Eigen vector (UB there)
+      if (r >= pa.tot && (flags[i] & 2)) atomicOr(err, 2);
+      ++r;
+    } else {
+      row[i] = -1;
+    }
   }
 }
 
 // ---------------------------------------------------------------------
-// Host side: problem upload + the reference's scalar LM control.
+// Host side: problem upload + the enqueue / poll loop.
 struct ScaleProblem {
   me_ctx* c;
   ScaleArgs a;
@@ -372,17 +608,17 @@ struct ScaleProblem {
   double* je;
   double* red;  // 4 doubles
   int* err;
-  double* host; // pinned
+  ScaleLM* lm;
+  char* host;   // pinned: input staging | LM state
+  ScaleLM* hlm;
 };
-
-enum { NO_STOP = 0, SMALL_GRADIENT, SMALL_INCREMENT, MAX_ITERATIONS, SMALL_DECREASE_FUNCTION, SMALL_REPROJ_ERROR,
-       NO_CONVERGENCE };
 
 int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   ME_CHECK(c, s->n_left >= 0 && s->n_right >= 0, "scale: negative track count");
   ME_CHECK(c, s->window_size > 0 && s->cols > 0 && s->rows > 0 && s->stride >= s->cols, "scale: bad image / window");
   ME_CHECK(c, (2 * s->window_size + 1) * (2 * s->window_size + 1) <= 255,
            "scale: window_size %d gives patches above the 255-px lane histogram", s->window_size);
+  ME_CHECK(c, s->tracks_mem == ME_HOST || s->tracks_mem == ME_DEVICE, "scale: bad tracks_mem");
   P.c = c;
   const int n = s->n_left + s->n_right;
   P.n = n;
@@ -405,64 +641,83 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   a.bb_rows = s->bb_rows;
   a.weighting = weighting;
   a.invN = 1.0f;
-  // rows: triangulated & unmasked tracks in order (optimisation.cpp:157-194); the
-  // right loop tests mask(pts.second.size()+i) (A-6), compute_jacobian mask(pts.first.size()+i)
   const bool has_mask = s->mask && s->mask_len > 0;
-  auto mask_at = [&](int idx) { return !has_mask || (idx < s->mask_len && s->mask[idx]); };
   int tot = 0;
   if (has_mask) {
     for (int i = 0; i < s->mask_len; ++i) tot += s->mask[i] ? 1 : 0;
   } else {
     tot = n;
   }
-  std::vector<int> row(n > 0 ? n : 1, -1);
-  std::vector<uint8_t> flags(n > 0 ? n : 1, 0);
-  int k = 0;
-  for (int i = 0; i < s->n_left; ++i) {
-    uint8_t f = 0;
-    bool tri = s->tri_left[i] != 0;
-    if (s->last_left[i] == s->lframe) f |= 2;
-    if (mask_at(i)) f |= 4;
-    if (tri) f |= 8;
-    if (mask_at(i) && tri) {
-      f |= 1;
-      row[i] = k++;
-    }
-    flags[i] = f;
-  }
-  for (int i = 0; i < s->n_right; ++i) {
-    uint8_t f = 0;
-    bool tri = s->tri_right[i] != 0;
-    if (s->last_right[i] == s->lframe) f |= 2;
-    if (mask_at(s->n_left + i)) f |= 4;
-    if (tri) f |= 8;
-    if (mask_at(s->n_right + i) && tri) {
-      f |= 1;
-      row[s->n_left + i] = k++;
-    }
-    flags[s->n_left + i] = f;
-  }
-  // rows beyond tot_nb_elements would write outside the reference's Eigen vector (UB there)
-  for (int i = 0; i < n; ++i)
-    if (row[i] >= tot && (flags[i] & 2))
-      return me_set_error(c, ME_ERR_INVALID, "scale: mask selects fewer rows (%d) than triangulated tracks", tot);
   P.rows = tot;
-  // device buffers: [X (4n doubles)][row (n ints)][flags (n bytes)]
-  size_t bx = 32 * (size_t)n, brow = 4 * (size_t)n, bfl = (size_t)n;
+  a.nrows = tot;
+  const size_t nn = (size_t)(n > 0 ? n : 1), nr = (size_t)(tot > 0 ? tot : 1);
+  // device layout: [XL 4nL | XR 4nR][tri nL | tri nR][last nL | last nR][mask][flags n][row n]
+  //                [res rows][res2 rows][jj n][je n][red 8][err][ScaleLM]
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const bool dev = s->tracks_mem == ME_DEVICE;
+  const size_t bX = 32 * nn, bTri = nn, bLast = 4 * nn, bMask = has_mask ? (size_t)s->mask_len : 1;
+  const size_t oX = 0, oTri = oX + up(bX), oLast = oTri + up(bTri), oMask = oLast + up(bLast);
+  const size_t in_span = oMask + up(bMask);
+  const size_t oFl = in_span, oRow = oFl + up(nn), oRes = oRow + up(4 * nn), oRes2 = oRes + up(8 * nr);
+  const size_t oJJ = oRes2 + up(8 * nr), oJE = oJJ + up(8 * nn), oRed = oJE + up(8 * nn), oErr = oRed + 256;
+  const size_t oLM = oErr + 256, total = oLM + up(sizeof(ScaleLM));
   void* d;
-  ME_TRY(me_scratch(c, SLOT_SC_TRACKS, bx + brow + bfl + 64, &d));
+  ME_TRY(me_scratch(c, SLOT_SC_TRACKS, total, &d));
   char* base = (char*)d;
-  std::vector<double> X(4 * (size_t)(n > 0 ? n : 1));
-  if (s->n_left) std::memcpy(X.data(), s->X_left, 32 * (size_t)s->n_left);
-  if (s->n_right) std::memcpy(X.data() + 4 * (size_t)s->n_left, s->X_right, 32 * (size_t)s->n_right);
-  if (n) {
-    ME_HIP(c, hipMemcpyAsync(base, X.data(), bx, hipMemcpyHostToDevice, c->stream));
-    ME_HIP(c, hipMemcpyAsync(base + bx, row.data(), brow, hipMemcpyHostToDevice, c->stream));
-    ME_HIP(c, hipMemcpyAsync(base + bx + brow, flags.data(), bfl, hipMemcpyHostToDevice, c->stream));
+  void* ph;
+  ME_TRY(me_pinned(c, up(in_span) + up(sizeof(ScaleLM)) + 256, &ph));
+  P.host = (char*)ph;
+  P.hlm = (ScaleLM*)(P.host + up(in_span));  // separate from the input staging (async H2D)
+  PrepArgs pa;
+  pa.mask = has_mask ? (const uint8_t*)(base + oMask) : nullptr;
+  pa.mask_len = has_mask ? s->mask_len : 0;
+  pa.nL = s->n_left;
+  pa.nR = s->n_right;
+  pa.tot = tot;
+  pa.lframe = s->lframe;
+  if (!dev) {  // pack every host array at its device offset: one H2D copy
+    char* h = P.host;
+    if (s->n_left) std::memcpy(h + oX, s->X_left, 32 * (size_t)s->n_left);
+    if (s->n_right) std::memcpy(h + oX + 32 * (size_t)s->n_left, s->X_right, 32 * (size_t)s->n_right);
+    if (s->n_left) std::memcpy(h + oTri, s->tri_left, s->n_left);
+    if (s->n_right) std::memcpy(h + oTri + s->n_left, s->tri_right, s->n_right);
+    if (s->n_left) std::memcpy(h + oLast, s->last_left, 4 * (size_t)s->n_left);
+    if (s->n_right) std::memcpy(h + oLast + 4 * (size_t)s->n_left, s->last_right, 4 * (size_t)s->n_right);
+    if (has_mask) std::memcpy(h + oMask, s->mask, s->mask_len);
+    ME_HIP(c, hipMemcpyAsync(base, h, in_span, hipMemcpyHostToDevice, c->stream));
+    P.td.XL = (const double*)(base + oX);
+    P.td.XR = P.td.XL + 4 * (size_t)s->n_left;
+    pa.tri_l = (const uint8_t*)(base + oTri);
+    pa.tri_r = pa.tri_l + s->n_left;
+    pa.last_l = (const uint32_t*)(base + oLast);
+    pa.last_r = pa.last_l + s->n_left;
+  } else {
+    if (has_mask) {
+      std::memcpy(P.host, s->mask, s->mask_len);
+      ME_HIP(c, hipMemcpyAsync(base + oMask, P.host, s->mask_len, hipMemcpyHostToDevice, c->stream));
+    }
+    P.td.XL = s->X_left;
+    P.td.XR = s->X_right;
+    pa.tri_l = s->tri_left;
+    pa.tri_r = s->tri_right;
+    pa.last_l = s->last_left;
+    pa.last_r = s->last_right;
   }
-  P.td.X = (const double*)base;
-  P.td.row = (const int*)(base + bx);
-  P.td.flags = (const uint8_t*)(base + bx + brow);
+  P.td.flags = (const uint8_t*)(base + oFl);
+  P.td.row = (const int*)(base + oRow);
+  P.res = (double*)(base + oRes);
+  P.res2 = (double*)(base + oRes2);
+  P.jj = (double*)(base + oJJ);
+  P.je = (double*)(base + oJE);
+  P.red = (double*)(base + oRed);
+  P.err = (int*)(base + oErr);
+  P.lm = (ScaleLM*)(base + oLM);
+  // zero: residual rows never owned by a track stay 0; error flag
+  ME_HIP(c, hipMemsetAsync(base + oRes, 0, oRes2 - oRes + up(8 * nr), c->stream));
+  ME_HIP(c, hipMemsetAsync(base + oErr, 0, 4, c->stream));
+  hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
+                     (int*)(base + oRow), P.err);
+  ME_TRY(me_check_launch(c, "scale_prep_kernel"));
   if (s->img_mem == ME_DEVICE) {
     a.imgL = s->imgL;
     a.imgR = s->imgR;
@@ -476,82 +731,43 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
     a.imgL = (const uint8_t*)dl;
     a.imgR = (const uint8_t*)dr;
   }
-  void *dres, *dres2, *dneq;
-  size_t nr = (size_t)(tot > 0 ? tot : 1);
-  ME_TRY(me_scratch(c, SLOT_SC_RES, 8 * nr, &dres));
-  ME_TRY(me_scratch(c, SLOT_SC_RES2, 8 * nr, &dres2));
-  ME_TRY(me_scratch(c, SLOT_SC_NEQ, 16 * (size_t)(n > 0 ? n : 1) + 64 + 16, &dneq));
-  P.res = (double*)dres;
-  P.res2 = (double*)dres2;
-  P.jj = (double*)dneq;
-  P.je = P.jj + (n > 0 ? n : 1);
-  P.red = P.je + (n > 0 ? n : 1);
-  P.err = (int*)(P.red + 8);
-  void* ph;
-  ME_TRY(me_pinned(c, 256, &ph));
-  P.host = (double*)ph;
-  ME_HIP(c, hipMemsetAsync(P.err, 0, 4, c->stream));
   return ME_OK;
 }
 
 int blocks_for(int n) { return n > 0 ? (n + kTracksPerBlock - 1) / kTracksPerBlock : 1; }
 
-int check_err(ScaleProblem& P) {
-  // err flag is read back with the scalars
-  int e = 0;
-  std::memcpy(&e, (char*)P.host + 32, 4);
-  if (e) return me_set_error(P.c, ME_ERR_INVALID, "scale: ROI outside the image (reference: cv::Exception)");
+int check_err(me_ctx* c, int e) {
+  if (e & 2) return me_set_error(c, ME_ERR_INVALID, "scale: mask selects fewer rows than triangulated tracks");
+  if (e & 1) return me_set_error(c, ME_ERR_INVALID, "scale: ROI outside the image (reference: cv::Exception)");
   return ME_OK;
 }
 
-// residuals at `scale` into dst; returns e = sum r^2 (host)
-int eval_residuals(ScaleProblem& P, double scale, double* dst, double* e_out) {
+ScaleArgs with_invN(ScaleArgs a, int P) {
+  a.invN = (float)(1.0 / (double)(P * P));
+  return a;
+}
+
+// one evaluation (no LM state): residual rows at a.scale, reduce, read back
+int eval_once_residuals(ScaleProblem& P, double* e_out) {
   me_ctx* c = P.c;
-  ScaleArgs a = P.a;
-  a.scale = scale;
-  a.invN = (float)(1.0 / (double)((2 * a.w + 1) * (2 * a.w + 1)));
-  ME_HIP(c, hipMemsetAsync(dst, 0, 8 * (size_t)(P.rows > 0 ? P.rows : 1), c->stream));
+  ScaleArgs a = with_invN(P.a, 2 * P.a.w + 1);
   if (P.n > 0) {
     me_ktimer t(c, ME_KT_SCALE_RES);
-    hipLaunchKernelGGL(scale_residual_kernel, dim3(blocks_for(P.n)), dim3(kScBlock), 0, c->stream, a, P.td, dst,
-                       P.err);
+    hipLaunchKernelGGL(scale_residual_kernel, dim3(blocks_for(P.n)), dim3(kScBlock), 0, c->stream, a, P.td, P.res,
+                       P.err, (const ScaleLM*)nullptr, 0, 0);
   }
-  ME_TRY(me_check_launch(c, "scale_residual_kernel"));
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedBlock), 0, c->stream, (const double*)dst,
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedBlock), 0, c->stream, (const double*)P.res,
                      (const double*)nullptr, P.rows, 1, P.red);
-  ME_TRY(me_check_launch(c, "reduce_kernel"));
+  ME_TRY(me_check_launch(c, "scale residuals"));
   ME_HIP(c, hipMemcpyAsync(P.host, P.red, 16, hipMemcpyDeviceToHost, c->stream));
-  ME_HIP(c, hipMemcpyAsync((char*)P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
-  ME_TRY(check_err(P));
-  *e_out = P.host[0];
+  int e;
+  std::memcpy(&e, P.host + 32, 4);
+  ME_TRY(check_err(c, e));
+  if (e_out) std::memcpy(e_out, P.host, 8);
   return ME_OK;
 }
-
-int eval_neq(ScaleProblem& P, double scale, const double* dres, double* JJ, double* e) {
-  me_ctx* c = P.c;
-  ScaleArgs a = P.a;
-  a.scale = scale;
-  a.invN = (float)(1.0 / (double)(4 * a.w * a.w));
-  if (P.n > 0) {
-    me_ktimer t(c, ME_KT_SCALE_NEQ);
-    hipLaunchKernelGGL(scale_neq_kernel, dim3(blocks_for(P.n)), dim3(kScBlock), 0, c->stream, a, P.td, dres, P.jj,
-                       P.je, P.err);
-  }
-  ME_TRY(me_check_launch(c, "scale_neq_kernel"));
-  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedBlock), 0, c->stream, (const double*)P.jj,
-                     (const double*)P.je, P.n, 0, P.red);
-  ME_TRY(me_check_launch(c, "reduce_kernel"));
-  ME_HIP(c, hipMemcpyAsync(P.host, P.red, 16, hipMemcpyDeviceToHost, c->stream));
-  ME_HIP(c, hipMemcpyAsync((char*)P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
-  ME_HIP(c, hipStreamSynchronize(c->stream));
-  ME_TRY(check_err(P));
-  *JJ = P.host[0];
-  *e = P.host[1];
-  return ME_OK;
-}
-
-double ldlt1(double JJ, double e) { return std::fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
 
 }  // namespace
 
@@ -575,8 +791,7 @@ extern "C" int me_scale_residuals(me_ctx* c, const me_scale_state* s, int weight
   ME_HIP(c, hipSetDevice(c->device));
   ScaleProblem P;
   ME_TRY(upload(c, s, weighting, P));
-  double e;
-  ME_TRY(eval_residuals(P, s->scale, P.res, &e));
+  ME_TRY(eval_once_residuals(P, nullptr));
   if (P.rows > 0) {
     ME_HIP(c, hipMemcpyAsync(res, P.res, 8 * (size_t)P.rows, hipMemcpyDeviceToHost, c->stream));
     ME_HIP(c, hipStreamSynchronize(c->stream));
@@ -592,7 +807,24 @@ extern "C" int me_scale_normal_equations(me_ctx* c, const me_scale_state* s, int
   ScaleProblem P;
   ME_TRY(upload(c, s, weighting, P));
   if (P.rows > 0) ME_HIP(c, hipMemcpyAsync(P.res, res, 8 * (size_t)P.rows, hipMemcpyHostToDevice, c->stream));
-  return eval_neq(P, s->scale, P.res, JJ, e);
+  ScaleArgs a = with_invN(P.a, 2 * P.a.w);
+  if (P.n > 0) {
+    me_ktimer t(c, ME_KT_SCALE_NEQ);
+    hipLaunchKernelGGL(scale_neq_kernel, dim3(blocks_for(P.n)), dim3(kScBlock), 0, c->stream, a, P.td,
+                       (const double*)P.res, P.jj, P.je, P.err, (const ScaleLM*)nullptr);
+  }
+  hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedBlock), 0, c->stream, (const double*)P.jj,
+                     (const double*)P.je, P.n, 0, P.red);
+  ME_TRY(me_check_launch(c, "scale normal equations"));
+  ME_HIP(c, hipMemcpyAsync(P.host, P.red, 16, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  int err;
+  std::memcpy(&err, P.host + 32, 4);
+  ME_TRY(check_err(c, err));
+  std::memcpy(JJ, P.host, 8);
+  std::memcpy(e, P.host + 8, 8);
+  return ME_OK;
 }
 
 extern "C" int me_scale_jacobian(me_ctx* c, const me_scale_state* s, int weighting, double* JJ) {
@@ -600,22 +832,26 @@ extern "C" int me_scale_jacobian(me_ctx* c, const me_scale_state* s, int weighti
   ME_HIP(c, hipSetDevice(c->device));
   ScaleProblem P;
   ME_TRY(upload(c, s, weighting, P));
-  ScaleArgs a = P.a;
-  a.invN = (float)(1.0 / (double)(4 * a.w * a.w));
+  ScaleArgs a = with_invN(P.a, 2 * P.a.w);
   if (P.n > 0)
     hipLaunchKernelGGL(scale_jac_kernel, dim3(blocks_for(P.n)), dim3(kScBlock), 0, c->stream, a, P.td, P.jj, P.err);
-  ME_TRY(me_check_launch(c, "scale_jac_kernel"));
   hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(kRedBlock), 0, c->stream, (const double*)P.jj,
                      (const double*)nullptr, P.n, 0, P.red);
+  ME_TRY(me_check_launch(c, "scale_jac_kernel"));
   ME_HIP(c, hipMemcpyAsync(P.host, P.red, 16, hipMemcpyDeviceToHost, c->stream));
-  ME_HIP(c, hipMemcpyAsync((char*)P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
-  ME_TRY(check_err(P));
-  *JJ = P.host[0];
+  int err;
+  std::memcpy(&err, P.host + 32, 4);
+  ME_TRY(check_err(c, err));
+  std::memcpy(JJ, P.host, 8);
   return ME_OK;
 }
 
-// optimisation.cpp:29-147 with run_GN_step (:674-683) / run_LM_step (:685-730)
+// optimisation.cpp:29-147 with run_GN_step (:674-683) / run_LM_step (:685-730).
+// The control runs on the device (scale_ctrl_kernel); the host enqueues
+// blocks of phase-predicated launches [A, B, C, C, D] and polls the state
+// every kBlocksPerPoll blocks (a block whose phase does not match is a no-op).
 extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_params* pin, int test, int* stop_out,
                                  int* iterations, double* trace, int trace_cap, long* mi_evals) {
   if (!c || !s || !pin) return ME_ERR_INVALID;
@@ -631,80 +867,70 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   }
   ScaleProblem P;
   ME_TRY(upload(c, s, p.weighting, P));
-  long nevals = 0;
-  // MI evaluations per residual pass / neq pass are counted on the host from
-  // the in-view masks the kernels produce; here we count launches * tracks.
-  int stop = NO_STOP;
-  double scale = s->scale;
-  int k = 0, ntrace = 0;
-  do {
-    double e1;
-    ME_TRY(eval_residuals(P, scale, P.res, &e1));
-    nevals += P.n;
-    double mre = e1 / (double)(P.rows * 1);
-    if (mre < p.abs_tol) stop = SMALL_REPROJ_ERROR;
-    double JJ, e;
-    if (test) {
-      JJ = 75;
-      e = 1;
-    } else {
-      ME_TRY(eval_neq(P, scale, P.res, &JJ, &e));
-      nevals += 2 * (long)P.n;
+  // initial state
+  ScaleLM* h0 = P.hlm;
+  std::memset(h0, 0, offsetof(ScaleLM, trace));
+  h0->scale = s->scale;
+  h0->mu = p.mu;
+  h0->v = p.v;
+  h0->phase = PH_A;
+  h0->stop = NO_STOP;
+  ME_HIP(c, hipMemcpyAsync(P.lm, h0, offsetof(ScaleLM, trace), hipMemcpyHostToDevice, c->stream));
+  LMParams lp;
+  lp.type = p.type;
+  lp.minim = p.minim;
+  lp.max_nb_iter = p.max_nb_iter;
+  lp.test = test;
+  lp.abs_tol = p.abs_tol;
+  lp.grad_tol = p.grad_tol;
+  lp.incr_tol = p.incr_tol;
+  lp.rel_tol = p.rel_tol;
+  lp.alpha = p.alpha;
+  lp.rows = P.rows;
+  lp.n = P.n;
+  const ScaleArgs aR = with_invN(P.a, 2 * P.a.w + 1), aN = with_invN(P.a, 2 * P.a.w);
+  const int nb = blocks_for(P.n);
+  hipStream_t st = c->stream;
+  auto res = [&](int phase, int use_tmp, double* dst) {
+    if (P.n > 0) {
+      me_ktimer t(c, ME_KT_SCALE_RES);
+      hipLaunchKernelGGL(scale_residual_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, dst, P.err,
+                         (const ScaleLM*)P.lm, phase, use_tmp);
     }
-    if (k == 0) p.mu = JJ;
-    if (std::sqrt(e * e) < p.grad_tol) stop = SMALL_GRADIENT;
-    double dX = 0;
-    if (p.type == 0) {
-      JJ += p.mu;
-      dX = ldlt1(JJ, e);
-      scale += p.alpha * dX;
-    } else {
-      for (;;) {
-        JJ += p.mu;
-        dX = ldlt1(JJ, e);
-        if (std::sqrt(dX * dX) <= p.incr_tol) {
-          stop = SMALL_INCREMENT;
-          break;
-        }
-        double tmp_scale = scale + p.alpha * dX;
-        double e2;
-        ME_TRY(eval_residuals(P, tmp_scale, P.res2, &e2));
-        nevals += P.n;
-        double rho = (p.minim ? -1.0 : 1.0) * (e2 - e1);
-        if (rho > 0) {
-          p.mu *= std::max(1.0 / 3.0, 1 - std::pow(2 * rho - 1, 3));
-          p.v = 2;
-          double dd = std::sqrt(e1) - std::sqrt(e2);
-          if (dd * dd < p.rel_tol * std::sqrt(e1)) stop = SMALL_DECREASE_FUNCTION;
-          scale = tmp_scale;
-          break;
-        } else {
-          p.mu *= p.v;
-          double v2 = 2 * p.v;
-          if (v2 <= p.v) {
-            stop = NO_CONVERGENCE;
-            break;
-          }
-          p.v = v2;
-        }
+    hipLaunchKernelGGL(scale_ctrl_kernel, dim3(1), dim3(kRedBlock), 0, st, P.lm, lp, phase, (const double*)dst,
+                       (const double*)nullptr, (const int*)P.err);
+  };
+  constexpr int kBlocksPerPoll = 2;
+  const long max_blocks = 64L * (p.max_nb_iter + 2);
+  ScaleLM& hs = *P.hlm;
+  for (long blk = 0;; blk += kBlocksPerPoll) {
+    for (int b = 0; b < kBlocksPerPoll; ++b) {
+      res(PH_A, 0, P.res);
+      if (P.n > 0 && !test) {
+        me_ktimer t(c, ME_KT_SCALE_NEQ);
+        hipLaunchKernelGGL(scale_neq_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res, P.jj,
+                           P.je, P.err, (const ScaleLM*)P.lm);
       }
+      hipLaunchKernelGGL(scale_ctrl_kernel, dim3(1), dim3(kRedBlock), 0, st, P.lm, lp, (int)PH_B,
+                         (const double*)P.jj, (const double*)P.je, (const int*)P.err);
+      res(PH_C, 1, P.res2);
+      res(PH_C, 1, P.res2);
+      res(PH_D, 0, P.res2);
     }
-    if (!stop && std::sqrt(dX * dX) <= p.incr_tol) stop = SMALL_INCREMENT;
-    double e2;
-    ME_TRY(eval_residuals(P, scale, P.res2, &e2));
-    nevals += P.n;
-    if (p.type == 0 && (e2 - e1) * (e2 - e1) < p.rel_tol) stop = SMALL_DECREASE_FUNCTION;
-    if (trace && ntrace < trace_cap) {
-      trace[2 * ntrace] = e1;
-      trace[2 * ntrace + 1] = scale;
-    }
-    ntrace++;
-  } while (!stop && k++ < p.max_nb_iter);
-  if (k == p.max_nb_iter) stop = MAX_ITERATIONS;
-  s->scale = scale;
-  if (stop_out) *stop_out = stop;
-  if (iterations) *iterations = ntrace;
-  if (mi_evals) *mi_evals = nevals;
+    ME_TRY(me_check_launch(c, "scale optimise"));
+    ME_HIP(c, hipMemcpyAsync(&hs, P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
+    ME_HIP(c, hipStreamSynchronize(st));
+    if (hs.phase == PH_DONE) break;
+    if (blk + kBlocksPerPoll >= max_blocks) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
+  }
+  if (hs.err) return check_err(c, hs.err);
+  const int nt = std::min(std::min(hs.ntrace, kTraceCap), std::max(trace_cap, 0));
+  if (trace && nt > 0)
+    ME_HIP(c, hipMemcpy(trace, P.lm->trace, 16 * (size_t)nt, hipMemcpyDeviceToHost));
+  s->scale = hs.scale;
+  if (stop_out) *stop_out = hs.stop;
+  if (iterations) *iterations = hs.ntrace;
+  if (mi_evals) *mi_evals = hs.nevals;
   return ME_OK;
 }
 

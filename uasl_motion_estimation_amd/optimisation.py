@@ -61,19 +61,26 @@ class OptimisationParams:
         return p
 
 
-def scale_struct(sp, keep: list, img_mem: int = ME_HOST, dev_imgs=None) -> ScaleStateC:
-    """ScaleStateC from a flattened problem (synthetic.ScaleProblem or ScaleState.flatten())."""
+def scale_struct(sp, keep: list, img_mem: int = ME_HOST, dev_imgs=None, dev_tracks: dict | None = None) -> ScaleStateC:
+    """ScaleStateC from a flattened problem (synthetic.ScaleProblem or ScaleState.flatten()).
+    dev_tracks: device pointers {X_left, X_right, tri_left, tri_right, last_left, last_right}
+    for a window already resident in HBM (tracks_mem = ME_DEVICE)."""
     s = ScaleStateC()
     s.n_left, s.n_right = len(sp.X_left), len(sp.X_right)
-    for name in ("X_left", "X_right"):
+    s.tracks_mem = ME_DEVICE if dev_tracks else ME_HOST
+    if dev_tracks:
+        for name, t in (("X_left", c_double), ("X_right", c_double), ("tri_left", c_uint8), ("tri_right", c_uint8),
+                        ("last_left", c_uint32), ("last_right", c_uint32)):
+            setattr(s, name, ctypes.cast(dev_tracks[name], POINTER(t)))
+    for name in (() if dev_tracks else ("X_left", "X_right")):
         a = np.ascontiguousarray(getattr(sp, name), np.float64).reshape(-1)
         keep.append(a)
         setattr(s, name, _p(a))
-    for name in ("tri_left", "tri_right"):
+    for name in (() if dev_tracks else ("tri_left", "tri_right")):
         a = np.ascontiguousarray(getattr(sp, name), np.uint8)
         keep.append(a)
         setattr(s, name, _p(a, c_uint8))
-    for name in ("last_left", "last_right"):
+    for name in (() if dev_tracks else ("last_left", "last_right")):
         a = np.ascontiguousarray(getattr(sp, name), np.uint32)
         keep.append(a)
         setattr(s, name, _p(a, c_uint32))
@@ -136,11 +143,11 @@ def scale_jacobian(sp, weighting=False, ctx: Context | None = None) -> float:
 
 
 def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx: Context | None = None,
-                   img_mem: int = ME_HOST, dev_imgs=None) -> dict:
+                   img_mem: int = ME_HOST, dev_imgs=None, dev_tracks: dict | None = None) -> dict:
     ctx = ctx or default_context()
     params = params or OptimisationParams()
     keep = []
-    s = scale_struct(sp, keep, img_mem, dev_imgs)
+    s = scale_struct(sp, keep, img_mem, dev_imgs, dev_tracks)
     p = params.to_c()
     stop, it, nmi = c_int(), c_int(), c_long()
     trace = np.zeros(2 * 400)
@@ -161,6 +168,25 @@ def scale_inliers(sp, threshold: float, weighting=False, ctx: Context | None = N
     ctx.check(ctx.lib.me_scale_inliers(ctx.h, byref(s), int(weighting), threshold, _p(idx, c_int), cap, byref(n)),
               "me_scale_inliers")
     return idx[:n.value]
+
+
+class DeviceScaleTracks:
+    """The track arrays of a ScaleState window resident in HBM (tracks_mem = ME_DEVICE)."""
+
+    def __init__(self, sp, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        self.d = {}
+        for name, dt in (("X_left", np.float64), ("X_right", np.float64), ("tri_left", np.uint8),
+                         ("tri_right", np.uint8), ("last_left", np.uint32), ("last_right", np.uint32)):
+            a = np.ascontiguousarray(getattr(sp, name), dt)
+            self.d[name] = self.ctx.malloc(max(a.nbytes, 16))
+            if a.nbytes:
+                self.ctx.h2d(self.d[name], a)
+
+    def close(self):
+        for v in self.d.values():
+            self.ctx.free(v)
+        self.d = {}
 
 
 @dataclass
@@ -355,6 +381,64 @@ def ba_solve_sharded(bp_local, allreduce, options: SolverOptions | None = None, 
     keep.append(cb)
     ctx.check(ctx.lib.me_ba_solve_sharded(ctx.h, byref(p), byref(o), cb, None, byref(s)), "me_ba_solve_sharded")
     return cams, pts, _summary(s)
+
+
+class DeviceBAProblem:
+    """A BA window resident in HBM (me_ba_problem.mem == ME_DEVICE): the five
+    input arrays live on the ctx device; solves update cams/pts in place on
+    the device.  `reset()` restores the starting parameters (device copy)."""
+
+    def __init__(self, bp, ctx: Context | None = None):
+        self.ctx = ctx or default_context()
+        self.bp = bp
+        arrays = dict(cams=np.ascontiguousarray(bp.cams, np.float64), pts=np.ascontiguousarray(bp.pts, np.float64),
+                      obs=np.ascontiguousarray(bp.obs, np.float64),
+                      cam_idx=np.ascontiguousarray(bp.cam_idx, np.int32),
+                      pt_idx=np.ascontiguousarray(bp.pt_idx, np.int32))
+        self.nbytes = {k: v.nbytes for k, v in arrays.items()}
+        self.d = {}
+        for k in ("cams", "pts", "obs", "cam_idx", "pt_idx", "cams0", "pts0"):
+            src = arrays[k[:-1]] if k.endswith("0") else arrays[k]
+            self.d[k] = self.ctx.malloc(max(src.nbytes, 16))
+            self.ctx.h2d(self.d[k], src)
+        self.n_cams, self.n_pts, self.n_obs = len(bp.cams), len(bp.pts), len(bp.obs)
+
+    def reset(self):
+        self.ctx.d2d(self.d["cams"], self.d["cams0"], self.nbytes["cams"])
+        self.ctx.d2d(self.d["pts"], self.d["pts0"], self.nbytes["pts"])
+
+    def struct(self) -> BAProblemC:
+        p = BAProblemC()
+        p.n_cams, p.n_pts, p.n_obs = self.n_cams, self.n_pts, self.n_obs
+        p.cams = ctypes.cast(self.d["cams"], POINTER(c_double))
+        p.pts = ctypes.cast(self.d["pts"], POINTER(c_double))
+        p.obs = ctypes.cast(self.d["obs"], POINTER(c_double))
+        p.cam_idx = ctypes.cast(self.d["cam_idx"], POINTER(c_int32))
+        p.pt_idx = ctypes.cast(self.d["pt_idx"], POINTER(c_int32))
+        p.K0[:] = [float(x) for x in np.asarray(self.bp.K0).ravel()]
+        p.K1[:] = [float(x) for x in np.asarray(self.bp.K1).ravel()]
+        p.baseline, p.feat_var = float(self.bp.baseline), float(self.bp.feat_var)
+        p.fixed_frames, p.mem = int(self.bp.fixed_frames), ME_DEVICE
+        return p
+
+    def solve(self, options: SolverOptions | None = None) -> dict:
+        p = self.struct()
+        o = (options or SolverOptions()).to_c()
+        s = BASummaryC()
+        self.ctx.check(self.ctx.lib.me_ba_solve(self.ctx.h, byref(p), byref(o), byref(s)), "me_ba_solve")
+        return _summary(s)
+
+    def download(self):
+        cams = np.zeros((self.n_cams, 6))
+        pts = np.zeros((self.n_pts, 3))
+        self.ctx.d2h(cams, self.d["cams"])
+        self.ctx.d2h(pts, self.d["pts"])
+        return cams, pts
+
+    def close(self):
+        for v in self.d.values():
+            self.ctx.free(v)
+        self.d = {}
 
 
 def shard_landmarks(bp, rank: int, world: int):
