@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     return ap.parse_args()
 
 
@@ -119,27 +120,70 @@ def cpu_step(fd, ba_iters, stats):
     stats["ba_iters"] += s["iterations"]
 
 
-# algorithmic bytes per launch of each kernel family
-def alg_bytes(family: str, cfg: dict, frames) -> float:
-    N, win = cfg["n_feats"], cfg["window"]
+# Algorithmic work per launch of each kernel family: (bound,
+# amount, unit, peak).  Bytes are the algorithmic HBM bytes of one launch;
+# flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
+# is a single-workgroup dependency chain with no HBM/MFMA roofline.
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
+
+
+def alg_work(family: str, cfg: dict, frames):
+    N = cfg["n_feats"]
+    hbm = lambda b: ("hbm", float(b), "GB/s", PEAK_HBM_GBS)  # noqa: E731
     if family == "SCALE_RES":
-        return 262.0 * N                  # 2x121 px + 2 corners + out per track
+        return hbm(262.0 * N)                  # 2x121 px + 2 corners + out per track
     if family == "SCALE_NEQ":
-        return 234.0 * N                  # x0 100 B + x1∪x2 110 B + corners + out
+        return hbm(234.0 * N)                  # x0 100 B + x1 u x2 110 B + corners + out
     if family == "KLT":
-        return (2 * 22 * 22 + 2 * 2 * 22 * 22 + 16) * 4.0 * N  # I, dIx, dIy windows (+1 border) + 3 levels
+        return hbm((2 * 22 * 22 + 2 * 2 * 22 * 22 + 16) * 4.0 * N)  # I, dIx, dIy windows (+1 border) x 3 levels
     fd = frames[0].ba
     no, npt = len(fd.obs), len(fd.pts)
+    n6 = 6 * (len(fd.cams) - fd.fixed_frames)
     if family == "BA_LINEARIZE":
-        return no * (32 + 8 + 24 + 48 + 320.0)   # obs, idx, point, camera in; r + J out
+        return hbm(no * (32 + 8 + 24 + 48 + 320.0 + 72 + 144 + 216))  # in: obs, idx, point, camera; out: r+J, V_o/g_o, W_o, camera pieces
     if family == "BA_POINTS":
-        return no * (320 + 144.0) + npt * 72.0  # J in, W out, V/g per point
+        return hbm(no * 72.0 + npt * (72 + 72 + 72 + 24))             # V_o/g_o in; V, g, L_p, z out
     if family == "BA_SCHUR":
-        m = win - fd.fixed_frames
-        return 2 * 8.0 * (3 * npt) * (6 * m)    # dense Y written + read by the MFMA GEMM
+        return ("mfma", 2.0 * 3 * npt * (n6 * (n6 + 1) / 2 + n6), "TFLOP/s", PEAK_F64_MFMA_TFS)
     if family == "BA_STEP":
-        return no * (320 + 32 + 8 + 72.0)
-    return 0.0
+        return hbm(no * (144 + 24 + 320 + 32 + 8 + 72.0))
+    return None
+
+
+def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
+    """Batched MI patch scores (A1, 11x11) on n_pairs pairs of the resident
+    frame images: the north-star MI kernel measured on its own (HIP events
+    on the ctx stream), algorithmic bytes 262 B per pair."""
+    from uasl_motion_estimation_amd.mutual_information import mi_scores_device
+
+    fd = frames[0]
+    H, W = fd.cur.left.shape
+    rng = np.random.default_rng(7)
+    xyL = np.stack([rng.integers(0, W - 11, n_pairs), rng.integers(0, H - 11, n_pairs)], -1).astype(np.int32)
+    xyR = xyL.copy()
+    xyR[:, 0] = np.clip(xyL[:, 0] - rng.integers(0, 40, n_pairs), 0, W - 11)
+    dL, dR, dout = ctx.malloc(xyL.nbytes), ctx.malloc(xyR.nbytes), ctx.malloc(4 * n_pairs)
+    ctx.h2d(dL, xyL)
+    ctx.h2d(dR, xyR)
+    run = lambda: mi_scores_device(ctx, fd.d_curL, W, fd.d_curR, W, W, H, dL, dR, n_pairs, (11, 11), dout)  # noqa: E731
+    run()
+    run()
+    ctx.synchronize()
+    ctx.timing_reset()
+    ctx.timing(True)
+    for _ in range(reps):
+        run()
+    ctx.synchronize()
+    ctx.timing(False)
+    n, ms = ctx.timing_read("MI")
+    for p in (dL, dR, dout):
+        ctx.free(p)
+    avg = ms / max(n, 1)
+    achieved = 262.0 * n_pairs / (avg * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None, "kernel": "mi_batch_kernel",
+            "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
 
 
 def main():
@@ -206,16 +250,18 @@ def main():
         dist.all_reduce(cnt)
         frames_total, ba_total = int(cnt[0].item()), int(cnt[1].item())
     value = frames_total / t_max
-    # dominant kernel family by measured device time
-    dom = max((f for f in fams if fams[f][0] > 0 and alg_bytes(f, cfg, frames) > 0), key=lambda f: fams[f][1])
+    # dominant kernel family (by measured device time) among those with a roofline
+    rl = {f: alg_work(f, cfg, frames) for f in fams if fams[f][0] > 0}
+    dom = max((f for f in rl if rl[f] is not None), key=lambda f: fams[f][1])
+    bound, amount, unit, peak = rl[dom]
     n_l, ms_l = fams[dom]
     avg_ms = ms_l / n_l
-    bytes_launch = alg_bytes(dom, cfg, frames)
-    achieved = bytes_launch / (avg_ms * 1e-3) / 1e9
-    peak = 8000.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": peak, "unit": "GB/s",
+    scale_u = 1e9 if unit == "GB/s" else 1e12
+    achieved = amount / (avg_ms * 1e-3) / scale_u
+    roofline = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 5), "traffic": None, "kernel": dom,
-                "avg_launch_ms": round(avg_ms, 5), "alg_bytes_per_launch": bytes_launch}
+                "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount}
+    mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cstats = dict(ba_iters=0)
@@ -248,6 +294,7 @@ def main():
                        "parallelism": f"{world} independent streams (one per GPU)"},
             "ba_iter_per_s": round(ba_total / t_max, 2),
             "roofline": roofline,
+            "mi_roofline": mi_rl,
             "cpu_baseline": cpu,
             "kernel_ms": {f: [fams[f][0], round(fams[f][1], 3)] for f in fams},
             "gen_s": round(gen_s, 1),

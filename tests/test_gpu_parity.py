@@ -30,6 +30,23 @@ def test_mi_scores_bit_exact(ctx, oracle, patch):
     assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
 
 
+@pytest.mark.parametrize("patch", [(11, 11), (10, 10), (12, 12), (13, 13), (3, 7), (1, 1)])
+def test_mi_large_batch_bit_exact(ctx, oracle, patch):
+    """>= 32768 pairs take the 8-lane table-driven batch kernel; corners hug the
+    right / bottom image edges so the realigned row loads hit their bounds."""
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    pw, ph = patch
+    W, H = 161, 97
+    L, R, xyL, xyR = S.random_patches(200 + pw, W, H, 40000, pw, ph)
+    xyL[:500, 0] = W - pw
+    xyL[500:1000, 1] = H - ph
+    xyR[1000:1500] = [W - pw, H - ph]
+    got = mi_scores(L, R, xyL, xyR, patch, ctx=ctx)
+    ref = oracle.mi_scores(L, R, xyL, xyR, pw, ph)
+    assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
+
+
 def test_mi_edge_patches(ctx, oracle):
     from uasl_motion_estimation_amd.mutual_information import computeEntropy, computeMutualInformation
 

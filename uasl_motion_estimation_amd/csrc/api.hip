@@ -135,6 +135,8 @@ void me_destroy(me_ctx* c) {
   drain_timers(c);
   for (void* p : c->slot_ptr)
     if (p) hipFree(p);
+  for (float* t : c->mi_table)
+    if (t) hipFree(t);
   if (c->pinned) hipHostFree(c->pinned);
   for (auto e : c->event_pool) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->own_stream);

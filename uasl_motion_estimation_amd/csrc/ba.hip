@@ -624,7 +624,7 @@ constexpr int kLoadBatch = 32;
 
 __host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
 // dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
-__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 256; }
+__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 2 * 192; }
 __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
 
 // wave-local ordering of LDS (and, for the global fallback, L1) traffic
@@ -632,11 +632,6 @@ __device__ __forceinline__ void solve_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ double readlane_f64(double x, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-  return __hiloint2double(hi, lo);
 }
 template <int S>
 __device__ __forceinline__ double quad_bcast(double x) {
@@ -646,41 +641,41 @@ __device__ __forceinline__ double quad_bcast(double x) {
   return __hiloint2double(hi, lo);
 }
 
-// Diagonal block of the blocked Cholesky, held by one wave: lane = 4 i + g
-// holds a[q] = A[i][4g+q] and y[q] = Y[i][4g+q] (Y -> X = L^-1).  Four
-// rounds of 4 pivots: the 4x4 pivot block is read with v_readlane and
-// factored + inverted redundantly by every lane (uniform values), the four
-// pivot rows travel through LDS once (xch) in parallel with that, and a
-// rank-4 update finishes the round.  1/sqrt by v_rsq_f64 + two Newton steps.
+// Diagonal block of the blocked Cholesky, spread over the four SIMDs: wave w
+// (< 4) owns rows 4w..4w+3, lane = 16 (i - 4w) + c holds A[i][c] and Y[i][c]
+// (Y -> X = L^-1).  Four rounds of 4 pivots; per round one LDS exchange
+// (pivot rows of wave R + column group R of every row) behind one barrier,
+// the 4x4 pivot block factored and inverted redundantly by every lane
+// (uniform values), then 4-term updates.  1/sqrt by v_rsq_f64 + two Newton
+// steps.  Measured on gfx950: dependent FP64 FMA ~8.5 cycles, rsq ~19,
+// LDS round trip ~105, barrier ~80 -- so the round is bound by the pivot
+// chain, and splitting the updates over 4 SIMDs removes the single-wave
+// issue bottleneck of the previous one-wave version.
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double r = __builtin_amdgcn_rsq(p);
   r = r * fma(-0.5 * p * r, r, 1.5);
   r = r * fma(-0.5 * p * r, r, 1.5);
   return r;
 }
+constexpr int kXchDoubles = 192;  // per buffer: pivot rows A (64) | pivot rows Y (64) | column group (64)
 template <int R>
-__device__ __forceinline__ void chol4_round(double (&a)[4], double (&y)[4], int i, int g, int nreal, bool& ok,
-                                            double* Ablk, int ld, double* X, double* xch) {
-  double* xb = xch + 128 * (R & 1);
-  if ((i >> 2) == R) {  // pivot rows 4R..4R+3 publish A and Y (their group-g columns)
-    double* d = xb + 8 * (4 * (i - 4 * R) + g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      d[q] = a[q];
-      d[4 + q] = y[q];
+__device__ __forceinline__ void chol4w_round(double& a, double& y, bool act, int w, int i, int c, int lane,
+                                             int nreal, bool& ok, double* Ablk, int ld, double* X, double* xch) {
+  double* xb = xch + kXchDoubles * (R & 1);
+  if (act) {
+    if (w == R) {
+      xb[lane] = a;       // A[4R+u][c], u = lane >> 4
+      xb[64 + lane] = y;  // Y[4R+u][c]
     }
+    if ((c >> 2) == R) xb[128 + 4 * i + (c & 3)] = a;  // A[i][4R+u]
   }
-  // pivot block P[t][u] = A[4R+t][4R+u] (u <= t): lane 4(4R+t) + R, register u
-  double P[4][4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int u = 0; u <= t; ++u) P[t][u] = readlane_f64(a[u], 4 * (4 * R + t) + R);
-  // uniform 4x4 Cholesky and its inverse M = L44^-1 (lower)
+  __syncthreads();
+  if (!act) return;
+  // uniform 4x4 Cholesky of the pivot block and its inverse M = L44^-1
   double Lq[4][4], rinv[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    double piv = P[t][t];
+    double piv = xb[16 * t + 4 * R + t];
 #pragma unroll
     for (int u = 0; u < t; ++u) piv = fma(-Lq[t][u], Lq[t][u], piv);
     const bool pad = 4 * R + t >= nreal;  // padding / right-hand-side row: never a failure
@@ -691,7 +686,7 @@ __device__ __forceinline__ void chol4_round(double (&a)[4], double (&y)[4], int 
     Lq[t][t] = piv * r;
 #pragma unroll
     for (int v = t + 1; v < 4; ++v) {
-      double x = P[v][t];
+      double x = xb[16 * v + 4 * R + t];
 #pragma unroll
       for (int u = 0; u < t; ++u) x = fma(-Lq[v][u], Lq[t][u], x);
       Lq[v][t] = x * r;
@@ -709,65 +704,51 @@ __device__ __forceinline__ void chol4_round(double (&a)[4], double (&y)[4], int 
       M[t][u] = -x * rinv[t];
     }
   }
-  // own row: A[i][4R+u] from lane 4i + R (quad broadcast)
-  double ar[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) ar[u] = quad_bcast<R>(a[u]);
-  solve_wave_sync();
-  double xa[4][4], xy[4][4];
+  double ar[4], xa[4], xy[4];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    const double* d = xb + 8 * (4 * u + g);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xa[u][q] = d[q];      // A[4R+u][4g+q] = A[4g+q][4R+u]
-      xy[u][q] = d[4 + q];  // Y[4R+u][4g+q]
-    }
+    ar[u] = xb[128 + 4 * i + u];   // A[i][4R+u]
+    xa[u] = xb[16 * u + c];        // A[4R+u][c] = A[c][4R+u]
+    xy[u] = xb[64 + 16 * u + c];   // Y[4R+u][c]
   }
-  // L[i][4R+t], L[4g+q][4R+t], X[4R+t][4g+q]
-  double Lr[4], Lc[4][4], Xg[4][4];
+  double Lr[4], Lc[4], Xg[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    double s = 0.0;
+    double sr = 0.0, sc = 0.0, sx = 0.0;
 #pragma unroll
-    for (int u = 0; u <= t; ++u) s = fma(ar[u], M[t][u], s);
-    Lr[t] = s;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      double c = 0.0, x = 0.0;
-#pragma unroll
-      for (int u = 0; u <= t; ++u) {
-        c = fma(xa[u][q], M[t][u], c);
-        x = fma(M[t][u], xy[u][q], x);
-      }
-      Lc[q][t] = c;
-      Xg[t][q] = x;
+    for (int u = 0; u <= t; ++u) {
+      sr = fma(ar[u], M[t][u], sr);
+      sc = fma(xa[u], M[t][u], sc);
+      sx = fma(M[t][u], xy[u], sx);
     }
+    Lr[t] = sr;  // L[i][4R+t]
+    Lc[t] = sc;  // L[c][4R+t]
+    Xg[t] = sx;  // X[4R+t][c]
   }
-  if (g == R && i >= 4 * R) {
+  if ((c >> 2) == R && c <= i) {
+    double v = Lr[0];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (4 * R + t <= i) Ablk[i * ld + 4 * R + t] = (4 * R + t == i) ? Lq[t][t] : Lr[t];
+    for (int t = 1; t < 4; ++t)
+      if ((c & 3) == t) v = Lr[t];
+    if (c == i) v = Lq[c & 3][c & 3];
+    Ablk[i * ld + c] = v;
   }
-  if ((i >> 2) == R) {
+  if (w == R) {
+    double v = Xg[0];
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
-      if (4 * R + t == i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) X[i * 16 + 4 * g + q] = Xg[t][q];
+    for (int t = 1; t < 4; ++t)
+      if ((i & 3) == t) v = Xg[t];
+    X[i * 16 + c] = v;
   }
-  if (i > 4 * R + 3) {
+  if (w > R) {
+    double av = a, yv = y;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      double av = a[q], yv = y[q];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        av = fma(-Lr[t], Lc[q][t], av);
-        yv = fma(-Lr[t], Xg[t][q], yv);
-      }
-      a[q] = av;
-      y[q] = yv;
+    for (int t = 0; t < 4; ++t) {
+      av = fma(-Lr[t], Lc[t], av);
+      yv = fma(-Lr[t], Xg[t], yv);
     }
+    a = av;
+    y = yv;
   }
 }
 
@@ -783,8 +764,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   double* X = smem;
   double* u = X + 256 * (size_t)Ts;
-  double* xch = u + N;  // diagonal-block row exchange (2 x 128)
-  double* A = kLds ? xch + 256 : b.Abuf;
+  double* xch = u + N;  // diagonal-block exchange (2 x kXchDoubles)
+  double* A = kLds ? xch + 2 * kXchDoubles : b.Abuf;
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
@@ -828,23 +809,23 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   for (int J = 0; J < Ts; ++J) {
     const int j0 = 16 * J;
     SOLVE_START(1);
-    // (a) diagonal block + its inverse
-    if (wave == 0) {
-      const int i = lane >> 2, gq = lane & 3;
+    // (a) diagonal block + its inverse (waves 0-3; every wave joins the barriers)
+    {
+      const bool act = wave < 4;
+      const int i = 4 * wave + (lane >> 4), c = lane & 15;
       double* Ablk = A + (long)j0 * ld + j0;
-      double a[4], y[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = Ablk[i * ld + 4 * gq + q];
-        y[q] = (4 * gq + q == i) ? 1.0 : 0.0;
+      double a = 0.0, y = 0.0;
+      if (act) {
+        a = Ablk[i * ld + c];
+        y = (c == i) ? 1.0 : 0.0;
       }
       bool ok = true;
       double* XJw = X + 256 * J;
-      chol4_round<0>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4_round<1>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4_round<2>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4_round<3>(a, y, i, gq, n - j0, ok, Ablk, ld, XJw, xch);
-      if (!ok) sfail = 1;  // benign race: every writer stores 1
+      chol4w_round<0>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4w_round<1>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4w_round<2>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
+      chol4w_round<3>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
+      if (act && !ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
     SOLVE_STAMP(1);
@@ -903,14 +884,14 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     return;
   }
   SOLVE_START(5);
-  // backward solve L^T y = z (z = row n of L), wave 0, block by block
-  if (wave == 0) {
-    for (int c = lane; c < N; c += 64) u[c] = c < n ? A[(long)n * ld + c] : 0.0;
-    solve_wave_sync();
-    for (int J = (n - 1) >> 4; J >= 0; --J) {
-      const int j0 = 16 * J;
+  // backward solve L^T y = z (z = row n of L), block by block: wave 0 forms
+  // y_J = X_J^T z_J, then every wave updates the entries above the block
+  for (int c = tid; c < N; c += nt) u[c] = c < n ? A[(long)n * ld + c] : 0.0;
+  __syncthreads();
+  for (int J = (n - 1) >> 4; J >= 0; --J) {
+    const int j0 = 16 * J;
+    if (wave == 0) {
       const double* XJ = X + 256 * J;
-      // y_J = X_J^T z_J: 4 lanes per component, 4 terms each, quad reduce
       const int t = lane >> 2, gq = lane & 3;
       double s = 0.0;
 #pragma unroll
@@ -919,20 +900,24 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       s += __shfl_xor(s, 2, 64);
       solve_wave_sync();
       if (gq == 0) u[j0 + t] = j0 + t < n ? s : 0.0;
-      solve_wave_sync();
+    }
+    __syncthreads();
+    if (j0 > 0) {
       double yj[16];
 #pragma unroll
       for (int m = 0; m < 16; ++m) yj[m] = u[j0 + m];
-      for (int cc = lane; cc < j0; cc += 64) {
-        double acc = 0;
+      for (int cc = tid; cc < j0; cc += nt) {
+        double a0 = 0.0, a1 = 0.0;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc += A[(long)(j0 + m) * ld + cc] * yj[m];
-        u[cc] -= acc;
+        for (int m = 0; m < 16; m += 2) {
+          a0 = fma(A[(long)(j0 + m) * ld + cc], yj[m], a0);
+          a1 = fma(A[(long)(j0 + m + 1) * ld + cc], yj[m + 1], a1);
+        }
+        u[cc] -= a0 + a1;
       }
-      solve_wave_sync();
     }
+    __syncthreads();
   }
-  __syncthreads();
   SOLVE_STAMP(5);
   for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
   // candidate cameras

@@ -31,7 +31,12 @@ struct me_ctx {
   long launches[ME_KT_COUNT] = {0};
   double total_ms[ME_KT_COUNT] = {0};
   long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
+  // MI term tables, one per patch pixel count N (built on first use, mi.hip)
+  float* mi_table[256] = {nullptr};
 };
+
+// Device table of every MI term value for patches of N pixels (mi.hip).
+int me_mi_table(me_ctx* ctx, int npx, const float** out);
 
 int me_set_error(me_ctx* ctx, int code, const char* fmt, ...);
 

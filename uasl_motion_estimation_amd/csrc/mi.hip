@@ -17,29 +17,179 @@ using namespace me_dev;
 
 namespace {
 
-constexpr int kMiBlock = 256;
-// below this many pairs the batch cannot fill 256 CUs one pair per lane
-constexpr int kGroupThreshold = 65536;
+// below this many pairs the 8-lane batch kernel leaves most CUs idle: 16 lanes per pair
+constexpr int kGroupThreshold = 32768;
 
-__global__ __launch_bounds__(kMiBlock) void mi_pairs_kernel(const uint8_t* __restrict__ imgL, int strideL,
+// Term table: every value the reference's MI term can take for patches of N
+// pixels, T(cJ, cL, cR) = pJ * log2f(pJ / (pL * pR)) with p = fl32(c * fl32(1/N)),
+// computed once per N by the same device function (so bit-identical), stored
+// for cL >= cR (pL * pR commutes exactly) and 1 <= cJ <= cR:
+//   index(a, b, cJ) = (a-1) a (a+1) / 6 + b (b-1) / 2 + cJ - 1,  a = max, b = min.
+// N = 121: 302 621 floats (1.2 MB, L2-resident per XCD).  It replaces ~35
+// instructions (a correctly rounded division and the table-driven double
+// polynomial of log2f) per term with one gather.
+__host__ __device__ inline long mi_tab_index(int a, int b, int cJ) {
+  return (long)(a - 1) * a * (a + 1) / 6 + (long)b * (b - 1) / 2 + cJ - 1;
+}
+__host__ __device__ inline long mi_tab_size(int N) { return mi_tab_index(N + 1, 1, 1); }
+
+__global__ void mi_table_kernel(int N, float invN, float* __restrict__ tab) {
+  const int a = blockIdx.x + 1;  // cL (the larger marginal)
+  for (int b = threadIdx.x + 1; b <= a; b += blockDim.x)
+    for (int cJ = 1; cJ <= b; ++cJ) tab[mi_tab_index(a, b, cJ)] = mi_term(cJ, a, b, invN);
+}
+
+__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xff; }
+
+// Batched MI, 8 lanes per patch pair (32 pairs per 256-thread workgroup, ~34 KB
+// LDS: 4 workgroups / 16 waves per CU):
+//  * histogram: a lane takes whole patch rows (dword loads realigned with
+//    v_alignbyte), joint / marginal u8 counts and the occupancy bitmap by LDS
+//    atomics in the group's shared histogram;
+//  * terms: lane l walks bitmap words l and l + 8, each set bit is one
+//    non-empty joint bin in row-major order, its term comes from the table
+//    and lands at its rank (prefix of the bitmap popcounts) in a term list;
+//  * sum: lane 0 of the group adds the list in order -- the reference's
+//    left-to-right float sum over non-empty bins, bit for bit.
+constexpr int kMiG = 8;
+constexpr int kMiBlock = 256;
+constexpr int kMiPairsPerBlock = kMiBlock / kMiG;
+constexpr int kMiHistWords = 123;  // joint 100 | left 5 | right 5 | bitmap 13
+
+template <int LIST>
+__global__ __launch_bounds__(kMiBlock) void mi_batch_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                             const uint8_t* __restrict__ imgR, int strideR,
+                                                            long bytesL, long bytesR,
                                                             const int32_t* __restrict__ xyL,
                                                             const int32_t* __restrict__ xyR, int n, int pw, int ph,
-                                                            float invN, float* __restrict__ out) {
-  __shared__ uint32_t lds[kHistWords * kMiBlock];
-  LaneHist<kMiBlock> h{&lds[threadIdx.x]};
-  for (int k = blockIdx.x * kMiBlock + threadIdx.x; k < n; k += gridDim.x * kMiBlock) {
+                                                            const float* __restrict__ tab, float* __restrict__ out) {
+  constexpr int W = kMiHistWords + LIST;
+  __shared__ uint32_t lds[kMiPairsPerBlock * W];
+  const int gl = threadIdx.x & (kMiG - 1), grp = threadIdx.x / kMiG;
+  uint32_t* h = lds + grp * W;
+  float* list = reinterpret_cast<float*>(h + kMiHistWords);
+  for (int k = blockIdx.x * kMiPairsPerBlock + grp; k < n; k += gridDim.x * kMiPairsPerBlock) {
+    for (int i = gl; i < kMiHistWords; i += kMiG) h[i] = 0u;
+    wave_sync();
     const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
     const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
-    const uint8_t* pl = imgL + (long)cl.y * strideL + cl.x;
-    const uint8_t* pr = imgR + (long)cr.y * strideR + cr.x;
-    h.clear();
-    for (int y = 0; y < ph; ++y) {
-      for (int x = 0; x < pw; ++x) h.add(pl[x], pr[x]);
-      pl += strideL;
-      pr += strideR;
+    if (pw <= 12 && ph <= 2 * kMiG) {
+      // rows gl and gl + 8: both rows' loads are issued before any histogram update
+      uint32_t pl[2][3], pr[2][3];
+      bool fast[2], live[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = gl + u * kMiG;
+        live[u] = r < ph;
+        const long offL = (long)(cl.y + r) * strideL + cl.x, offR = (long)(cr.y + r) * strideR + cr.x;
+        // dword-aligned 16-byte windows by absolute address (inputs may be offset views)
+        const int sl = (int)(((uintptr_t)imgL + offL) & 3), sr = (int)(((uintptr_t)imgR + offR) & 3);
+        const long aL = offL - sl, aR = offR - sr;
+        fast[u] = live[u] && aL + 16 <= bytesL && aR + 16 <= bytesR && aL >= 0 && aR >= 0;
+        uint4 dl = {0, 0, 0, 0}, dr = {0, 0, 0, 0};
+        if (fast[u]) {
+          dl = *reinterpret_cast<const uint4*>(imgL + aL);
+          dr = *reinterpret_cast<const uint4*>(imgR + aR);
+        } else if (live[u]) {  // first / last bytes of an image: byte loads, never outside it
+          uint32_t tl[4] = {0, 0, 0, 0}, tr[4] = {0, 0, 0, 0};
+          for (int x = 0; x < pw; ++x) {
+            const int q = sl + x, qr = sr + x;
+            tl[q >> 2] |= (uint32_t)imgL[offL + x] << (8 * (q & 3));
+            tr[qr >> 2] |= (uint32_t)imgR[offR + x] << (8 * (qr & 3));
+          }
+          dl = {tl[0], tl[1], tl[2], tl[3]};
+          dr = {tr[0], tr[1], tr[2], tr[3]};
+        }
+        pl[u][0] = __builtin_amdgcn_alignbyte(dl.y, dl.x, sl);
+        pl[u][1] = __builtin_amdgcn_alignbyte(dl.z, dl.y, sl);
+        pl[u][2] = __builtin_amdgcn_alignbyte(dl.w, dl.z, sl);
+        pr[u][0] = __builtin_amdgcn_alignbyte(dr.y, dr.x, sr);
+        pr[u][1] = __builtin_amdgcn_alignbyte(dr.z, dr.y, sr);
+        pr[u][2] = __builtin_amdgcn_alignbyte(dr.w, dr.z, sr);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!live[u]) continue;
+#pragma unroll
+        for (int x = 0; x < 12; ++x) {
+          if (x < pw) {
+            const int bl = bin20(byte_of(pl[u][x >> 2], x & 3)), br = bin20(byte_of(pr[u][x >> 2], x & 3));
+            const int code = bl * 20 + br;
+            atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
+            atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
+            atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
+            atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
+          }
+        }
+      }
+    } else {
+      for (int r = gl; r < ph; r += kMiG) {
+        const long offL = (long)(cl.y + r) * strideL + cl.x, offR = (long)(cr.y + r) * strideR + cr.x;
+        for (int x = 0; x < pw; ++x) {
+          const int bl = bin20(imgL[offL + x]), br = bin20(imgR[offR + x]);
+          const int code = bl * 20 + br;
+          atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
+          atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
+          atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
+          atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
+        }
+      }
     }
-    out[k] = h.mi(invN);
+    wave_sync();
+    // ranks: exclusive prefix of the bitmap-word popcounts (words gl, gl + 8)
+    const uint32_t b0 = h[110 + gl], b1 = gl + 8 < 13 ? h[118 + gl] : 0u;
+    const int c0 = __builtin_popcount(b0), c1 = __builtin_popcount(b1);
+    int s0 = c0, s1 = c1;
+#pragma unroll
+    for (int off = 1; off < kMiG; off <<= 1) {
+      const int t0 = __shfl_up(s0, off, kMiG), t1 = __shfl_up(s1, off, kMiG);
+      if (gl >= off) {
+        s0 += t0;
+        s1 += t1;
+      }
+    }
+    const int tot0 = __shfl(s0, kMiG - 1, kMiG);
+    const int total = tot0 + __shfl(s1, kMiG - 1, kMiG);
+    // (1) table index of every non-empty bin at its rank (LDS only)
+    int* slot = reinterpret_cast<int*>(list);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      uint32_t bits = half ? b1 : b0;
+      int idx = half ? tot0 + s1 - c1 : s0 - c0;
+      const int wd = half ? gl + 8 : gl;
+      while (bits) {
+        const int b = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        const int code = wd * 32 + b;
+        const int i = code / 20, j = code - i * 20;
+        const int cJ = byte_of(h[code >> 2], code & 3);
+        const int cL = byte_of(h[100 + (i >> 2)], i & 3);
+        const int cR = byte_of(h[105 + (j >> 2)], j & 3);
+        slot[idx++] = (int)mi_tab_index(max(cL, cR), min(cL, cR), cJ);
+      }
+    }
+    wave_sync();
+    // (2) gather the terms, ranks strided over the group: 8 independent loads in flight per lane
+    for (int r0 = gl; r0 < total; r0 += 8 * kMiG) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + u * kMiG;
+        v[u] = r < total ? tab[slot[r]] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + u * kMiG;
+        if (r < total) list[r] = v[u];
+      }
+    }
+    wave_sync();
+    if (gl == 0) {
+      float MI = 0.0f;
+      for (int t = 0; t < total; ++t) MI += list[t];
+      out[k] = MI;
+    }
+    wave_sync();
   }
 }
 
@@ -121,8 +271,8 @@ inline float inv_count(long n) { return (float)(1.0 / (double)n); }
 }  // namespace
 
 // Shared launcher (also used by scale.hip for raw device buffers).
-int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, const int32_t* dxyL,
-                       const int32_t* dxyR, int n, int pw, int ph, float* dout) {
+int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, int width, int height,
+                       const int32_t* dxyL, const int32_t* dxyR, int n, int pw, int ph, float* dout) {
   if (n <= 0) return ME_OK;
   me_ktimer t(c, ME_KT_MI);
   if (n < kGroupThreshold) {
@@ -133,11 +283,33 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
                        dxyR, n, pw, ph, inv_count((long)pw * ph), dout);
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
-  int blocks = (n + kMiBlock - 1) / kMiBlock;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(mi_pairs_kernel, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, dxyL, dxyR, n, pw,
-                     ph, inv_count((long)pw * ph), dout);
-  return me_check_launch(c, "mi_pairs_kernel");
+  const int npx = pw * ph;
+  const float* tab;
+  ME_TRY(me_mi_table(c, npx, &tab));
+  int blocks = (n + kMiPairsPerBlock - 1) / kMiPairsPerBlock;
+  if (blocks > 4096) blocks = 4096;
+  // bounds of the realigned 16-byte row loads: never read past the images
+  const long img_bytes_L = (long)sL * (height - 1) + width, img_bytes_R = (long)sR * (height - 1) + width;
+  if (npx <= 128)
+    hipLaunchKernelGGL(mi_batch_kernel<128>, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
+                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, dout);
+  else
+    hipLaunchKernelGGL(mi_batch_kernel<256>, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
+                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, dout);
+  return me_check_launch(c, "mi_batch_kernel");
+}
+
+int me_mi_table(me_ctx* c, int npx, const float** out) {
+  if (npx < 1 || npx > 255) return me_set_error(c, ME_ERR_INVALID, "MI table: %d px outside [1, 255]", npx);
+  if (!c->mi_table[npx]) {
+    float* t;
+    ME_HIP(c, hipMalloc(&t, 4 * (size_t)mi_tab_size(npx)));
+    hipLaunchKernelGGL(mi_table_kernel, dim3(npx), dim3(128), 0, c->stream, npx, inv_count(npx), t);
+    ME_TRY(me_check_launch(c, "mi_table_kernel"));
+    c->mi_table[npx] = t;
+  }
+  *out = c->mi_table[npx];
+  return ME_OK;
 }
 
 extern "C" int me_mi_scores(me_ctx* c, me_mem mem, const uint8_t* imgL, int strideL, const uint8_t* imgR,
@@ -150,7 +322,8 @@ extern "C" int me_mi_scores(me_ctx* c, me_mem mem, const uint8_t* imgL, int stri
   ME_CHECK(c, strideL >= width && strideR >= width, "me_mi_scores: stride < width");
   if (n == 0) return ME_OK;
   ME_HIP(c, hipSetDevice(c->device));
-  if (mem == ME_DEVICE) return me_launch_mi_pairs(c, imgL, strideL, imgR, strideR, xyL, xyR, n, pw, ph, out);
+  if (mem == ME_DEVICE)
+    return me_launch_mi_pairs(c, imgL, strideL, imgR, strideR, width, height, xyL, xyR, n, pw, ph, out);
   // host path: validate corners (the reference would throw cv::Exception on an out-of-image ROI)
   for (int k = 0; k < n; ++k) {
     int lx = xyL[2 * k], ly = xyL[2 * k + 1], rx = xyR[2 * k], ry = xyR[2 * k + 1];
@@ -169,7 +342,8 @@ extern "C" int me_mi_scores(me_ctx* c, me_mem mem, const uint8_t* imgL, int stri
   ME_HIP(c, hipMemcpyAsync(dR, imgR, br, hipMemcpyHostToDevice, c->stream));
   ME_HIP(c, hipMemcpyAsync(dxl, xyL, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
   ME_HIP(c, hipMemcpyAsync(dxr, xyR, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  ME_TRY(me_launch_mi_pairs(c, (const uint8_t*)dL, strideL, (const uint8_t*)dR, strideR, (const int32_t*)dxl,
+  ME_TRY(me_launch_mi_pairs(c, (const uint8_t*)dL, strideL, (const uint8_t*)dR, strideR, width, height,
+                            (const int32_t*)dxl,
                             (const int32_t*)dxr, n, pw, ph, (float*)dout));
   ME_HIP(c, hipMemcpyAsync(out, dout, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
