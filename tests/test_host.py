@@ -119,3 +119,18 @@ def test_ctypes_struct_layout_matches_header(tmp_path):
     sizes = dict(zip(out[0::2], map(int, out[1::2])))
     for cname, pyname in _STRUCTS.items():
         assert sizes[cname] == ctypes.sizeof(getattr(_lib, pyname)), cname
+
+
+def test_mi_table_index_arithmetic_is_exact():
+    """mi.hip mi_c3: (a-1)a(a+1)/6 as trunc(fl32((a*a - 1) * a) * fl32(1/6)),
+    and code/20 as (205 code) >> 12, for every value the kernels can see."""
+    a = np.arange(1, 256, dtype=np.int64)
+    p = (a - 1) * a * (a + 1)
+    assert p.max() < 2 ** 24
+    af = a.astype(np.float32)
+    pf = (af * af - np.float32(1.0)) * af
+    assert np.array_equal(pf.astype(np.int64), p)
+    q = (pf * np.float32(1.0 / 6.0)).astype(np.uint32).astype(np.int64)
+    assert np.array_equal(q, p // 6)
+    code = np.arange(400)
+    assert np.array_equal((code * 205) >> 12, code // 20)

@@ -122,6 +122,8 @@ int me_create(me_ctx** out, int dev) {
     return ME_ERR_HIP;
   }
   c->stream = c->own_stream;
+  if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c->num_cu <= 0)
+    c->num_cu = 256;
   c->slot_ptr.assign(SLOT_COUNT, nullptr);
   c->slot_size.assign(SLOT_COUNT, 0);
   *out = c;

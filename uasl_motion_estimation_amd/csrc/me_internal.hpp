@@ -15,6 +15,7 @@ struct me_timer_pair {
 
 struct me_ctx {
   int device = 0;
+  int num_cu = 256;  // compute units of the device (grid sizing of streaming kernels)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;

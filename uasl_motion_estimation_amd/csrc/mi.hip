@@ -39,157 +39,203 @@ __global__ void mi_table_kernel(int N, float invN, float* __restrict__ tab) {
     for (int cJ = 1; cJ <= b; ++cJ) tab[mi_tab_index(a, b, cJ)] = mi_term(cJ, a, b, invN);
 }
 
-__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xff; }
+// Batched MI, one lane per patch pair (measured on 11x11 patches of the
+// synthetic stream: ~26 non-empty joint bins per pair, p90 41, so the 121
+// pixel updates dominate and the term walk must stay cheap):
+//  * lane-private histogram, word w of lane l at lds[64 w + l]: every LDS
+//    access of the wave hits 64 distinct banks whatever the data, no atomics
+//    collide and no barrier is ever needed (nothing crosses lanes);
+//  * per pixel one packed-u8 ds_add (joint) and one ds_or (occupancy bitmap);
+//    the marginals are derived afterwards from the joint rows (v_sad_u8 row
+//    sums, packed-byte column sums), cheaper than two more atomics per pixel;
+//  * term walk: one flat loop over the lane's set bitmap bits in ascending
+//    code order (= the reference's i-outer / j-inner order), int32 index
+//    math, terms from the per-N table, summed left to right as they arrive
+//    (bit-identical to the reference's float loop).
+constexpr int kLaneBlock = 64;
+constexpr int kLaneBm = 100, kLaneMarg = 114, kLaneWords = 124;  // bitmap word 13 (113) stays 0
+constexpr int kLaneUnroll = 4;
 
-// Batched MI, 8 lanes per patch pair (32 pairs per 256-thread workgroup, ~34 KB
-// LDS: 4 workgroups / 16 waves per CU):
-//  * histogram: a lane takes whole patch rows (dword loads realigned with
-//    v_alignbyte), joint / marginal u8 counts and the occupancy bitmap by LDS
-//    atomics in the group's shared histogram;
-//  * terms: lane l walks bitmap words l and l + 8, each set bit is one
-//    non-empty joint bin in row-major order, its term comes from the table
-//    and lands at its rank (prefix of the bitmap popcounts) in a term list;
-//  * sum: lane 0 of the group adds the list in order -- the reference's
-//    left-to-right float sum over non-empty bins, bit for bit.
-constexpr int kMiG = 8;
-constexpr int kMiBlock = 256;
-constexpr int kMiPairsPerBlock = kMiBlock / kMiG;
-constexpr int kMiHistWords = 123;  // joint 100 | left 5 | right 5 | bitmap 13
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
 
-template <int LIST>
-__global__ __launch_bounds__(kMiBlock) void mi_batch_kernel(const uint8_t* __restrict__ imgL, int strideL,
-                                                            const uint8_t* __restrict__ imgR, int strideR,
-                                                            long bytesL, long bytesR,
-                                                            const int32_t* __restrict__ xyL,
-                                                            const int32_t* __restrict__ xyR, int n, int pw, int ph,
-                                                            const float* __restrict__ tab, float* __restrict__ out) {
-  constexpr int W = kMiHistWords + LIST;
-  __shared__ uint32_t lds[kMiPairsPerBlock * W];
-  const int gl = threadIdx.x & (kMiG - 1), grp = threadIdx.x / kMiG;
-  uint32_t* h = lds + grp * W;
-  float* list = reinterpret_cast<float*>(h + kMiHistWords);
-  for (int k = blockIdx.x * kMiPairsPerBlock + grp; k < n; k += gridDim.x * kMiPairsPerBlock) {
-    for (int i = gl; i < kMiHistWords; i += kMiG) h[i] = 0u;
-    wave_sync();
-    const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
-    const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
-    if (pw <= 12 && ph <= 2 * kMiG) {
-      // rows gl and gl + 8: both rows' loads are issued before any histogram update
-      uint32_t pl[2][3], pr[2][3];
-      bool fast[2], live[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int r = gl + u * kMiG;
-        live[u] = r < ph;
-        const long offL = (long)(cl.y + r) * strideL + cl.x, offR = (long)(cr.y + r) * strideR + cr.x;
-        // dword-aligned 16-byte windows by absolute address (inputs may be offset views)
-        const int sl = (int)(((uintptr_t)imgL + offL) & 3), sr = (int)(((uintptr_t)imgR + offR) & 3);
-        const long aL = offL - sl, aR = offR - sr;
-        fast[u] = live[u] && aL + 16 <= bytesL && aR + 16 <= bytesR && aL >= 0 && aR >= 0;
-        uint4 dl = {0, 0, 0, 0}, dr = {0, 0, 0, 0};
-        if (fast[u]) {
-          dl = *reinterpret_cast<const uint4*>(imgL + aL);
-          dr = *reinterpret_cast<const uint4*>(imgR + aR);
-        } else if (live[u]) {  // first / last bytes of an image: byte loads, never outside it
-          uint32_t tl[4] = {0, 0, 0, 0}, tr[4] = {0, 0, 0, 0};
-          for (int x = 0; x < pw; ++x) {
-            const int q = sl + x, qr = sr + x;
-            tl[q >> 2] |= (uint32_t)imgL[offL + x] << (8 * (q & 3));
-            tr[qr >> 2] |= (uint32_t)imgR[offR + x] << (8 * (qr & 3));
-          }
-          dl = {tl[0], tl[1], tl[2], tl[3]};
-          dr = {tr[0], tr[1], tr[2], tr[3]};
-        }
-        pl[u][0] = __builtin_amdgcn_alignbyte(dl.y, dl.x, sl);
-        pl[u][1] = __builtin_amdgcn_alignbyte(dl.z, dl.y, sl);
-        pl[u][2] = __builtin_amdgcn_alignbyte(dl.w, dl.z, sl);
-        pr[u][0] = __builtin_amdgcn_alignbyte(dr.y, dr.x, sr);
-        pr[u][1] = __builtin_amdgcn_alignbyte(dr.z, dr.y, sr);
-        pr[u][2] = __builtin_amdgcn_alignbyte(dr.w, dr.z, sr);
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (!live[u]) continue;
-#pragma unroll
-        for (int x = 0; x < 12; ++x) {
-          if (x < pw) {
-            const int bl = bin20(byte_of(pl[u][x >> 2], x & 3)), br = bin20(byte_of(pr[u][x >> 2], x & 3));
-            const int code = bl * 20 + br;
-            atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
-            atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
-            atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
-            atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
-          }
-        }
-      }
-    } else {
-      for (int r = gl; r < ph; r += kMiG) {
-        const long offL = (long)(cl.y + r) * strideL + cl.x, offR = (long)(cr.y + r) * strideR + cr.x;
-        for (int x = 0; x < pw; ++x) {
-          const int bl = bin20(imgL[offL + x]), br = bin20(imgR[offR + x]);
-          const int code = bl * 20 + br;
-          atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
-          atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
-          atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
-          atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
-        }
-      }
+// (a-1) a (a+1) / 6 for 1 <= a <= 255: the product is < 2^24 (exact in float)
+// and the quotient is an integer < 2^22, so the rounded float product is within
+// 0.21 of it (checked exhaustively in tests/test_host.py).
+// fl32(1/6) > 1/6 and the quotient k < 2^22 is representable, so the rounded
+// product lies in [k, k + 0.21] and truncation gives k.
+__device__ __forceinline__ int mi_c3(int a) {
+  const float af = (float)a;
+  const float p = __builtin_fmaf(af, af, -1.0f) * af;  // exact: < 2^24
+  return (int)(uint32_t)(p * (1.0f / 6.0f));
+}
+
+// v_mul_u32_u24 (full rate); the compiler otherwise folds these into the
+// quarter-rate v_mul_lo_u32.
+__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// One patch row (PW <= 12 bytes) as three realigned dwords: FAST = the
+// 16-byte window around the row lies inside the image (checked once per pair).
+template <bool FAST>
+__device__ __forceinline__ void load_row12(const uint8_t* __restrict__ img, long off, int pw, uint32_t d[3]) {
+  const int sh = (int)(((uintptr_t)img + off) & 3);
+  uint4 v = {0, 0, 0, 0};
+  if (FAST) {
+    v = *reinterpret_cast<const uint4*>(img + off - sh);
+  } else {  // first / last bytes of an image: byte loads, never outside it
+    uint32_t t[4] = {0, 0, 0, 0};
+    for (int x = 0; x < pw; ++x) {
+      const int q = sh + x;
+      t[q >> 2] |= (uint32_t)img[off + x] << (8 * (q & 3));
     }
-    wave_sync();
-    // ranks: exclusive prefix of the bitmap-word popcounts (words gl, gl + 8)
-    const uint32_t b0 = h[110 + gl], b1 = gl + 8 < 13 ? h[118 + gl] : 0u;
-    const int c0 = __builtin_popcount(b0), c1 = __builtin_popcount(b1);
-    int s0 = c0, s1 = c1;
+    v = {t[0], t[1], t[2], t[3]};
+  }
+  d[0] = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+  d[1] = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+  d[2] = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+}
+
+template <int PW>
+__device__ __forceinline__ void lane_hist_row(uint32_t* h, const uint32_t pl[3], const uint32_t pr[3], int pw) {
 #pragma unroll
-    for (int off = 1; off < kMiG; off <<= 1) {
-      const int t0 = __shfl_up(s0, off, kMiG), t1 = __shfl_up(s1, off, kMiG);
-      if (gl >= off) {
-        s0 += t0;
-        s1 += t1;
-      }
+  for (int x = 0; x < 12; ++x) {
+    if (PW > 0 ? x < PW : x < pw) {
+      const int bl = bin20((pl[x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[x >> 2] >> (8 * (x & 3))) & 0xff);
+      const int code = bl * 20 + br;
+      atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
+      atomicOr(&h[64 * (kLaneBm + (code >> 5))], 1u << (code & 31));
     }
-    const int tot0 = __shfl(s0, kMiG - 1, kMiG);
-    const int total = tot0 + __shfl(s1, kMiG - 1, kMiG);
-    // (1) table index of every non-empty bin at its rank (LDS only)
-    int* slot = reinterpret_cast<int*>(list);
+  }
+}
+
+template <int PW, int PH, bool FAST>
+__device__ __forceinline__ void lane_hist_pair(uint32_t* h, const uint8_t* __restrict__ imgL, int strideL, long oL,
+                                               const uint8_t* __restrict__ imgR, int strideR, long oR, int pw,
+                                               int ph) {
+  if (PH > 0) {  // every row's loads issued before the first histogram update
+    uint32_t pl[PH > 0 ? PH : 1][3], pr[PH > 0 ? PH : 1][3];
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      uint32_t bits = half ? b1 : b0;
-      int idx = half ? tot0 + s1 - c1 : s0 - c0;
-      const int wd = half ? gl + 8 : gl;
-      while (bits) {
-        const int b = __builtin_ctz(bits);
+    for (int r = 0; r < PH; ++r) {
+      load_row12<FAST>(imgL, oL + (long)r * strideL, PW, pl[r]);
+      load_row12<FAST>(imgR, oR + (long)r * strideR, PW, pr[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < PH; ++r) lane_hist_row<PW>(h, pl[r], pr[r], pw);
+  } else {
+    for (int r = 0; r < ph; ++r) {
+      uint32_t pl[3], pr[3];
+      load_row12<FAST>(imgL, oL + (long)r * strideL, pw, pl);
+      load_row12<FAST>(imgR, oR + (long)r * strideR, pw, pr);
+      lane_hist_row<PW>(h, pl, pr, pw);
+    }
+  }
+}
+
+// PW, PH > 0: patch size known at compile time (11x11 residual, 10x10 finite-difference ROIs).
+template <int PW, int PH>
+__global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __restrict__ imgL, int strideL,
+                                                             const uint8_t* __restrict__ imgR, int strideR,
+                                                             long bytesL, long bytesR,
+                                                             const int32_t* __restrict__ xyL,
+                                                             const int32_t* __restrict__ xyR, int n, int pw, int ph,
+                                                             const float* __restrict__ tab, int tab_bytes,
+                                                             float* __restrict__ out) {
+  __shared__ uint32_t lds[kLaneWords * kLaneBlock];
+  const int lane = threadIdx.x;
+  uint32_t* h = lds + lane;
+  for (int w = 0; w < kLaneWords; ++w) h[64 * w] = 0u;
+  // table entry of (a, b, cJ) is c3(a) + b(b-1)/2 + cJ - 1; buffer loads past tab_bytes return 0
+  const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)tab, (short)0, tab_bytes, 0x00020000);
+  for (int k0 = blockIdx.x * kLaneBlock; k0 < n; k0 += gridDim.x * kLaneBlock) {
+    const int k = k0 + lane;
+    if (k < n) {
+      const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
+      const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
+      const long oL = (long)cl.y * strideL + cl.x, oR = (long)cr.y * strideR + cr.x;
+      const int rows = PH > 0 ? PH : ph;
+      // 16-byte windows start at most 3 bytes before a row and end at most 16 after its start
+      const bool fast = oL >= 3 && oR >= 3 && oL + (long)(rows - 1) * strideL + 16 <= bytesL &&
+                        oR + (long)(rows - 1) * strideR + 16 <= bytesR;
+      if (fast)
+        lane_hist_pair<PW, PH, true>(h, imgL, strideL, oL, imgR, strideR, oR, pw, ph);
+      else
+        lane_hist_pair<PW, PH, false>(h, imgL, strideL, oL, imgR, strideR, oR, pw, ph);
+    }
+    // marginals from the joint rows: row i is words 5i..5i+4 (bins j = 0..19)
+    uint32_t cl4[5] = {0, 0, 0, 0, 0}, cr4[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 20; ++i) {
+      uint32_t s = 0;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const uint32_t w = h[64 * (5 * i + q)];
+        s = __builtin_amdgcn_sad_u8(w, 0u, s);
+        cr4[q] += w;  // byte sums <= 255: no carries between the packed counts
+      }
+      cl4[i >> 2] |= s << (8 * (i & 3));
+    }
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      h[64 * (kLaneMarg + q)] = cl4[q];
+      h[64 * (kLaneMarg + 5 + q)] = cr4[q];
+    }
+    uint32_t nz = 0;  // non-empty bitmap words
+    int nnz = 0;
+#pragma unroll
+    for (int w = 0; w < 13; ++w) {
+      const uint32_t bw = h[64 * (kLaneBm + w)];
+      nz |= (bw != 0u ? 1u : 0u) << w;
+      nnz += __builtin_popcount(bw);
+    }
+    const int tmax = wave_max(nnz);
+    // Branch-free walk.  State: current word wd and its remaining bits, the
+    // words still to visit (nz), and the next non-empty word nw with its bits
+    // read one step ahead (nxt); word 13 is a permanent zero sentinel.  A
+    // finished lane keeps producing in-range garbage codes whose table reads
+    // are masked off, so the whole wave runs one uniform loop.
+    int wd = __builtin_ctz(nz | 0x2000u);
+    nz &= nz - 1u;
+    uint32_t bits = h[64 * (kLaneBm + wd)];
+    int nw = __builtin_ctz(nz | 0x2000u);
+    uint32_t nxt = h[64 * (kLaneBm + nw)];
+    float MI = 0.0f;
+    for (int t = 0; t < tmax; t += kLaneUnroll) {
+      float v[kLaneUnroll];
+#pragma unroll
+      for (int u = 0; u < kLaneUnroll; ++u) {
+        const int code = (wd << 5) | __builtin_ctz(bits | 0x80000000u);  // < 448
         bits &= bits - 1u;
-        const int code = wd * 32 + b;
-        const int i = code / 20, j = code - i * 20;
-        const int cJ = byte_of(h[code >> 2], code & 3);
-        const int cL = byte_of(h[100 + (i >> 2)], i & 3);
-        const int cR = byte_of(h[105 + (j >> 2)], j & 3);
-        slot[idx++] = (int)mi_tab_index(max(cL, cR), min(cL, cR), cJ);
+        const bool z = bits == 0u;
+        wd = z ? nw : wd;
+        bits = z ? nxt : bits;
+        nz = z ? nz & (nz - 1u) : nz;
+        nw = __builtin_ctz(nz | 0x2000u);
+        nxt = h[64 * (kLaneBm + nw)];  // unchanged unless z: same word as before
+        const int i = (int)(mul_u24((uint32_t)code, 205u) >> 12);  // exact code / 20 for code < 1024
+        const int j = code - (int)mul_u24((uint32_t)i, 20u);
+        const int cJ = (h[64 * (code >> 2)] >> ((code & 3) * 8)) & 0xff;
+        const int cL = (h[64 * (kLaneMarg + (i >> 2))] >> ((i & 3) * 8)) & 0xff;
+        const int cR = (h[64 * (kLaneMarg + 5 + (j >> 2))] >> ((j & 3) * 8)) & 0xff;
+        const int a = max(cL, cR), b = min(cL, cR);
+        const int idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + cJ;
+        // out-of-range buffer offsets read 0: a finished lane adds +0.0f, no branch
+        const int off = t + u < nnz ? 4 * (idx - 1) : 0x7ffffff0;
+        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
       }
-    }
-    wave_sync();
-    // (2) gather the terms, ranks strided over the group: 8 independent loads in flight per lane
-    for (int r0 = gl; r0 < total; r0 += 8 * kMiG) {
-      float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = r0 + u * kMiG;
-        v[u] = r < total ? tab[slot[r]] : 0.0f;
-      }
+      for (int u = 0; u < kLaneUnroll; ++u) MI += v[u];  // +0.0f for finished lanes: exact (MI is never -0)
+    }
+    // clean histogram for the next pair (joint + bitmap; the marginals are overwritten)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int r = r0 + u * kMiG;
-        if (r < total) list[r] = v[u];
-      }
-    }
-    wave_sync();
-    if (gl == 0) {
-      float MI = 0.0f;
-      for (int t = 0; t < total; ++t) MI += list[t];
-      out[k] = MI;
-    }
-    wave_sync();
+    for (int w = 0; w < kLaneBm + 13; ++w) h[64 * w] = 0u;
+    if (k < n) out[k] = MI;
   }
 }
 
@@ -284,19 +330,28 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
   const int npx = pw * ph;
+  if (pw > 12) {  // wider than one realigned 16-byte row load: the group kernel handles any shape
+    const int per = kGroupBlock / 16;
+    hipLaunchKernelGGL(mi_pairs_group_kernel, dim3((n + per - 1) / per), dim3(kGroupBlock), 0, c->stream, dL, sL, dR,
+                       sR, dxyL, dxyR, n, pw, ph, inv_count((long)npx), dout);
+    return me_check_launch(c, "mi_pairs_group_kernel");
+  }
   const float* tab;
   ME_TRY(me_mi_table(c, npx, &tab));
-  int blocks = (n + kMiPairsPerBlock - 1) / kMiPairsPerBlock;
-  if (blocks > 4096) blocks = 4096;
+  int blocks = (n + kLaneBlock - 1) / kLaneBlock;
+  if (blocks > 8192) blocks = 8192;
   // bounds of the realigned 16-byte row loads: never read past the images
   const long img_bytes_L = (long)sL * (height - 1) + width, img_bytes_R = (long)sR * (height - 1) + width;
-  if (npx <= 128)
-    hipLaunchKernelGGL(mi_batch_kernel<128>, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
-                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, dout);
+  if (pw == 11 && ph == 11)
+    hipLaunchKernelGGL((mi_lane_kernel<11, 11>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
+                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, (int)(4 * mi_tab_size(npx)), dout);
+  else if (pw == 10 && ph == 10)
+    hipLaunchKernelGGL((mi_lane_kernel<10, 10>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
+                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, (int)(4 * mi_tab_size(npx)), dout);
   else
-    hipLaunchKernelGGL(mi_batch_kernel<256>, dim3(blocks), dim3(kMiBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
-                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, dout);
-  return me_check_launch(c, "mi_batch_kernel");
+    hipLaunchKernelGGL((mi_lane_kernel<0, 0>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
+                       img_bytes_R, dxyL, dxyR, n, pw, ph, tab, (int)(4 * mi_tab_size(npx)), dout);
+  return me_check_launch(c, "mi_lane_kernel");
 }
 
 int me_mi_table(me_ctx* c, int npx, const float** out) {
