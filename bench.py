@@ -42,6 +42,11 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
+    ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
+                    help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
+                         "each timed launch adds two event records to the stream), every family, or none")
+    ap.add_argument("--profile-steps", type=int, default=3,
+                    help="untimed steps with every family timed, to pick the dominant family")
     return ap.parse_args()
 
 
@@ -145,10 +150,38 @@ def alg_work(family: str, cfg: dict, frames):
     if family == "BA_POINTS":
         return hbm(no * 72.0 + npt * (72 + 72 + 72 + 24))             # V_o/g_o in; V, g, L_p, z out
     if family == "BA_SCHUR":
-        return ("mfma", 2.0 * 3 * npt * (n6 * (n6 + 1) / 2 + n6), "TFLOP/s", PEAK_F64_MFMA_TFS)
+        # useful Schur-fill flops: per landmark with k observations by variable
+        # cameras 108 k + 216 k (k + 1) / 2 + 60 -- not the padded dense GEMM the kernel runs
+        k = np.bincount(fd.pt_idx[fd.cam_idx >= fd.fixed_frames], minlength=npt).astype(np.float64)
+        return ("mfma", float(np.sum(108.0 * k + 108.0 * k * (k + 1) + 60.0)), "TFLOP/s", PEAK_F64_MFMA_TFS)
     if family == "BA_STEP":
         return hbm(no * (144 + 24 + 320 + 32 + 8 + 72.0))
     return None
+
+
+# kernels of each timed family (the PMC traffic of a family launch is their sum)
+FAMILY_KERNELS = {
+    "SCALE_RES": ["scale_residual_kernel"], "SCALE_NEQ": ["scale_neq_kernel"], "KLT": ["klt_kernel"],
+    "BA_LINEARIZE": ["linearize_kernel"], "BA_POINTS": ["pt_assemble_kernel"],
+    "BA_SCHUR": ["y_block_kernel", "schur_gemm_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
+    "BA_STEP": ["obs_backsub_kernel", "pt_backsub_kernel", "obs_step_kernel"], "MI": ["mi_lane_kernel"],
+}
+
+
+def pmc_traffic(family: str):
+    """HBM bytes per family launch from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools_pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench); None if absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    ks = FAMILY_KERNELS.get(family, [])
+    if not ks or any(k not in d for k in ks):
+        return None
+    return float(sum(d[k]["traffic_bytes"] for k in ks))
 
 
 def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
@@ -182,7 +215,7 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
     avg = ms / max(n, 1)
     achieved = 262.0 * n_pairs / (avg * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": None, "kernel": "mi_batch_kernel",
+            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc_traffic("MI"), "kernel": "mi_lane_kernel",
             "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
 
 
@@ -218,13 +251,27 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    fam_names = ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_POINTS", "BA_SCHUR", "BA_SOLVE", "BA_STEP",
+                 "KLT", "PYR")
     stats = dict(frames=0, ba_iters=0, scale_iters=0)
     for i in range(args.warmup):
         gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
     ctx.synchronize()
-    # kernel timing with HIP events on the ctx stream, live in the timed region
+    # untimed profile steps with every family timed: per-family device time and
+    # the dominant family (by device time) among those with a roofline
     ctx.timing_reset()
     ctx.timing(True)
+    for i in range(args.profile_steps):
+        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+    ctx.synchronize()
+    ctx.timing(False)
+    prof = {f: ctx.timing_read(f) for f in fam_names}
+    rl = {f: alg_work(f, cfg, frames) for f in fam_names if prof[f][0] > 0}
+    dom = max((f for f in rl if rl[f] is not None), key=lambda f: prof[f][1])
+    # timed region: HIP events on the ctx stream around the dominant family only
+    ctx.timing_reset()
+    if args.timing != "none":
+        ctx.timing(True, None if args.timing == "all" else [dom])
     stats = dict(frames=0, ba_iters=0, scale_iters=0)
     barrier()
     torch.cuda.synchronize()
@@ -237,8 +284,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     barrier()
     ctx.timing(False)
-    fams = {f: ctx.timing_read(f) for f in ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_POINTS", "BA_SCHUR",
-                                            "BA_SOLVE", "BA_STEP", "KLT", "PYR")}
+    fams = {f: ctx.timing_read(f) for f in fam_names}
     t_max = elapsed
     frames_total = stats["frames"]
     ba_total = stats["ba_iters"]
@@ -250,17 +296,15 @@ def main():
         dist.all_reduce(cnt)
         frames_total, ba_total = int(cnt[0].item()), int(cnt[1].item())
     value = frames_total / t_max
-    # dominant kernel family (by measured device time) among those with a roofline
-    rl = {f: alg_work(f, cfg, frames) for f in fams if fams[f][0] > 0}
-    dom = max((f for f in rl if rl[f] is not None), key=lambda f: fams[f][1])
     bound, amount, unit, peak = rl[dom]
-    n_l, ms_l = fams[dom]
+    n_l, ms_l = fams[dom] if fams[dom][0] > 0 else prof[dom]
     avg_ms = ms_l / n_l
     scale_u = 1e9 if unit == "GB/s" else 1e12
     achieved = amount / (avg_ms * 1e-3) / scale_u
     roofline = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 5), "traffic": None, "kernel": dom,
-                "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount}
+                "frac": round(achieved / peak, 5), "traffic": pmc_traffic(dom), "kernel": dom,
+                "kernels": FAMILY_KERNELS.get(dom), "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount,
+                "timed_live": fams[dom][0] > 0}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -296,7 +340,7 @@ def main():
             "roofline": roofline,
             "mi_roofline": mi_rl,
             "cpu_baseline": cpu,
-            "kernel_ms": {f: [fams[f][0], round(fams[f][1], 3)] for f in fams},
+            "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
             "gen_s": round(gen_s, 1),
         }
         print(json.dumps(out))

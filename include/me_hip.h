@@ -61,12 +61,14 @@ int me_memcpy_d2h(me_ctx* ctx, void* dst, const void* src, size_t bytes);
 int me_memcpy_d2d(me_ctx* ctx, void* dst, const void* src, size_t bytes);
 
 /* Per-kernel timing with HIP events on the ctx stream (for bench.py's
-   roofline): enable, then read the number of launches and the summed
-   milliseconds of a kernel family. */
+   roofline): enable a bitmask of families (bit k = ME_KT k; ME_KT_ALL = every
+   family, 0 = off), then read the number of launches and the summed
+   milliseconds of a family.  Each timed launch adds two event records to the
+   stream, so time only the families a measurement needs. */
 enum { ME_KT_MI = 0, ME_KT_SCALE_RES = 1, ME_KT_SCALE_NEQ = 2, ME_KT_BA_LINEARIZE = 3, ME_KT_BA_POINTS = 4,
        ME_KT_BA_SCHUR = 5, ME_KT_BA_SOLVE = 6, ME_KT_BA_STEP = 7, ME_KT_KLT = 8, ME_KT_PYR = 9, ME_KT_NMS = 10,
-       ME_KT_COUNT = 16 };
-int me_timing_enable(me_ctx* ctx, int on);
+       ME_KT_COUNT = 16, ME_KT_ALL = 0xffff };
+int me_timing_enable(me_ctx* ctx, int family_mask);
 int me_timing_read(me_ctx* ctx, int kernel, long* launches, double* total_ms);
 int me_timing_reset(me_ctx* ctx);
 

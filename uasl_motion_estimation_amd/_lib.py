@@ -269,8 +269,12 @@ class Context:
         self.check(self.lib.me_memcpy_d2d(self.h, c_void_p(dst), c_void_p(src), int(nbytes)), "me_memcpy_d2d")
 
     # --- kernel timing (HIP events on the ctx stream) ---
-    def timing(self, on: bool = True):
-        self.check(self.lib.me_timing_enable(self.h, 1 if on else 0))
+    def timing(self, on: bool = True, families=None):
+        """Enable HIP-event timing of every kernel family, or only of `families` (names of KT)."""
+        mask = 0
+        if on:
+            mask = 0xFFFF if families is None else sum(1 << KT[f] for f in families)
+        self.check(self.lib.me_timing_enable(self.h, mask))
 
     def timing_reset(self):
         self.check(self.lib.me_timing_reset(self.h))

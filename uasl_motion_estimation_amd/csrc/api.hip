@@ -72,14 +72,14 @@ static hipEvent_t pool_get(me_ctx* c) {
 }
 
 me_ktimer::me_ktimer(me_ctx* ctx, int kernel) : c(ctx), k(kernel) {
-  if (c && c->timing) {
+  if (c && (c->timing >> kernel & 1)) {
     a = pool_get(c);
     b = pool_get(c);
     if (a) hipEventRecord(a, c->stream);
   }
 }
 me_ktimer::~me_ktimer() {
-  if (c && c->timing && a && b) {
+  if (c && a && b) {
     hipEventRecord(b, c->stream);
     c->pending.push_back({a, b, k});
   }
@@ -124,6 +124,12 @@ int me_create(me_ctx** out, int dev) {
   c->stream = c->own_stream;
   if (hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c->num_cu <= 0)
     c->num_cu = 256;
+  for (auto& e : c->poll_ev) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      me_destroy(c);
+      return ME_ERR_HIP;
+    }
+  }
   c->slot_ptr.assign(SLOT_COUNT, nullptr);
   c->slot_size.assign(SLOT_COUNT, 0);
   *out = c;
@@ -141,6 +147,8 @@ void me_destroy(me_ctx* c) {
     if (t) hipFree(t);
   if (c->pinned) hipHostFree(c->pinned);
   for (auto e : c->event_pool) hipEventDestroy(e);
+  for (auto e : c->poll_ev)
+    if (e) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->own_stream);
   delete c;
 }
@@ -184,8 +192,8 @@ int me_memcpy_d2d(me_ctx* c, void* d, const void* s, size_t n) {
   return ME_OK;
 }
 
-int me_timing_enable(me_ctx* c, int on) {
-  c->timing = on != 0;
+int me_timing_enable(me_ctx* c, int family_mask) {
+  c->timing = family_mask & ME_KT_ALL;
   return ME_OK;
 }
 int me_timing_read(me_ctx* c, int k, long* launches, double* ms) {

@@ -1418,6 +1418,7 @@ struct Plan {
   double* Uraw = nullptr;
   double* cpart = nullptr;  // camera assembly partials (m x ck x 27)
   double* host = nullptr;  // pinned staging (inputs in, State / results out)
+  State* hstate[2] = {nullptr, nullptr};  // pinned slots of the pipelined State polls
   bool dev = false;        // problem arrays are device-resident
   size_t solve_lds = 0;
   int use_lds = 0;
@@ -1554,8 +1555,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   b.bvec = b.S + (size_t)g.n6 * g.n6;
   b.diagU = b.bvec + g.n6;
   void* hp;
-  ME_TRY(me_pinned(c, std::max(8 * out_doubles, dev ? (size_t)0 : input_span) + 64, &hp));
+  const size_t stage = rup((long)std::max(8 * out_doubles, dev ? (size_t)0 : input_span), 64);
+  ME_TRY(me_pinned(c, stage + 2 * rup(sizeof(State), 64), &hp));
   P.host = (double*)hp;
+  P.hstate[0] = (State*)((char*)hp + stage);
+  P.hstate[1] = (State*)((char*)hp + stage + rup(sizeof(State), 64));
   P.dev = dev;
   hipStream_t s = c->stream;
   if (!dev) {
@@ -1692,15 +1696,6 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   return me_check_launch(c, "BA iteration");
 }
 
-int read_state(Plan& P, State* st) {
-  me_ctx* c = P.c;
-  ME_HIP(c, hipMemcpyAsync(P.host, P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
-  ME_HIP(c, hipStreamSynchronize(c->stream));
-  std::memcpy(st, P.host, sizeof(State));
-  std::memcpy(P.c->dbg, st->stamps, sizeof(st->stamps));
-  return ME_OK;
-}
-
 int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
@@ -1744,13 +1739,25 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
   ME_HIP(c, hipSetDevice(c->device));
   Plan P;
   ME_TRY(plan_build(c, p, opt, P, 0));
-  // enqueue the whole solve; poll the device state every `chunk` iterations
+  // Enqueue the solve in chunks of iterations.  The device State after each
+  // chunk is copied to a pinned slot behind an event, and the host inspects
+  // chunk k only after chunk k + 1 is queued, so the GPU never drains while
+  // the host polls; after convergence at most one chunk of no-op launches
+  // (every kernel tests State::done first) is left in the queue.
   const int chunk = 4;
-  for (int it = 0; it <= opt->max_num_iterations; it += chunk) {
-    for (int k = 0; k < chunk && it + k <= opt->max_num_iterations; ++k) ME_TRY(enqueue_iteration(P, ar, user));
-    State st;
-    ME_TRY(read_state(P, &st));
-    if (st.done) break;
+  int it = 0;
+  auto enqueue_chunk = [&](int slot) -> int {
+    for (int k = 0; k < chunk && it <= opt->max_num_iterations; ++k, ++it) ME_TRY(enqueue_iteration(P, ar, user));
+    ME_HIP(c, hipMemcpyAsync(P.hstate[slot], P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+    ME_HIP(c, hipEventRecord(c->poll_ev[slot], c->stream));
+    return ME_OK;
+  };
+  ME_TRY(enqueue_chunk(0));
+  for (int cur = 0;; cur ^= 1) {
+    const bool more = it <= opt->max_num_iterations;
+    if (more) ME_TRY(enqueue_chunk(cur ^ 1));
+    ME_HIP(c, hipEventSynchronize(c->poll_ev[cur]));
+    if (P.hstate[cur]->done || !more) break;
   }
   return finish(P, p, sum);
 }

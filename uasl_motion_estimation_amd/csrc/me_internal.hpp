@@ -26,11 +26,12 @@ struct me_ctx {
   void* pinned = nullptr;
   size_t pinned_size = 0;
   // kernel timing
-  bool timing = false;
+  int timing = 0;  // bitmask of timed kernel families (ME_KT_*)
   std::vector<me_timer_pair> pending;
   std::vector<hipEvent_t> event_pool;
   long launches[ME_KT_COUNT] = {0};
   double total_ms[ME_KT_COUNT] = {0};
+  hipEvent_t poll_ev[2] = {nullptr, nullptr};  // device-state read-back events of iterative solves
   long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
   // MI term tables, one per patch pixel count N (built on first use, mi.hip)
   float* mi_table[256] = {nullptr};

@@ -611,6 +611,7 @@ struct ScaleProblem {
   ScaleLM* lm;
   char* host;   // pinned: input staging | LM state
   ScaleLM* hlm;
+  ScaleLM* hlm2;  // second pinned poll slot
 };
 
 int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
@@ -665,9 +666,10 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   ME_TRY(me_scratch(c, SLOT_SC_TRACKS, total, &d));
   char* base = (char*)d;
   void* ph;
-  ME_TRY(me_pinned(c, up(in_span) + up(sizeof(ScaleLM)) + 256, &ph));
+  ME_TRY(me_pinned(c, up(in_span) + 2 * up(sizeof(ScaleLM)) + 256, &ph));
   P.host = (char*)ph;
   P.hlm = (ScaleLM*)(P.host + up(in_span));  // separate from the input staging (async H2D)
+  P.hlm2 = (ScaleLM*)(P.host + up(in_span) + up(sizeof(ScaleLM)));
   PrepArgs pa;
   pa.mask = has_mask ? (const uint8_t*)(base + oMask) : nullptr;
   pa.mask_len = has_mask ? s->mask_len : 0;
@@ -900,10 +902,15 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     hipLaunchKernelGGL(scale_ctrl_kernel, dim3(1), dim3(kRedBlock), 0, st, P.lm, lp, phase, (const double*)dst,
                        (const double*)nullptr, (const int*)P.err);
   };
+  // LM iterations are enqueued in blocks; the device state after each block
+  // is copied to one of two pinned slots behind an event, and the host reads
+  // block k's state only after block k + 1 is queued (the GPU never drains
+  // while the host polls; kernels of a finished solve return at once).
   constexpr int kBlocksPerPoll = 2;
   const long max_blocks = 64L * (p.max_nb_iter + 2);
-  ScaleLM& hs = *P.hlm;
-  for (long blk = 0;; blk += kBlocksPerPoll) {
+  ScaleLM* slot[2] = {P.hlm, P.hlm2};
+  long blk = 0;
+  auto enqueue_blocks = [&](int sl) -> int {
     for (int b = 0; b < kBlocksPerPoll; ++b) {
       res(PH_A, 0, P.res);
       if (P.n > 0 && !test) {
@@ -917,12 +924,22 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
       res(PH_C, 1, P.res2);
       res(PH_D, 0, P.res2);
     }
+    blk += kBlocksPerPoll;
     ME_TRY(me_check_launch(c, "scale optimise"));
-    ME_HIP(c, hipMemcpyAsync(&hs, P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
-    ME_HIP(c, hipStreamSynchronize(st));
-    if (hs.phase == PH_DONE) break;
-    if (blk + kBlocksPerPoll >= max_blocks) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
+    ME_HIP(c, hipMemcpyAsync(slot[sl], P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
+    ME_HIP(c, hipEventRecord(c->poll_ev[sl], st));
+    return ME_OK;
+  };
+  ME_TRY(enqueue_blocks(0));
+  int cur = 0;
+  for (;; cur ^= 1) {
+    const bool more = blk < max_blocks;
+    if (more) ME_TRY(enqueue_blocks(cur ^ 1));
+    ME_HIP(c, hipEventSynchronize(c->poll_ev[cur]));
+    if (slot[cur]->phase == PH_DONE) break;
+    if (!more) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
   }
+  ScaleLM& hs = *slot[cur];
   if (hs.err) return check_err(c, hs.err);
   const int nt = std::min(std::min(hs.ntrace, kTraceCap), std::max(trace_cap, 0));
   if (trace && nt > 0)
