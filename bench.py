@@ -155,7 +155,7 @@ def alg_work(family: str, cfg: dict, frames):
         k = np.bincount(fd.pt_idx[fd.cam_idx >= fd.fixed_frames], minlength=npt).astype(np.float64)
         return ("mfma", float(np.sum(108.0 * k + 108.0 * k * (k + 1) + 60.0)), "TFLOP/s", PEAK_F64_MFMA_TFS)
     if family == "BA_STEP":
-        return hbm(no * (144 + 24 + 320 + 32 + 8 + 72.0))
+        return hbm(no * (144 + 320 + 32 + 8 + 8 + 48.0) + npt * (24 + 72 + 72 + 48))  # W_o, r+J, obs, idx, cams | point
     return None
 
 
@@ -164,7 +164,7 @@ FAMILY_KERNELS = {
     "SCALE_RES": ["scale_residual_kernel"], "SCALE_NEQ": ["scale_neq_kernel"], "KLT": ["klt_kernel"],
     "BA_LINEARIZE": ["linearize_kernel"], "BA_POINTS": ["pt_assemble_kernel"],
     "BA_SCHUR": ["y_block_kernel", "schur_gemm_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
-    "BA_STEP": ["obs_backsub_kernel", "pt_backsub_kernel", "obs_step_kernel"], "MI": ["mi_lane_kernel"],
+    "BA_STEP": ["pt_step_kernel"], "MI": ["mi_lane_kernel"],
 }
 
 

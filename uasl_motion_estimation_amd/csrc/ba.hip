@@ -947,104 +947,103 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   }
 }
 
-// Per CSR slot: t_q = W_q^T (Dc y_c) of the point back-substitution (3 doubles),
-// so the per-point kernel sums contiguous values instead of chasing
-// camera indices observation by observation.
-__global__ __launch_bounds__(kBlock) void obs_backsub_kernel(Geo g, Bufs b) {
-  const State* st = b.st;
-  if (st->done || st->fail) return;
-  const int q = blockIdx.x * kBlock + threadIdx.x;
-  if (q >= g.no) return;
-  const int ci = b.p_cam[q];
-  double* t = b.tq + 3 * (long)q;
-  if (ci < 0) {
-    t[0] = t[1] = t[2] = 0.0;
-    return;
-  }
-  const double* W = b.Wo + 18 * (long)q;
-  const double* y = b.yc + 6 * ci;
-  const double* cs = b.csc + 6 * ci;
-  double ys[6];
-  for (int a = 0; a < 6; ++a) ys[a] = cs[a] * y[a];
-  for (int c = 0; c < 3; ++c) {
-    double s = 0;
-    for (int a = 0; a < 6; ++a) s += W[a * 3 + c] * ys[a];
-    t[c] = s;
-  }
+// Point back-substitution and step evaluation, 16 lanes per point (one
+// launch for what were three: per-slot W^T Dc y_c, per-point solve, per-
+// observation model change / candidate cost).  The lanes of a point take its
+// CSR slots round-robin; the slot sums are reduced across the 16 lanes, every
+// lane then solves the point's 3x3 system redundantly (no broadcast), and
+// each lane evaluates the model cost change and the candidate cost of its own
+// observations.  Partials per workgroup, reduced in fixed order by
+// step_finalize (deterministic).
+constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
+
+template <int W>
+__device__ __forceinline__ double group_sum(double x) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+  return x;
 }
 
-
-__global__ __launch_bounds__(kPtBlock) void pt_backsub_kernel(Geo g, Bufs b) {
-  __shared__ double lds[8];
+__global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
+  __shared__ double lds[16];
   const State* st = b.st;
   if (st->done) return;
-  const int j = blockIdx.x * kPtBlock + threadIdx.x;
-  double s2 = 0, xn2 = 0;
-  if (j < g.np && !st->fail) {
+  const int gl = threadIdx.x & (kStepG - 1);
+  const int j = blockIdx.x * kStepPts + (threadIdx.x / kStepG);
+  double mc = 0, cc = 0, s2 = 0, xn2 = 0;
+  if (j < g.np && !st->fail) {  // uniform within a 16-lane group
+    const int beg = b.p_off[j], end = b.p_off[j + 1];
+    // (1) sum over the point's slots of W_q^T (Dc y_c)
+    double t[3] = {0.0, 0.0, 0.0};
+    for (int q = beg + gl; q < end; q += kStepG) {
+      const int ci = b.p_cam[q];
+      if (ci < 0) continue;
+      const double* W = b.Wo + 18 * (long)q;
+      const double* y = b.yc + 6 * ci;
+      const double* cs = b.csc + 6 * ci;
+      double ys[6];
+      for (int a = 0; a < 6; ++a) ys[a] = cs[a] * y[a];
+      for (int c = 0; c < 3; ++c) {
+        double s = 0;
+        for (int a = 0; a < 6; ++a) s += W[a * 3 + c] * ys[a];
+        t[c] += s;
+      }
+    }
+    for (int c = 0; c < 3; ++c) t[c] = group_sum<kStepG>(t[c]);
+    // (2) point step y_p = -(V + D/r)^-1 (g_p + sum) in the scaled space, candidate point
     const double* ps = b.psc + 3 * (long)j;
-    double rhs[3] = {-b.gps[3 * (long)j], -b.gps[3 * (long)j + 1], -b.gps[3 * (long)j + 2]};
-    double tsum[3] = {0, 0, 0};
-    for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q)
-      for (int c = 0; c < 3; ++c) tsum[c] += b.tq[3 * (long)q + c];
-    for (int c = 0; c < 3; ++c) rhs[c] -= tsum[c] * ps[c];
+    double rhs[3];
+    for (int c = 0; c < 3; ++c) rhs[c] = -b.gps[3 * (long)j + c] - t[c] * ps[c];
     const double* L = b.Lp + 9 * (long)j;
     double u[3], yp[3];
     fwd3(L, rhs, u);
     bwd3(L, u, yp);
     const int cur = st->cur;
     const double* x = b.pts[cur] + 3 * (long)j;
-    double* xc = b.pts[1 - cur] + 3 * (long)j;
+    double d[3], xc[3];
     for (int a = 0; a < 3; ++a) {
-      const double d = yp[a] * ps[a];
-      b.dp[3 * (long)j + a] = d;
-      double v = x[a] + d;
-      v = fmin(fmax(v, g.lo[a]), g.hi[a]);
-      xc[a] = v;
-      const double dd = v - x[a];
-      s2 += dd * dd;
-      xn2 += x[a] * x[a];
+      d[a] = yp[a] * ps[a];
+      xc[a] = fmin(fmax(x[a] + d[a], g.lo[a]), g.hi[a]);
     }
-  }
-  double v2[2] = {s2, xn2}, out[2];
-  block_sum<2>(v2, out, lds);
-  if (threadIdx.x == 0) {
-    b.part[R_STEP2 * g.pstride + blockIdx.x] = out[0];
-    b.part[R_XN2 * g.pstride + blockIdx.x] = out[1];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void obs_step_kernel(Geo g, Bufs b) {
-  __shared__ double lds[8];
-  const State* st = b.st;
-  if (st->done) return;
-  const int o = blockIdx.x * kBlock + threadIdx.x;
-  double mc = 0, cc = 0;
-  if (o < g.no && !st->fail) {
-    const double* L = b.lin + (long)o * kLinStride;
-    const int ci = b.cam_idx[o] - g.nf, pi = b.pt_idx[o];
-    const double* dp = b.dp + 3 * (long)pi;
-    for (int k = 0; k < 4; ++k) {
-      double jd = 0;
-      if (ci >= 0) {
-        const double* dc = b.dc + 6 * ci;
-        for (int j = 0; j < 6; ++j) jd += L[4 + k * 6 + j] * dc[j];
+    if (gl == 0) {
+      for (int a = 0; a < 3; ++a) {
+        b.dp[3 * (long)j + a] = d[a];
+        b.pts[1 - cur][3 * (long)j + a] = xc[a];
+        const double dd = xc[a] - x[a];
+        s2 += dd * dd;
+        xn2 += x[a] * x[a];
       }
-      jd += L[28 + k * 3 + 0] * dp[0] + L[28 + k * 3 + 1] * dp[1] + L[28 + k * 3 + 2] * dp[2];
-      mc -= jd * (L[k] + jd / 2.0);
     }
-    const int nb = 1 - st->cur;
-    double r[4];
-    stereo_residual(g, b.cams[nb] + 6 * b.cam_idx[o], b.pts[nb] + 3 * pi, b.obs + 4 * (long)o, r, nullptr, nullptr);
-    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
-    double rho0, sc;
-    huber(s, &rho0, &sc);
-    cc = 0.5 * rho0;
+    // (3) model cost change and candidate cost of the point's observations
+    const double* cams_c = b.cams[1 - cur];
+    for (int q = beg + gl; q < end; q += kStepG) {
+      const int o = b.p_obs[q];
+      const double* Lo = b.lin + (long)o * kLinStride;
+      const int ci = b.cam_idx[o] - g.nf;
+      for (int k = 0; k < 4; ++k) {
+        double jd = 0;
+        if (ci >= 0) {
+          const double* dc = b.dc + 6 * ci;
+          for (int i = 0; i < 6; ++i) jd += Lo[4 + k * 6 + i] * dc[i];
+        }
+        jd += Lo[28 + k * 3 + 0] * d[0] + Lo[28 + k * 3 + 1] * d[1] + Lo[28 + k * 3 + 2] * d[2];
+        mc -= jd * (Lo[k] + jd / 2.0);
+      }
+      double r[4];
+      stereo_residual(g, cams_c + 6 * b.cam_idx[o], xc, b.obs + 4 * (long)o, r, nullptr, nullptr);
+      const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+      double rho0, sc;
+      huber(s, &rho0, &sc);
+      cc += 0.5 * rho0;
+    }
   }
-  double v2[2] = {mc, cc}, out[2];
-  block_sum<2>(v2, out, lds);
+  double v4[4] = {mc, cc, s2, xn2}, out[4];
+  block_sum<4>(v4, out, lds);
   if (threadIdx.x == 0) {
     b.part[R_MODEL * g.pstride + blockIdx.x] = out[0];
     b.part[R_CAND * g.pstride + blockIdx.x] = out[1];
+    b.part[R_STEP2 * g.pstride + blockIdx.x] = out[2];
+    b.part[R_XN2 * g.pstride + blockIdx.x] = out[3];
   }
 }
 
@@ -1107,11 +1106,9 @@ __global__ __launch_bounds__(kFinBlock) void step_finalize_kernel(Geo g, Bufs b,
   State* st = b.st;
   if (st->done) return;
   double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) {
+  for (int i = threadIdx.x; i < g.nblk_step; i += kFinBlock) {
     v[0] += b.part[R_MODEL * g.pstride + i];
     v[1] += b.part[R_CAND * g.pstride + i];
-  }
-  for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) {
     v[2] += b.part[R_STEP2 * g.pstride + i];
     v[3] += b.part[R_XN2 * g.pstride + i];
   }
@@ -1460,7 +1457,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.jacobi = opt->jacobi_scaling ? 1 : 0;
   g.ck = (int)std::min(64L, std::max(1L, rup(std::max(g.no, 1), (long)std::max(g.m, 1) * kBlock) /
                                              ((long)std::max(g.m, 1) * kBlock)));
-  g.pstride = std::max(g.nblk_obs, g.nblk_pts);
+  g.nblk_step = (int)std::max(1L, rup(std::max(g.np, 1), kStepPts) / kStepPts);
+  g.pstride = std::max({g.nblk_obs, g.nblk_pts, g.nblk_step});
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
   g.baseline = p->baseline;
@@ -1487,7 +1485,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   o.max_invalid = opt->max_num_consecutive_invalid_steps;
   const bool dev = p->mem == ME_DEVICE;
   // one arena; the five inputs first and contiguous (one H2D for host input)
-  const long nb = std::max(g.nblk_obs, g.nblk_pts);
+  const long nb = g.pstride;
   Bufs& b = P.b;
   std::vector<std::pair<size_t, void**>> items;
   auto add = [&](size_t bytes, void* dst) { items.push_back({rup((long)std::max<size_t>(bytes, 8), 256), (void**)dst}); };
@@ -1512,7 +1510,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);
   add((size_t)g.no, &b.dup);
   add(8 * solve_a_doubles(g.Ts), &b.Abuf);
-  add(8 * 3 * (size_t)g.no, &b.tq);
   add(8 * 18 * (size_t)g.no, &b.Wo);
   add(8 * (size_t)g.n6, &b.csc);
   add(8 * 3 * (size_t)g.np, &b.psc);
@@ -1684,9 +1681,7 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
-    hipLaunchKernelGGL(obs_backsub_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
-    hipLaunchKernelGGL(pt_backsub_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b);
-    hipLaunchKernelGGL(obs_step_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    hipLaunchKernelGGL(pt_step_kernel, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
   }
   hipLaunchKernelGGL(step_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
   if (ar) {

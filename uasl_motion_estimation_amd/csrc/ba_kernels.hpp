@@ -15,9 +15,9 @@
 //                  split-K partials (deterministic, no atomics).
 //   cam_solve      one workgroup: S = U + D/radius - sum(partials), dense
 //                  Cholesky, y_c = -S^-1 b, candidate cameras.
-//   pt_backsub     one lane per point: y_p, candidate points (bounds
-//                  projection), step norms.
-//   obs_step       per observation: model cost change and candidate cost.
+//   pt_step        16 lanes per point: y_p, candidate point (bounds
+//                  projection), step norms, and the model cost change and
+//                  candidate cost of the point's observations.
 //   decide         one workgroup: Ceres LM acceptance / radius / termination.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -61,7 +61,7 @@ struct State {
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, pstride, jacobi, ck;
+  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, nblk_step, pstride, jacobi, ck;
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -104,7 +104,6 @@ struct Bufs {
   double* yc;         // n6
   double* dc;         // n6 camera step (unscaled)
   double* dp;         // 3np point step (unscaled)
-  double* tq;         // 3 per CSR slot: W_q^T Dc y_c
   double* part;       // R_COUNT * max(nblk_obs, nblk_pts)
   double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
   State* st;
