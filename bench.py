@@ -162,8 +162,8 @@ def alg_work(family: str, cfg: dict, frames):
 # kernels of each timed family (the PMC traffic of a family launch is their sum)
 FAMILY_KERNELS = {
     "SCALE_RES": ["scale_residual_kernel"], "SCALE_NEQ": ["scale_neq_kernel"], "KLT": ["klt_kernel"],
-    "BA_LINEARIZE": ["linearize_kernel"], "BA_POINTS": ["pt_assemble_kernel"],
-    "BA_SCHUR": ["y_block_kernel", "schur_gemm_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
+    "BA_LINEARIZE": ["linearize_kernel"],
+    "BA_SCHUR": ["pt_schur_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
     "BA_STEP": ["pt_step_kernel"], "MI": ["mi_lane_kernel"],
 }
 

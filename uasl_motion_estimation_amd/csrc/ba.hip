@@ -48,6 +48,14 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* 
   __syncthreads();
 }
 
+// sum over aligned groups of W lanes (xor butterfly: every lane gets the total)
+template <int W>
+__device__ __forceinline__ double group_sum(double x) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+  return x;
+}
+
 __device__ __forceinline__ double block_max(double v, double* lds) {
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_down(v, off, 64));
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -334,62 +342,235 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
   x[0] = (y[0] - L[3] * x[1] - L[6] * x[2]) / L[0];
 }
 
-// One lane per point.  After a linearisation: sum V_o, g_o over the point's
-// CSR range, Jacobi scaling at iteration 0 (diag V = squared column norms),
-// projected-gradient max-norm contribution.  Every iteration: V + D/radius ->
-// Cholesky L_p and z_p = L_p^-1 g_p (the point half of the Schur step).
-__global__ __launch_bounds__(kPtBlock) void pt_assemble_kernel(Geo g, Bufs b, Opts o) {
-  __shared__ double lds[4];
+// Point blocks and Schur complement in one pass over the landmarks.  A
+// workgroup (8 waves) takes sub-chunks of P landmarks; per sub-chunk:
+//  (A) a group of 32 lanes per landmark, one CSR slot per lane, every load
+//      issued in one round: V = sum V_o, g = sum g_o (after a linearisation;
+//      Jacobi scaling at iteration 0; projected-gradient max-norm), then
+//      V + D/radius -> Cholesky L_p, z_p = L_p^-1 g_p on every lane of the
+//      group (butterfly sums leave the totals on all of them: no staging);
+//  (B) each lane writes its slot's entries of the landmark's 3 rows of
+//      Y = (Dc W Dp) L_p^-T into LDS (duplicate residual blocks of one camera
+//      add in CSR order, no atomics), z_p as the extra column n6 (so Y^T Y
+//      also yields Y^T z);
+//  (C) S partial tiles D(16x16) += A(16x4) B(4x16) on v_mfma_f64_16x16x4f64
+//      (A[i][k] = Y[k][16I+i], B[k][j] = Y[k][16J+j]), one wave per tile,
+//      accumulated over all the workgroup's sub-chunks in registers.  A K-step
+//      of 4 rows is skipped for a tile when the rows' camera band (a track's
+//      cameras are contiguous in CSR order) misses the tile's columns.
+// Partials (workgroup x tile) are summed in fixed order by s_assemble:
+// deterministic, no atomics.  Operand map of the MFMA: lane l holds
+// A[l&15][l>>4] and B[l>>4][l&15]; result register i holds D[(l>>4)+4i][l&15].
+constexpr int kSchurBlock = 512;
+constexpr int kSchurPts = 16;                       // landmarks per sub-chunk (48 rows of Y)
+constexpr int kSchurLanes = kSchurBlock / kSchurPts;  // lanes per landmark in (A) and (B)
+__host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
+
+template <int W>
+__device__ __forceinline__ int group_min(int x) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off, W));
+  return x;
+}
+template <int W>
+__device__ __forceinline__ int group_max(int x) {
+#pragma unroll
+  for (int off = W / 2; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, W));
+  return x;
+}
+
+template <int NT>
+__global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+  extern __shared__ double smem[];
+  __shared__ double red[8];
   State* st = b.st;
   if (st->done) return;
-  const int need_lin = st->need_lin;
-  const int j = blockIdx.x * kPtBlock + threadIdx.x;
-  double gm = 0;
-  double Vs[9], gs[3];
-  if (j < g.np) {
-    if (need_lin) {
-      double V[6] = {0, 0, 0, 0, 0, 0}, gr[3] = {0, 0, 0};
-      for (int q = b.p_off[j]; q < b.p_off[j + 1]; ++q) {
-        const double* X = b.obsx + (long)q * kObsxStride;
-        for (int i = 0; i < 6; ++i) V[i] += X[i];
-        for (int a = 0; a < 3; ++a) gr[a] += X[6 + a];
-      }
-      double* ps = b.psc + 3 * (long)j;
-      if (!st->scaled) {
-        ps[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
-        ps[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
-        ps[2] = g.jacobi ? 1.0 / (1.0 + sqrt(V[5])) : 1.0;
-      }
-      const double p0 = ps[0], p1 = ps[1], p2 = ps[2];
-      Vs[0] = V[0] * p0 * p0; Vs[1] = V[1] * p0 * p1; Vs[2] = V[2] * p0 * p2;
-      Vs[3] = Vs[1];          Vs[4] = V[3] * p1 * p1; Vs[5] = V[4] * p1 * p2;
-      Vs[6] = Vs[2];          Vs[7] = Vs[5];          Vs[8] = V[5] * p2 * p2;
-      gs[0] = gr[0] * p0;
-      gs[1] = gr[1] * p1;
-      gs[2] = gr[2] * p2;
-      double* Vo = b.V + 9 * (long)j;
-      for (int i = 0; i < 9; ++i) Vo[i] = Vs[i];
-      for (int a = 0; a < 3; ++a) b.gps[3 * (long)j + a] = gs[a];
-      const double* x = b.pts[st->cur] + 3 * (long)j;
-      for (int a = 0; a < 3; ++a) {
-        const double xp = fmin(fmax(x[a] - gr[a], g.lo[a]), g.hi[a]);
-        gm = fmax(gm, fabs(x[a] - xp));
-      }
-    } else {
-      for (int i = 0; i < 9; ++i) Vs[i] = b.V[9 * (long)j + i];
-      for (int a = 0; a < 3; ++a) gs[a] = b.gps[3 * (long)j + a];
+  const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
+  const double radius = st->radius;
+  const int P = g.spts, Rz = g.Rpad, rows = 3 * P, nks = rows / 4;
+  double* Y = smem;
+  int* band = reinterpret_cast<int*>(Y + (size_t)rows * Rz);  // per landmark: first / last camera column, live
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int gi = tid / kSchurLanes, gl = tid & (kSchurLanes - 1);
+  // this wave's tiles (wave-uniform: scalar registers)
+  int tI[NT], tJ[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    int p = wave + 8 * u, I = 0;
+    if (p >= g.npairs) p = -1;
+    int rem = p < 0 ? 0 : p;
+    while (rem >= g.T - I) {
+      rem -= g.T - I;
+      ++I;
     }
-    const double radius = st->radius;
-    double A[9];
-    for (int i = 0; i < 9; ++i) A[i] = Vs[i];
-    for (int a = 0; a < 3; ++a) A[4 * a] += fmin(fmax(Vs[4 * a], o.min_diag), o.max_diag) / radius;
-    double* L = b.Lp + 9 * (long)j;
-    if (!chol3(A, L)) st->fail = 1;
-    else fwd3(L, gs, b.zp + 3 * (long)j);
+    tI[u] = p < 0 ? -1 : I;
+    tJ[u] = p < 0 ? -1 : I + rem;
+  }
+  double4_t acc[NT];
+#pragma unroll
+  for (int u = 0; u < NT; ++u) acc[u] = double4_t{0.0, 0.0, 0.0, 0.0};
+  double gm = 0;
+  for (int sc = blockIdx.x; sc < g.nsub; sc += gridDim.x) {
+    const int j = sc * P + gi;
+    double* Yp = Y + (size_t)(3 * gi) * Rz;  // this landmark's 3 rows, written by its own lane group only
+    for (int i = gl; i < 3 * Rz / 2; i += kSchurLanes) reinterpret_cast<double2*>(Yp)[i] = double2{0.0, 0.0};
+    if (j < g.np) {
+      // (A) every load of the landmark and of this lane's first CSR slot in one round
+      const int beg = b.p_off[j], end = b.p_off[j + 1];
+      const int q0 = beg + gl;
+      int ci0 = -1, cprev0 = -1;
+      double w0[18], cs0[6], X0[9];
+      for (int i = 0; i < 9; ++i) X0[i] = 0.0;
+      if (q0 < end) {
+        ci0 = b.p_cam[q0];
+        if (q0 > beg) cprev0 = b.p_cam[q0 - 1];
+        if (need_lin)
+          for (int i = 0; i < 9; ++i) X0[i] = b.obsx[(long)q0 * kObsxStride + i];
+        if (ci0 >= 0) {
+          for (int i = 0; i < 18; ++i) w0[i] = b.Wo[18 * (long)q0 + i];
+          for (int a = 0; a < 6; ++a) cs0[a] = b.csc[6 * ci0 + a];
+        }
+      }
+      double Vs[9], gs[3], pv[3], xv[3];
+      if (need_lin) {
+        for (int a = 0; a < 3; ++a) xv[a] = b.pts[cur][3 * (long)j + a];
+        if (scaled)
+          for (int a = 0; a < 3; ++a) pv[a] = b.psc[3 * (long)j + a];
+        double V[9];  // V_o (6 unique) | g_o (3)
+        for (int i = 0; i < 9; ++i) V[i] = X0[i];
+        for (int q = q0 + kSchurLanes; q < end; q += kSchurLanes)
+          for (int i = 0; i < 9; ++i) V[i] += b.obsx[(long)q * kObsxStride + i];
+        for (int i = 0; i < 9; ++i) V[i] = group_sum<kSchurLanes>(V[i]);
+        if (!scaled) {
+          pv[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
+          pv[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
+          pv[2] = g.jacobi ? 1.0 / (1.0 + sqrt(V[5])) : 1.0;
+        }
+        const double p0 = pv[0], p1 = pv[1], p2 = pv[2];
+        Vs[0] = V[0] * p0 * p0; Vs[1] = V[1] * p0 * p1; Vs[2] = V[2] * p0 * p2;
+        Vs[3] = Vs[1];          Vs[4] = V[3] * p1 * p1; Vs[5] = V[4] * p1 * p2;
+        Vs[6] = Vs[2];          Vs[7] = Vs[5];          Vs[8] = V[5] * p2 * p2;
+        gs[0] = V[6] * p0;
+        gs[1] = V[7] * p1;
+        gs[2] = V[8] * p2;
+        if (gl == 0) {
+          if (!scaled)
+            for (int a = 0; a < 3; ++a) b.psc[3 * (long)j + a] = pv[a];
+          for (int i = 0; i < 9; ++i) b.V[9 * (long)j + i] = Vs[i];
+          for (int a = 0; a < 3; ++a) b.gps[3 * (long)j + a] = gs[a];
+          for (int a = 0; a < 3; ++a) {
+            const double xp = fmin(fmax(xv[a] - V[6 + a], g.lo[a]), g.hi[a]);
+            gm = fmax(gm, fabs(xv[a] - xp));
+          }
+        }
+      } else {
+        for (int i = 0; i < 9; ++i) Vs[i] = b.V[9 * (long)j + i];
+        for (int a = 0; a < 3; ++a) {
+          gs[a] = b.gps[3 * (long)j + a];
+          pv[a] = b.psc[3 * (long)j + a];
+        }
+      }
+      // point block, redundantly on every lane of the group (the sums are group-uniform)
+      double A[9], L[9], z[3];
+      for (int i = 0; i < 9; ++i) A[i] = Vs[i];
+      for (int a = 0; a < 3; ++a) A[4 * a] += fmin(fmax(Vs[4 * a], o.min_diag), o.max_diag) / radius;
+      const bool ok = chol3(A, L);
+      fwd3(L, gs, z);
+      const double rL0 = 1.0 / L[0], rL4 = 1.0 / L[4], rL8 = 1.0 / L[8];
+      if (gl == 0) {
+        if (!ok) st->fail = 1;
+        for (int i = 0; i < 9; ++i) b.Lp[9 * (long)j + i] = L[i];
+        for (int a = 0; a < 3; ++a) b.zp[3 * (long)j + a] = z[a];
+      }
+      // (B) this lane's slots -> the landmark's rows of Y (first slot of each camera run only;
+      // duplicate residual blocks of one camera are summed in CSR order)
+      int lo = 1 << 29, hi = -1;
+      for (int q = q0; q < end; q += kSchurLanes) {
+        int ci, cp;
+        double w[18], cs[6];
+        if (q == q0) {
+          ci = ci0;
+          cp = cprev0;
+          if (ci >= 0) {
+            for (int i = 0; i < 18; ++i) w[i] = w0[i];
+            for (int a = 0; a < 6; ++a) cs[a] = cs0[a];
+          }
+        } else {
+          ci = b.p_cam[q];
+          cp = b.p_cam[q - 1];
+          if (ci >= 0) {
+            for (int i = 0; i < 18; ++i) w[i] = b.Wo[18 * (long)q + i];
+            for (int a = 0; a < 6; ++a) cs[a] = b.csc[6 * ci + a];
+          }
+        }
+        if (ci < 0) continue;
+        lo = min(lo, 6 * ci);
+        hi = max(hi, 6 * ci + 5);
+        if (cp == ci) continue;  // not the first slot of its camera run
+        for (int r = q + 1; r < end && b.p_cam[r] == ci; ++r)
+          for (int i = 0; i < 18; ++i) w[i] += b.Wo[18 * (long)r + i];
+        for (int a = 0; a < 6; ++a) {
+          const int col = 6 * ci + a;
+          const double wa[3] = {w[3 * a] * cs[a] * pv[0], w[3 * a + 1] * cs[a] * pv[1], w[3 * a + 2] * cs[a] * pv[2]};
+          double y[3];  // L y = wa with the diagonal reciprocals hoisted out of the slot loop
+          y[0] = wa[0] * rL0;
+          y[1] = (wa[1] - L[3] * y[0]) * rL4;
+          y[2] = (wa[2] - L[6] * y[0] - L[7] * y[1]) * rL8;
+          for (int k = 0; k < 3; ++k) Yp[(size_t)k * Rz + col] = y[k];
+        }
+      }
+      lo = group_min<kSchurLanes>(lo);
+      hi = group_max<kSchurLanes>(hi);
+      if (gl == 0) {
+        for (int k = 0; k < 3; ++k) Yp[(size_t)k * Rz + g.n6] = z[k];
+        band[3 * gi] = lo;
+        band[3 * gi + 1] = hi;
+        band[3 * gi + 2] = 1;  // z_p (column n6, tile T-1) is live for every landmark
+      }
+    } else if (gl == 0) {
+      band[3 * gi] = 1 << 29;
+      band[3 * gi + 1] = -1;
+      band[3 * gi + 2] = 0;
+    }
+    __syncthreads();
+    // (C) partial tiles on the matrix cores.  The K-step's camera band is
+    // wave-uniform (scalar registers, scalar branches); the operands of all its
+    // live tiles are read before the first MFMA of the step.
+    for (int ks = 0; ks < nks; ++ks) {
+      const int pa = (4 * ks) / 3, pb = min((4 * ks + 3) / 3, P - 1);
+      const int lo = __builtin_amdgcn_readfirstlane(min(band[3 * pa], band[3 * pb]));
+      const int hi = __builtin_amdgcn_readfirstlane(max(band[3 * pa + 1], band[3 * pb + 1]));
+      const int live = __builtin_amdgcn_readfirstlane(band[3 * pa + 2] | band[3 * pb + 2]);
+      const double* Yr = Y + (size_t)(4 * ks + (lane >> 4)) * Rz + (lane & 15);
+      bool hit[NT];
+      double av[NT], bv[NT];
+#pragma unroll
+      for (int u = 0; u < NT; ++u) {
+        const int I = tI[u], J = tJ[u];
+        // a tile is touched by these rows iff both its column blocks meet the camera band or the z column
+        const bool hitI = (hi >= 16 * I && lo <= 16 * I + 15) || (live && I == g.T - 1);
+        const bool hitJ = (hi >= 16 * J && lo <= 16 * J + 15) || (live && J == g.T - 1);
+        hit[u] = I >= 0 && hitI && hitJ;
+        av[u] = hit[u] ? Yr[16 * I] : 0.0;
+        bv[u] = hit[u] ? Yr[16 * J] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < NT; ++u)
+        if (hit[u]) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc[u], 0, 0, 0);
+    }
+    __syncthreads();
   }
   if (need_lin) {
-    const double r = block_max(gm, lds);
-    if (threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+    const double r = block_max(gm, red);
+    if (tid == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+  }
+#pragma unroll
+  for (int u = 0; u < NT; ++u) {
+    const int p = wave + 8 * u;
+    if (p >= g.npairs) continue;
+    double* dst = b.Spart + ((long)blockIdx.x * g.npairs + p) * 256;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[((lane >> 4) + 4 * i) * 16 + (lane & 15)] = acc[u][i];
   }
 }
 
@@ -397,16 +578,15 @@ __global__ __launch_bounds__(kPtBlock) void pt_assemble_kernel(Geo g, Bufs b, Op
 // partials (fixed order), Ceres gradient-tolerance test (IterationZero /
 // HandleSuccessfulStep), max-iteration and min-radius tests.
 constexpr int kFinBlock = 256;
-__global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, Opts o, const double* gc_raw,
-                                                                 int use_scal) {
-  __shared__ double lds[16];
+__device__ void lin_finalize_body(const Geo& g, const Bufs& b, const Opts& o, const double* gc_raw, int use_scal,
+                                  double* lds /* 16 */) {
   State* st = b.st;
   if (st->done) return;
   if (st->need_lin) {
     double c = 0, m = 0;
     if (!use_scal) {
       for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
-      for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+      for (int i = threadIdx.x; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
     }
     for (int i = threadIdx.x; i < g.n6; i += kFinBlock) m = fmax(m, fabs(gc_raw[i]));
     double v[1] = {c}, out[1];
@@ -441,6 +621,12 @@ __global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, 
   st->iterations += 1;
 }
 
+__global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, Opts o, const double* gc_raw,
+                                                                 int use_scal) {
+  __shared__ double lds[16];
+  lin_finalize_body(g, b, o, gc_raw, use_scal, lds);
+}
+
 // Sharded mode: local partial sums into scal (all-reduced by the host callback)
 __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) {
   __shared__ double lds[16];
@@ -449,7 +635,7 @@ __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) 
   double c = 0, m = 0;
   if (st->need_lin) {
     for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
-    for (int i = threadIdx.x; i < g.nblk_pts; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+    for (int i = threadIdx.x; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
   }
   double v[1] = {c}, out[1];
   block_sum<1>(v, out, lds);
@@ -460,140 +646,60 @@ __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) 
   }
 }
 
-// One lane per (point, column of a variable camera): column col = 6 c + a of
-// the point's 3 rows of the dense K-major Y = (Dc W Dp) L_p^-T, with W summed
-// over the point's observations by camera c (duplicate residual blocks add in
-// CSR order, no atomics) and zeros where c does not see the point.  Every
-// entry of Y's live region is rewritten each iteration (no memset; the
-// padding is zeroed once per solve); consecutive lanes store consecutive
-// columns.
-__global__ __launch_bounds__(kBlock) void y_block_kernel(Geo g, Bufs b) {
-  const State* st = b.st;
-  if (st->done || st->fail) return;
-  const long gid = (long)blockIdx.x * kBlock + threadIdx.x;
-  if (gid >= (long)g.np * g.n6) return;
-  const int j = (int)(gid / g.n6), col = (int)(gid - (long)j * g.n6);
-  const int ci = col / 6, a = col - 6 * ci;
-  double w[3] = {0.0, 0.0, 0.0};
-  const int beg = b.p_off[j], end = b.p_off[j + 1];
-  for (int q = beg; q < end; ++q) {
-    if (b.p_cam[q] != ci) continue;
-    const double* W = b.Wo + 18 * (long)q + 3 * a;
-    w[0] += W[0];
-    w[1] += W[1];
-    w[2] += W[2];
+// S = U - sum over the Schur workgroups' partial tiles, b = g - Y^T z, diag(U)
+// (sharded mode: the local pieces, no LM diagonal).  256 threads = 32
+// elements x 8 partial groups: group k sums partials k, k + 8, ... in order,
+// then the 8 group sums are added in order (deterministic); consecutive
+// threads read consecutive doubles of a tile row.
+constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
+// The grid's last workgroup runs the linearisation bookkeeping of
+// lin_finalize_kernel instead (one launch less per iteration): the assembly
+// blocks do not read what it writes, and the camera solve that follows
+// reads both.
+__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal) {
+  __shared__ double part[kSaGroups][kSaElems];
+  static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
+  if (blockIdx.x == gridDim.x - 1) {
+    lin_finalize_body(g, b, o, gc_raw, use_scal, &part[0][0]);
+    return;
   }
-  const double* L = b.Lp + 9 * (long)j;
-  const double* ps = b.psc + 3 * (long)j;
-  const double cs = b.csc[col];
-  const double wa[3] = {w[0] * cs * ps[0], w[1] * cs * ps[1], w[2] * cs * ps[2]};
-  double y[3];
-  fwd3(L, wa, y);
-  double* dst = b.Y + (long)(3 * j) * g.Rpad + col;
-  dst[0] = y[0];
-  dst[g.Rpad] = y[1];
-  dst[2 * (long)g.Rpad] = y[2];
-}
-
-// S partial tiles on the FP64 matrix cores: D(16x16) += A(16x4) B(4x16) with
-// A[i][k] = Y[k][16I+i], B[k][j] = Y[k][16J+j] (or z[k] for the b column).
-// Operand map of v_mfma_f64_16x16x4f64: lane l holds A[l&15][l>>4] and
-// B[l>>4][l&15]; result reg i holds D[(l>>4) + 4i][l&15].
-__global__ __launch_bounds__(kBlock) void schur_gemm_kernel(Geo g, Bufs b) {
-  __shared__ double tile[4][256];
-  const State* st = b.st;
-  if (st->done || st->fail) return;
-  const int p = blockIdx.x, s = blockIdx.y;
-  const int ntri = g.T * (g.T + 1) / 2;
-  int I, J;
-  if (p < ntri) {
-    int rem = p;
-    I = 0;
-    while (rem >= g.T - I) {
-      rem -= g.T - I;
-      ++I;
-    }
-    J = I + rem;
-  } else {
-    I = p - ntri;
-    J = g.T;
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int KC = g.Kpad / g.ksplit, KW = KC / 4;
-  const int k0 = s * KC + wave * KW;
-  double4_t acc = {0.0, 0.0, 0.0, 0.0};
-  const int col = lane & 15, kr = lane >> 4;
-  const double* Ya = b.Y + 16 * I + col;
-  if (J < g.T) {
-    const double* Yb = b.Y + 16 * J + col;
-    for (int k = k0; k < k0 + KW; k += 4) {
-      const long row = (long)(k + kr) * g.Rpad;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ya[row], Yb[row], acc, 0, 0, 0);
-    }
-  } else {
-    for (int k = k0; k < k0 + KW; k += 4) {
-      const int kk = k + kr;
-      const long row = (long)kk * g.Rpad;
-      const double z = (col == 0 && kk < g.K3) ? b.zp[kk] : 0.0;
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Ya[row], z, acc, 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) tile[wave][(kr + 4 * i) * 16 + col] = acc[i];
-  __syncthreads();
-  const int e = threadIdx.x;
-  const double v = ((tile[0][e] + tile[1][e]) + tile[2][e]) + tile[3][e];
-  b.Spart[((long)s * g.npairs + p) * 256 + e] = v;
-}
-
-// Sum of the split-K partials of one S element, in split order.  The loads
-// are issued four at a time (independent addresses) so the latency of these
-// cross-XCD reads is paid once per group, not once per split.
-__device__ __forceinline__ double sum_splits(const Geo& g, const double* Spart, long off) {
-  const long stride = (long)g.npairs * 256;
-  double s = 0;
-  int q = 0;
-  for (; q + 4 <= g.ksplit; q += 4) {
-    const double a0 = Spart[off + (q + 0) * stride], a1 = Spart[off + (q + 1) * stride];
-    const double a2 = Spart[off + (q + 2) * stride], a3 = Spart[off + (q + 3) * stride];
-    s += a0;
-    s += a1;
-    s += a2;
-    s += a3;
-  }
-  for (; q < g.ksplit; ++q) s += Spart[off + q * stride];
-  return s;
-}
-
-__device__ __forceinline__ double gemm_part(const Geo& g, const double* Spart, int r, int c) {
-  int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
-  if (I > J) {
-    int t = I; I = J; J = t;
-    t = rr; rr = cc; cc = t;
-  }
-  const int p = I * g.T - I * (I - 1) / 2 + (J - I);
-  return sum_splits(g, Spart, (long)p * 256 + rr * 16 + cc);
-}
-__device__ __forceinline__ double gemm_zpart(const Geo& g, const double* Spart, int r) {
-  const int ntri = g.T * (g.T + 1) / 2;
-  const int p = ntri + (r >> 4);
-  return sum_splits(g, Spart, (long)p * 256 + (r & 15) * 16);
-}
-
-// Sharded mode: S_local = U - YY^T, b_local = g - Yz, diag(U) (no LM diagonal)
-__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b) {
   const State* st = b.st;
   if (st->done) return;
   const int n = g.n6;
-  const int idx = blockIdx.x * kBlock + threadIdx.x;
+  const int e = threadIdx.x % kSaElems, grp = threadIdx.x / kSaElems;
+  const int idx = blockIdx.x * kSaElems + e;
+  int r = -1, c = -1;
   if (idx < n * n) {
-    const int r = idx / n, c = idx - r * n;
+    r = idx / n;
+    c = idx - r * n;
+  } else if (idx < n * n + n) {
+    r = idx - n * n;
+    c = n;  // Y^T z: column n6 of the partial tiles
+  }
+  double acc = 0.0;
+  if (r >= 0 && !st->fail) {
+    int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
+    if (I > J) {  // the partials hold the upper block triangle: S is symmetric
+      int t = I; I = J; J = t;
+      t = rr; rr = cc; cc = t;
+    }
+    const int p = I * g.T - I * (I - 1) / 2 + (J - I);
+    const double* src = b.Spart + (long)p * 256 + rr * 16 + cc;
+    const long stride = (long)g.npairs * 256;
+    for (int q = grp; q < g.ksplit; q += kSaGroups) acc += src[q * stride];
+  }
+  part[grp][e] = acc;
+  __syncthreads();
+  if (grp != 0) return;
+  double sum = 0.0;
+#pragma unroll
+  for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
+  if (idx < n * n) {
     double v = 0;
     if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
-    b.S[idx] = st->fail ? 0.0 : v - gemm_part(g, b.Spart, r, c);
+    b.S[idx] = st->fail ? 0.0 : v - sum;
   } else if (idx < n * n + n) {
-    const int r = idx - n * n;
-    b.bvec[r] = st->fail ? 0.0 : b.gcs[r] - gemm_zpart(g, b.Spart, r);
+    b.bvec[r] = st->fail ? 0.0 : b.gcs[r] - sum;
     b.diagU[r] = b.U[36 * (r / 6) + (r % 6) * 7];
   } else if (idx == n * n + n) {
     b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
@@ -956,13 +1062,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 // observations.  Partials per workgroup, reduced in fixed order by
 // step_finalize (deterministic).
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
-
-template <int W>
-__device__ __forceinline__ double group_sum(double x) {
-#pragma unroll
-  for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
-  return x;
-}
 
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
   __shared__ double lds[16];
@@ -1418,6 +1517,7 @@ struct Plan {
   State* hstate[2] = {nullptr, nullptr};  // pinned slots of the pipelined State polls
   bool dev = false;        // problem arrays are device-resident
   size_t solve_lds = 0;
+  size_t schur_lds = 0;
   int use_lds = 0;
   int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
 };
@@ -1445,20 +1545,21 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.nf = std::min(std::max(p->fixed_frames, 0), p->n_cams);
   g.m = g.nc - g.nf;
   g.n6 = 6 * g.m;
-  g.Rpad = (int)rup(std::max(g.n6, 1), 16);
+  g.Rpad = (int)rup(g.n6 + 1, 16);  // camera columns | z_p column n6 | zero padding
   g.T = g.Rpad / 16;
   g.Ts = (g.n6 + 1 + 15) / 16;
-  g.K3 = 3 * g.np;
-  g.ksplit = (int)std::max(1L, std::min(64L, rup(std::max(g.K3, 1), 512) / 512));
-  g.Kpad = (int)rup(std::max(g.K3, 1), 16L * g.ksplit);
-  g.npairs = g.T * (g.T + 1) / 2 + g.T;
+  g.npairs = g.T * (g.T + 1) / 2;
+  g.spts = kSchurPts;
+  g.nsub = (int)std::max(1L, ((long)g.np + g.spts - 1) / g.spts);
+  g.ksplit = std::min(g.nsub, 256);  // Schur workgroups = partial slices summed by s_assemble
+  ME_CHECK(c, g.npairs <= 8 * 24, "BA: %d variable cameras exceed the Schur tile budget", g.m);
   g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
   g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kPtBlock) / kPtBlock);
   g.jacobi = opt->jacobi_scaling ? 1 : 0;
   g.ck = (int)std::min(64L, std::max(1L, rup(std::max(g.no, 1), (long)std::max(g.m, 1) * kBlock) /
                                              ((long)std::max(g.m, 1) * kBlock)));
   g.nblk_step = (int)std::max(1L, rup(std::max(g.np, 1), kStepPts) / kStepPts);
-  g.pstride = std::max({g.nblk_obs, g.nblk_pts, g.nblk_step});
+  g.pstride = std::max({g.nblk_obs, g.nblk_pts, g.nblk_step, g.ksplit});
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
   g.baseline = p->baseline;
@@ -1519,7 +1620,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * 3 * (size_t)g.np, &b.gps);
   add(8 * 9 * (size_t)g.np, &b.Lp);
   add(8 * 3 * (size_t)g.np, &b.zp);
-  add(8 * (size_t)g.Kpad * g.Rpad, &b.Y);
   add(8 * 256 * (size_t)g.ksplit * g.npairs, &b.Spart);
   add(8 * (size_t)g.n6 * g.n6 + 8 * (size_t)(2 * g.n6 + 2), &b.S);  // S | b | diagU | fail (contiguous for all-reduce)
   add(8 * (size_t)g.n6, &b.yc);
@@ -1577,7 +1677,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     b.pt_idx = p->pt_idx;
   }
   ME_HIP(c, hipMemsetAsync(b.work, 0, work_bytes, s));
-  ME_HIP(c, hipMemsetAsync(b.Y, 0, 8 * (size_t)g.Kpad * g.Rpad, s));  // padding rows/columns stay zero
   const double* cams_in = dev ? p->cams : b.cams[0];
   const double* pts_in = dev ? p->pts : b.pts[0];
   const long nthr = std::max({(long)g.nblk_obs * kBlock, (long)g.np, 6L * g.nc, 3L * g.np});
@@ -1595,6 +1694,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   ME_CHECK(c, P.solve_lds <= 150 * 1024, "BA: %d variable cameras exceed the camera-solve workspace", g.m);
   ME_HIP(c, hipFuncSetAttribute(P.use_lds ? (const void*)cam_solve_kernel<true> : (const void*)cam_solve_kernel<false>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
+  P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
+  ME_CHECK(c, P.schur_lds <= 150 * 1024, "BA: %d variable cameras exceed the Schur workspace", g.m);
+  for (const void* k : {(const void*)pt_schur_kernel<4>, (const void*)pt_schur_kernel<8>,
+                        (const void*)pt_schur_kernel<16>, (const void*)pt_schur_kernel<24>})
+    ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
   return ME_OK;
 }
 
@@ -1627,30 +1731,38 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     }
   }
   {
-    me_ktimer t(c, ME_KT_BA_POINTS);
-    hipLaunchKernelGGL(pt_assemble_kernel, dim3(g.nblk_pts), dim3(kPtBlock), 0, s, g, P.b, P.o);
+    // point blocks + Schur partial tiles (BA_SCHUR family)
+    me_ktimer t(c, ME_KT_BA_SCHUR);
+    const int per_wave = (g.npairs + 7) / 8;
+    const dim3 grd(g.ksplit), blk(kSchurBlock);
+    if (per_wave <= 4)
+      hipLaunchKernelGGL(pt_schur_kernel<4>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+    else if (per_wave <= 8)
+      hipLaunchKernelGGL(pt_schur_kernel<8>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+    else if (per_wave <= 16)
+      hipLaunchKernelGGL(pt_schur_kernel<16>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+    else
+      hipLaunchKernelGGL(pt_schur_kernel<24>, grd, blk, P.schur_lds, s, g, P.b, P.o);
   }
   if (ar) {
     hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
     ME_AR(P.b.scal + R_COST, 1);
     ME_AR(P.b.scal + R_GMAX_PT, -1);
   }
-  hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o,
-                     (const double*)(ar ? P.gc_glob : P.gc_raw), ar ? 1 : 0);
   return me_check_launch(c, "BA linearize");
 }
 
-// Schur stage: point blocks, dense Y, S partial tiles on the FP64 MFMA
-int enqueue_schur(Plan& P) {
+// S / b assembly; its last workgroup closes the linearisation (lin_finalize).
+int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
-  hipStream_t s = c->stream;
-  if (g.m > 0) {
-    me_ktimer t(c, ME_KT_BA_SCHUR);
-    hipLaunchKernelGGL(y_block_kernel, dim3(blocks((long)g.np * g.n6, kBlock)), dim3(kBlock), 0, s, g, P.b);
-    hipLaunchKernelGGL(schur_gemm_kernel, dim3(g.npairs, g.ksplit), dim3(kBlock), 0, s, g, P.b);
-  }
-  return me_check_launch(c, "BA schur");
+  const double* gc = ar ? P.gc_glob : P.gc_raw;
+  if (g.m > 0)
+    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kSaElems) + 1), dim3(kBlock), 0,
+                       c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
+  else
+    hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
+  return me_check_launch(c, "BA assemble");
 }
 
 int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
@@ -1658,13 +1770,11 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   const Geo& g = P.g;
   hipStream_t s = c->stream;
   ME_TRY(enqueue_linearize(P, ar, user));
-  ME_TRY(enqueue_schur(P));
-  // S = U - sum of split-K partials is assembled by a wide kernel (coalesced,
+  // S = U - sum of the Schur partials is assembled by a wide kernel (coalesced,
   // all CUs) rather than inside the one-workgroup solve, whose dependent
   // cross-XCD loads would otherwise dominate the iteration.
+  ME_TRY(enqueue_assemble(P, ar));
   if (g.m > 0) {
-    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0, s, g,
-                       P.b);
     if (ar) {
       ME_AR(P.b.S, g.n6 * g.n6 + 2 * g.n6);  // S | b | diag(U) are contiguous
       ME_AR(P.b.scal + R_COUNT, 1);          // linear-solver failure flag
@@ -1840,12 +1950,7 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
   if (rc < 0) return rc;
   const Geo& g = P.g;
   ME_TRY(enqueue_linearize(P, nullptr, nullptr));
-  ME_TRY(enqueue_schur(P));
-  if (g.m > 0) {
-    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kBlock)), dim3(kBlock), 0,
-                       c->stream, g, P.b);
-  }
-  ME_TRY(me_check_launch(c, "reduced system"));
+  ME_TRY(enqueue_assemble(P, nullptr));
   std::vector<double> Sh((size_t)g.n6 * g.n6 + 2 * g.n6);
   if (g.m > 0)
     ME_HIP(c, hipMemcpyAsync(Sh.data(), P.b.S, 8 * Sh.size(), hipMemcpyDeviceToHost, c->stream));

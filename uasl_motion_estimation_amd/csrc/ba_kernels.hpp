@@ -7,12 +7,11 @@
 //                  analytic Jacobian, HuberLoss(1.0) corrector, cost.
 //   cam_assemble   one workgroup per variable camera: Jacobi column norms
 //                  (iteration 0), scaled U = Jc'Jc, g_c = Jc'r.
-//   pt_assemble    one lane per point: V = Jp'Jp, g_p, W_o = Jc'Jp per obs.
-//   pt_schur       one lane per point: V + D/radius -> Cholesky L_p,
-//                  Y_o = W_o L_p^-T, z_p = L_p^-1 g_p.
-//   y_scatter      dense Y (3 rows per point x 6m cols, K-major) for the GEMM.
-//   schur_gemm     S -= Y Y^T and b -= Y z on v_mfma_f64_16x16x4f64 tiles,
-//                  split-K partials (deterministic, no atomics).
+//   pt_schur       per landmark sub-chunk: V = Jp'Jp, g_p, V + D/radius ->
+//                  Cholesky L_p, z_p = L_p^-1 g_p, the landmark's rows of
+//                  Y = W L_p^-T (and z_p) in LDS, partial tiles of Y^T [Y | z]
+//                  on v_mfma_f64_16x16x4f64 (deterministic, no atomics).
+//   s_assemble     S = U - sum of the partial tiles, b = g - Y^T z.
 //   cam_solve      one workgroup: S = U + D/radius - sum(partials), dense
 //                  Cholesky, y_c = -S^-1 b, candidate cameras.
 //   pt_step        16 lanes per point: y_p, candidate point (bounds
@@ -61,7 +60,8 @@ struct State {
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, Ts, K3, Kpad, ksplit, npairs, nblk_obs, nblk_pts, nblk_step, pstride, jacobi, ck;
+  int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_pts, nblk_step, pstride, jacobi,
+      ck;
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -95,9 +95,7 @@ struct Bufs {
   double* gps;        // 3np scaled gradient
   double* Lp;         // np * 9 Cholesky of V + D/radius
   double* zp;         // 3np
-  double* Yo;         // no * 18 (W_o L^-T)
-  double* Y;          // Kpad * Rpad dense, K-major
-  double* Spart;      // ksplit * npairs * 256
+  double* Spart;      // ksplit (Schur workgroups) * npairs * 256 partial tiles of Y^T [Y | z]
   double* S;          // n6 * n6 (assembled / reduced)
   double* bvec;       // n6
   double* diagU;      // n6 (for the sharded all-reduce)
