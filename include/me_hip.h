@@ -223,6 +223,38 @@ int me_klt_track(me_ctx* ctx, me_mem mem, const uint8_t* prev, const uint8_t* ne
 int me_nms_scanline3x3(me_ctx* ctx, me_mem mem, const double* response, int width, int height, uint8_t* mask_out,
                        double* maxima, int cap, int* n_out);
 
+/* ---- A19 / §8f-1: frame-to-frame stereo VO ---------------------------
+ * Replaces bool me::StereoVisualOdometry::process(const std::vector<StereoOdoMatchesf>&,
+ * cv::Mat init) (include/MotionEstimation/vo/StereoVisualOdometry.h:41,
+ * src/vo/StereoVisualOdometry.cpp:34-92) with getMotion() (:331-342) and
+ * getInliers_idx() (.h:47).  Parameters are StereoVisualOdometry::parameters
+ * (StereoVisualOdometry.h:24-33 + VisualOdometry.h:19-33).  matches: n x 8
+ * floats {f1.x, f1.y, f2.x, f2.y, f3.x, f3.y, f4.x, f4.y} (StereoOdoMatchesf:
+ * previous left/right, current left/right).  The RANSAC triples come from
+ * the context's glibc-compatible rand() stream (unseeded: as the
+ * reference's rand(), reseed with me_vo_srand).  The reference's GN/LM loop
+ * can run forever (StereoVisualOdometry.cpp:277); such a run is cut at
+ * max_outer passes and reported as ME_ERR_STATE.  ok = process()'s result;
+ * motion = getMotion() (4x4 row-major); state = the 6 state values
+ * (Euler angles, translation); pts3d = getPts3D() (n x 4 homogeneous,
+ * filled when n >= 6); inliers = getInliers_idx() (capacity n).  Any of
+ * state, pts3d and inliers may be NULL. */
+typedef struct {
+  int method;                /* VisualOdometry::Method: 0 GN, 1 LM */
+  double step_size, eps, e1, e2, e3, e4;
+  int max_iter, nb_fixed_frames, ransac, n_ransac;
+  double inlier_threshold;
+  double baseline;
+  int weighting;
+  double fu1, fv1, fu2, fv2, cu1, cu2, cv1, cv2;
+} me_vo_params;
+void me_vo_default_params(me_vo_params* p);
+int me_vo_srand(me_ctx* ctx, unsigned seed);
+int me_vo_rand(me_ctx* ctx, int* out);  /* one draw of the context's rand() stream (tests) */
+int me_vo_process(me_ctx* ctx, const float* matches, int n, const double* init6, const me_vo_params* p,
+                  int max_outer, double* motion, double* state, double* pts3d, int* inliers, int* n_inliers,
+                  int* ok);
+
 #ifdef __cplusplus
 }
 #endif

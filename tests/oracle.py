@@ -405,3 +405,47 @@ def scharr(img):
     dy = np.zeros((h, w), np.int16)
     lib().oracle_scharr(img.ctypes.data, w, h, w, dx.ctypes.data, dy.ctypes.data)
     return dx, dy
+
+
+# ----------------------------------------------------------------- stereo VO
+class OVOParams(ctypes.Structure):
+    _fields_ = [("method", c_int), ("e1", c_double), ("e2", c_double), ("e3", c_double), ("e4", c_double),
+                ("max_iter", c_int), ("ransac", c_int), ("n_ransac", c_int), ("inlier_threshold", c_double),
+                ("baseline", c_double), ("fu1", c_double), ("fv1", c_double), ("fu2", c_double), ("fv2", c_double),
+                ("cu1", c_double), ("cu2", c_double), ("cv1", c_double), ("cv2", c_double)]
+
+
+def libc_rand_seq(seed: int, count: int) -> np.ndarray:
+    """`count` values of glibc rand() after srand(seed) (the reference's sampler, :150)."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.rand.restype = c_int
+    libc.srand(ctypes.c_uint(seed))
+    return np.array([libc.rand() for _ in range(count)], np.int32)
+
+
+def vo_process(matches, params: dict, rand_seq=None, init=None, max_outer=10000):
+    """oracle_vo_process: returns (rc, motion (4,4), inliers).  rc 1/0 = process()
+    result, -2 = the reference would never leave optimize(), -3 = rand_seq too short."""
+    L = lib()
+    if not getattr(L, "_vo_decl", False):
+        L.oracle_vo_process.argtypes = [c_void_p, c_int, c_void_p, POINTER(OVOParams), c_void_p, c_int, c_void_p,
+                                        c_void_p, POINTER(c_int), c_int]
+        L.oracle_vo_process.restype = c_int
+        L._vo_decl = True
+    d = dict(method=0, e1=1e-3, e2=1e-12, e3=1e-12, e4=1e-15, max_iter=100, ransac=1, n_ransac=200,
+             inlier_threshold=2.0, baseline=1.0, fu1=1.0, fv1=1.0, fu2=1.0, fv2=1.0, cu1=0.0, cu2=0.0, cv1=0.0,
+             cv2=0.0)
+    d.update({k: v for k, v in params.items() if k in d})
+    p = OVOParams(**{k: (int(v) if isinstance(v, bool) else v) for k, v in d.items()})
+    m = np.ascontiguousarray(matches, np.float32).reshape(-1, 8)
+    if rand_seq is None:
+        rand_seq = libc_rand_seq(1, 8 * d["n_ransac"] + 64)
+    rs = np.ascontiguousarray(rand_seq, np.int32)
+    ini = None if init is None else np.ascontiguousarray(init, np.float64)
+    motion = np.zeros(16)
+    inl = np.zeros(max(len(m), 1), np.int32)
+    nin = c_int(0)
+    rc = L.oracle_vo_process(m.ctypes.data, len(m), None if ini is None else ini.ctypes.data, ctypes.byref(p),
+                             rs.ctypes.data, len(rs), motion.ctypes.data, inl.ctypes.data, ctypes.byref(nin),
+                             max_outer)
+    return rc, motion.reshape(4, 4), inl[:nin.value].copy()

@@ -124,7 +124,20 @@ EXPORTS = [
     "me_ba_solve_sharded",
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
+    "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
 ]
+
+class VOParamsC(ctypes.Structure):
+    """me_vo_params (include/me_hip.h)."""
+    _fields_ = [
+        ("method", c_int), ("step_size", c_double), ("eps", c_double),
+        ("e1", c_double), ("e2", c_double), ("e3", c_double), ("e4", c_double),
+        ("max_iter", c_int), ("nb_fixed_frames", c_int), ("ransac", c_int), ("n_ransac", c_int),
+        ("inlier_threshold", c_double), ("baseline", c_double), ("weighting", c_int),
+        ("fu1", c_double), ("fv1", c_double), ("fu2", c_double), ("fv2", c_double),
+        ("cu1", c_double), ("cu2", c_double), ("cv1", c_double), ("cv2", c_double),
+    ]
+
 
 _lib = None
 
@@ -180,6 +193,11 @@ def load_library(path: str = LIB_PATH):
                                  c_void_p, c_int, P(KLTParamsC)]),
         "me_nms_scanline3x3": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int,
                                        P(c_int)]),
+        "me_vo_default_params": (None, [P(VOParamsC)]),
+        "me_vo_srand": (c_int, [c_void_p, ctypes.c_uint]),
+        "me_vo_rand": (c_int, [c_void_p, P(c_int)]),
+        "me_vo_process": (c_int, [c_void_p, c_void_p, c_int, P(c_double), P(VOParamsC), c_int, P(c_double),
+                                  P(c_double), P(c_double), P(c_int), P(c_int), P(c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

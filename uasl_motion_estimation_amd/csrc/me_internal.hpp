@@ -32,6 +32,10 @@ struct me_ctx {
   long launches[ME_KT_COUNT] = {0};
   double total_ms[ME_KT_COUNT] = {0};
   hipEvent_t poll_ev[2] = {nullptr, nullptr};  // device-state read-back events of iterative solves
+  // glibc-compatible rand() stream of the RANSAC sampling (vo.hip)
+  int32_t rand_st[31] = {0};
+  int rand_f = 3, rand_r = 0;
+  bool rand_init = false;
   long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
   // MI term tables, one per patch pixel count N (built on first use, mi.hip)
   float* mi_table[256] = {nullptr};
@@ -79,6 +83,6 @@ struct me_ktimer {
 enum {
   SLOT_IMG_L = 0, SLOT_IMG_R, SLOT_XY_L, SLOT_XY_R, SLOT_MI_OUT, SLOT_RED, SLOT_GENERIC,
   SLOT_SC_TRACKS, SLOT_SC_RES, SLOT_SC_RES2, SLOT_SC_NEQ, SLOT_SC_IMGL, SLOT_SC_IMGR,
-  SLOT_KLT_PYR, SLOT_KLT_PTS, SLOT_NMS,
+  SLOT_KLT_PYR, SLOT_KLT_PTS, SLOT_NMS, SLOT_VO,
   SLOT_COUNT
 };

@@ -379,3 +379,52 @@ def random_patches(seed: int, width: int, height: int, n: int, pw: int, ph: int)
     xyR = np.stack([np.clip(xyL[:, 0] - d, 0, width - pw), np.clip(xyL[:, 1] + rng.integers(-1, 2, n), 0,
                                                                      height - ph)], -1).astype(np.int32)
     return L, Rimg, np.ascontiguousarray(xyL), np.ascontiguousarray(xyR)
+
+
+def vo_matches(seed: int, n: int, width: int = 1280, height: int = 720, noise: float = 0.0,
+               state=(0.004, -0.006, 0.003, 0.05, -0.02, 0.5), n_outliers: int = 0):
+    """Quad matches (n, 8) float32 {f1, f2, f3, f4} of a stereo rig moving by
+    `state` (Euler angles, translation) in the StereoVisualOdometry convention
+    (project3D :22-32, reproject :116-141: X_cur = R4(state)^T X_prev + t).
+    Returns (matches, params dict for vo.Parameters).  `noise` px of Gaussian
+    noise on f3/f4; the first `n_outliers` rows get f3/f4 shifted 20-60 px."""
+    rng = np.random.default_rng(seed)
+    K = intrinsics(width, height)
+    f, cu, cv = K[0, 0], K[0, 2], K[1, 2]
+    b = BASELINE
+    r, p, y = state[:3]
+    cr, sr, cp, sp, cy, sy = (math.cos(r), math.sin(r), math.cos(p), math.sin(p), math.cos(y), math.sin(y))
+    R = np.array([[cp * cy, cp * sy, -sp],
+                  [sp * sr * cy - cr * sy, sr * sp * sy + cr * cy, cp * sr],
+                  [cr * sp * cy + sr * sy, cr * sp * sy - sr * cy, cp * cr]])
+    out = np.zeros((n, 8), np.float32)
+    k = 0
+    while k < n:
+        u = rng.uniform(20, width - 20)
+        v = rng.uniform(20, height - 20)
+        Z = rng.uniform(5.0, 40.0)
+        d = f * b / Z
+        # f1/f2 as float32 first: project3D works on the float features
+        f1 = np.float32([u, v])
+        f2 = np.float32([u - d, v])
+        dd = float(f1[0] - cu) - float(f2[0] - cu)
+        if dd <= 0:
+            continue
+        Xp = np.array([(float(f1[0]) - cu) * b / dd, (float(f1[1]) - cv) * b / dd, f * b / dd])
+        Xc = R.T @ Xp + np.asarray(state[3:6])
+        if Xc[2] < 1.0:
+            continue
+        u3, v3 = f * Xc[0] / Xc[2] + cu, f * Xc[1] / Xc[2] + cv
+        u4 = (f * Xc[0] - b * f) / Xc[2] + cu
+        if not (0 <= u3 < width and 0 <= v3 < height and 0 <= u4 < width):
+            continue
+        f3 = np.array([u3, v3]) + (rng.normal(0, noise, 2) if noise else 0)
+        f4 = np.array([u4, v3]) + (rng.normal(0, noise, 2) if noise else 0)
+        if k < n_outliers:
+            sh = rng.uniform(20, 60, 2) * rng.choice([-1, 1], 2)
+            f3 = f3 + sh
+            f4 = f4 + sh
+        out[k] = (f1[0], f1[1], f2[0], f2[1], f3[0], f3[1], f4[0], f4[1])
+        k += 1
+    params = dict(baseline=b, fu1=f, fv1=f, fu2=f, fv2=f, cu1=cu, cu2=cu, cv1=cv, cv2=cv)
+    return out, params
