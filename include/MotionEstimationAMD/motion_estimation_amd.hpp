@@ -7,8 +7,8 @@
 //   me::computeMutualInformation  <- include/MotionEstimation/core/mutual_information.h:20
 //   me::computeEntropy            <- src/core/mutual_information.cpp:28-45
 //   me::nonMaxSupScanline3x3      <- include/MotionEstimation/core/feature_types.h:270
-//   me::optimisation::StereoBundleAdjuster
-//                                 <- BundleAdjuster<4> (include/MotionEstimation/optimisation/BundleAdjuster.h:182-278,431-476)
+//   me::optimisation::BundleAdjuster<M> (StereoBundleAdjuster = <4>, MonoBundleAdjuster = <2>)
+//                                 <- BundleAdjuster<M> (include/MotionEstimation/optimisation/BundleAdjuster.h:182-528)
 // Errors: the reference asserts on empty input (mutual_information.cpp:57);
 // here invalid input throws std::invalid_argument, device/runtime failures
 // throw std::runtime_error.  BundleAdjuster misuse reports through std::cerr
@@ -127,28 +127,41 @@ struct CalibrationParameters {
   bool compute_cov = false;
 };
 
-// Observation<4> (BundleAdjuster.h:47-69): left (x, y), right (x, y).
-struct StereoObservation {
-  std::array<double, 4> xy;
+// Observation<M> (BundleAdjuster.h:22-32): M = 4 left (x, y), right (x, y);
+// M = 2 one image (x, y) whose camID picks the residual of BundleAdjuster<2>.
+template <int M>
+struct Observation {
+  std::array<double, M> xy;
   int camIdx;
   int ptIdx;
+  int camID = 0;
 };
+using StereoObservation = Observation<4>;
+using MonoObservation = Observation<2>;
 
-// BundleAdjuster<4> over libme_hip.so.  Parameters: cameras {t, angle-axis}
+// BundleAdjuster<M> over libme_hip.so.  Parameters: cameras {t, angle-axis}
 // (Matx61d, :286-300), points {X, Y, Z}.  optimise() runs the device LM with
 // the reference's Ceres options (function_tolerance 1e-3, Huber(1), point
 // bounds, fixed leading frames), the 1 s time cap replaced by
-// max_num_iterations (SURVEY A-9).
-class StereoBundleAdjuster {
+// max_num_iterations (SURVEY A-9).  M = 4: StereoReprojectionError
+// (:142-180, :431-476); M = 2: StandardReprojectionError / StereoRightError by
+// camID, K[0] only, zero baseline -> 0.5 (:71-139, :378-429).  With
+// compute_cov the pose covariances follow the solve (extract_covariance,
+// :478-528; fixed cameras get zero blocks).
+template <int M>
+class BundleAdjuster {
+  static_assert(M == 2 || M == 4, "BundleAdjuster<M>: M is 2 or 4");
+
  public:
   enum class Status { UNINITIALISED, INITIALISED, SUCCESSFUL, FAILED };
 
-  StereoBundleAdjuster(const CalibrationParameters& params, std::vector<std::array<double, 6>> cams,
-                       std::vector<std::array<double, 3>> pts, std::vector<StereoObservation> obs,
-                       amd::Context& ctx = amd::Context::thread_default())
+  BundleAdjuster(const CalibrationParameters& params, std::vector<std::array<double, 6>> cams,
+                 std::vector<std::array<double, 3>> pts, std::vector<Observation<M>> obs,
+                 amd::Context& ctx = amd::Context::thread_default())
       : calib_(params), cams_(std::move(cams)), pts_(std::move(pts)), obs_(std::move(obs)), ctx_(&ctx) {
-    if (calib_.K.size() < 2) {  // StereoReprojectionError needs K[1] (BundleAdjuster.h:163)
-      std::cerr << "[Bundle Adjuster] stereo BA needs two calibration matrices" << std::endl;
+    if (calib_.K.size() < (M == 4 ? 2u : 1u)) {  // StereoReprojectionError needs K[1] (BundleAdjuster.h:163)
+      std::cerr << "[Bundle Adjuster] " << (M == 4 ? "stereo BA needs two calibration matrices"
+                                                   : "BA needs a calibration matrix") << std::endl;
       return;
     }
     if (!cams_.empty() && !pts_.empty() && !obs_.empty()) status_ = Status::INITIALISED;
@@ -161,12 +174,14 @@ class StereoBundleAdjuster {
       std::cerr << "[Bundle Adjuster] parameters and observations must be initialised first" << std::endl;
       return status_;
     }
-    std::vector<double> o(4 * obs_.size());
-    std::vector<int32_t> ci(obs_.size()), pi(obs_.size());
+    if (M == 2 && calib_.baseline == 0) calib_.baseline = 0.5;  // BundleAdjuster.h:389-390
+    std::vector<double> o(M * obs_.size());
+    std::vector<int32_t> ci(obs_.size()), pi(obs_.size()), cid(obs_.size());
     for (size_t k = 0; k < obs_.size(); ++k) {
-      for (int a = 0; a < 4; ++a) o[4 * k + a] = obs_[k].xy[a];
+      for (int a = 0; a < M; ++a) o[M * k + a] = obs_[k].xy[a];
       ci[k] = obs_[k].camIdx;
       pi[k] = obs_[k].ptIdx;
+      cid[k] = obs_[k].camID;
     }
     me_ba_problem p{};
     p.n_cams = (int)cams_.size();
@@ -177,9 +192,11 @@ class StereoBundleAdjuster {
     p.obs = o.data();
     p.cam_idx = ci.data();
     p.pt_idx = pi.data();
+    p.obs_dim = M;
+    p.cam_id = cid.data();
     for (int a = 0; a < 9; ++a) {
       p.K0[a] = calib_.K[0][a];
-      p.K1[a] = calib_.K[1][a];
+      p.K1[a] = calib_.K[calib_.K.size() > 1 ? 1 : 0][a];
     }
     p.baseline = calib_.baseline;
     p.feat_var = calib_.feat_var;
@@ -189,11 +206,24 @@ class StereoBundleAdjuster {
       std::cerr << "[Bundle Adjuster] " << me_last_error(ctx_->get()) << std::endl;
       return status_ = Status::FAILED;
     }
+    if (calib_.compute_cov) {
+      std::vector<double> cov(36 * cams_.size());
+      int ok = 0;
+      rc = me_ba_covariance(ctx_->get(), &p, cov.data(), &ok);
+      if (rc != ME_OK || !ok) {
+        std::cerr << "[Bundle Adjuster] error computing the covariance matrix" << std::endl;
+      } else {
+        covs_.assign(cams_.size(), {});
+        for (size_t i = 0; i < cams_.size(); ++i) std::copy(&cov[36 * i], &cov[36 * i] + 36, covs_[i].begin());
+      }
+    }
     return status_ = (summary_.status == 2 ? Status::SUCCESSFUL : Status::FAILED);
   }
 
   const std::vector<std::array<double, 3>>& getPoints() const { return pts_; }
   const std::vector<std::array<double, 6>>& getCameraParams() const { return cams_; }
+  // 6x6 row-major per camera (empty unless compute_cov and the covariance succeeded)
+  const std::vector<std::array<double, 36>>& getPosesCovariance() const { return covs_; }
   int getNbPoints() const { return (int)pts_.size(); }
   int getNbCameras() const { return (int)cams_.size(); }
   int getNbObservations() const { return (int)obs_.size(); }
@@ -209,12 +239,15 @@ class StereoBundleAdjuster {
   CalibrationParameters calib_;
   std::vector<std::array<double, 6>> cams_;
   std::vector<std::array<double, 3>> pts_;
-  std::vector<StereoObservation> obs_;
+  std::vector<Observation<M>> obs_;
+  std::vector<std::array<double, 36>> covs_;
   amd::Context* ctx_;
   Status status_ = Status::UNINITIALISED;
   me_ba_options opts_ = defaults();
   me_ba_summary summary_{};
 };
+using StereoBundleAdjuster = BundleAdjuster<4>;
+using MonoBundleAdjuster = BundleAdjuster<2>;
 
 }  // namespace optimisation
 }  // namespace me

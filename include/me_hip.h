@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define ME_ABI_VERSION 1
+#define ME_ABI_VERSION 2
 
 enum {
   ME_OK = 0,
@@ -153,7 +153,11 @@ int me_scale_inliers(me_ctx* ctx, const me_scale_state* s, int weighting, double
  * and the Ceres solve it wraps: StereoReprojectionError residual/Jacobian,
  * HuberLoss(1.0), LM trust region with Jacobi scaling, point-first Schur
  * elimination, box bounds on points.  cams are Matx61d {t, angle-axis}
- * (BundleAdjuster.h:297-310), observations Observation<4>. */
+ * (BundleAdjuster.h:297-310), observations Observation<4>.
+ * obs_dim = 2 selects BundleAdjuster<2>::optimise (BundleAdjuster.h:378-429):
+ * Observation<2> {x, y} with cam_id = Observation::camID, residual
+ * StandardReprojectionError (:71-103) for camID 0 and StereoRightError
+ * (:106-139) otherwise, K[0] only, a zero baseline replaced by 0.5 (:389-390). */
 typedef struct {
   int n_cams, n_pts, n_obs;
   double* cams;              /* n_cams*6, updated in place */
@@ -167,6 +171,8 @@ typedef struct {
   me_mem mem;                /* ME_HOST: the arrays above are host memory (copied in/out);
                                 ME_DEVICE: device memory on the ctx device, cams/pts updated in
                                 place on the device (me_ba_solve / me_ba_solve_sharded only) */
+  int obs_dim;               /* 4 (or 0): Observation<4>; 2: Observation<2> (BundleAdjuster<2>) */
+  const int32_t* cam_id;     /* obs_dim 2: Observation::camID per observation; ignored otherwise */
 } me_ba_problem;
 
 typedef struct {
@@ -193,11 +199,19 @@ int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_sum
 /* Cost (Ceres ½Σρ) at the problem's current parameters. */
 int me_ba_cost(me_ctx* ctx, const me_ba_problem* p, double* cost);
 /* Residuals (sigma-scaled, uncorrected) and Jacobian blocks per observation:
-   res 4/obs, Jc 24/obs (row-major 4x6), Jp 12/obs (4x3). */
+   res D/obs, Jc 6D/obs (row-major Dx6), Jp 3D/obs (Dx3), D = obs_dim (4 or 2). */
 int me_ba_evaluate(me_ctx* ctx, const me_ba_problem* p, double* res, double* Jc, double* Jp);
 /* Reduced camera system of the first LM step at trust radius `radius`
    (scaled coordinates), S (6m x 6m row-major) and b (6m), m = non-fixed cams. */
 int me_ba_reduced_system(me_ctx* ctx, const me_ba_problem* p, double radius, double* S, double* b);
+/* Pose covariance at the problem's current parameters: replaces
+   BundleAdjuster<M>::extract_covariance (BundleAdjuster.h:478-528), i.e.
+   ceres::Covariance over the camera blocks with the loss function applied:
+   cov[36 i .. 36 i + 35] = 6x6 row-major block i of (J^T J)^-1, obtained as
+   the inverse of the point-eliminated camera system; constant (fixed) cameras
+   get zero blocks as in Ceres.  *ok = 0 (and cov untouched) when J^T J is not
+   positive definite (Ceres reports a rank-deficient Jacobian). */
+int me_ba_covariance(me_ctx* ctx, const me_ba_problem* p, double* cov /* n_cams*36 */, int* ok);
 
 /* Landmark-sharded solve: this rank holds all cameras and a
    subset of the points with their observations.  At each exchange point the

@@ -65,9 +65,44 @@ void aa_rotate(const Jet<N> aa[3], const Jet<N> pt[3], Jet<N> out[3]) {
   }
 }
 
+// BundleAdjuster<2>::optimise replaces a zero baseline by 0.5 (BundleAdjuster.h:389-390)
+double eff_baseline(const oracle_ba_problem* p) {
+  return p->obs_dim == 2 && p->baseline == 0 ? 0.5 : p->baseline;
+}
+
+// StandardReprojectionError (BundleAdjuster.h:71-103, camID 0) / StereoRightError
+// (:106-139, otherwise) -- the residuals of BundleAdjuster<2> (:395-398); rows 2, 3 zero
+void eval_obs_mono(const oracle_ba_problem* p, int o, const double* cam, const double* pt, double r[4],
+                   double Jc[24], double Jp[12]) {
+  typedef Jet<9> J9;
+  J9 c[6], X[3];
+  for (int i = 0; i < 6; ++i) c[i] = J9(cam[i], i);
+  for (int i = 0; i < 3; ++i) X[i] = J9(pt[i], 6 + i);
+  J9 P[3];
+  aa_rotate<9>(c + 3, X, P);
+  if (p->cam_id[o] == 0) P[0] = P[0] + c[0];
+  else P[0] = P[0] + (c[0] - eff_baseline(p));  // p[0] += camera[0] - calib->baseline
+  P[1] = P[1] + c[1];
+  P[2] = P[2] + c[2];
+  const double sinv = 1.0 / std::sqrt(p->feat_var);
+  J9 x = p->K0[0] * (P[0] / P[2]) + p->K0[2];
+  J9 y = p->K0[4] * (P[1] / P[2]) + p->K0[5];
+  const double* f = p->obs + 2 * o;
+  J9 res[2] = {sinv * (x - f[0]), sinv * (y - f[1])};
+  for (int k = 0; k < 4; ++k) {
+    r[k] = k < 2 ? res[k].a : 0.0;
+    if (Jc) for (int j = 0; j < 6; ++j) Jc[k * 6 + j] = k < 2 ? res[k].v[j] : 0.0;
+    if (Jp) for (int j = 0; j < 3; ++j) Jp[k * 3 + j] = k < 2 ? res[k].v[6 + j] : 0.0;
+  }
+}
+
 // StereoReprojectionError::operator() (BundleAdjuster.h:153-171)
 void eval_obs(const oracle_ba_problem* p, int o, const double* cam, const double* pt, double r[4], double Jc[24],
               double Jp[12]) {
+  if (p->obs_dim == 2) {
+    eval_obs_mono(p, o, cam, pt, r, Jc, Jp);
+    return;
+  }
   typedef Jet<9> J9;
   J9 c[6], X[3];
   for (int i = 0; i < 6; ++i) c[i] = J9(cam[i], i);
@@ -105,8 +140,8 @@ void huber(double s, double rho[3]) {
 struct Bounds { double lo[3], hi[3]; };
 Bounds point_bounds(const oracle_ba_problem* p) {
   // BundleAdjuster.h:442-443, 455-460
-  const double Zmax = p->K0[0] * p->baseline / 0.1;
-  const double Zmin = p->K0[0] * p->baseline / (2 * p->K0[2]);
+  const double Zmax = p->K0[0] * eff_baseline(p) / 0.1;
+  const double Zmin = p->K0[0] * eff_baseline(p) / (2 * p->K0[2]);
   Bounds b;
   b.hi[0] = Zmax / p->K0[0] * p->K0[2]; b.hi[1] = Zmax / p->K0[4] * p->K0[5]; b.hi[2] = Zmax;
   b.lo[0] = -Zmax / p->K0[0] * p->K0[2]; b.lo[1] = -Zmax / p->K0[4] * p->K0[5]; b.lo[2] = Zmin;
@@ -291,9 +326,66 @@ extern "C" void oracle_ba_default_options(oracle_ba_options* o) {
 }
 
 extern "C" void oracle_ba_evaluate(const oracle_ba_problem* p, double* res, double* Jc, double* Jp) {
-  for (int o = 0; o < p->n_obs; ++o)
-    eval_obs(p, o, p->cams + 6 * p->cam_idx[o], p->pts + 3 * p->pt_idx[o], res + 4 * o, Jc ? Jc + 24 * o : nullptr,
-             Jp ? Jp + 12 * o : nullptr);
+  const int D = p->obs_dim == 2 ? 2 : 4;
+  for (int o = 0; o < p->n_obs; ++o) {
+    double r[4], jc[24], jp[12];
+    eval_obs(p, o, p->cams + 6 * p->cam_idx[o], p->pts + 3 * p->pt_idx[o], r, jc, jp);
+    for (int k = 0; k < D; ++k) res[D * o + k] = r[k];
+    if (Jc) for (int k = 0; k < 6 * D; ++k) Jc[6 * D * o + k] = jc[k];
+    if (Jp) for (int k = 0; k < 3 * D; ++k) Jp[3 * D * o + k] = jp[k];
+  }
+}
+
+// ceres::Covariance over the camera blocks (BundleAdjuster.h:478-528): Jacobian with the
+// loss function applied (Covariance::Options::apply_loss_function = true), constant
+// cameras excluded, (J^T J)^-1 formed densely here (Ceres: sparse QR; the same matrix).
+extern "C" int oracle_ba_covariance(const oracle_ba_problem* p, double* cov) {
+  const int nc = p->n_cams, np = p->n_pts;
+  const int nf = std::min(std::max(p->fixed_frames, 0), nc), m = nc - nf;
+  const int n = 6 * m + 3 * np;
+  Linearisation L;
+  linearise(p, p->cams, p->pts, L);
+  std::vector<double> H((size_t)n * n, 0.0);
+  for (int o = 0; o < p->n_obs; ++o) {
+    const int ci = p->cam_idx[o] - nf, pi = p->pt_idx[o];
+    int col[9], nv = 0;
+    double J[4][9];
+    for (int k = 0; k < 4; ++k) {
+      int q = 0;
+      if (ci >= 0) for (int j = 0; j < 6; ++j) J[k][q++] = L.Jc[24 * o + 6 * k + j];
+      for (int j = 0; j < 3; ++j) J[k][q++] = L.Jp[12 * o + 3 * k + j];
+    }
+    if (ci >= 0) for (int j = 0; j < 6; ++j) col[nv++] = 6 * ci + j;
+    for (int j = 0; j < 3; ++j) col[nv++] = 6 * m + 3 * pi + j;
+    for (int a = 0; a < nv; ++a)
+      for (int b = 0; b < nv; ++b) {
+        double s = 0;
+        for (int k = 0; k < 4; ++k) s += J[k][a] * J[k][b];
+        H[(size_t)col[a] * n + col[b]] += s;
+      }
+  }
+  if (!cholesky(H, n)) return 0;
+  // X = L^-1 columns of the camera parameters only, cov = X^T X restricted to them
+  std::vector<double> X((size_t)6 * m * n, 0.0);
+  for (int c = 0; c < 6 * m; ++c) {
+    double* x = &X[(size_t)c * n];
+    for (int k = c; k < n; ++k) {
+      double acc = k == c ? 1.0 : 0.0;
+      for (int l = c; l < k; ++l) acc -= H[(size_t)k * n + l] * x[l];
+      x[k] = acc / H[(size_t)k * n + k];
+    }
+  }
+  for (int i = 0; i < nc; ++i)
+    for (int a = 0; a < 6; ++a)
+      for (int b = 0; b < 6; ++b) {
+        double v = 0;
+        if (i >= nf) {
+          const int pp = 6 * (i - nf) + a, qq = 6 * (i - nf) + b;
+          for (int k = std::max(pp, qq); k < n; ++k) v += X[(size_t)pp * n + k] * X[(size_t)qq * n + k];
+        }
+        cov[36 * i + 6 * a + b] = v;
+      }
+  return 1;
 }
 
 extern "C" double oracle_ba_cost(const oracle_ba_problem* p) { return total_cost(p, p->cams, p->pts); }

@@ -84,6 +84,8 @@ typedef struct {
   double K0[9], K1[9];
   double baseline, feat_var;
   int fixed_frames;
+  int obs_dim;            /* 4 (or 0): Observation<4>; 2: BundleAdjuster<2> Observation<2> {x,y} */
+  const int32_t* cam_id;  /* obs_dim 2: Observation::camID (0 Standard-, else StereoRightError) */
 } oracle_ba_problem;
 
 typedef struct {
@@ -104,7 +106,7 @@ typedef struct {
 } oracle_ba_summary;
 
 void oracle_ba_default_options(oracle_ba_options* o);
-/* residuals (4/obs, sigma-scaled, uncorrected) + analytic-by-Jets jacobians */
+/* residuals (D/obs, D = obs_dim, sigma-scaled, uncorrected) + jacobians by Jets (Dx6, Dx3) */
 void oracle_ba_evaluate(const oracle_ba_problem* p, double* res, double* Jc, double* Jp);
 double oracle_ba_cost(const oracle_ba_problem* p);
 int oracle_ba_solve(oracle_ba_problem* p, const oracle_ba_options* o, oracle_ba_summary* s,
@@ -112,6 +114,9 @@ int oracle_ba_solve(oracle_ba_problem* p, const oracle_ba_options* o, oracle_ba_
 /* one linearisation at the given params: reduced camera system of the first
    LM step (scaled coordinates, radius r).  S is (6m)x(6m), b 6m, m = non-fixed cams. */
 int oracle_ba_reduced_system(const oracle_ba_problem* p, double radius, double* S, double* b);
+/* pose covariance (BundleAdjuster.h:478-528 / ceres::Covariance): dense (J^T J)^-1 over all
+   variable parameters by Cholesky, camera blocks out (zero for constant cameras); 0 if not PD */
+int oracle_ba_covariance(const oracle_ba_problem* p, double* cov /* n_cams*36 */);
 int oracle_ba_reduced_system_ex(const oracle_ba_problem* p, double radius, int jacobi, double* S, double* b);
 
 /* ---- A11: nonMaxSupScanline3x3 (src/core/feature_types.cpp:253-351) ---- */

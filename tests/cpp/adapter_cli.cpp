@@ -3,7 +3,7 @@
 // of libme_hip.so).  Used by tests/test_cpp_adapter.py to show that a C++
 // host built like the reference's src/ gets the same results as the Python
 // mirror and the oracle.
-//   adapter_cli ba  <in.bin> <out.bin>   BundleAdjuster<4>-style solve
+//   adapter_cli ba  <in.bin> <out.bin>   BundleAdjuster<M>-style solve (M = 4 or 2, optional covariance)
 //   adapter_cli mi  <in.bin> <out.bin>   computeMutualInformation / computeEntropy
 //   adapter_cli nms <in.bin> <out.bin>   nonMaxSupScanline3x3
 #include <cstdio>
@@ -39,27 +39,34 @@ Reader read_file(const char* path) {
   return r;
 }
 
-int run_ba(Reader& in, FILE* out) {
+template <int M>
+int solve_ba(Reader& in, FILE* out, int nc, int np, int no, int fixed, int compute_cov) {
   using namespace me::optimisation;
-  const int nc = in.get<int32_t>(), np = in.get<int32_t>(), no = in.get<int32_t>(), fixed = in.get<int32_t>();
   CalibrationParameters calib;
   calib.K.resize(2);
   in.get(calib.K[0].data(), 9);
   in.get(calib.K[1].data(), 9);
   calib.baseline = in.get<double>();
   calib.feat_var = in.get<double>();
+  calib.compute_cov = compute_cov != 0;
   std::vector<std::array<double, 6>> cams(nc);
   std::vector<std::array<double, 3>> pts(np);
   in.get(cams[0].data(), 6 * (size_t)nc);
   in.get(pts[0].data(), 3 * (size_t)np);
-  std::vector<double> o(4 * (size_t)no);
+  std::vector<double> o(M * (size_t)no);
   in.get(o.data(), o.size());
-  std::vector<int32_t> ci(no), pi(no);
+  std::vector<int32_t> ci(no), pi(no), cid(no, 0);
   in.get(ci.data(), no);
   in.get(pi.data(), no);
-  std::vector<StereoObservation> obs(no);
-  for (int k = 0; k < no; ++k) obs[k] = {{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, ci[k], pi[k]};
-  StereoBundleAdjuster ba(calib, cams, pts, obs);
+  if (M == 2) in.get(cid.data(), no);
+  std::vector<Observation<M>> obs(no);
+  for (int k = 0; k < no; ++k) {
+    for (int a = 0; a < M; ++a) obs[k].xy[a] = o[M * k + a];
+    obs[k].camIdx = ci[k];
+    obs[k].ptIdx = pi[k];
+    obs[k].camID = cid[k];
+  }
+  BundleAdjuster<M> ba(calib, cams, pts, obs);
   const auto status = ba.optimise(fixed);
   const int32_t st = (int32_t)status, it = ba.summary().iterations;
   const double cost = ba.summary().final_cost;
@@ -68,7 +75,17 @@ int run_ba(Reader& in, FILE* out) {
   fwrite(&cost, 8, 1, out);
   fwrite(ba.getCameraParams()[0].data(), 8, 6 * (size_t)nc, out);
   fwrite(ba.getPoints()[0].data(), 8, 3 * (size_t)np, out);
+  const int32_t ncov = (int32_t)ba.getPosesCovariance().size();
+  fwrite(&ncov, 4, 1, out);
+  for (const auto& c : ba.getPosesCovariance()) fwrite(c.data(), 8, 36, out);
   return 0;
+}
+
+// payload: nc np no fixed obs_dim compute_cov | K0 K1 | baseline feat_var | cams pts obs cam_idx pt_idx [cam_id]
+int run_ba(Reader& in, FILE* out) {
+  const int nc = in.get<int32_t>(), np = in.get<int32_t>(), no = in.get<int32_t>(), fixed = in.get<int32_t>();
+  const int od = in.get<int32_t>(), cov = in.get<int32_t>();
+  return od == 2 ? solve_ba<2>(in, out, nc, np, no, fixed, cov) : solve_ba<4>(in, out, nc, np, no, fixed, cov);
 }
 
 int run_mi(Reader& in, FILE* out) {

@@ -54,6 +54,7 @@ class OBAProblem(ctypes.Structure):
         ("K0", c_double * 9), ("K1", c_double * 9),
         ("baseline", c_double), ("feat_var", c_double),
         ("fixed_frames", c_int),
+        ("obs_dim", c_int), ("cam_id", POINTER(c_int32)),
     ]
 
 
@@ -120,6 +121,7 @@ def lib():
         L.oracle_ba_cost.argtypes = [P(OBAProblem)]
         L.oracle_ba_solve.argtypes = [P(OBAProblem), P(OBAOptions), P(OBASummary), P(c_double), c_int]
         L.oracle_ba_reduced_system.argtypes = [P(OBAProblem), c_double, P(c_double), P(c_double)]
+        L.oracle_ba_covariance.argtypes = [P(OBAProblem), P(c_double)]
         L.oracle_ba_reduced_system_ex.argtypes = [P(OBAProblem), c_double, c_int, P(c_double), P(c_double)]
         L.oracle_nms_scanline3x3.argtypes = [P(c_double), c_int, c_int, P(c_uint8), P(c_double), c_int]
         L.oracle_klt_track.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, P(c_float), P(c_float), P(c_uint8),
@@ -301,6 +303,11 @@ def ba_struct(bp, keep=None):
     p.baseline = bp.baseline
     p.feat_var = bp.feat_var
     p.fixed_frames = bp.fixed_frames
+    p.obs_dim = int(getattr(bp, "obs_dim", 4))
+    if p.obs_dim == 2:
+        cid = np.ascontiguousarray(bp.cam_id, np.int32)
+        keep.append(cid)
+        p.cam_id = _p(cid, c_int32)
     return p, keep, cams, pts
 
 
@@ -314,12 +321,20 @@ def ba_options(**kw):
 
 def ba_evaluate(bp):
     p, keep, _, _ = ba_struct(bp)
-    no = len(bp.obs)
-    r = np.zeros(4 * no)
-    Jc = np.zeros(24 * no)
-    Jp = np.zeros(12 * no)
+    no, D = len(bp.obs), p.obs_dim
+    r = np.zeros(D * no)
+    Jc = np.zeros(6 * D * no)
+    Jp = np.zeros(3 * D * no)
     lib().oracle_ba_evaluate(ctypes.byref(p), _p(r), _p(Jc), _p(Jp))
-    return r.reshape(no, 4), Jc.reshape(no, 4, 6), Jp.reshape(no, 4, 3)
+    return r.reshape(no, D), Jc.reshape(no, D, 6), Jp.reshape(no, D, 3)
+
+
+def ba_covariance(bp):
+    """Pose covariance blocks (n_cams, 6, 6) at the problem's parameters, or None (not PD)."""
+    p, keep, _, _ = ba_struct(bp)
+    cov = np.zeros(36 * len(bp.cams))
+    ok = lib().oracle_ba_covariance(ctypes.byref(p), _p(cov))
+    return cov.reshape(-1, 6, 6) if ok else None
 
 
 def ba_cost(bp):

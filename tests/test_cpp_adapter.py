@@ -64,22 +64,54 @@ def test_cpp_nms_bit_exact(tmp_path, oracle):
     assert np.array_equal(mx, rmx) and np.array_equal(mask, rmask)
 
 
-@pytest.mark.gpu
-def test_cpp_bundle_adjuster_matches_oracle(tmp_path, oracle):
-    bp = S.ba_problem(20261020, 150, 6, 640, 480)
-    payload = struct.pack("<iiii", len(bp.cams), len(bp.pts), len(bp.obs), bp.fixed_frames)
+def _ba_payload(bp, compute_cov=0):
+    od = getattr(bp, "obs_dim", 4)
+    payload = struct.pack("<iiiiii", len(bp.cams), len(bp.pts), len(bp.obs), bp.fixed_frames, od, compute_cov)
     payload += np.asarray(bp.K0, np.float64).tobytes() + np.asarray(bp.K1, np.float64).tobytes()
     payload += struct.pack("<dd", bp.baseline, bp.feat_var)
     payload += np.ascontiguousarray(bp.cams, np.float64).tobytes() + np.ascontiguousarray(bp.pts).tobytes()
     payload += np.ascontiguousarray(bp.obs, np.float64).tobytes()
     payload += np.ascontiguousarray(bp.cam_idx, np.int32).tobytes() + np.ascontiguousarray(bp.pt_idx).tobytes()
-    _, out = _run("ba", payload, tmp_path)
+    if od == 2:
+        payload += np.ascontiguousarray(bp.cam_id, np.int32).tobytes()
+    return payload
+
+
+def _ba_result(out, bp):
     status, iters, cost = struct.unpack_from("<iid", out)
     off = 16
     cams = np.frombuffer(out, np.float64, 6 * len(bp.cams), off).reshape(-1, 6)
-    pts = np.frombuffer(out, np.float64, 3 * len(bp.pts), off + 48 * len(bp.cams)).reshape(-1, 3)
+    off += 48 * len(bp.cams)
+    pts = np.frombuffer(out, np.float64, 3 * len(bp.pts), off).reshape(-1, 3)
+    off += 24 * len(bp.pts)
+    (ncov,) = struct.unpack_from("<i", out, off)
+    cov = np.frombuffer(out, np.float64, 36 * ncov, off + 4).reshape(-1, 6, 6)
+    return status, iters, cost, cams, pts, cov
+
+
+@pytest.mark.gpu
+def test_cpp_bundle_adjuster_matches_oracle(tmp_path, oracle):
+    bp = S.ba_problem(20261020, 150, 6, 640, 480)
+    _, out = _run("ba", _ba_payload(bp), tmp_path)
+    status, iters, cost, cams, pts, cov = _ba_result(out, bp)
     rc, rp, rs = oracle.ba_solve(bp)
     assert status == 2 and iters == rs["iterations"]  # Status::SUCCESSFUL
+    assert len(cov) == 0
     np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(cost, rs["final_cost"], rtol=1e-8)
+
+
+@pytest.mark.gpu
+def test_cpp_mono_bundle_adjuster_with_covariance(tmp_path, oracle):
+    bp = S.ba_problem_mono(20261021, 150, 6, 640, 480)
+    _, out = _run("ba", _ba_payload(bp, compute_cov=1), tmp_path)
+    status, iters, cost, cams, pts, cov = _ba_result(out, bp)
+    rc, rp, rs = oracle.ba_solve(bp)
+    assert status == 2 and iters == rs["iterations"]
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+    after = bp.copy()
+    after.cams, after.pts = rc, rp
+    rcov = oracle.ba_covariance(after)
+    np.testing.assert_allclose(cov, rcov, rtol=1e-5, atol=1e-8 * np.abs(rcov).max())

@@ -83,6 +83,7 @@ class BAProblemC(ctypes.Structure):
         ("K0", c_double * 9), ("K1", c_double * 9),
         ("baseline", c_double), ("feat_var", c_double),
         ("fixed_frames", c_int), ("mem", c_int),
+        ("obs_dim", c_int), ("cam_id", POINTER(c_int32)),
     ]
 
 
@@ -121,7 +122,7 @@ EXPORTS = [
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
-    "me_ba_solve_sharded",
+    "me_ba_solve_sharded", "me_ba_covariance",
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
@@ -186,6 +187,7 @@ def load_library(path: str = LIB_PATH):
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
         "me_ba_evaluate": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_double), P(c_double)]),
         "me_ba_reduced_system": (c_int, [c_void_p, P(BAProblemC), c_double, P(c_double), P(c_double)]),
+        "me_ba_covariance": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_int)]),
         "me_ba_solve_sharded": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), ALLREDUCE_FN, c_void_p,
                                         P(BASummaryC)]),
         "me_klt_default_params": (None, [P(KLTParamsC)]),

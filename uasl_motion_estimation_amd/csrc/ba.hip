@@ -152,6 +152,47 @@ __device__ __forceinline__ void stereo_residual(const Geo& g, const double* cam,
   }
 }
 
+// BundleAdjuster<2> residuals: StandardReprojectionError (BundleAdjuster.h:71-103)
+// for camID 0, StereoRightError (:106-139, p.x += cam[0] - baseline) otherwise;
+// both project with K[0].  Rows 2, 3 are zero so the 4-row pipeline is shared
+// (zero rows add nothing to J^T J, J^T r or the Huber argument).
+__device__ __forceinline__ void mono_residual(const Geo& g, const double* cam, const double* X, const double* f,
+                                              bool right, double* r, double* Jc, double* Jp) {
+  double P[3], dPdw[9], dPdX[9];
+  rotate(cam + 3, X, P, Jc ? dPdw : nullptr, Jc ? dPdX : nullptr);
+  P[0] = P[0] + (right ? cam[0] - g.baseline : cam[0]);
+  P[1] = P[1] + cam[1];
+  P[2] = P[2] + cam[2];
+  const double x = g.K0[0] * (P[0] / P[2]) + g.K0[2];
+  const double y = g.K0[4] * (P[1] / P[2]) + g.K0[5];
+  r[0] = g.sinv * (x - f[0]);
+  r[1] = g.sinv * (y - f[1]);
+  r[2] = 0.0;
+  r[3] = 0.0;
+  if (!Jc) return;
+  const double iz = 1.0 / P[2], iz2 = iz * iz;
+  double dr[2][3] = {{g.sinv * g.K0[0] * iz, 0.0, -g.sinv * g.K0[0] * P[0] * iz2},
+                     {0.0, g.sinv * g.K0[4] * iz, -g.sinv * g.K0[4] * P[1] * iz2}};
+  for (int k = 0; k < 2; ++k) {
+    for (int j = 0; j < 3; ++j) Jc[k * 6 + j] = dr[k][j];
+    for (int j = 0; j < 3; ++j) {
+      Jc[k * 6 + 3 + j] = dr[k][0] * dPdw[0 * 3 + j] + dr[k][1] * dPdw[1 * 3 + j] + dr[k][2] * dPdw[2 * 3 + j];
+      Jp[k * 3 + j] = dr[k][0] * dPdX[0 * 3 + j] + dr[k][1] * dPdX[1 * 3 + j] + dr[k][2] * dPdX[2 * 3 + j];
+    }
+  }
+  for (int k = 12; k < 24; ++k) Jc[k] = 0.0;
+  for (int k = 6; k < 12; ++k) Jp[k] = 0.0;
+}
+
+// residual (+ optional Jacobian) of observation o for the window's model
+__device__ __forceinline__ void obs_residual(const Geo& g, const Bufs& b, long o, const double* cam, const double* X,
+                                             double* r, double* Jc, double* Jp) {
+  if (g.od == 4)
+    stereo_residual(g, cam, X, b.obs + 4 * o, r, Jc, Jp);
+  else
+    mono_residual(g, cam, X, b.obs + 2 * o, b.cam_id[o] != 0, r, Jc, Jp);
+}
+
 // ceres::HuberLoss(1.0): rho0 and sqrt(rho1) (Corrector with rho'' <= 0)
 __device__ __forceinline__ void huber(double s, double* rho0, double* sqrt_rho1) {
   if (s > 1.0) {
@@ -181,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
     const int ci = b.cam_idx[o], pi = b.pt_idx[o];
     double* L = b.lin + (long)o * kLinStride;
     double r[4], Jc[24], Jp[12];
-    stereo_residual(g, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, b.obs + 4 * (long)o, r, Jc, Jp);
+    obs_residual(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
     const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
     double rho0, sc;
     huber(s, &rho0, &sc);
@@ -1129,7 +1170,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
         mc -= jd * (Lo[k] + jd / 2.0);
       }
       double r[4];
-      stereo_residual(g, cams_c + 6 * b.cam_idx[o], xc, b.obs + 4 * (long)o, r, nullptr, nullptr);
+      obs_residual(g, b, o, cams_c + 6 * b.cam_idx[o], xc, r, nullptr, nullptr);
       const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
       double rho0, sc;
       huber(s, &rho0, &sc);
@@ -1235,8 +1276,7 @@ __global__ __launch_bounds__(kBlock) void cost_kernel(Geo g, Bufs b, int which, 
   double c = 0;
   if (o < g.no) {
     double r[4];
-    stereo_residual(g, b.cams[which] + 6 * b.cam_idx[o], b.pts[which] + 3 * b.pt_idx[o], b.obs + 4 * (long)o, r,
-                    nullptr, nullptr);
+    obs_residual(g, b, o, b.cams[which] + 6 * b.cam_idx[o], b.pts[which] + 3 * b.pt_idx[o], r, nullptr, nullptr);
     const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
     double rho0, sc;
     huber(s, &rho0, &sc);
@@ -1251,12 +1291,81 @@ __global__ __launch_bounds__(kBlock) void eval_kernel(Geo g, Bufs b, double* res
   const int o = blockIdx.x * kBlock + threadIdx.x;
   if (o >= g.no) return;
   double r[4], jc[24], jp[12];
-  stereo_residual(g, b.cams[0] + 6 * b.cam_idx[o], b.pts[0] + 3 * b.pt_idx[o], b.obs + 4 * (long)o, r, jc, jp);
-  for (int k = 0; k < 4; ++k) res[4 * (long)o + k] = r[k];
+  obs_residual(g, b, o, b.cams[0] + 6 * b.cam_idx[o], b.pts[0] + 3 * b.pt_idx[o], r, jc, jp);
+  const int od = g.od;  // output rows per observation: Observation<M>::data size
+  for (int k = 0; k < od; ++k) res[od * (long)o + k] = r[k];
   if (Jc)
-    for (int k = 0; k < 24; ++k) Jc[24 * (long)o + k] = jc[k];
+    for (int k = 0; k < 6 * od; ++k) Jc[6 * od * (long)o + k] = jc[k];
   if (Jp)
-    for (int k = 0; k < 12; ++k) Jp[12 * (long)o + k] = jp[k];
+    for (int k = 0; k < 3 * od; ++k) Jp[3 * od * (long)o + k] = jp[k];
+}
+
+// Pose covariance (BundleAdjuster<M>::extract_covariance, BundleAdjuster.h:478-528):
+// the camera blocks of (J^T J)^-1 are the blocks of S^-1, S the undamped,
+// unscaled point-eliminated camera system.  One workgroup: in-place dense
+// Cholesky of S (global memory, the matrix is at most 300 x 300), X = L^-1 one
+// column per thread, then cov_i = (X^T X) over camera i's six columns.  Not on
+// the frame path (compute_cov is off by default, BundleAdjuster.h:41-42).
+constexpr int kCovBlock = 1024;
+__global__ __launch_bounds__(kCovBlock) void cov_kernel(Geo g, Bufs b, double* X, double* cov, int* ok_out) {
+  __shared__ int sfail;
+  const int n = g.n6, tid = threadIdx.x;
+  double* A = b.S;  // row-major n x n, symmetric
+  if (tid == 0) sfail = b.st->fail || b.st->bad_input;
+  __syncthreads();
+  for (int j = 0; j < n && !sfail; ++j) {
+    if (tid == 0) {
+      const double d = A[(long)j * n + j];
+      if (!(d > 0.0)) sfail = 1;
+      else A[(long)j * n + j] = sqrt(d);
+    }
+    __syncthreads();
+    if (sfail) break;
+    const double djj = A[(long)j * n + j];
+    for (int i = j + 1 + tid; i < n; i += kCovBlock) A[(long)i * n + j] /= djj;
+    __syncthreads();
+    const int m = n - j - 1;  // trailing lower triangle, m(m+1)/2 entries
+    for (long e = tid; e < (long)m * (m + 1) / 2; e += kCovBlock) {
+      int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) / 2.0);
+      while ((long)i * (i + 1) / 2 > e) --i;
+      while ((long)(i + 1) * (i + 2) / 2 <= e) ++i;
+      const int k = (int)(e - (long)i * (i + 1) / 2);
+      const int ii = j + 1 + i, kk = j + 1 + k;
+      A[(long)ii * n + kk] -= A[(long)ii * n + j] * A[(long)kk * n + j];
+    }
+    __syncthreads();
+  }
+  if (sfail) {
+    if (tid == 0) *ok_out = 0;
+    return;
+  }
+  // X = L^-1, column c by forward substitution (X column-major: X[c * n + k] = (L^-1)[k][c])
+  for (int c = tid; c < n; c += kCovBlock) {
+    double* x = X + (long)c * n;
+    for (int k = 0; k < c; ++k) x[k] = 0.0;
+    for (int k = c; k < n; ++k) {
+      double acc = k == c ? 1.0 : 0.0;
+      for (int l = c; l < k; ++l) acc -= A[(long)k * n + l] * x[l];
+      x[k] = acc / A[(long)k * n + k];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < 36 * g.nc; e += kCovBlock) {
+    const int ci = e / 36, a = (e % 36) / 6, c = e % 6;
+    double v = 0.0;
+    if (ci >= g.nf) {  // constant cameras: zero block (ceres::Covariance)
+      const int p = 6 * (ci - g.nf) + a, q = 6 * (ci - g.nf) + c;
+      const double *xp = X + (long)p * n, *xq = X + (long)q * n;
+      for (int k = max(p, q); k < n; ++k) v += xp[k] * xq[k];
+    }
+    cov[e] = v;
+  }
+  if (tid == 0) *ok_out = 1;
+}
+
+// Ceres covariance ignores the point bounds: an infeasible point does not stop it.
+__global__ void cov_prep_kernel(Bufs b) {
+  if (!b.st->bad_input) b.st->done = 0;
 }
 
 // ---------------------------------------------------------------- device plan
@@ -1528,7 +1637,12 @@ int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base) {
   ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
   ME_CHECK(c, p->n_cams <= kMaxScanCams, "BA: at most %d cameras per window", kMaxScanCams);
-  ME_CHECK(c, p->feat_var > 0 && p->baseline != 0.0, "BA: wrong calibration parameters (BundleAdjuster.h:147)");
+  ME_CHECK(c, p->obs_dim == 0 || p->obs_dim == 2 || p->obs_dim == 4, "BA: obs_dim must be 2 or 4 (Observation<M>)");
+  const bool mono = p->obs_dim == 2;
+  ME_CHECK(c, p->feat_var > 0 && (mono || p->baseline != 0.0), "BA: wrong calibration parameters (BundleAdjuster.h:147)");
+  ME_CHECK(c, !mono || p->cam_id || p->n_obs == 0, "BA: obs_dim 2 needs cam_id (Observation::camID)");
+  // BundleAdjuster<2>::optimise: a zero baseline is replaced by 0.5 (BundleAdjuster.h:389-390)
+  const double baseline = mono && p->baseline == 0 ? 0.5 : p->baseline;
   ME_CHECK(c, p->mem == ME_HOST || p->mem == ME_DEVICE, "BA: bad memory kind");
   if (p->mem == ME_HOST) {  // device-resident input is validated on the device (State::bad_input)
     for (int i = 0; i < p->n_obs; ++i) {
@@ -1543,6 +1657,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.np = p->n_pts;
   g.no = p->n_obs;
   g.nf = std::min(std::max(p->fixed_frames, 0), p->n_cams);
+  g.od = mono ? 2 : 4;
   g.m = g.nc - g.nf;
   g.n6 = 6 * g.m;
   g.Rpad = (int)rup(g.n6 + 1, 16);  // camera columns | z_p column n6 | zero padding
@@ -1562,10 +1677,10 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.pstride = std::max({g.nblk_obs, g.nblk_pts, g.nblk_step, g.ksplit});
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
-  g.baseline = p->baseline;
+  g.baseline = baseline;
   g.sinv = 1.0 / std::sqrt(p->feat_var);
-  const double Zmax = p->K0[0] * p->baseline / 0.1;
-  const double Zmin = p->K0[0] * p->baseline / (2 * p->K0[2]);
+  const double Zmax = p->K0[0] * baseline / 0.1;
+  const double Zmin = p->K0[0] * baseline / (2 * p->K0[2]);
   g.hi[0] = Zmax / p->K0[0] * p->K0[2];
   g.hi[1] = Zmax / p->K0[4] * p->K0[5];
   g.hi[2] = Zmax;
@@ -1592,9 +1707,10 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   auto add = [&](size_t bytes, void* dst) { items.push_back({rup((long)std::max<size_t>(bytes, 8), 256), (void**)dst}); };
   add(8 * 6 * (size_t)g.nc, &b.cams[0]);
   add(8 * 3 * (size_t)g.np, &b.pts[0]);
-  add(8 * 4 * (size_t)g.no, &b.obs);
+  add(8 * g.od * (size_t)g.no, &b.obs);
   add(4 * (size_t)g.no, &b.cam_idx);
   add(4 * (size_t)g.no, &b.pt_idx);
+  add(mono ? 4 * (size_t)g.no : 0, &b.cam_id);
   const size_t n_inputs = items.size();
   add(8 * 6 * (size_t)g.nc, &b.cams[1]);
   add(8 * 3 * (size_t)g.np, &b.pts[1]);
@@ -1662,11 +1778,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   if (!dev) {
     // pack the inputs at their arena offsets in pinned memory: one H2D copy
     char* h = (char*)hp;
-    const void* src[5] = {p->cams, p->pts, p->obs, p->cam_idx, p->pt_idx};
-    const size_t len[5] = {8 * 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np, 8 * 4 * (size_t)g.no, 4 * (size_t)g.no,
-                           4 * (size_t)g.no};
+    const void* src[6] = {p->cams, p->pts, p->obs, p->cam_idx, p->pt_idx, p->cam_id};
+    const size_t len[6] = {8 * 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np, 8 * g.od * (size_t)g.no, 4 * (size_t)g.no,
+                           4 * (size_t)g.no, mono ? 4 * (size_t)g.no : 0};
     size_t off = 0;
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < 6; ++k) {
       if (len[k]) std::memcpy(h + off, src[k], len[k]);
       off += items[k].first;
     }
@@ -1675,6 +1791,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     b.obs = p->obs;
     b.cam_idx = p->cam_idx;
     b.pt_idx = p->pt_idx;
+    if (mono) b.cam_id = p->cam_id;
   }
   ME_HIP(c, hipMemsetAsync(b.work, 0, work_bytes, s));
   const double* cams_in = dev ? p->cams : b.cams[0];
@@ -1925,15 +2042,16 @@ extern "C" int me_ba_evaluate(me_ctx* c, const me_ba_problem* p, double* res, do
   if (rc < 0) return rc;
   const int no = P.g.no;
   void* d;
-  ME_TRY(me_scratch(c, SLOT_GENERIC, 8 * 40 * (size_t)std::max(no, 1), &d));
+  const size_t od = P.g.od;
+  ME_TRY(me_scratch(c, SLOT_GENERIC, 8 * 10 * od * (size_t)std::max(no, 1), &d));
   double* dres = (double*)d;
-  double* djc = dres + 4 * (size_t)no;
-  double* djp = djc + 24 * (size_t)no;
+  double* djc = dres + od * (size_t)no;
+  double* djp = djc + 6 * od * (size_t)no;
   hipLaunchKernelGGL(eval_kernel, dim3(blocks(no, kBlock)), dim3(kBlock), 0, c->stream, P.g, P.b, dres, djc, djp);
   ME_TRY(me_check_launch(c, "eval_kernel"));
-  ME_HIP(c, hipMemcpyAsync(res, dres, 8 * 4 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
-  if (Jc) ME_HIP(c, hipMemcpyAsync(Jc, djc, 8 * 24 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
-  if (Jp) ME_HIP(c, hipMemcpyAsync(Jp, djp, 8 * 12 * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(res, dres, 8 * od * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  if (Jc) ME_HIP(c, hipMemcpyAsync(Jc, djc, 8 * 6 * od * (size_t)no, hipMemcpyDeviceToHost, c->stream));
+  if (Jp) ME_HIP(c, hipMemcpyAsync(Jp, djp, 8 * 3 * od * (size_t)no, hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
   return ME_OK;
 }
@@ -1963,6 +2081,39 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
       S[(size_t)i * n + j] = v;
     }
   for (int i = 0; i < n; ++i) bout[i] = Sh[(size_t)n * n + i];
+  return ME_OK;
+}
+
+extern "C" int me_ba_covariance(me_ctx* c, const me_ba_problem* p, double* cov, int* ok) {
+  if (!c || !p || !cov || !ok) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  me_ba_options o;
+  me_ba_default_options(&o);
+  o.jacobi_scaling = 0;                  // S unscaled: its inverse is the covariance directly
+  o.initial_trust_region_radius = INFINITY;  // D / radius = 0: no LM damping
+  Plan P;
+  ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
+  int rc = plan_build(c, p, &o, P, 0);
+  if (rc < 0) return rc;
+  const Geo& g = P.g;
+  hipLaunchKernelGGL(cov_prep_kernel, dim3(1), dim3(1), 0, c->stream, P.b);
+  ME_TRY(enqueue_linearize(P, nullptr, nullptr));
+  ME_TRY(enqueue_assemble(P, nullptr));
+  void* d;
+  const size_t nx = (size_t)g.n6 * g.n6;
+  ME_TRY(me_scratch(c, SLOT_GENERIC, 8 * (nx + 36 * (size_t)g.nc) + 64, &d));
+  double* X = (double*)d;
+  double* dcov = X + nx;
+  int* dok = (int*)(dcov + 36 * (size_t)g.nc);
+  hipLaunchKernelGGL(cov_kernel, dim3(1), dim3(kCovBlock), 0, c->stream, g, P.b, X, dcov, dok);
+  ME_TRY(me_check_launch(c, "cov_kernel"));
+  std::vector<double> h(36 * (size_t)g.nc);
+  int hok = 0;
+  ME_HIP(c, hipMemcpyAsync(h.data(), dcov, 8 * h.size(), hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(&hok, dok, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  *ok = hok;
+  if (hok) std::memcpy(cov, h.data(), 8 * h.size());
   return ME_OK;
 }
 

@@ -2,9 +2,13 @@
 // (SURVEY §8a A13-A17).  Included by ba.hip only.
 //
 // Replaces the Ceres solve behind BundleAdjuster<4>::optimise
-// (include/MotionEstimation/optimisation/BundleAdjuster.h:431-476):
-//   linearize      per observation: StereoReprojectionError (:153-171) value +
-//                  analytic Jacobian, HuberLoss(1.0) corrector, cost.
+// (include/MotionEstimation/optimisation/BundleAdjuster.h:431-476) and
+// BundleAdjuster<2>::optimise (:378-429):
+//   linearize      per observation: StereoReprojectionError (:153-171), or
+//                  StandardReprojectionError (:71-103) / StereoRightError
+//                  (:106-139) chosen by camID for <2>, value + analytic
+//                  Jacobian (2-row residuals padded with zero rows, so every
+//                  later stage is shared), HuberLoss(1.0) corrector, cost.
 //   cam_assemble   one workgroup per variable camera: Jacobi column norms
 //                  (iteration 0), scaled U = Jc'Jc, g_c = Jc'r.
 //   pt_schur       per landmark sub-chunk: V = Jp'Jp, g_p, V + D/radius ->
@@ -62,6 +66,7 @@ enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 struct Geo {
   int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_pts, nblk_step, pstride, jacobi,
       ck;
+  int od;                  // residual rows per observation: 4 StereoReprojectionError, 2 Standard/StereoRight
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -73,6 +78,7 @@ struct Bufs {
   const double* obs;
   const int* cam_idx;
   const int* pt_idx;
+  const int* cam_id;  // od == 2: Observation::camID (0 left -> StandardReprojectionError, else StereoRightError)
   int* p_off;         // CSR by point (obs sorted by cam inside a point)
   int* p_obs;
   int* pos;           // obs -> CSR slot

@@ -341,6 +341,11 @@ def ba_struct(bp, keep: list):
     p.K0[:] = [float(x) for x in np.asarray(bp.K0).ravel()]
     p.K1[:] = [float(x) for x in np.asarray(bp.K1).ravel()]
     p.baseline, p.feat_var, p.fixed_frames = float(bp.baseline), float(bp.feat_var), int(bp.fixed_frames)
+    p.obs_dim = int(getattr(bp, "obs_dim", 4))
+    if p.obs_dim == 2:  # BundleAdjuster<2>: Observation<2> + camID
+        cid = np.ascontiguousarray(bp.cam_id, np.int32)
+        keep.append(cid)
+        p.cam_id = _p(cid, c_int32)
     return p, cams, pts
 
 
@@ -395,9 +400,14 @@ class DeviceBAProblem:
                       obs=np.ascontiguousarray(bp.obs, np.float64),
                       cam_idx=np.ascontiguousarray(bp.cam_idx, np.int32),
                       pt_idx=np.ascontiguousarray(bp.pt_idx, np.int32))
+        self.obs_dim = int(getattr(bp, "obs_dim", 4))
+        names = ["cams", "pts", "obs", "cam_idx", "pt_idx", "cams0", "pts0"]
+        if self.obs_dim == 2:
+            arrays["cam_id"] = np.ascontiguousarray(bp.cam_id, np.int32)
+            names.append("cam_id")
         self.nbytes = {k: v.nbytes for k, v in arrays.items()}
         self.d = {}
-        for k in ("cams", "pts", "obs", "cam_idx", "pt_idx", "cams0", "pts0"):
+        for k in names:
             src = arrays[k[:-1]] if k.endswith("0") else arrays[k]
             self.d[k] = self.ctx.malloc(max(src.nbytes, 16))
             self.ctx.h2d(self.d[k], src)
@@ -419,6 +429,9 @@ class DeviceBAProblem:
         p.K1[:] = [float(x) for x in np.asarray(self.bp.K1).ravel()]
         p.baseline, p.feat_var = float(self.bp.baseline), float(self.bp.feat_var)
         p.fixed_frames, p.mem = int(self.bp.fixed_frames), ME_DEVICE
+        p.obs_dim = self.obs_dim
+        if self.obs_dim == 2:
+            p.cam_id = ctypes.cast(self.d["cam_id"], POINTER(c_int32))
         return p
 
     def solve(self, options: SolverOptions | None = None) -> dict:
@@ -459,6 +472,8 @@ def shard_landmarks(bp, rank: int, world: int):
     local.obs = np.ascontiguousarray(np.asarray(bp.obs)[sel])
     local.cam_idx = np.ascontiguousarray(np.asarray(bp.cam_idx)[sel], dtype=np.int32)
     local.pt_idx = np.ascontiguousarray(pidx[sel] - lo, dtype=np.int32)
+    if getattr(bp, "obs_dim", 4) == 2:
+        local.cam_id = np.ascontiguousarray(np.asarray(bp.cam_id)[sel], dtype=np.int32)
     return local, (lo, hi)
 
 
@@ -514,12 +529,25 @@ def ba_evaluate(bp, ctx: Context | None = None):
     ctx = ctx or default_context()
     keep = []
     p, _, _ = ba_struct(bp, keep)
-    no = len(bp.obs)
-    r = np.zeros(4 * no)
-    Jc = np.zeros(24 * no)
-    Jp = np.zeros(12 * no)
+    no, D = len(bp.obs), p.obs_dim
+    r = np.zeros(D * no)
+    Jc = np.zeros(6 * D * no)
+    Jp = np.zeros(3 * D * no)
     ctx.check(ctx.lib.me_ba_evaluate(ctx.h, byref(p), _p(r), _p(Jc), _p(Jp)), "me_ba_evaluate")
-    return r.reshape(no, 4), Jc.reshape(no, 4, 6), Jp.reshape(no, 4, 3)
+    return r.reshape(no, D), Jc.reshape(no, D, 6), Jp.reshape(no, D, 3)
+
+
+def ba_covariance(bp, ctx: Context | None = None):
+    """Pose covariance blocks (n_cams, 6, 6) at the problem's current parameters
+    (BundleAdjuster<M>::extract_covariance, BundleAdjuster.h:478-528), or None
+    when J^T J is not positive definite (Ceres: rank-deficient Jacobian)."""
+    ctx = ctx or default_context()
+    keep = []
+    p, _, _ = ba_struct(bp, keep)
+    cov = np.zeros(36 * len(bp.cams))
+    ok = c_int(0)
+    ctx.check(ctx.lib.me_ba_covariance(ctx.h, byref(p), _p(cov), byref(ok)), "me_ba_covariance")
+    return cov.reshape(-1, 6, 6) if ok.value else None
 
 
 def ba_reduced_system(bp, radius: float = 1e4, ctx: Context | None = None):
@@ -545,13 +573,26 @@ class _BAArrays:
     baseline: float
     feat_var: float
     fixed_frames: int
+    obs_dim: int = 4
+    cam_id: np.ndarray = None
 
 
 class BundleAdjuster:
-    """BundleAdjuster<4> (stereo windowed BA, BundleAdjuster.h:182-476)."""
+    """BundleAdjuster<M> (windowed BA, BundleAdjuster.h:182-528): M = 4 stereo
+    tracks (StereoReprojectionError), M = 2 mono tracks (Standard/StereoRight
+    error by the track's camera ID).  ``M`` defaults from the track features."""
 
     def __init__(self, params: CalibrationParameters, cams: list, obs: list, ctx: Context | None = None,
-                 options: SolverOptions | None = None):
+                 options: SolverOptions | None = None, M: int | None = None):
+        if M is None:
+            M = 4
+            if obs:
+                f = obs[0].getFeat(0) if obs[0].getNbFeatures() else None
+                M = 2 if f is not None and not hasattr(f[0], "__len__") else 4
+        if M not in (2, 4):
+            raise ValueError("BundleAdjuster<M>: M is 2 (mono) or 4 (stereo)")
+        self.M = M
+        self.m_camera_covs = []
         self.calib_params = params
         self.m_status = Status.UNINITIALISED
         self.m_camera_params = []
@@ -583,35 +624,58 @@ class BundleAdjuster:
             if init_points:
                 p = track.get3DLocation()
                 self.m_point_params.append(np.array([p[0] / p[3], p[1] / p[3], p[2] / p[3]]))
-            for i in range(track.getNbFeatures()):
+            for i in range(track.getNbFeatures()):  # <2>: BundleAdjuster.h:322-344
                 fi = track.getFrameIdx(i)
                 if fi - first_frame >= 0:
-                    (xl, yl), (xr, yr) = track.getFeat(i)
-                    self.m_observations.append(((xl, yl, xr, yr), fi - first_frame, pt_idx, track.getCameraID()))
+                    if self.M == 4:
+                        (xl, yl), (xr, yr) = track.getFeat(i)
+                        data = (xl, yl, xr, yr)
+                    else:
+                        x, y = track.getFeat(i)
+                        data = (x, y)
+                    self.m_observations.append((data, fi - first_frame, pt_idx, track.getCameraID()))
         self.m_status = Status.INITIALISED
 
     def _arrays(self, fixed: int) -> _BAArrays:
         K = self.calib_params.K
         K0 = np.asarray(K[0], np.float64)
-        if len(K) < 2:
+        if self.M == 4 and len(K) < 2:
             raise ValueError("StereoReprojectionError reads K[1] (BundleAdjuster.h:163): give two intrinsics")
-        K1 = np.asarray(K[1], np.float64)
-        obs = np.array([o[0] for o in self.m_observations], np.float64).reshape(-1, 4)
+        K1 = np.asarray(K[1] if len(K) > 1 else K[0], np.float64)  # <2> uses K[0] only
+        obs = np.array([o[0] for o in self.m_observations], np.float64).reshape(-1, self.M)
         ci = np.array([o[1] for o in self.m_observations], np.int32)
         pi = np.array([o[2] for o in self.m_observations], np.int32)
+        cid = np.array([o[3] for o in self.m_observations], np.int32)
+        if self.M == 2 and self.calib_params.baseline == 0:  # BundleAdjuster.h:389-390 (mutates calib)
+            self.calib_params.baseline = 0.5
         return _BAArrays(np.array(self.m_camera_params).reshape(-1, 6), np.array(self.m_point_params).reshape(-1, 3),
-                         obs, ci, pi, K0, K1, self.calib_params.baseline, self.calib_params.feat_var, fixed)
+                         obs, ci, pi, K0, K1, self.calib_params.baseline, self.calib_params.feat_var, fixed,
+                         self.M, cid)
 
     def optimise(self, fixedFrames: int) -> Status:
         if self.m_status != Status.INITIALISED:
             print("[Bundle Adjuster] system should be initiliased to perform optimisation!")
             return self.m_status
-        cams, pts, summ = ba_solve(self._arrays(fixedFrames), self.options, self.ctx)
+        arrays = self._arrays(fixedFrames)
+        cams, pts, summ = ba_solve(arrays, self.options, self.ctx)
         self.m_camera_params = [c.copy() for c in cams]
         self.m_point_params = [p.copy() for p in pts]
         self.summary = summ
+        if self.calib_params.compute_cov:  # BundleAdjuster.h:424-425,471-472
+            arrays.cams, arrays.pts = cams, pts
+            cov = ba_covariance(arrays, self.ctx)
+            if cov is None:
+                print("[Bundle Adjuster] error computing the covariance matrix")
+            else:
+                self.m_camera_covs = [c.copy() for c in cov]
         self.m_status = Status.SUCCESSFUL if summ["status"] == 2 else Status.FAILED
         return self.m_status
+
+    def getPosesCovariance(self):
+        return [c.copy() for c in self.m_camera_covs]
+
+    def getPointsCovariance(self):  # never filled by the reference (BundleAdjuster.h:505-506,519-526)
+        return []
 
     def getPoints(self):
         return [p.copy() for p in self.m_point_params]

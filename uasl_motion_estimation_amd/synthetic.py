@@ -107,10 +107,13 @@ class BAProblem:
     fixed_frames: int
     cams_true: np.ndarray = field(default=None)
     pts_true: np.ndarray = field(default=None)
+    obs_dim: int = 4                      # 2: BundleAdjuster<2> (obs (O, 2) + cam_id)
+    cam_id: np.ndarray = field(default=None)
 
     def copy(self):
         return BAProblem(self.cams.copy(), self.pts.copy(), self.obs, self.cam_idx, self.pt_idx, self.K0, self.K1,
-                         self.baseline, self.feat_var, self.fixed_frames, self.cams_true, self.pts_true)
+                         self.baseline, self.feat_var, self.fixed_frames, self.cams_true, self.pts_true,
+                         self.obs_dim, self.cam_id)
 
 
 def ba_problem(seed: int, n_pts: int, window: int, width: int, height: int, noise: float = 0.5,
@@ -189,6 +192,27 @@ def ba_problem(seed: int, n_pts: int, window: int, width: int, height: int, nois
     Zmax = K[0, 0] * b / 0.1
     pts[:, 2] = np.clip(pts[:, 2], K[0, 0] * b / (2 * K[0, 2]) + 1e-3, Zmax - 1e-3)
     return BAProblem(cams, pts, obs, cidx, pidx, K.copy(), K.copy(), b, noise ** 2, fixed, cams_true, pts_true)
+
+
+def ba_problem_mono(seed: int, n_pts: int, window: int, width: int, height: int, noise: float = 0.5,
+                    fixed: int = 2, min_len: int = 3, right_frac: float = 0.3) -> BAProblem:
+    """BundleAdjuster<2> window: the stereo window's tracks, each kept in ONE
+    image (WBA_Point::camID 0 = left, 1 = right, BundleAdjuster.h:395-398) as
+    Observation<2> {x, y}; tracks shorter than ``min_len`` frames dropped."""
+    bp = ba_problem(seed, n_pts, window, width, height, noise=noise, fixed=fixed)
+    rng = np.random.default_rng(seed + 7)
+    cnt = np.bincount(bp.pt_idx, minlength=len(bp.pts))
+    keep_pt = cnt >= min_len
+    new_id = np.cumsum(keep_pt) - 1
+    side = (rng.random(len(bp.pts)) < right_frac).astype(np.int32)  # per track
+    sel = keep_pt[bp.pt_idx]
+    o4 = bp.obs[sel]
+    pid = bp.pt_idx[sel]
+    cid = side[pid]
+    obs = np.where(cid[:, None] == 0, o4[:, 0:2], o4[:, 2:4])
+    return BAProblem(bp.cams, bp.pts[keep_pt].copy(), np.ascontiguousarray(obs), bp.cam_idx[sel].copy(),
+                     new_id[pid].astype(np.int32), bp.K0, bp.K1, bp.baseline, bp.feat_var, fixed, bp.cams_true,
+                     bp.pts_true[keep_pt], 2, np.ascontiguousarray(cid, np.int32))
 
 
 # ------------------------------------------------------------------ images
