@@ -15,6 +15,21 @@
 
 using namespace me_dev;
 
+// development timing experiments only (tools/mi_exp.sh builds variants out of tree):
+// 1 no term walk, 2 walk without the table gather, 3 no histogram updates
+#ifndef MI_EXP
+#define MI_EXP 0
+#endif
+#ifndef MI_MREG
+#define MI_MREG 0  // marginal counts: 1 registers (byte select), 0 LDS words
+#endif
+#ifndef MI_UCLR
+#define MI_UCLR 1  // joint-word clear in the walk: 1 unconditional store, 0 predicated
+#endif
+#ifndef MI_PERM
+#define MI_PERM 37  // histogram update order: pixel p = (k * MI_PERM) mod (PW PH), 1 = row-major
+#endif
+
 namespace {
 
 // below this many pairs the 8-lane batch kernel leaves most CUs idle: 16 lanes per pair
@@ -45,15 +60,17 @@ __global__ void mi_table_kernel(int N, float invN, float* __restrict__ tab) {
 //  * lane-private histogram, word w of lane l at lds[64 w + l]: every LDS
 //    access of the wave hits 64 distinct banks whatever the data, no atomics
 //    collide and no barrier is ever needed (nothing crosses lanes);
-//  * per pixel one packed-u8 ds_add (joint) and one ds_or (occupancy bitmap);
-//    the marginals are derived afterwards from the joint rows (v_sad_u8 row
-//    sums, packed-byte column sums), cheaper than two more atomics per pixel;
+//  * per pixel one packed-u8 ds_add (joint); the marginals and the occupancy
+//    bitmap are derived afterwards from one read of the joint words (v_sad_u8
+//    row sums, packed-byte column sums, carry-free non-zero-byte flags), and
+//    the walk clears each joint word as it leaves it: per pair 121 LDS atomics
+//    instead of 242, and no separate clearing pass;
 //  * term walk: one flat loop over the lane's set bitmap bits in ascending
 //    code order (= the reference's i-outer / j-inner order), int32 index
 //    math, terms from the per-N table, summed left to right as they arrive
 //    (bit-identical to the reference's float loop).
 constexpr int kLaneBlock = 64;
-constexpr int kLaneBm = 100, kLaneMarg = 114, kLaneWords = 124;  // bitmap word 13 (113) stays 0
+constexpr int kLaneBm = 100, kLaneMarg = 114, kLaneWords = MI_MREG ? 114 : 124;  // joint | bitmap | 0 | marginals
 constexpr int kLaneUnroll = 4;
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -109,8 +126,8 @@ __device__ __forceinline__ void lane_hist_row(uint32_t* h, const uint32_t pl[3],
     if (PW > 0 ? x < PW : x < pw) {
       const int bl = bin20((pl[x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[x >> 2] >> (8 * (x & 3))) & 0xff);
       const int code = bl * 20 + br;
-      atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
-      atomicOr(&h[64 * (kLaneBm + (code >> 5))], 1u << (code & 31));
+      if (MI_EXP != 3) atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
+      else if (code == 1023) h[0] = 1u;
     }
   }
 }
@@ -126,8 +143,16 @@ __device__ __forceinline__ void lane_hist_pair(uint32_t* h, const uint8_t* __res
       load_row12<FAST>(imgL, oL + (long)r * strideL, PW, pl[r]);
       load_row12<FAST>(imgR, oR + (long)r * strideR, PW, pr[r]);
     }
+    // updates in a scattered static order: neighbouring pixels often share a
+    // joint bin, and back-to-back atomics on one LDS word serialise
 #pragma unroll
-    for (int r = 0; r < PH; ++r) lane_hist_row<PW>(h, pl[r], pr[r], pw);
+    for (int k = 0; k < PW * PH; ++k) {
+      const int p = (k * MI_PERM) % (PW * PH), r = p / PW, x = p % PW;
+      const int bl = bin20((pl[r][x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[r][x >> 2] >> (8 * (x & 3))) & 0xff);
+      const int code = bl * 20 + br;
+      if (MI_EXP != 3) atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
+      else if (code == 1023) h[0] = 1u;
+    }
   } else {
     for (int r = 0; r < ph; ++r) {
       uint32_t pl[3], pr[3];
@@ -168,44 +193,62 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
       else
         lane_hist_pair<PW, PH, false>(h, imgL, strideL, oL, imgR, strideR, oR, pw, ph);
     }
-    // marginals from the joint rows: row i is words 5i..5i+4 (bins j = 0..19)
+    // marginals from the joint rows (row i is words 5i..5i+4, bins j = 0..19)
+    // and the occupancy bitmap of the joint bins from the same reads: bit c
+    // of the 416-bit map <=> joint count of code c non-zero.  Counts are
+    // <= 121, so (w + 0x7f7f7f7f) & 0x80808080 flags the non-zero bytes
+    // without carries, and one multiply gathers the four flags (bytes 0..3
+    // -> bits 28..31, no overlapping partial products) into a nibble placed at
+    // the word's static bitmap position.
     uint32_t cl4[5] = {0, 0, 0, 0, 0}, cr4[5] = {0, 0, 0, 0, 0};
+    uint32_t bm[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < 20; ++i) {
       uint32_t s = 0;
 #pragma unroll
       for (int q = 0; q < 5; ++q) {
-        const uint32_t w = h[64 * (5 * i + q)];
+        const int jw = 5 * i + q;
+        const uint32_t w = h[64 * jw];
         s = __builtin_amdgcn_sad_u8(w, 0u, s);
         cr4[q] += w;  // byte sums <= 255: no carries between the packed counts
+        const uint32_t f = (w + 0x7f7f7f7fu) & 0x80808080u;
+        bm[jw >> 3] |= ((f * 0x00204081u) >> 28) << (4 * (jw & 7));
       }
       cl4[i >> 2] |= s << (8 * (i & 3));
     }
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      h[64 * (kLaneMarg + q)] = cl4[q];
-      h[64 * (kLaneMarg + 5 + q)] = cr4[q];
-    }
     uint32_t nz = 0;  // non-empty bitmap words
     int nnz = 0;
+    if (!MI_MREG) {
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        h[64 * (kLaneMarg + q)] = cl4[q];
+        h[64 * (kLaneMarg + 5 + q)] = cr4[q];
+      }
+    }
 #pragma unroll
     for (int w = 0; w < 13; ++w) {
-      const uint32_t bw = h[64 * (kLaneBm + w)];
-      nz |= (bw != 0u ? 1u : 0u) << w;
-      nnz += __builtin_popcount(bw);
+      h[64 * (kLaneBm + w)] = bm[w];
+      nz |= (bm[w] != 0u ? 1u : 0u) << w;
+      nnz += __builtin_popcount(bm[w]);
     }
-    const int tmax = wave_max(nnz);
+    const int tmax = MI_EXP == 1 ? 0 : wave_max(nnz);
     // Branch-free walk.  State: current word wd and its remaining bits, the
     // words still to visit (nz), and the next non-empty word nw with its bits
     // read one step ahead (nxt); word 13 is a permanent zero sentinel.  A
     // finished lane keeps producing in-range garbage codes whose table reads
-    // are masked off, so the whole wave runs one uniform loop.
+    // are masked off, so the whole wave runs one uniform loop.  The marginal
+    // counts stay in registers (byte select); the table gathers of one
+    // iteration are summed in the next one, so their L2 latency overlaps a
+    // whole iteration of the walk (same left-to-right order of the float sum).
     int wd = __builtin_ctz(nz | 0x2000u);
     nz &= nz - 1u;
     uint32_t bits = h[64 * (kLaneBm + wd)];
     int nw = __builtin_ctz(nz | 0x2000u);
     uint32_t nxt = h[64 * (kLaneBm + nw)];
     float MI = 0.0f;
+    float vp[kLaneUnroll];
+#pragma unroll
+    for (int u = 0; u < kLaneUnroll; ++u) vp[u] = 0.0f;
     for (int t = 0; t < tmax; t += kLaneUnroll) {
       float v[kLaneUnroll];
 #pragma unroll
@@ -220,21 +263,46 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
         nxt = h[64 * (kLaneBm + nw)];  // unchanged unless z: same word as before
         const int i = (int)(mul_u24((uint32_t)code, 205u) >> 12);  // exact code / 20 for code < 1024
         const int j = code - (int)mul_u24((uint32_t)i, 20u);
-        const int cJ = (h[64 * (code >> 2)] >> ((code & 3) * 8)) & 0xff;
-        const int cL = (h[64 * (kLaneMarg + (i >> 2))] >> ((i & 3) * 8)) & 0xff;
-        const int cR = (h[64 * (kLaneMarg + 5 + (j >> 2))] >> ((j & 3) * 8)) & 0xff;
+        const int cw = code >> 2;
+        const uint32_t hw = h[64 * cw];
+        const int cJ = (hw >> ((code & 3) * 8)) & 0xff;
+        // the joint histogram is cleared as the walk leaves each non-empty
+        // word (every such word is visited; ascending codes never return);
+        // otherwise the word is stored back unchanged (no branch)
+        const int ncode = (wd << 5) | __builtin_ctz(bits | 0x80000000u);
+        const bool clr = t + u < nnz && ((ncode >> 2) != cw || t + u + 1 >= nnz);
+        if (MI_UCLR)
+          h[64 * cw] = clr ? 0u : hw;
+        else if (clr)
+          h[64 * cw] = 0u;
+        const int qi = i >> 2, qj = j >> 2;  // i <= 22 for a finished lane's garbage code
+        uint32_t wl, wr;
+        if (MI_MREG) {
+          wl = qi == 0 ? cl4[0] : qi == 1 ? cl4[1] : qi == 2 ? cl4[2] : qi == 3 ? cl4[3] : cl4[4];
+          wr = qj == 0 ? cr4[0] : qj == 1 ? cr4[1] : qj == 2 ? cr4[2] : qj == 3 ? cr4[3] : cr4[4];
+        } else {
+          wl = h[64 * (kLaneMarg + qi)];
+          wr = h[64 * (kLaneMarg + 5 + qj)];
+        }
+        const int cL = (wl >> ((i & 3) * 8)) & 0xff;
+        const int cR = (wr >> ((j & 3) * 8)) & 0xff;
         const int a = max(cL, cR), b = min(cL, cR);
         const int idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + cJ;
         // out-of-range buffer offsets read 0: a finished lane adds +0.0f, no branch
         const int off = t + u < nnz ? 4 * (idx - 1) : 0x7ffffff0;
-        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
+        if (MI_EXP == 2)
+          v[u] = (float)(off >> 2);
+        else
+          v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
       }
 #pragma unroll
-      for (int u = 0; u < kLaneUnroll; ++u) MI += v[u];  // +0.0f for finished lanes: exact (MI is never -0)
-    }
-    // clean histogram for the next pair (joint + bitmap; the marginals are overwritten)
+      for (int u = 0; u < kLaneUnroll; ++u) MI += vp[u];  // previous iteration: +0.0f when finished (MI is never -0)
 #pragma unroll
-    for (int w = 0; w < kLaneBm + 13; ++w) h[64 * w] = 0u;
+      for (int u = 0; u < kLaneUnroll; ++u) vp[u] = v[u];
+    }
+#pragma unroll
+    for (int u = 0; u < kLaneUnroll; ++u) MI += vp[u];
+    // the joint words were cleared by the walk; bitmap and marginals are rewritten per pair
     if (k < n) out[k] = MI;
   }
 }
