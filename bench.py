@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--ba-iters", type=int, default=10)
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lib", default=None, help="development A/B only: load this libme_hip.so build")
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
@@ -161,7 +162,7 @@ def alg_work(family: str, cfg: dict, frames):
 
 # kernels of each timed family (the PMC traffic of a family launch is their sum)
 FAMILY_KERNELS = {
-    "SCALE_RES": ["scale_residual_kernel"], "SCALE_NEQ": ["scale_neq_kernel"], "KLT": ["klt_kernel"],
+    "SCALE_RES": ["scale_res_ctrl_kernel"], "SCALE_NEQ": ["scale_neq_ctrl_kernel"], "KLT": ["klt_kernel"],
     "BA_LINEARIZE": ["linearize_kernel"],
     "BA_SCHUR": ["pt_schur_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
     "BA_STEP": ["pt_step_kernel"], "MI": ["mi_lane_kernel"],
@@ -237,6 +238,10 @@ def main():
     from uasl_motion_estimation_amd.klt import klt_params
     from uasl_motion_estimation_amd.optimisation import SolverOptions
 
+    if args.lib:
+        from uasl_motion_estimation_amd import _lib
+
+        _lib.load_library(args.lib)
     cfg = S.CONFIGS[args.config]
     seed = S.SEED0 + args.config + 1000 * rank
     t0 = time.time()

@@ -237,13 +237,9 @@ __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int 
   return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN);
 }
 
-// A4: compute_residuals
-__global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
-                                                                  int* __restrict__ err, const ScaleLM* lm, int phase,
-                                                                  int use_tmp) {
-  if (lm_skip(lm, phase)) return;
-  lm_scale(a, lm, use_tmp);
-  SCALE_GROUP_SETUP();
+// A4: compute_residuals, one track per 16-lane group
+__device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHist<16>& h,
+                               double* __restrict__ res, int* __restrict__ err) {
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
   if (row < 0 || row >= a.nrows) return;
@@ -279,13 +275,19 @@ __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, T
   if (h.gl == 0) res[row] = (double)mi * wv;
 }
 
-// A5: compute_normal_equations — per track J^2*w and J*r_k
-__global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackDev td, const double* __restrict__ res,
-                                                             double* __restrict__ jj, double* __restrict__ je,
-                                                             int* __restrict__ err, const ScaleLM* lm) {
-  if (lm_skip(lm, PH_B)) return;
-  lm_scale(a, lm, 0);
+__global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
+                                                                  int* __restrict__ err, const ScaleLM* lm, int phase,
+                                                                  int use_tmp) {
+  if (lm_skip(lm, phase)) return;
+  lm_scale(a, lm, use_tmp);
   SCALE_GROUP_SETUP();
+  residual_track(a, td, t, h, res, err);
+}
+
+// A5: compute_normal_equations — per track J^2*w and J*r_k
+__device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHist<16>& h,
+                          const double* __restrict__ res, double* __restrict__ jj, double* __restrict__ je,
+                          int* __restrict__ err) {
   if (h.gl == 0) {
     jj[t] = 0.0;
     je[t] = 0.0;
@@ -327,6 +329,15 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackD
     jj[t] = J * J * wv;
     je[t] = J * res[row];
   }
+}
+
+__global__ __launch_bounds__(kScBlock) void scale_neq_kernel(ScaleArgs a, TrackDev td, const double* __restrict__ res,
+                                                             double* __restrict__ jj, double* __restrict__ je,
+                                                             int* __restrict__ err, const ScaleLM* lm) {
+  if (lm_skip(lm, PH_B)) return;
+  lm_scale(a, lm, 0);
+  SCALE_GROUP_SETUP();
+  neq_track(a, td, t, h, res, jj, je, err);
 }
 
 // A6: compute_jacobian — JJ only; right tracks use poses.first / K.first and
@@ -379,33 +390,44 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
 // Fixed-order reduction of one workgroup: sum(x^2) (square) or sum(x) over n
 // entries into *ox, and sum(y) into *oy (y may be null).
 constexpr int kRedBlock = 1024;
+// Per virtual thread v < 1024: strided partial over i = v, v + 1024, ...;
+// then the pairwise tree over the 1024 partials.  A block of B threads (B
+// divides 1024) plays 1024 / B virtual threads each, so the float result does
+// not depend on the block size.
+template <int B>
 __device__ __forceinline__ void block_reduce2(const double* __restrict__ x, const double* __restrict__ y, int n,
                                               int square, double* ox, double* oy) {
+  static_assert(kRedBlock % B == 0, "block size must divide 1024");
   __shared__ double sx[kRedBlock], sy[kRedBlock];
-  double ax = 0, ay = 0;
-  for (int i = threadIdx.x; i < n; i += kRedBlock) {
-    double v = x[i];
-    ax += square ? v * v : v;
-    if (y) ay += y[i];
+#pragma unroll
+  for (int k = 0; k < kRedBlock / B; ++k) {
+    const int v = threadIdx.x + B * k;
+    double ax = 0, ay = 0;
+    for (int i = v; i < n; i += kRedBlock) {
+      double w = x[i];
+      ax += square ? w * w : w;
+      if (y) ay += y[i];
+    }
+    sx[v] = ax;
+    sy[v] = ay;
   }
-  sx[threadIdx.x] = ax;
-  sy[threadIdx.x] = ay;
   __syncthreads();
   for (int s = kRedBlock / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      sx[threadIdx.x] += sx[threadIdx.x + s];
-      sy[threadIdx.x] += sy[threadIdx.x + s];
+    for (int v = threadIdx.x; v < s; v += B) {
+      sx[v] += sx[v + s];
+      sy[v] += sy[v + s];
     }
     __syncthreads();
   }
   *ox = sx[0];
   *oy = sy[0];
+  __syncthreads();  // sx / sy are reused by the next reduction of a persistent block
 }
 
 __global__ __launch_bounds__(kRedBlock) void reduce_kernel(const double* __restrict__ x, const double* __restrict__ y,
                                                            int n, int square, double* __restrict__ out) {
   double ox, oy;
-  block_reduce2(x, y, n, square, &ox, &oy);
+  block_reduce2<kRedBlock>(x, y, n, square, &ox, &oy);
   if (threadIdx.x == 0) {
     out[0] = ox;
     out[1] = oy;
@@ -437,15 +459,14 @@ __device__ void lm_propose(ScaleLM* lm, const LMParams& p) {
 // One workgroup: reduce the evaluation of `phase`, then thread 0 runs the
 // reference's scalar control for that phase (optimisation.cpp:29-147,
 // run_GN_step :674-683, run_LM_step :685-730).
-__global__ __launch_bounds__(kRedBlock) void scale_ctrl_kernel(ScaleLM* lm, LMParams p, int phase,
-                                                               const double* __restrict__ x,
-                                                               const double* __restrict__ y, const int* err) {
-  if (lm->phase != phase) return;
+template <int B>
+__device__ void scale_ctrl_body(ScaleLM* lm, const LMParams& p, int phase, const double* __restrict__ x,
+                                const double* __restrict__ y, const int* err) {
   double sx = 0, sy = 0;
   if (phase == PH_B) {
-    if (!p.test) block_reduce2(x, y, p.n, 0, &sx, &sy);
+    if (!p.test) block_reduce2<B>(x, y, p.n, 0, &sx, &sy);
   } else {
-    block_reduce2(x, nullptr, p.rows, 1, &sx, &sy);
+    block_reduce2<B>(x, nullptr, p.rows, 1, &sx, &sy);
   }
   if (threadIdx.x != 0) return;
   if (*err) {  // ROI outside the image (the reference throws cv::Exception) / bad mask
@@ -536,6 +557,58 @@ __global__ __launch_bounds__(kRedBlock) void scale_ctrl_kernel(ScaleLM* lm, LMPa
   }
 }
 
+// Phase kernels with the control fused in: every workgroup evaluates its
+// tracks, then arrives on a counter (release); the last workgroup to arrive
+// (acquire) reduces the phase in the 1024-virtual-thread order and runs the
+// scalar control (optimisation.cpp:29-147), then re-arms the counter.  One
+// launch per LM phase instead of two; a launch whose phase is not the current
+// one returns at once (every workgroup reads the phase before the last one can
+// change it).
+__device__ __forceinline__ bool last_block_arrives(unsigned* cnt) {
+  __shared__ int slast;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    slast = k == gridDim.x - 1;
+  }
+  __syncthreads();
+  return slast != 0;
+}
+
+__global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
+                                                                  int* __restrict__ err, ScaleLM* lm, LMParams p,
+                                                                  int phase, int use_tmp, unsigned* cnt) {
+  if (lm->phase != phase) return;
+  lm_scale(a, lm, use_tmp);
+  __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  const int t = blockIdx.x * kTracksPerBlock + grp;
+  if (t < a.nL + a.nR) residual_track(a, td, t, h, res, err);
+  if (!last_block_arrives(cnt)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  scale_ctrl_body<kScBlock>(lm, p, phase, res, nullptr, err);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, TrackDev td,
+                                                                  const double* __restrict__ res,
+                                                                  double* __restrict__ jj, double* __restrict__ je,
+                                                                  int* __restrict__ err, ScaleLM* lm, LMParams p,
+                                                                  unsigned* cnt) {
+  if (lm->phase != PH_B) return;
+  lm_scale(a, lm, 0);
+  __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  const int t = blockIdx.x * kTracksPerBlock + grp;
+  if (!p.test && t < a.nL + a.nR) neq_track(a, td, t, h, res, jj, je, err);
+  if (!last_block_arrives(cnt)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  scale_ctrl_body<kScBlock>(lm, p, PH_B, jj, je, err);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Track flags / residual rows (optimisation.cpp:157-194) from the raw track
 // arrays: bit0 = owns a residual row (triangulated and unmasked; the right
 // loop tests mask(pts.second.size()+i), SURVEY A-6), bit1 = seen in the last
@@ -608,6 +681,7 @@ struct ScaleProblem {
   double* je;
   double* red;  // 4 doubles
   int* err;
+  unsigned* bar;  // arrival counter of the fused phase + control kernels
   ScaleLM* lm;
   char* host;   // pinned: input staging | LM state
   ScaleLM* hlm;
@@ -713,10 +787,11 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   P.je = (double*)(base + oJE);
   P.red = (double*)(base + oRed);
   P.err = (int*)(base + oErr);
+  P.bar = (unsigned*)(base + oErr + 64);
   P.lm = (ScaleLM*)(base + oLM);
   // zero: residual rows never owned by a track stay 0; error flag
   ME_HIP(c, hipMemsetAsync(base + oRes, 0, oRes2 - oRes + up(8 * nr), c->stream));
-  ME_HIP(c, hipMemsetAsync(base + oErr, 0, 4, c->stream));
+  ME_HIP(c, hipMemsetAsync(base + oErr, 0, 256, c->stream));  // error flag | grid barrier
   hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
                      (int*)(base + oRow), P.err);
   ME_TRY(me_check_launch(c, "scale_prep_kernel"));
@@ -851,9 +926,8 @@ extern "C" int me_scale_jacobian(me_ctx* c, const me_scale_state* s, int weighti
 }
 
 // optimisation.cpp:29-147 with run_GN_step (:674-683) / run_LM_step (:685-730).
-// The control runs on the device (scale_ctrl_kernel); the host enqueues
-// blocks of phase-predicated launches [A, B, C, C, D] and polls the state
-// every kBlocksPerPoll blocks (a block whose phase does not match is a no-op).
+// The control runs on the device (fused into the phase kernels); the host
+// enqueues blocks of phase-predicated launches and polls the state.
 extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_params* pin, int test, int* stop_out,
                                  int* iterations, double* trace, int trace_cap, long* mi_evals) {
   if (!c || !s || !pin) return ME_ERR_INVALID;
@@ -894,47 +968,39 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   const int nb = blocks_for(P.n);
   hipStream_t st = c->stream;
   auto res = [&](int phase, int use_tmp, double* dst) {
-    if (P.n > 0) {
-      me_ktimer t(c, ME_KT_SCALE_RES);
-      hipLaunchKernelGGL(scale_residual_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, dst, P.err,
-                         (const ScaleLM*)P.lm, phase, use_tmp);
-    }
-    hipLaunchKernelGGL(scale_ctrl_kernel, dim3(1), dim3(kRedBlock), 0, st, P.lm, lp, phase, (const double*)dst,
-                       (const double*)nullptr, (const int*)P.err);
+    me_ktimer t(c, ME_KT_SCALE_RES);
+    hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, dst, P.err, P.lm, lp, phase,
+                       use_tmp, P.bar);
   };
-  // LM iterations are enqueued in blocks; the device state after each block
-  // is copied to one of two pinned slots behind an event, and the host reads
-  // block k's state only after block k + 1 is queued (the GPU never drains
-  // while the host polls; kernels of a finished solve return at once).
-  constexpr int kBlocksPerPoll = 2;
+  // LM phases are enqueued in blocks [A, B, C, C, D] (one launch each, the
+  // control fused into the last workgroup); the device state after each
+  // block is copied to one of two pinned slots behind an event, and the host
+  // reads block k's state only after block k + 1 is queued (the GPU never
+  // drains while the host polls; launches of a finished solve return at once).
   const long max_blocks = 64L * (p.max_nb_iter + 2);
   ScaleLM* slot[2] = {P.hlm, P.hlm2};
   long blk = 0;
-  auto enqueue_blocks = [&](int sl) -> int {
-    for (int b = 0; b < kBlocksPerPoll; ++b) {
-      res(PH_A, 0, P.res);
-      if (P.n > 0 && !test) {
-        me_ktimer t(c, ME_KT_SCALE_NEQ);
-        hipLaunchKernelGGL(scale_neq_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res, P.jj,
-                           P.je, P.err, (const ScaleLM*)P.lm);
-      }
-      hipLaunchKernelGGL(scale_ctrl_kernel, dim3(1), dim3(kRedBlock), 0, st, P.lm, lp, (int)PH_B,
-                         (const double*)P.jj, (const double*)P.je, (const int*)P.err);
-      res(PH_C, 1, P.res2);
-      res(PH_C, 1, P.res2);
-      res(PH_D, 0, P.res2);
+  auto enqueue_block = [&](int sl) -> int {
+    res(PH_A, 0, P.res);
+    {
+      me_ktimer t(c, ME_KT_SCALE_NEQ);
+      hipLaunchKernelGGL(scale_neq_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res, P.jj,
+                         P.je, P.err, P.lm, lp, P.bar);
     }
-    blk += kBlocksPerPoll;
+    res(PH_C, 1, P.res2);
+    res(PH_C, 1, P.res2);
+    res(PH_D, 0, P.res2);
+    ++blk;
     ME_TRY(me_check_launch(c, "scale optimise"));
     ME_HIP(c, hipMemcpyAsync(slot[sl], P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
     ME_HIP(c, hipEventRecord(c->poll_ev[sl], st));
     return ME_OK;
   };
-  ME_TRY(enqueue_blocks(0));
+  ME_TRY(enqueue_block(0));
   int cur = 0;
   for (;; cur ^= 1) {
     const bool more = blk < max_blocks;
-    if (more) ME_TRY(enqueue_blocks(cur ^ 1));
+    if (more) ME_TRY(enqueue_block(cur ^ 1));
     ME_HIP(c, hipEventSynchronize(c->poll_ev[cur]));
     if (slot[cur]->phase == PH_DONE) break;
     if (!more) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
