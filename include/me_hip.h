@@ -89,6 +89,17 @@ int me_mutual_information(me_ctx* ctx, me_mem mem, const uint8_t* L, int strideL
 /* me::computeEntropy (src/core/mutual_information.cpp:28-45). */
 int me_entropy(me_ctx* ctx, me_mem mem, const uint8_t* img, int stride, int w, int h, float* out);
 
+/* ---- A3: the other patch utilities of src/core/mutual_information.cpp -
+ * Batched over n pairs of rows x cols float patches stored contiguously
+ * (pair k at A + k * rows * cols, row-major).  me_compare_pc replaces
+ * me::comparePC (mutual_information.cpp:14-25, bit-exact); me_ccoeff_normed
+ * replaces me::applyCCOEFFNormed (:136-140; OpenCV MatExpr rounding restated,
+ * parity unpinned); me_quantise replaces me::quantise(img, {lo, hi}) (:48-53),
+ * in place, lo != hi. */
+int me_compare_pc(me_ctx* ctx, me_mem mem, const float* A, const float* B, int n, int rows, int cols, float* out);
+int me_ccoeff_normed(me_ctx* ctx, me_mem mem, const float* A, const float* B, int n, int rows, int cols, float* out);
+int me_quantise(me_ctx* ctx, me_mem mem, uint8_t* img, int stride, int w, int h, int lo, int hi);
+
 /* ---- A4-A9: ScaleState optimiser --------------------------------------
  * Replaces me::optimisation::Optimiser<ScaleState, std::vector<std::pair<cv::Mat,cv::Mat>>>
  * (include/MotionEstimation/optimisation/optimisation.h:76-125,

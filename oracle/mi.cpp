@@ -1,3 +1,4 @@
+#include <utility>
 // oracle/mi.cpp — TEST INFRASTRUCTURE: CPU restatement of the reference MI
 // (src/core/mutual_information.cpp:28-86).  Parity unpinned (see oracle.h).
 //
@@ -135,4 +136,56 @@ extern "C" long oracle_log2f_mismatches(uint32_t lo, uint32_t hi) {
     if (std::memcmp(&a, &b, 4) != 0) bad++;
   }
   return bad;
+}
+
+
+// ---- A3: src/core/mutual_information.cpp:14-25 (comparePC), written with
+// the reference's own expressions: pow(float, 2) promotes to double (C++11),
+// sqrt(float) is the float overload; compiled without FMA contraction.
+static float compare_pc_one(const float* PC1, const float* PC2, int rows, int cols) {
+  float sum = 0, sum1 = 0, sum2 = 0;
+  for (int i = 0; i < rows; i++)
+    for (int j = 0; j < cols; j++) {
+      sum += PC1[i * cols + j] * PC2[i * cols + j];
+      sum1 += std::pow(PC1[i * cols + j], 2);
+      sum2 += std::pow(PC2[i * cols + j], 2);
+    }
+  return sum / std::sqrt(sum1 * sum2);
+}
+
+extern "C" void oracle_compare_pc(const float* A, const float* B, int n, int rows, int cols, float* out) {
+  for (int k = 0; k < n; ++k) out[k] = compare_pc_one(A + (long)k * rows * cols, B + (long)k * rows * cols, rows, cols);
+}
+
+// :136-140 applyCCOEFFNormed.  (r - 1) / N * sum(r) is one OpenCV MatExpr
+// (alpha = sum / N, shift = -sum / N in double) evaluated by convertTo, i.e.
+// float src * (float)alpha + (float)shift (fused in OpenCV's SIMD path);
+// cv::sum accumulates in double.  OpenCV is not present: parity unpinned.
+static float ccoeff_one(const float* r1, const float* r2, int npx) {
+  double s1 = 0, s2 = 0;
+  for (int i = 0; i < npx; ++i) { s1 += (double)r1[i]; s2 += (double)r2[i]; }
+  const double inv = 1.0 / (double)npx;
+  const float a1 = (float)(inv * s1), b1 = (float)(-inv * s1), a2 = (float)(inv * s2), b2 = (float)(-inv * s2);
+  double s12 = 0, s11 = 0, s22 = 0;
+  for (int i = 0; i < npx; ++i) {
+    const float u = std::fma(r1[i], a1, b1), v = std::fma(r2[i], a2, b2);
+    s12 += (double)(u * v);
+    s11 += (double)(u * u);
+    s22 += (double)(v * v);
+  }
+  return (float)(s12 / std::sqrt(s11 * s22));
+}
+
+extern "C" void oracle_ccoeff_normed(const float* A, const float* B, int n, int rows, int cols, float* out) {
+  for (int k = 0; k < n; ++k) out[k] = ccoeff_one(A + (long)k * rows * cols, B + (long)k * rows * cols, rows * cols);
+}
+
+// :48-53 quantise, the reference's expression per pixel (row by row for a strided image)
+extern "C" void oracle_quantise(uint8_t* img, int stride, int w, int h, int lo, int hi) {
+  const std::pair<uint8_t, uint8_t> range{(uint8_t)lo, (uint8_t)hi};
+  for (int y = 0; y < h; ++y) {
+    uint8_t* img_ptr = img + (long)y * stride;
+    for (int i = 0; i < w; i++)
+      img_ptr[i] = (uint8_t)(img_ptr[i] / (256 / (int)(range.second - range.first))) + range.first;
+  }
 }

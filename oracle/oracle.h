@@ -25,6 +25,11 @@ extern "C" {
 /* ---- A1/A2: mutual information (src/core/mutual_information.cpp:28-86) ---- */
 float oracle_mutual_information(const uint8_t* L, int strideL, const uint8_t* R, int strideR, int w, int h);
 float oracle_entropy(const uint8_t* img, int stride, int w, int h);
+/* A3 (mutual_information.cpp:14-25, 136-140, 48-53): batched over n pairs of
+   rows x cols float patches, pair k at A + k*rows*cols */
+void oracle_compare_pc(const float* A, const float* B, int n, int rows, int cols, float* out);
+void oracle_ccoeff_normed(const float* A, const float* B, int n, int rows, int cols, float* out);
+void oracle_quantise(uint8_t* img, int stride, int w, int h, int lo, int hi);
 /* histogram dump: hl[20], hr[20], hj[400] integer counts */
 void oracle_mi_histograms(const uint8_t* L, int strideL, const uint8_t* R, int strideR, int w, int h,
                           int32_t* hl, int32_t* hr, int32_t* hj);

@@ -100,6 +100,9 @@ def lib():
         L.oracle_mutual_information.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int]
         L.oracle_entropy.restype = c_float
         L.oracle_entropy.argtypes = [c_void_p, c_int, c_int, c_int]
+        for f in (L.oracle_compare_pc, L.oracle_ccoeff_normed):
+            f.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+        L.oracle_quantise.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int]
         L.oracle_mi_histograms.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_void_p]
         L.oracle_mi_scores.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -148,6 +151,35 @@ def entropy(img: np.ndarray) -> float:
     img = np.ascontiguousarray(img, np.uint8)
     h, w = img.shape
     return float(np.float32(lib().oracle_entropy(img.ctypes.data, w, w, h)))
+
+
+def _pairs(A, B):
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    if A.ndim == 2:
+        A, B = A[None], B[None]
+    return A, B
+
+
+def compare_pc(A, B):
+    A, B = _pairs(A, B)
+    out = np.zeros(len(A), np.float32)
+    lib().oracle_compare_pc(A.ctypes.data, B.ctypes.data, len(A), A.shape[1], A.shape[2], out.ctypes.data)
+    return out
+
+
+def ccoeff_normed(A, B):
+    A, B = _pairs(A, B)
+    out = np.zeros(len(A), np.float32)
+    lib().oracle_ccoeff_normed(A.ctypes.data, B.ctypes.data, len(A), A.shape[1], A.shape[2], out.ctypes.data)
+    return out
+
+
+def quantise(img, lo, hi):
+    img = np.array(img, np.uint8, copy=True, order="C")
+    h, w = img.shape
+    lib().oracle_quantise(img.ctypes.data, w, w, h, lo, hi)
+    return img
 
 
 def histograms(L, R):

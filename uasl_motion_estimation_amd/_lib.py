@@ -118,7 +118,7 @@ EXPORTS = [
     "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
     "me_get_stream", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_timing_enable", "me_timing_read", "me_timing_reset",
-    "me_mi_scores", "me_mutual_information", "me_entropy",
+    "me_mi_scores", "me_mutual_information", "me_entropy", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
@@ -173,6 +173,9 @@ def load_library(path: str = LIB_PATH):
                                  c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_mutual_information": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                                           c_void_p]),
+        "me_compare_pc": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+        "me_ccoeff_normed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+        "me_quantise": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int]),
         "me_entropy": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_optim_default_params": (None, [P(OptimParamsC)]),
         "me_scale_residuals": (c_int, [c_void_p, P(ScaleStateC), c_int, P(c_double), P(c_int)]),

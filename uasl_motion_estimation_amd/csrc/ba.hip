@@ -184,10 +184,12 @@ __device__ __forceinline__ void mono_residual(const Geo& g, const double* cam, c
   for (int k = 6; k < 12; ++k) Jp[k] = 0.0;
 }
 
-// residual (+ optional Jacobian) of observation o for the window's model
+// residual (+ optional Jacobian) of observation o; OD = rows of the model
+// (a template parameter: one branch-free kernel instance per model)
+template <int OD>
 __device__ __forceinline__ void obs_residual(const Geo& g, const Bufs& b, long o, const double* cam, const double* X,
                                              double* r, double* Jc, double* Jp) {
-  if (g.od == 4)
+  if (OD == 4)
     stereo_residual(g, cam, X, b.obs + 4 * o, r, Jc, Jp);
   else
     mono_residual(g, cam, X, b.obs + 2 * o, b.cam_id[o] != 0, r, Jc, Jp);
@@ -211,6 +213,7 @@ constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups ove
 // Per observation: corrected residual / Jacobian, cost, and the unscaled
 // per-observation normal-equation pieces W_o = Jc^T Jp (6x3), V_o = Jp^T Jp
 // (6 unique), g_o = Jp^T r, so the per-point stage only sums.
+template <int OD>
 __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
   __shared__ double lds[4];
   const State* st = b.st;
@@ -222,7 +225,7 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
     const int ci = b.cam_idx[o], pi = b.pt_idx[o];
     double* L = b.lin + (long)o * kLinStride;
     double r[4], Jc[24], Jp[12];
-    obs_residual(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
+    obs_residual<OD>(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
     const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
     double rho0, sc;
     huber(s, &rho0, &sc);
@@ -1104,6 +1107,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 // step_finalize (deterministic).
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 
+template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
   __shared__ double lds[16];
   const State* st = b.st;
@@ -1170,7 +1174,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
         mc -= jd * (Lo[k] + jd / 2.0);
       }
       double r[4];
-      obs_residual(g, b, o, cams_c + 6 * b.cam_idx[o], xc, r, nullptr, nullptr);
+      obs_residual<OD>(g, b, o, cams_c + 6 * b.cam_idx[o], xc, r, nullptr, nullptr);
       const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
       double rho0, sc;
       huber(s, &rho0, &sc);
@@ -1270,13 +1274,14 @@ __global__ void decide_kernel(Geo g, Bufs b, Opts o) {
   decide(b, o);
 }
 
+template <int OD>
 __global__ __launch_bounds__(kBlock) void cost_kernel(Geo g, Bufs b, int which, double* part) {
   __shared__ double lds[4];
   const int o = blockIdx.x * kBlock + threadIdx.x;
   double c = 0;
   if (o < g.no) {
     double r[4];
-    obs_residual(g, b, o, b.cams[which] + 6 * b.cam_idx[o], b.pts[which] + 3 * b.pt_idx[o], r, nullptr, nullptr);
+    obs_residual<OD>(g, b, o, b.cams[which] + 6 * b.cam_idx[o], b.pts[which] + 3 * b.pt_idx[o], r, nullptr, nullptr);
     const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
     double rho0, sc;
     huber(s, &rho0, &sc);
@@ -1287,12 +1292,13 @@ __global__ __launch_bounds__(kBlock) void cost_kernel(Geo g, Bufs b, int which, 
   if (threadIdx.x == 0) part[blockIdx.x] = out[0];
 }
 
+template <int OD>
 __global__ __launch_bounds__(kBlock) void eval_kernel(Geo g, Bufs b, double* res, double* Jc, double* Jp) {
   const int o = blockIdx.x * kBlock + threadIdx.x;
   if (o >= g.no) return;
   double r[4], jc[24], jp[12];
-  obs_residual(g, b, o, b.cams[0] + 6 * b.cam_idx[o], b.pts[0] + 3 * b.pt_idx[o], r, jc, jp);
-  const int od = g.od;  // output rows per observation: Observation<M>::data size
+  obs_residual<OD>(g, b, o, b.cams[0] + 6 * b.cam_idx[o], b.pts[0] + 3 * b.pt_idx[o], r, jc, jp);
+  constexpr int od = OD;  // output rows per observation: Observation<M>::data size
   for (int k = 0; k < od; ++k) res[od * (long)o + k] = r[k];
   if (Jc)
     for (int k = 0; k < 6 * od; ++k) Jc[6 * od * (long)o + k] = jc[k];
@@ -1833,7 +1839,10 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   hipStream_t s = c->stream;
   {
     me_ktimer t(c, ME_KT_BA_LINEARIZE);
-    hipLaunchKernelGGL(linearize_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    if (g.od == 4)
+      hipLaunchKernelGGL(linearize_kernel<4>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    else
+      hipLaunchKernelGGL(linearize_kernel<2>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
   if (g.m > 0) {
     hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart);
@@ -1908,7 +1917,10 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
-    hipLaunchKernelGGL(pt_step_kernel, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
+    if (g.od == 4)
+      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
+    else
+      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
   }
   hipLaunchKernelGGL(step_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
   if (ar) {
@@ -2021,7 +2033,10 @@ extern "C" int me_ba_cost(me_ctx* c, const me_ba_problem* p, double* cost) {
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
   std::vector<double> part(P.g.nblk_obs);
-  hipLaunchKernelGGL(cost_kernel, dim3(P.g.nblk_obs), dim3(kBlock), 0, c->stream, P.g, P.b, 0, P.b.part);
+  if (P.g.od == 4)
+    hipLaunchKernelGGL(cost_kernel<4>, dim3(P.g.nblk_obs), dim3(kBlock), 0, c->stream, P.g, P.b, 0, P.b.part);
+  else
+    hipLaunchKernelGGL(cost_kernel<2>, dim3(P.g.nblk_obs), dim3(kBlock), 0, c->stream, P.g, P.b, 0, P.b.part);
   ME_TRY(me_check_launch(c, "cost_kernel"));
   ME_HIP(c, hipMemcpyAsync(part.data(), P.b.part, 8 * part.size(), hipMemcpyDeviceToHost, c->stream));
   ME_HIP(c, hipStreamSynchronize(c->stream));
@@ -2047,7 +2062,10 @@ extern "C" int me_ba_evaluate(me_ctx* c, const me_ba_problem* p, double* res, do
   double* dres = (double*)d;
   double* djc = dres + od * (size_t)no;
   double* djp = djc + 6 * od * (size_t)no;
-  hipLaunchKernelGGL(eval_kernel, dim3(blocks(no, kBlock)), dim3(kBlock), 0, c->stream, P.g, P.b, dres, djc, djp);
+  if (od == 4)
+    hipLaunchKernelGGL(eval_kernel<4>, dim3(blocks(no, kBlock)), dim3(kBlock), 0, c->stream, P.g, P.b, dres, djc, djp);
+  else
+    hipLaunchKernelGGL(eval_kernel<2>, dim3(blocks(no, kBlock)), dim3(kBlock), 0, c->stream, P.g, P.b, dres, djc, djp);
   ME_TRY(me_check_launch(c, "eval_kernel"));
   ME_HIP(c, hipMemcpyAsync(res, dres, 8 * od * (size_t)no, hipMemcpyDeviceToHost, c->stream));
   if (Jc) ME_HIP(c, hipMemcpyAsync(Jc, djc, 8 * 6 * od * (size_t)no, hipMemcpyDeviceToHost, c->stream));
