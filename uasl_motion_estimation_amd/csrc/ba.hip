@@ -273,34 +273,30 @@ __global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
 // contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
 // k + ck, ... of 256 slots of camera c into a partial; cam_reduce adds the ck
 // partials in order.
-__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart) {
-  __shared__ double lds[4 * 27];
-  const State* st = b.st;
-  if (st->done || !st->need_lin) return;
-  const int ci = blockIdx.x, k = blockIdx.y;
-  const int beg = b.c_off[ci], end = b.c_off[ci + 1];
-  double v[27];
-  for (int i = 0; i < 27; ++i) v[i] = 0;
-  for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock)
-    for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
-  double out[27];
-  block_sum<27>(v, out, lds);
+// the last workgroup to arrive on a counter (release by every arrival,
+// acquire by the last); the last one re-arms the counter for the next launch
+__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected) {
+  __shared__ int slast;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    double* P = cpart + 27 * ((long)ci * g.ck + k);
-    for (int u = 0; u < 27; ++u) P[u] = out[u];
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    slast = k == expected - 1;
+    if (slast) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  __syncthreads();
+  if (slast) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return slast != 0;
 }
 
-// One wavefront per variable camera: lane u < 27 sums component u of the
-// partials (fixed order) -> raw U, column norms, raw gradient; unless
-// sharded, the Jacobi scaling (iteration 0) and the scaled blocks.
-__global__ __launch_bounds__(64) void cam_reduce_kernel(Geo g, Bufs b, int sharded, const double* cpart,
-                                                        double* colnorm, double* gc_raw, double* Uraw) {
+// Camera ci: lane u < 27 sums component u of the ck partials (fixed order)
+// -> raw U, column norms, raw gradient; unless sharded, the Jacobi scaling
+// (iteration 0) and the scaled blocks.  Called by every thread of a block.
+__device__ void cam_reduce_body(const Geo& g, const Bufs& b, int sharded, const double* cpart, double* colnorm,
+                                double* gc_raw, double* Uraw, int ci) {
   __shared__ double tot[27];
   __shared__ double csl[6];
   const State* st = b.st;
-  if (st->done || !st->need_lin) return;
-  const int ci = blockIdx.x, u = threadIdx.x;
+  const int u = threadIdx.x;
   if (u < 27) {
     double sum = 0.0;
     for (int k = 0; k < g.ck; ++k) sum += cpart[27 * ((long)ci * g.ck + k) + u];
@@ -334,6 +330,32 @@ __global__ __launch_bounds__(64) void cam_reduce_kernel(Geo g, Bufs b, int shard
   } else if (u < 27) {
     b.gcs[6 * ci + u - 21] = tot[u] * csl[u - 21];
   }
+}
+
+// Unscaled U = Jc^T Jc (21 unique) and g = Jc^T r per variable camera, in
+// two deterministic stages over the per-observation pieces linearize wrote
+// contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
+// k + ck, ... of 256 slots of camera c into a partial; the last of the ck
+// workgroups of camera c to finish adds the ck partials in order.
+__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart, int sharded,
+                                                              double* colnorm, double* gc_raw, double* Uraw) {
+  __shared__ double lds[4 * 27];
+  const State* st = b.st;
+  if (st->done || !st->need_lin) return;
+  const int ci = blockIdx.x, k = blockIdx.y;
+  const int beg = b.c_off[ci], end = b.c_off[ci + 1];
+  double v[27];
+  for (int i = 0; i < 27; ++i) v[i] = 0;
+  for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock)
+    for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
+  double out[27];
+  block_sum<27>(v, out, lds);
+  if (threadIdx.x == 0) {
+    double* P = cpart + 27 * ((long)ci * g.ck + k);
+    for (int u = 0; u < 27; ++u) P[u] = out[u];
+  }
+  if (!last_arrival(b.cnt + ci, g.ck)) return;
+  cam_reduce_body(g, b, sharded, cpart, colnorm, gc_raw, Uraw, ci);
 }
 
 // Sharded mode: scaling from the all-reduced column norms, then scale the
@@ -1105,10 +1127,86 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 // each lane evaluates the model cost change and the candidate cost of its own
 // observations.  Partials per workgroup, reduced in fixed order by
 // step_finalize (deterministic).
+// Step partials -> scal (fixed order).  In single-GPU mode the same workgroup
+// then runs the Ceres step handling (decide); in sharded mode the host
+// all-reduces scal between step_partials and a decide-only launch.
+__device__ void decide(Bufs& b, const Opts& o) {
+  State* st = b.st;
+  st->accepted = 0;
+  const double model_change = b.scal[R_MODEL];
+  const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
+  st->fail = 0;  // consumed: the next iteration starts clean
+  if (fail || !(model_change > 0.0)) {
+    st->invalid_count += 1;
+    if (st->invalid_count >= o.max_invalid) {
+      st->done = 1;
+      st->termination = 2;
+      return;
+    }
+    st->radius = st->radius / st->decrease;
+    st->decrease *= 2.0;
+    return;
+  }
+  st->invalid_count = 0;
+  const double cand_cost = b.scal[R_CAND];
+  const double step_norm = sqrt(b.scal[R_STEP2] + st->cam_step2);
+  const double x_norm = sqrt(b.scal[R_XN2] + st->cam_xn2);
+  st->cand_cost = cand_cost;
+  st->model_change = model_change;
+  if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) {
+    st->done = 1;
+    st->termination = 0;
+    return;
+  }
+  if (fabs(st->x_cost - cand_cost) <= o.function_tolerance * st->x_cost) {
+    st->done = 1;
+    st->termination = 0;
+    return;
+  }
+  const double q = (st->x_cost - cand_cost) / model_change;
+  st->last_q = q;
+  if (q > o.min_rel_decrease) {
+    st->cur = 1 - st->cur;
+    st->x_cost = cand_cost;
+    st->successful += 1;
+    st->accepted = 1;
+    const double t = 2.0 * q - 1.0;
+    st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - pow(t, 3.0));
+    st->radius = fmin(o.max_radius, st->radius);
+    st->decrease = 2.0;
+    st->need_lin = 1;
+  } else {
+    st->radius = st->radius / st->decrease;
+    st->decrease *= 2.0;
+  }
+}
+
+__device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_decide) {
+  __shared__ double lds[32];
+  State* st = b.st;
+  double v[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < g.nblk_step; i += kFinBlock) {
+    v[0] += b.part[R_MODEL * g.pstride + i];
+    v[1] += b.part[R_CAND * g.pstride + i];
+    v[2] += b.part[R_STEP2 * g.pstride + i];
+    v[3] += b.part[R_XN2 * g.pstride + i];
+  }
+  double out[4];
+  block_sum<4>(v, out, lds);
+  if (threadIdx.x == 0) {
+    b.scal[R_MODEL] = out[0];
+    b.scal[R_CAND] = out[1];
+    b.scal[R_STEP2] = out[2];
+    b.scal[R_XN2] = out[3];
+    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
+    if (do_decide) decide(b, o);
+  }
+}
+
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 
 template <int OD>
-__global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
+__global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
   const State* st = b.st;
   if (st->done) return;
@@ -1189,83 +1287,10 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b) {
     b.part[R_STEP2 * g.pstride + blockIdx.x] = out[2];
     b.part[R_XN2 * g.pstride + blockIdx.x] = out[3];
   }
-}
-
-// Step partials -> scal (fixed order).  In single-GPU mode the same workgroup
-// then runs the Ceres step handling (decide); in sharded mode the host
-// all-reduces scal between step_partials and a decide-only launch.
-__device__ void decide(Bufs& b, const Opts& o) {
-  State* st = b.st;
-  st->accepted = 0;
-  const double model_change = b.scal[R_MODEL];
-  const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
-  st->fail = 0;  // consumed: the next iteration starts clean
-  if (fail || !(model_change > 0.0)) {
-    st->invalid_count += 1;
-    if (st->invalid_count >= o.max_invalid) {
-      st->done = 1;
-      st->termination = 2;
-      return;
-    }
-    st->radius = st->radius / st->decrease;
-    st->decrease *= 2.0;
-    return;
-  }
-  st->invalid_count = 0;
-  const double cand_cost = b.scal[R_CAND];
-  const double step_norm = sqrt(b.scal[R_STEP2] + st->cam_step2);
-  const double x_norm = sqrt(b.scal[R_XN2] + st->cam_xn2);
-  st->cand_cost = cand_cost;
-  st->model_change = model_change;
-  if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) {
-    st->done = 1;
-    st->termination = 0;
-    return;
-  }
-  if (fabs(st->x_cost - cand_cost) <= o.function_tolerance * st->x_cost) {
-    st->done = 1;
-    st->termination = 0;
-    return;
-  }
-  const double q = (st->x_cost - cand_cost) / model_change;
-  st->last_q = q;
-  if (q > o.min_rel_decrease) {
-    st->cur = 1 - st->cur;
-    st->x_cost = cand_cost;
-    st->successful += 1;
-    st->accepted = 1;
-    const double t = 2.0 * q - 1.0;
-    st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - pow(t, 3.0));
-    st->radius = fmin(o.max_radius, st->radius);
-    st->decrease = 2.0;
-    st->need_lin = 1;
-  } else {
-    st->radius = st->radius / st->decrease;
-    st->decrease *= 2.0;
-  }
-}
-
-__global__ __launch_bounds__(kFinBlock) void step_finalize_kernel(Geo g, Bufs b, Opts o, int do_decide) {
-  __shared__ double lds[32];
-  State* st = b.st;
-  if (st->done) return;
-  double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_step; i += kFinBlock) {
-    v[0] += b.part[R_MODEL * g.pstride + i];
-    v[1] += b.part[R_CAND * g.pstride + i];
-    v[2] += b.part[R_STEP2 * g.pstride + i];
-    v[3] += b.part[R_XN2 * g.pstride + i];
-  }
-  double out[4];
-  block_sum<4>(v, out, lds);
-  if (threadIdx.x == 0) {
-    b.scal[R_MODEL] = out[0];
-    b.scal[R_CAND] = out[1];
-    b.scal[R_STEP2] = out[2];
-    b.scal[R_XN2] = out[3];
-    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
-    if (do_decide) decide(b, o);
-  }
+  // the last workgroup to finish reduces the partials (step_finalize) and,
+  // single-GPU, runs the Ceres step handling
+  if (!last_arrival(b.cnt + g.m, gridDim.x)) return;
+  step_finalize_body(g, b, o, do_decide);
 }
 
 __global__ void decide_kernel(Geo g, Bufs b, Opts o) {
@@ -1755,6 +1780,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * (size_t)g.n6, &P.gc_glob);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
+  add(4 * (size_t)(g.m + 1), &b.cnt);  // last-arrival counters: per camera (cam_assemble) | pt_step
   const size_t work_bytes = 4 * (2 * (size_t)g.np + (size_t)g.nblk_obs * g.nc + 4);
   add(work_bytes, &b.work);
   const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
@@ -1800,6 +1826,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     if (mono) b.cam_id = p->cam_id;
   }
   ME_HIP(c, hipMemsetAsync(b.work, 0, work_bytes, s));
+  ME_HIP(c, hipMemsetAsync(b.cnt, 0, 4 * (size_t)(g.m + 1), s));
   const double* cams_in = dev ? p->cams : b.cams[0];
   const double* pts_in = dev ? p->pts : b.pts[0];
   const long nthr = std::max({(long)g.nblk_obs * kBlock, (long)g.np, 6L * g.nc, 3L * g.np});
@@ -1845,9 +1872,8 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
       hipLaunchKernelGGL(linearize_kernel<2>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
   if (g.m > 0) {
-    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart);
-    hipLaunchKernelGGL(cam_reduce_kernel, dim3(g.m), dim3(64), 0, s, g, P.b, ar ? 1 : 0,
-                       (const double*)P.cpart, P.colnorm, P.gc_raw, P.Uraw);
+    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart, ar ? 1 : 0,
+                       P.colnorm, P.gc_raw, P.Uraw);
     if (ar) {
       ME_AR(P.colnorm, g.n6);
       hipLaunchKernelGGL(cam_finish_kernel, dim3(blocks(g.m, 64)), dim3(64), 0, s, g, P.b, (const double*)P.colnorm,
@@ -1917,12 +1943,12 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
+    // (step partials reduced and, single-GPU, the step decided in its last workgroup)
     if (g.od == 4)
-      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
+      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
     else
-      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b);
+      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
   }
-  hipLaunchKernelGGL(step_finalize_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
   if (ar) {
     ME_AR(P.b.scal + R_MODEL, 5);  // model change, candidate cost, step^2, |x|^2, failure flag
     hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o);

@@ -9,8 +9,9 @@
 //                  (:106-139) chosen by camID for <2>, value + analytic
 //                  Jacobian (2-row residuals padded with zero rows, so every
 //                  later stage is shared), HuberLoss(1.0) corrector, cost.
-//   cam_assemble   one workgroup per variable camera: Jacobi column norms
-//                  (iteration 0), scaled U = Jc'Jc, g_c = Jc'r.
+//   cam_assemble   ck workgroups per variable camera, the last to finish
+//                  reduces: Jacobi column norms (iteration 0), scaled
+//                  U = Jc'Jc, g_c = Jc'r.
 //   pt_schur       per landmark sub-chunk: V = Jp'Jp, g_p, V + D/radius ->
 //                  Cholesky L_p, z_p = L_p^-1 g_p, the landmark's rows of
 //                  Y = W L_p^-T (and z_p) in LDS, partial tiles of Y^T [Y | z]
@@ -20,8 +21,9 @@
 //                  Cholesky, y_c = -S^-1 b, candidate cameras.
 //   pt_step        16 lanes per point: y_p, candidate point (bounds
 //                  projection), step norms, and the model cost change and
-//                  candidate cost of the point's observations.
-//   decide         one workgroup: Ceres LM acceptance / radius / termination.
+//                  candidate cost of the point's observations; its last
+//                  workgroup reduces them and runs decide (Ceres LM
+//                  acceptance / radius / termination).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -112,6 +114,7 @@ struct Bufs {
   double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
   State* st;
   int* work;          // plan build: cnt_p[np] | fill_p[np] | blk_cam[nblk_obs*nc] | flags[4] (zeroed)
+  unsigned* cnt;      // last-arrival counters: m (cam_assemble, per camera) + 1 (pt_step); re-armed by the last
   double* out;        // State | cams[cur] | pts[cur] for the single read-back
 };
 
