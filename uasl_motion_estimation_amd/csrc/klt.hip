@@ -27,10 +27,14 @@ __device__ __forceinline__ int refl(int i, int n) {
   return i;
 }
 
-__global__ void pyr_down_kernel(const uint8_t* __restrict__ src, int w, int h, int ss, uint8_t* __restrict__ dst,
-                                int dw, int dh, int ds) {
+// one pyramid level of both images (blockIdx.z: 0 prev, 1 next)
+__global__ void pyr_down_kernel(const uint8_t* __restrict__ srcI, const uint8_t* __restrict__ srcJ, int w, int h,
+                                int ss, uint8_t* __restrict__ dstI, uint8_t* __restrict__ dstJ, int dw, int dh,
+                                int ds) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
   if (x >= dw || y >= dh) return;
+  const uint8_t* src = blockIdx.z ? srcJ : srcI;
+  uint8_t* dst = blockIdx.z ? dstJ : dstI;
   const int k[5] = {1, 4, 6, 4, 1};
   int s = 0;
 #pragma unroll
@@ -44,10 +48,26 @@ __global__ void pyr_down_kernel(const uint8_t* __restrict__ src, int w, int h, i
   dst[(long)y * ds + x] = (uint8_t)((s + 128) >> 8);
 }
 
-__global__ void scharr_kernel(const uint8_t* __restrict__ I, int w, int h, int stride, int16_t* __restrict__ dx,
-                              int16_t* __restrict__ dy) {
+constexpr int kMaxLevels = 8;
+struct Pyr {
+  int nl;
+  int w[kMaxLevels], h[kMaxLevels];
+  int is[kMaxLevels];                // row stride of I[l] and J[l] (level 0: the caller's images)
+  const uint8_t* I[kMaxLevels];      // prev levels (stride = w)
+  const int16_t* dx[kMaxLevels];
+  const int16_t* dy[kMaxLevels];
+  const uint8_t* J[kMaxLevels];      // next levels
+};
+
+// Scharr derivatives of every level of the prev pyramid in one launch (blockIdx.z = level)
+__global__ void scharr_levels_kernel(Pyr P) {
+  const int l = blockIdx.z;
+  const int w = P.w[l], h = P.h[l], stride = P.is[l];
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y * blockDim.y + threadIdx.y;
   if (x >= w || y >= h) return;
+  const uint8_t* I = P.I[l];
+  int16_t* dx = const_cast<int16_t*>(P.dx[l]);
+  int16_t* dy = const_cast<int16_t*>(P.dy[l]);
   const uint8_t* r0 = I + (long)refl(y - 1, h) * stride;
   const uint8_t* r1 = I + (long)y * stride;
   const uint8_t* r2 = I + (long)refl(y + 1, h) * stride;
@@ -57,16 +77,6 @@ __global__ void scharr_kernel(const uint8_t* __restrict__ I, int w, int h, int s
   dx[(long)y * w + x] = (int16_t)(t0p - t0m);
   dy[(long)y * w + x] = (int16_t)(3 * (t1p + t1m) + 10 * t1);
 }
-
-constexpr int kMaxLevels = 8;
-struct Pyr {
-  int nl;
-  int w[kMaxLevels], h[kMaxLevels];
-  const uint8_t* I[kMaxLevels];      // prev levels (stride = w)
-  const int16_t* dx[kMaxLevels];
-  const int16_t* dy[kMaxLevels];
-  const uint8_t* J[kMaxLevels];      // next levels
-};
 
 __device__ __forceinline__ long wave_sum64(long v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -89,7 +99,7 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
   int iv[kMaxWinPx], ixv[kMaxWinPx], iyv[kMaxWinPx];
   const float px0 = pin[2 * f], py0 = pin[2 * f + 1];
   for (int L = P.nl - 1; L >= 0; --L) {
-    const int W = P.w[L], H = P.h[L];
+    const int W = P.w[L], H = P.h[L], SI = P.is[L];
     const float sc = 1.0f / (float)(1 << L);
     const float px = px0 * sc, py = py0 * sc;
     if (L == P.nl - 1) {
@@ -122,8 +132,8 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       iyv[q] = 0;
       if (k < npx) {
         const int y = k / win, x = k - y * win;
-        const long o = (long)(iy0 + y) * W + ix0 + x;
-        const long v = (long)I[o] * iw00 + (long)I[o + 1] * iw01 + (long)I[o + W] * iw10 + (long)I[o + W + 1] * iw11;
+        const long o = (long)(iy0 + y) * W + ix0 + x, oi = (long)(iy0 + y) * SI + ix0 + x;
+        const long v = (long)I[oi] * iw00 + (long)I[oi + 1] * iw01 + (long)I[oi + SI] * iw10 + (long)I[oi + SI + 1] * iw11;
         const long gx = (long)DX[o] * iw00 + (long)DX[o + 1] * iw01 + (long)DX[o + W] * iw10 + (long)DX[o + W + 1] * iw11;
         const long gy = (long)DY[o] * iw00 + (long)DY[o + 1] * iw01 + (long)DY[o + W] * iw10 + (long)DY[o + W + 1] * iw11;
         iv[q] = descale(v, 9);
@@ -165,8 +175,8 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
         const int k = lane + 64 * q;
         if (k < npx) {
           const int y = k / win, x = k - y * win;
-          const long o = (long)(jy0 + y) * W + jx0 + x;
-          const long v = (long)J[o] * jw00 + (long)J[o + 1] * jw01 + (long)J[o + W] * jw10 + (long)J[o + W + 1] * jw11;
+          const long o = (long)(jy0 + y) * SI + jx0 + x;
+          const long v = (long)J[o] * jw00 + (long)J[o + 1] * jw01 + (long)J[o + SI] * jw10 + (long)J[o + SI + 1] * jw11;
           const long diff = descale(v, 9) - iv[q];
           b1 += diff * ixv[q];
           b2 += diff * iyv[q];
@@ -224,37 +234,36 @@ static int build_pyramids(me_ctx* c, const uint8_t* dprev, const uint8_t* dnext,
   ME_TRY(me_scratch(c, SLOT_KLT_PYR, bytes + 1024, &base));
   char* p = (char*)base;
   P.nl = nl;
-  uint8_t* Ilev[kMaxLevels];
-  uint8_t* Jlev[kMaxLevels];
   for (int l = 0; l < nl; ++l) {
     P.w[l] = W[l];
     P.h[l] = H[l];
     size_t npx = (size_t)W[l] * H[l];
-    Ilev[l] = (uint8_t*)p;
-    p += (npx + 63) / 64 * 64;
-    Jlev[l] = (uint8_t*)p;
-    p += (npx + 63) / 64 * 64;
+    if (l == 0) {  // level 0 is read in place from the caller's images
+      P.I[0] = dprev;
+      P.J[0] = dnext;
+      P.is[0] = stride;
+    } else {
+      P.I[l] = (const uint8_t*)p;
+      p += (npx + 63) / 64 * 64;
+      P.J[l] = (const uint8_t*)p;
+      p += (npx + 63) / 64 * 64;
+      P.is[l] = W[l];
+    }
     P.dx[l] = (int16_t*)p;
     p += (2 * npx + 63) / 64 * 64;
     P.dy[l] = (int16_t*)p;
     p += (2 * npx + 63) / 64 * 64;
-    P.I[l] = Ilev[l];
-    P.J[l] = Jlev[l];
   }
   hipStream_t s = c->stream;
-  ME_HIP(c, hipMemcpy2DAsync(Ilev[0], w, dprev, stride, w, h, hipMemcpyDeviceToDevice, s));
-  ME_HIP(c, hipMemcpy2DAsync(Jlev[0], w, dnext, stride, w, h, hipMemcpyDeviceToDevice, s));
   me_ktimer t(c, ME_KT_PYR);
-  for (int l = 1; l < nl; ++l) {
-    dim3 blk(32, 8), grd((W[l] + 31) / 32, (H[l] + 7) / 8);
-    hipLaunchKernelGGL(pyr_down_kernel, grd, blk, 0, s, Ilev[l - 1], W[l - 1], H[l - 1], W[l - 1], Ilev[l], W[l], H[l],
-                       W[l]);
-    hipLaunchKernelGGL(pyr_down_kernel, grd, blk, 0, s, Jlev[l - 1], W[l - 1], H[l - 1], W[l - 1], Jlev[l], W[l], H[l],
-                       W[l]);
+  for (int l = 1; l < nl; ++l) {  // both images per launch
+    dim3 blk(32, 8), grd((W[l] + 31) / 32, (H[l] + 7) / 8, 2);
+    hipLaunchKernelGGL(pyr_down_kernel, grd, blk, 0, s, P.I[l - 1], P.J[l - 1], W[l - 1], H[l - 1], P.is[l - 1],
+                       const_cast<uint8_t*>(P.I[l]), const_cast<uint8_t*>(P.J[l]), W[l], H[l], P.is[l]);
   }
-  for (int l = 0; l < nl; ++l) {
-    dim3 blk(32, 8), grd((W[l] + 31) / 32, (H[l] + 7) / 8);
-    hipLaunchKernelGGL(scharr_kernel, grd, blk, 0, s, P.I[l], W[l], H[l], W[l], (int16_t*)P.dx[l], (int16_t*)P.dy[l]);
+  {  // derivatives of every prev level in one launch
+    dim3 blk(32, 8), grd((W[0] + 31) / 32, (H[0] + 7) / 8, nl);
+    hipLaunchKernelGGL(scharr_levels_kernel, grd, blk, 0, s, P);
   }
   return me_check_launch(c, "pyramid kernels");
 }
