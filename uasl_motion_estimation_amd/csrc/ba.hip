@@ -453,6 +453,10 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
   if (st->done) return;
   const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
   const double radius = st->radius;
+  // all allowed steps taken: this pass only evaluates the gradient for the
+  // closing test (Ceres HandleSuccessfulStep); no Schur complement is needed
+  const bool final_pass = st->iterations >= o.max_num_iterations;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->final_pass = final_pass;
   const int P = g.spts, Rz = g.Rpad, rows = 3 * P, nks = rows / 4;
   double* Y = smem;
   int* band = reinterpret_cast<int*>(Y + (size_t)rows * Rz);  // per landmark: first / last camera column, live
@@ -536,6 +540,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
           pv[a] = b.psc[3 * (long)j + a];
         }
       }
+      if (!final_pass) {  // (uniform)
       // point block, redundantly on every lane of the group (the sums are group-uniform)
       double A[9], L[9], z[3];
       for (int i = 0; i < 9; ++i) A[i] = Vs[i];
@@ -593,6 +598,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
         band[3 * gi + 1] = hi;
         band[3 * gi + 2] = 1;  // z_p (column n6, tile T-1) is live for every landmark
       }
+      }  // !final_pass
     } else if (gl == 0) {
       band[3 * gi] = 1 << 29;
       band[3 * gi + 1] = -1;
@@ -602,7 +608,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
     // (C) partial tiles on the matrix cores.  The K-step's camera band is
     // wave-uniform (scalar registers, scalar branches); the operands of all its
     // live tiles are read before the first MFMA of the step.
-    for (int ks = 0; ks < nks; ++ks) {
+    for (int ks = 0; ks < (final_pass ? 0 : nks); ++ks) {
       const int pa = (4 * ks) / 3, pb = min((4 * ks + 3) / 3, P - 1);
       const int lo = __builtin_amdgcn_readfirstlane(min(band[3 * pa], band[3 * pb]));
       const int hi = __builtin_amdgcn_readfirstlane(max(band[3 * pa + 1], band[3 * pb + 1]));
@@ -630,6 +636,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
     const double r = block_max(gm, red);
     if (tid == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
   }
+  if (final_pass) return;
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
     const int p = wave + 8 * u;
@@ -730,7 +737,7 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
     return;
   }
   const State* st = b.st;
-  if (st->done) return;
+  if (st->done || st->final_pass) return;  // final pass: no step follows, S is not needed
   const int n = g.n6;
   const int e = threadIdx.x % kSaElems, grp = threadIdx.x / kSaElems;
   const int idx = blockIdx.x * kSaElems + e;
@@ -1543,7 +1550,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_scan_kernel(Geo g, Bufs b, Op
     st->done = 0;
     st->termination = 1;
     st->iterations = st->successful = st->invalid_count = 0;
-    st->fail = st->scaled = st->accepted = 0;
+    st->fail = st->scaled = st->accepted = st->final_pass = 0;
     st->bad_input = w.flags[F_BAD];
     st->infeasible = w.flags[F_INFEASIBLE];
     st->radius = o.initial_radius;

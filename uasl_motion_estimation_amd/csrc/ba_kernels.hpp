@@ -54,7 +54,8 @@ struct State {
   int accepted;
   int bad_input;      // device-resident input: an observation indexes outside the window
   int infeasible;     // a starting point violates the box bounds (Ceres IsFeasible -> FAILURE)
-  int pad[4];
+  int final_pass;     // set by pt_schur: this linearisation only feeds the closing gradient test
+  int pad[3];
   double radius, decrease;
   double x_cost, cand_cost, model_change, initial_cost;
   double cam_step2, cam_xn2, cam_gmax;
