@@ -42,6 +42,9 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lib", default=None, help="development A/B only: load this libme_hip.so build")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
+                         "thread each), reported as multi_stream; the headline value stays one stream per GPU")
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
@@ -220,6 +223,53 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
             "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
 
 
+def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
+    """S independent stereo streams on this GPU, each sequential (its own
+    context = HIP stream + scratch, its own host thread; ctypes releases the
+    GIL inside the library): whole-GPU throughput of small latency-bound
+    frames.  Returns frames/s over all streams and the per-stream rate."""
+    import threading
+
+    from uasl_motion_estimation_amd._lib import Context
+
+    S_ = args.streams
+    ctxs = [Context(local_rank) for _ in range(S_)]
+    fr = []
+    for k, c in enumerate(ctxs):
+        f = make_frames(cfg, seed + 7919 * (k + 1), args.frames)
+        upload_images(c, f)
+        fr.append(f)
+    stats = [dict(frames=0, ba_iters=0, scale_iters=0) for _ in range(S_)]
+    for k in range(S_):
+        for i in range(args.warmup):
+            gpu_step(ctxs[k], fr[k][i % len(fr[k])], kp, ba_opts, stats[k])
+        ctxs[k].synchronize()
+    stats = [dict(frames=0, ba_iters=0, scale_iters=0) for _ in range(S_)]
+    errs = []
+
+    def run(k):
+        try:
+            for i in range(args.steps):
+                gpu_step(ctxs[k], fr[k][i % len(fr[k])], kp, ba_opts, stats[k])
+            ctxs[k].synchronize()
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    barrier()
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=run, args=(k,)) for k in range(S_)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    el = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    nfr = sum(st["frames"] for st in stats)
+    return {"streams": S_, "frames": nfr, "value": round(nfr / el, 2), "unit": "frames/s",
+            "per_stream": round(nfr / el / S_, 2), "ba_iter_per_s": round(sum(st["ba_iters"] for st in stats) / el, 1)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -311,6 +361,7 @@ def main():
                 "kernels": FAMILY_KERNELS.get(dom), "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount,
                 "timed_live": fams[dom][0] > 0}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
+    multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cstats = dict(ba_iters=0)
@@ -344,6 +395,7 @@ def main():
             "ba_iter_per_s": round(ba_total / t_max, 2),
             "roofline": roofline,
             "mi_roofline": mi_rl,
+            "multi_stream": multi,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
             "gen_s": round(gen_s, 1),
