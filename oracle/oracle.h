@@ -149,6 +149,12 @@ int oracle_vo_process(const float* matches, int n, const double* init6, const or
                       const int* rand_seq, int rand_len, double* motion, int* inliers, int* n_inliers,
                       int max_outer);
 
+/* ---- pose-covariance propagation (src/core/feature_types.cpp:171-251) ---- */
+void oracle_pose_mul_cov(const double* q1, const double* t1, const double* c1, const double* q2, const double* t2,
+                         const double* c2, int reverse, double* q3, double* t3, double* c3);
+void oracle_pose_invert_cov(double* q, double* t, double* cov);
+void oracle_pose_scale_cov(double* t, double* cov, double s, double var);
+
 #ifdef __cplusplus
 }
 #endif

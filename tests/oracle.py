@@ -103,6 +103,9 @@ def lib():
         for f in (L.oracle_compare_pc, L.oracle_ccoeff_normed):
             f.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
         L.oracle_quantise.argtypes = [c_void_p, c_int, c_int, c_int, c_int, c_int]
+        L.oracle_pose_mul_cov.argtypes = [c_void_p] * 6 + [c_int] + [c_void_p] * 3
+        L.oracle_pose_invert_cov.argtypes = [c_void_p] * 3
+        L.oracle_pose_scale_cov.argtypes = [c_void_p, c_void_p, c_double, c_double]
         L.oracle_mi_histograms.argtypes = [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                            c_void_p]
         L.oracle_mi_scores.argtypes = [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
@@ -180,6 +183,31 @@ def quantise(img, lo, hi):
     h, w = img.shape
     lib().oracle_quantise(img.ctypes.data, w, w, h, lo, hi)
     return img
+
+
+def _d(a):
+    return np.array(a, np.float64, copy=True, order="C")
+
+
+def pose_mul_cov(q1, t1, c1, q2, t2, c2, reverse=False):
+    """(q3, t3, cov3) of poseMultiplicationWithCovariance[Reverse] (feature_types.cpp:171-219)."""
+    a = [_d(x) for x in (q1, t1, c1, q2, t2, c2)]
+    q3, t3, c3 = np.zeros(4), np.zeros(3), np.zeros(36)
+    lib().oracle_pose_mul_cov(*[x.ctypes.data for x in a], int(reverse), q3.ctypes.data, t3.ctypes.data,
+                              c3.ctypes.data)
+    return q3, t3, c3.reshape(6, 6)
+
+
+def pose_invert_cov(q, t, c):
+    q, t, c = _d(q), _d(t), _d(c)
+    lib().oracle_pose_invert_cov(q.ctypes.data, t.ctypes.data, c.ctypes.data)
+    return q, t, c.reshape(6, 6)
+
+
+def pose_scale_cov(t, c, s, var):
+    t, c = _d(t), _d(c)
+    lib().oracle_pose_scale_cov(t.ctypes.data, c.ctypes.data, float(s), float(var))
+    return t, c.reshape(6, 6)
 
 
 def histograms(L, R):

@@ -165,6 +165,81 @@ class CamPose:
         T[:3, 3] = self.position
         return T
 
+    def __mul__(self, pose: "CamPose") -> "CamPose":
+        """CamPose::operator* (feature_types.h:223-228): R1 R2 | R1 t2 + t1, keeps this ID and Cov."""
+        return CamPose(self.ID, self.orientation * pose.orientation,
+                       self.orientation * np.asarray(pose.position) + np.asarray(self.position),
+                       np.array(self.Cov, np.float64, copy=True))
+
+
+# ------------------------------------------------ pose-covariance propagation
+# src/core/feature_types.cpp:171-251.  The reference writes a CV_32F identity
+# into a CV_64F Jacobian with Mat::copyTo, which reallocates the ROI header
+# instead of writing J: those blocks stay zero (reproduced, SURVEY §8f):
+# J[0:3, 6:9] in poseMultiplicationWithCovarianceReverse, J[3:6, 3:6] in
+# invertPoseWithCovariance.
+def poseMultiplicationWithCovariance(p1: CamPose, p2: CamPose, ID: int) -> CamPose:
+    """P3 = P1 * P2 with Cov3 = J diag(Cov1, Cov2) J^T (feature_types.cpp:171-194)."""
+    assert p1.Cov.size and p2.Cov.size, "Poses cannot be mulitplied (empty Cov matrix)"
+    p3 = p1 * p2
+    aug = np.zeros((12, 12))
+    aug[:6, :6], aug[6:, 6:] = p1.Cov, p2.Cov
+    q1, q2, q3 = p1.orientation, p2.orientation, p3.orientation
+    J = np.zeros((6, 12))
+    J[:3, :3] = np.eye(3)
+    J[:3, 3:6] = q1.getH_qvec(p2.position)
+    J[:3, 6:9] = q1.getR3()
+    J[3:, 3:6] = q3.getH() @ q2.getQr() @ q1.getG()
+    J[3:, 9:12] = q3.getH() @ q1.getQl() @ q2.getG()
+    p3.ID = ID
+    p3.Cov = J @ aug @ J.T
+    return p3
+
+
+def poseMultiplicationWithCovarianceReverse(p1: CamPose, p2: CamPose, ID: int) -> CamPose:
+    """P3 = P2 * P1 with propagated covariance (feature_types.cpp:196-219)."""
+    assert p1.Cov.size and p2.Cov.size, "Poses cannot be multiplied (empty Cov matrix)"
+    p3 = p2 * p1
+    aug = np.zeros((12, 12))
+    aug[:6, :6], aug[6:, 6:] = p1.Cov, p2.Cov
+    q1, q2, q3 = p1.orientation, p2.orientation, p3.orientation
+    J = np.zeros((6, 12))
+    J[:3, :3] = q2.getR3()
+    # J[:3, 6:9] stays 0: the reference's CV_32F identity never reaches J
+    J[:3, 9:12] = q2.getH_qvec(p1.position)
+    J[3:, 3:6] = q3.getH() @ q2.getQl() @ q1.getG()
+    J[3:, 9:12] = q3.getH() @ q1.getQr() @ q2.getG()
+    p3.ID = ID
+    p3.Cov = J @ aug @ J.T
+    return p3
+
+
+def invertPoseWithCovariance(p: CamPose) -> None:
+    """In place: P <- P^-1 with Cov <- J Cov J^T (feature_types.cpp:221-236)."""
+    assert p.Cov.size, "Pose cannot be inverted (empty Cov matrix)"
+    qc = p.orientation.conj()
+    J = np.zeros((6, 6))
+    J[:3, :3] = -qc.getR3()
+    J[:3, 3:6] = qc.getH_qvec(p.position)
+    # J[3:6, 3:6] stays 0 (the reference's -eye(CV_32F) never reaches J)
+    p.position = -(qc * np.asarray(p.position))
+    p.orientation = qc
+    p.Cov = J @ p.Cov @ J.T
+
+
+def ScalePoseWithCovariance(p: CamPose, scale) -> None:
+    """In place: t <- s t, Cov <- J diag(Cov, var_s) J^T (feature_types.cpp:238-251); scale = (s, var_s)."""
+    assert p.Cov.size, "Pose cannot be scaled (empty Cov matrix)"
+    aug = np.zeros((7, 7))
+    aug[:6, :6] = p.Cov
+    aug[6, 6] = scale[1]
+    J = np.zeros((6, 7))
+    J[:3, :3] = np.eye(3) * scale[0]
+    J[3:, 3:6] = np.eye(3)
+    J[:3, 6] = p.position
+    p.Cov = J @ aug @ J.T
+    p.position = np.asarray(p.position, np.float64) * scale[0]
+
 
 @dataclass
 class StereoMatch:
