@@ -268,6 +268,10 @@ class Context:
         self.check(self.lib.me_set_stream(self.h, c_void_p(stream_handle) if stream_handle else None),
                    "me_set_stream")
 
+    def stream_ptr(self) -> int:
+        """The context's HIP stream (me_get_stream) as an integer handle."""
+        return int(self.lib.me_get_stream(self.h) or 0)
+
     def synchronize(self):
         self.check(self.lib.me_synchronize(self.h), "me_synchronize")
 
