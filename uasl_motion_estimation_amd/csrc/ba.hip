@@ -1853,8 +1853,12 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
   ME_CHECK(c, P.schur_lds <= 150 * 1024, "BA: %d variable cameras exceed the Schur workspace", g.m);
-  for (const void* k : {(const void*)pt_schur_kernel<4>, (const void*)pt_schur_kernel<8>,
-                        (const void*)pt_schur_kernel<16>, (const void*)pt_schur_kernel<24>})
+  for (const void* k : {(const void*)pt_schur_kernel<3>, (const void*)pt_schur_kernel<4>,
+                        (const void*)pt_schur_kernel<5>, (const void*)pt_schur_kernel<6>,
+                        (const void*)pt_schur_kernel<7>, (const void*)pt_schur_kernel<8>,
+                        (const void*)pt_schur_kernel<9>, (const void*)pt_schur_kernel<10>,
+                        (const void*)pt_schur_kernel<12>, (const void*)pt_schur_kernel<16>,
+                        (const void*)pt_schur_kernel<24>})
     ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
   return ME_OK;
 }
@@ -1892,16 +1896,17 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   {
     // point blocks + Schur partial tiles (BA_SCHUR family)
     me_ktimer t(c, ME_KT_BA_SCHUR);
+    // NT = this wave's tile count, instantiated tight (every unused tile's
+    // accumulator costs 8 VGPRs; at 2 waves per SIMD the budget is 256)
     const int per_wave = (g.npairs + 7) / 8;
     const dim3 grd(g.ksplit), blk(kSchurBlock);
-    if (per_wave <= 4)
-      hipLaunchKernelGGL(pt_schur_kernel<4>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-    else if (per_wave <= 8)
-      hipLaunchKernelGGL(pt_schur_kernel<8>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-    else if (per_wave <= 16)
-      hipLaunchKernelGGL(pt_schur_kernel<16>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-    else
-      hipLaunchKernelGGL(pt_schur_kernel<24>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+#define ME_SCHUR_NT(N)                                                                  \
+  else if (per_wave <= N) hipLaunchKernelGGL(pt_schur_kernel<N>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+    if (per_wave <= 3) hipLaunchKernelGGL(pt_schur_kernel<3>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+    ME_SCHUR_NT(4) ME_SCHUR_NT(5) ME_SCHUR_NT(6) ME_SCHUR_NT(7) ME_SCHUR_NT(8) ME_SCHUR_NT(9) ME_SCHUR_NT(10)
+    ME_SCHUR_NT(12) ME_SCHUR_NT(16)
+    else hipLaunchKernelGGL(pt_schur_kernel<24>, grd, blk, P.schur_lds, s, g, P.b, P.o);
+#undef ME_SCHUR_NT
   }
   if (ar) {
     hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
