@@ -445,8 +445,9 @@ __device__ __forceinline__ int group_max(int x) {
   return x;
 }
 
-template <int NT>
-__global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+template <int NT, int BLK>
+__global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+  constexpr int SL = BLK / kSchurPts, NW = BLK / 64;  // lanes per landmark, waves
   extern __shared__ double smem[];
   __shared__ double red[8];
   State* st = b.st;
@@ -461,12 +462,12 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
   double* Y = smem;
   int* band = reinterpret_cast<int*>(Y + (size_t)rows * Rz);  // per landmark: first / last camera column, live
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gi = tid / kSchurLanes, gl = tid & (kSchurLanes - 1);
+  const int gi = tid / SL, gl = tid & (SL - 1);
   // this wave's tiles (wave-uniform: scalar registers)
   int tI[NT], tJ[NT];
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
-    int p = wave + 8 * u, I = 0;
+    int p = wave + NW * u, I = 0;
     if (p >= g.npairs) p = -1;
     int rem = p < 0 ? 0 : p;
     while (rem >= g.T - I) {
@@ -483,7 +484,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
   for (int sc = blockIdx.x; sc < g.nsub; sc += gridDim.x) {
     const int j = sc * P + gi;
     double* Yp = Y + (size_t)(3 * gi) * Rz;  // this landmark's 3 rows, written by its own lane group only
-    for (int i = gl; i < 3 * Rz / 2; i += kSchurLanes) reinterpret_cast<double2*>(Yp)[i] = double2{0.0, 0.0};
+    for (int i = gl; i < 3 * Rz / 2; i += SL) reinterpret_cast<double2*>(Yp)[i] = double2{0.0, 0.0};
     if (j < g.np) {
       // (A) every load of the landmark and of this lane's first CSR slot in one round
       const int beg = b.p_off[j], end = b.p_off[j + 1];
@@ -508,9 +509,9 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
           for (int a = 0; a < 3; ++a) pv[a] = b.psc[3 * (long)j + a];
         double V[9];  // V_o (6 unique) | g_o (3)
         for (int i = 0; i < 9; ++i) V[i] = X0[i];
-        for (int q = q0 + kSchurLanes; q < end; q += kSchurLanes)
+        for (int q = q0 + SL; q < end; q += SL)
           for (int i = 0; i < 9; ++i) V[i] += b.obsx[(long)q * kObsxStride + i];
-        for (int i = 0; i < 9; ++i) V[i] = group_sum<kSchurLanes>(V[i]);
+        for (int i = 0; i < 9; ++i) V[i] = group_sum<SL>(V[i]);
         if (!scaled) {
           pv[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
           pv[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
@@ -556,7 +557,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
       // (B) this lane's slots -> the landmark's rows of Y (first slot of each camera run only;
       // duplicate residual blocks of one camera are summed in CSR order)
       int lo = 1 << 29, hi = -1;
-      for (int q = q0; q < end; q += kSchurLanes) {
+      for (int q = q0; q < end; q += SL) {
         int ci, cp;
         double w[18], cs[6];
         if (q == q0) {
@@ -590,8 +591,8 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
           for (int k = 0; k < 3; ++k) Yp[(size_t)k * Rz + col] = y[k];
         }
       }
-      lo = group_min<kSchurLanes>(lo);
-      hi = group_max<kSchurLanes>(hi);
+      lo = group_min<SL>(lo);
+      hi = group_max<SL>(hi);
       if (gl == 0) {
         for (int k = 0; k < 3; ++k) Yp[(size_t)k * Rz + g.n6] = z[k];
         band[3 * gi] = lo;
@@ -639,7 +640,7 @@ __global__ __launch_bounds__(kSchurBlock) void pt_schur_kernel(Geo g, Bufs b, Op
   if (final_pass) return;
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
-    const int p = wave + 8 * u;
+    const int p = wave + NW * u;
     if (p >= g.npairs) continue;
     double* dst = b.Spart + ((long)blockIdx.x * g.npairs + p) * 256;
 #pragma unroll
@@ -1853,12 +1854,14 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
   ME_CHECK(c, P.schur_lds <= 150 * 1024, "BA: %d variable cameras exceed the Schur workspace", g.m);
-  for (const void* k : {(const void*)pt_schur_kernel<3>, (const void*)pt_schur_kernel<4>,
-                        (const void*)pt_schur_kernel<5>, (const void*)pt_schur_kernel<6>,
-                        (const void*)pt_schur_kernel<7>, (const void*)pt_schur_kernel<8>,
-                        (const void*)pt_schur_kernel<9>, (const void*)pt_schur_kernel<10>,
-                        (const void*)pt_schur_kernel<12>, (const void*)pt_schur_kernel<16>,
-                        (const void*)pt_schur_kernel<24>})
+  for (const void* k :
+       {(const void*)pt_schur_kernel<3, 512>, (const void*)pt_schur_kernel<4, 512>,
+        (const void*)pt_schur_kernel<5, 512>, (const void*)pt_schur_kernel<6, 512>,
+        (const void*)pt_schur_kernel<7, 512>, (const void*)pt_schur_kernel<8, 512>,
+        (const void*)pt_schur_kernel<9, 512>, (const void*)pt_schur_kernel<10, 512>,
+        (const void*)pt_schur_kernel<12, 512>, (const void*)pt_schur_kernel<16, 256>,
+        (const void*)pt_schur_kernel<20, 256>, (const void*)pt_schur_kernel<24, 256>,
+        (const void*)pt_schur_kernel<48, 256>})
     ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
   return ME_OK;
 }
@@ -1896,17 +1899,28 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   {
     // point blocks + Schur partial tiles (BA_SCHUR family)
     me_ktimer t(c, ME_KT_BA_SCHUR);
-    // NT = this wave's tile count, instantiated tight (every unused tile's
-    // accumulator costs 8 VGPRs; at 2 waves per SIMD the budget is 256)
-    const int per_wave = (g.npairs + 7) / 8;
-    const dim3 grd(g.ksplit), blk(kSchurBlock);
-#define ME_SCHUR_NT(N)                                                                  \
-  else if (per_wave <= N) hipLaunchKernelGGL(pt_schur_kernel<N>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-    if (per_wave <= 3) hipLaunchKernelGGL(pt_schur_kernel<3>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-    ME_SCHUR_NT(4) ME_SCHUR_NT(5) ME_SCHUR_NT(6) ME_SCHUR_NT(7) ME_SCHUR_NT(8) ME_SCHUR_NT(9) ME_SCHUR_NT(10)
-    ME_SCHUR_NT(12) ME_SCHUR_NT(16)
-    else hipLaunchKernelGGL(pt_schur_kernel<24>, grd, blk, P.schur_lds, s, g, P.b, P.o);
-#undef ME_SCHUR_NT
+    // NT = this wave's tile count, instantiated tight (an unused tile's
+    // accumulator costs 8 VGPRs).  512 threads (2 waves per SIMD, 256
+    // registers each) while the spill stays small -- measured faster than one
+    // wave per SIMD even with a 120 B spill at 9 tiles (config 4); beyond 12
+    // tiles per wave, 256 threads so the accumulators live in AGPRs.
+    const int pw8 = (g.npairs + 7) / 8, pw4 = (g.npairs + 3) / 4;
+    const dim3 grd(g.ksplit);
+#define ME_SCHUR(N, B) hipLaunchKernelGGL((pt_schur_kernel<N, B>), grd, dim3(B), P.schur_lds, s, g, P.b, P.o)
+    if (pw8 <= 3) ME_SCHUR(3, 512);
+    else if (pw8 <= 4) ME_SCHUR(4, 512);
+    else if (pw8 <= 5) ME_SCHUR(5, 512);
+    else if (pw8 <= 6) ME_SCHUR(6, 512);
+    else if (pw8 <= 7) ME_SCHUR(7, 512);
+    else if (pw8 <= 8) ME_SCHUR(8, 512);
+    else if (pw8 <= 9) ME_SCHUR(9, 512);
+    else if (pw8 <= 10) ME_SCHUR(10, 512);
+    else if (pw8 <= 12) ME_SCHUR(12, 512);
+    else if (pw4 <= 16) ME_SCHUR(16, 256);
+    else if (pw4 <= 20) ME_SCHUR(20, 256);
+    else if (pw4 <= 24) ME_SCHUR(24, 256);
+    else ME_SCHUR(48, 256);
+#undef ME_SCHUR
   }
   if (ar) {
     hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
