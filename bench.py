@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lib", default=None, help="development A/B only: load this libme_hip.so build")
+    ap.add_argument("--vo-matches", type=int, default=2000,
+                    help="matches of the StereoVisualOdometry::process line (SURVEY 8f rank 1; 0: off)")
     ap.add_argument("--streams", type=int, default=1,
                     help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
                          "thread each), reported as multi_stream; the headline value stays one stream per GPU")
@@ -223,6 +225,36 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
             "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
 
 
+def stereo_vo_line(ctx, n: int, reps: int = 5, cpu: bool = True):
+    """StereoVisualOdometry::process (src/vo/StereoVisualOdometry.cpp:34-114):
+    200 RANSAC hypotheses + GN refinement on n synthetic quad matches
+    (noise 0.005 px, the parity-test setup), device vs the oracle (1 thread)."""
+    from uasl_motion_estimation_amd import synthetic as S
+    from uasl_motion_estimation_amd.vo import Parameters, StereoVisualOdometry
+
+    m, p = S.vo_matches(12, n, noise=0.005)
+    vo = StereoVisualOdometry(Parameters(**{k: v for k, v in p.items() if k in Parameters.__dataclass_fields__}),
+                              ctx=ctx)
+    vo.srand(1)
+    vo.process(m)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        vo.srand(1)
+        ok = vo.process(m)
+    gpu_ms = (time.perf_counter() - t0) * 1e3 / reps
+    out = {"matches": n, "ms_per_process": round(gpu_ms, 3), "ok": bool(ok), "inliers": len(vo.getInliers_idx())}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle as O  # CPU baseline leg only
+
+        seq = O.libc_rand_seq(1, 16 * 200 + 64)
+        t0 = time.perf_counter()
+        O.vo_process(m, p, rand_seq=seq)
+        out["cpu_ms_per_process"] = round((time.perf_counter() - t0) * 1e3, 3)
+        out["cpu_cores"] = 1
+    return out
+
+
 def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
     """S independent stereo streams on this GPU, each sequential (its own
     context = HIP stream + scratch, its own host thread; ctypes releases the
@@ -362,6 +394,8 @@ def main():
                 "timed_live": fams[dom][0] > 0}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
+    vo_line = stereo_vo_line(ctx, args.vo_matches, cpu=rank == 0 and world == 1 and not args.no_cpu_baseline) \
+        if args.vo_matches > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cstats = dict(ba_iters=0)
@@ -396,6 +430,7 @@ def main():
             "roofline": roofline,
             "mi_roofline": mi_rl,
             "multi_stream": multi,
+            "stereo_vo": vo_line,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
             "gen_s": round(gen_s, 1),
