@@ -83,6 +83,10 @@ __device__ __forceinline__ long wave_sum64(long v) {
   return v;
 }
 __device__ __forceinline__ int descale(long v, int n) { return (int)((v + (1L << (n - 1))) >> n); }
+// 32-bit form: every per-pixel product below fits in int32 (|I w| <= 255 * 16384,
+// |DX w| <= 4080 * 16384, |diff * grad| <= 8160 * 4080, 7 pixels per lane), so
+// only the wave-wide sums need 64 bits -- same integers as the 64-bit form.
+__device__ __forceinline__ int descale32(int v, int n) { return (v + (1 << (n - 1))) >> n; }
 
 constexpr int kMaxWinPx = 7;  // pixels per lane: ceil(21*21/64)
 
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const uint8_t* I = P.I[L];
     const int16_t* DX = P.dx[L];
     const int16_t* DY = P.dy[L];
-    long A11 = 0, A12 = 0, A22 = 0;
+    int a11l = 0, a12l = 0, a22l = 0;
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
       const int k = lane + 64 * q;
@@ -133,20 +137,18 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       if (k < npx) {
         const int y = k / win, x = k - y * win;
         const long o = (long)(iy0 + y) * W + ix0 + x, oi = (long)(iy0 + y) * SI + ix0 + x;
-        const long v = (long)I[oi] * iw00 + (long)I[oi + 1] * iw01 + (long)I[oi + SI] * iw10 + (long)I[oi + SI + 1] * iw11;
-        const long gx = (long)DX[o] * iw00 + (long)DX[o + 1] * iw01 + (long)DX[o + W] * iw10 + (long)DX[o + W + 1] * iw11;
-        const long gy = (long)DY[o] * iw00 + (long)DY[o + 1] * iw01 + (long)DY[o + W] * iw10 + (long)DY[o + W + 1] * iw11;
-        iv[q] = descale(v, 9);
-        ixv[q] = descale(gx, 14);
-        iyv[q] = descale(gy, 14);
-        A11 += (long)ixv[q] * ixv[q];
-        A12 += (long)ixv[q] * iyv[q];
-        A22 += (long)iyv[q] * iyv[q];
+        const int v = I[oi] * iw00 + I[oi + 1] * iw01 + I[oi + SI] * iw10 + I[oi + SI + 1] * iw11;
+        const int gx = DX[o] * iw00 + DX[o + 1] * iw01 + DX[o + W] * iw10 + DX[o + W + 1] * iw11;
+        const int gy = DY[o] * iw00 + DY[o + 1] * iw01 + DY[o + W] * iw10 + DY[o + W + 1] * iw11;
+        iv[q] = descale32(v, 9);
+        ixv[q] = descale32(gx, 14);
+        iyv[q] = descale32(gy, 14);
+        a11l += ixv[q] * ixv[q];
+        a12l += ixv[q] * iyv[q];
+        a22l += iyv[q] * iyv[q];
       }
     }
-    A11 = wave_sum64(A11);
-    A12 = wave_sum64(A12);
-    A22 = wave_sum64(A22);
+    const long A11 = wave_sum64(a11l), A12 = wave_sum64(a12l), A22 = wave_sum64(a22l);
     const double a11 = (double)A11 * FLT_SCALE, a12 = (double)A12 * FLT_SCALE, a22 = (double)A22 * FLT_SCALE;
     const double D = a11 * a22 - a12 * a12;
     const double minEig = (a22 + a11 - sqrt((a11 - a22) * (a11 - a22) + 4.0 * a12 * a12)) / (2.0 * win * win);
@@ -169,21 +171,20 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       const int jw01 = (int)rintf(c * (1.f - d) * 16384.f);
       const int jw10 = (int)rintf((1.f - c) * d * 16384.f);
       const int jw11 = 16384 - jw00 - jw01 - jw10;
-      long b1 = 0, b2 = 0;
+      int b1l = 0, b2l = 0;
 #pragma unroll
       for (int q = 0; q < kMaxWinPx; ++q) {
         const int k = lane + 64 * q;
         if (k < npx) {
           const int y = k / win, x = k - y * win;
           const long o = (long)(jy0 + y) * SI + jx0 + x;
-          const long v = (long)J[o] * jw00 + (long)J[o + 1] * jw01 + (long)J[o + SI] * jw10 + (long)J[o + SI + 1] * jw11;
-          const long diff = descale(v, 9) - iv[q];
-          b1 += diff * ixv[q];
-          b2 += diff * iyv[q];
+          const int v = J[o] * jw00 + J[o + 1] * jw01 + J[o + SI] * jw10 + J[o + SI + 1] * jw11;
+          const int diff = descale32(v, 9) - iv[q];
+          b1l += diff * ixv[q];
+          b2l += diff * iyv[q];
         }
       }
-      b1 = wave_sum64(b1);
-      b2 = wave_sum64(b2);
+      const long b1 = wave_sum64(b1l), b2 = wave_sum64(b2l);
       const double b1d = (double)b1 * FLT_SCALE, b2d = (double)b2 * FLT_SCALE;
       const float ddx = (float)((a12 * b2d - a22 * b1d) * Dinv);
       const float ddy = (float)((a12 * b1d - a11 * b2d) * Dinv);
