@@ -279,7 +279,7 @@ __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected) {
   __shared__ int slast;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     slast = k == expected - 1;
     if (slast) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }

@@ -568,7 +568,7 @@ __device__ __forceinline__ bool last_block_arrives(unsigned* cnt) {
   __shared__ int slast;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     slast = k == gridDim.x - 1;
   }
   __syncthreads();
