@@ -103,20 +103,44 @@ def upload_images(ctx, frames):
     return keep
 
 
-def gpu_step(ctx, fd, kp, ba_opts, stats):
-    from uasl_motion_estimation_amd._lib import ME_DEVICE
-    from uasl_motion_estimation_amd.optimisation import scale_optimise
+class _Calls:
+    """The C-ABI argument blocks of one frame, built once (as a C++ caller
+    would keep them): per frame only the scalars that change are reset."""
 
-    H, W = fd.prev.shape
-    n = len(fd.klt_pts)
-    ctx.check(ctx.lib.me_klt_track(ctx.h, ME_DEVICE, ctypes.c_void_p(fd.d_prev), ctypes.c_void_p(fd.d_curL), W, H, W,
-                                   ctypes.c_void_p(fd.d_pts_in), ctypes.c_void_p(fd.d_pts_out),
-                                   ctypes.c_void_p(fd.d_status), n, ctypes.byref(kp)), "klt")
-    r = scale_optimise(fd.scale, ctx=ctx, img_mem=ME_DEVICE, dev_imgs=(fd.d_curL, fd.d_curR), dev_tracks=fd.dscale.d)
-    stats["scale_iters"] += r["iterations"]
+    def __init__(self, ctx, fd, kp, ba_opts):
+        from uasl_motion_estimation_amd._lib import ME_DEVICE, BASummaryC
+        from uasl_motion_estimation_amd.optimisation import OptimisationParams, scale_struct
+
+        H, W = fd.prev.shape
+        n = len(fd.klt_pts)
+        self.klt = (ctx.h, ME_DEVICE, ctypes.c_void_p(fd.d_prev), ctypes.c_void_p(fd.d_curL), W, H, W,
+                    ctypes.c_void_p(fd.d_pts_in), ctypes.c_void_p(fd.d_pts_out), ctypes.c_void_p(fd.d_status), n,
+                    ctypes.byref(kp))
+        self.keep = []
+        self.sc = scale_struct(fd.scale, self.keep, ME_DEVICE, (fd.d_curL, fd.d_curR), fd.dscale.d)
+        self.scale0 = self.sc.scale
+        self.sp = OptimisationParams().to_c()
+        self.stop, self.it, self.nmi = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
+        self.scale = (ctx.h, ctypes.byref(self.sc), ctypes.byref(self.sp), 0, ctypes.byref(self.stop),
+                      ctypes.byref(self.it), None, 0, ctypes.byref(self.nmi))
+        self.bp = fd.dba.struct()
+        self.bo = ba_opts.to_c()
+        self.bs = BASummaryC()
+        self.ba = (ctx.h, ctypes.byref(self.bp), ctypes.byref(self.bo), ctypes.byref(self.bs))
+
+
+def gpu_step(ctx, fd, kp, ba_opts, stats):
+    c = getattr(fd, "_calls", None)
+    if c is None or c.klt[0] is not ctx.h:
+        c = fd._calls = _Calls(ctx, fd, kp, ba_opts)
+    lib = ctx.lib
+    ctx.check(lib.me_klt_track(*c.klt), "klt")
+    c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
+    ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
+    stats["scale_iters"] += c.it.value
     fd.dba.reset()  # same starting point every time the frame is replayed (device copy)
-    s = fd.dba.solve(ba_opts)
-    stats["ba_iters"] += s["iterations"]
+    ctx.check(lib.me_ba_solve(*c.ba), "me_ba_solve")
+    stats["ba_iters"] += c.bs.iterations
     stats["frames"] += 1
 
 

@@ -1982,11 +1982,12 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   return me_check_launch(c, "BA iteration");
 }
 
-int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
+// Final state (and host parameters) -> pinned staging; enqueued behind the
+// last chunk so the read-back does not wait for a host round trip.
+int enqueue_output(Plan& P, me_ba_problem* p) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   constexpr size_t nst = sizeof(State) / 8;
-  static_assert(sizeof(State) % 8 == 0, "State is read back as doubles");
   double* cams_dst = P.dev ? p->cams : P.b.out + nst;
   double* pts_dst = P.dev ? p->pts : P.b.out + nst + 6 * (size_t)g.nc;
   const long n = std::max({(long)nst, 6L * g.nc, 3L * g.np});
@@ -1994,6 +1995,15 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum) {
   ME_TRY(me_check_launch(c, "BA output"));
   const size_t bytes = 8 * (P.dev ? nst : nst + 6 * (size_t)g.nc + 3 * (size_t)g.np);
   ME_HIP(c, hipMemcpyAsync(P.host, P.b.out, bytes, hipMemcpyDeviceToHost, c->stream));
+  return ME_OK;
+}
+
+int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = false) {
+  me_ctx* c = P.c;
+  const Geo& g = P.g;
+  constexpr size_t nst = sizeof(State) / 8;
+  static_assert(sizeof(State) % 8 == 0, "State is read back as doubles");
+  if (!output_queued) ME_TRY(enqueue_output(P, p));
   ME_HIP(c, hipStreamSynchronize(c->stream));
   State st;
   std::memcpy(&st, P.host, sizeof(State));
@@ -2038,14 +2048,26 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
     ME_HIP(c, hipEventRecord(c->poll_ev[slot], c->stream));
     return ME_OK;
   };
+  // once the last possible chunk is queued, the output follows it at once
+  bool out_q = false;
   ME_TRY(enqueue_chunk(0));
+  if (it > opt->max_num_iterations) {
+    ME_TRY(enqueue_output(P, p));
+    out_q = true;
+  }
   for (int cur = 0;; cur ^= 1) {
     const bool more = it <= opt->max_num_iterations;
-    if (more) ME_TRY(enqueue_chunk(cur ^ 1));
+    if (more) {
+      ME_TRY(enqueue_chunk(cur ^ 1));
+      if (it > opt->max_num_iterations) {
+        ME_TRY(enqueue_output(P, p));
+        out_q = true;
+      }
+    }
     ME_HIP(c, hipEventSynchronize(c->poll_ev[cur]));
     if (P.hstate[cur]->done || !more) break;
   }
-  return finish(P, p, sum);
+  return finish(P, p, sum, out_q);
 }
 
 }  // namespace
