@@ -429,7 +429,6 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
 // A[l&15][l>>4] and B[l>>4][l&15]; result register i holds D[(l>>4)+4i][l&15].
 constexpr int kSchurBlock = 512;
 constexpr int kSchurPts = 16;                       // landmarks per sub-chunk (48 rows of Y)
-constexpr int kSchurLanes = kSchurBlock / kSchurPts;  // lanes per landmark in (A) and (B)
 __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
 
 template <int W>
@@ -831,10 +830,13 @@ __device__ __forceinline__ double quad_bcast(double x) {
 // LDS round trip ~105, barrier ~80 -- so the round is bound by the pivot
 // chain, and splitting the updates over 4 SIMDs removes the single-wave
 // issue bottleneck of the previous one-wave version.
+#ifndef ME_RSQ_NR
+#define ME_RSQ_NR 2
+#endif
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double r = __builtin_amdgcn_rsq(p);
   r = r * fma(-0.5 * p * r, r, 1.5);
-  r = r * fma(-0.5 * p * r, r, 1.5);
+  if (ME_RSQ_NR > 1) r = r * fma(-0.5 * p * r, r, 1.5);
   return r;
 }
 constexpr int kXchDoubles = 192;  // per buffer: pivot rows A (64) | pivot rows Y (64) | column group (64)
