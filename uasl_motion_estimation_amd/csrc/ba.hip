@@ -427,7 +427,6 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
 // Partials (workgroup x tile) are summed in fixed order by s_assemble:
 // deterministic, no atomics.  Operand map of the MFMA: lane l holds
 // A[l&15][l>>4] and B[l>>4][l&15]; result register i holds D[(l>>4)+4i][l&15].
-constexpr int kSchurBlock = 512;
 constexpr int kSchurPts = 16;                       // landmarks per sub-chunk (48 rows of Y)
 __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
 
