@@ -329,3 +329,49 @@ def test_scale_device_resident_tracks_match_host(ctx, oracle):
     assert host["scale"] == dev["scale"]
     np.testing.assert_allclose(dev["scale"], ref["scale"], rtol=1e-9)
     np.testing.assert_allclose(dev["trace"], ref["trace"], rtol=1e-9)
+
+
+# ------------------------------------------------------------------ BA edge cases and large windows
+@pytest.mark.parametrize("w,n,iters", [(30, 150, 4), (40, 120, 3), (21, 200, 5)])
+def test_ba_large_windows_schur_variants(ctx, oracle, w, n, iters):
+    """Windows past config 3 select the wider Schur instances (9 / 16 tiles per
+    wave, with spills) -- same results as the restatement."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    bp = S.ba_problem(60 + w, n, w, 640, 480)
+    cams, pts, s = ba_solve(bp, SolverOptions.fixed_iterations(iters), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert s["iterations"] == rs["iterations"] and s["successful_steps"] == rs["successful_steps"]
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+def test_ba_all_cameras_fixed(ctx, oracle):
+    """fixedFrames >= window: every camera block constant, only the points move."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    bp = S.ba_problem(71, 80, 4, 640, 480, fixed=4)
+    cams, pts, s = ba_solve(bp, SolverOptions.fixed_iterations(5), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=5, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert np.array_equal(cams, bp.cams)
+    assert s["iterations"] == rs["iterations"]
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+def test_ba_duplicate_observations(ctx, oracle):
+    """Two residual blocks on the same (camera, point) pair are both summed (Ceres adds both)."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    bp = S.ba_problem(72, 100, 6, 640, 480)
+    k = np.arange(0, len(bp.obs), 7)
+    bp.obs = np.vstack([bp.obs, bp.obs[k] + 0.3])
+    bp.cam_idx = np.concatenate([bp.cam_idx, bp.cam_idx[k]]).astype(np.int32)
+    bp.pt_idx = np.concatenate([bp.pt_idx, bp.pt_idx[k]]).astype(np.int32)
+    cams, pts, s = ba_solve(bp, SolverOptions.fixed_iterations(6), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=6, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert s["successful_steps"] == rs["successful_steps"]
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)

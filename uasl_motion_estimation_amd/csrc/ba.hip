@@ -1860,9 +1860,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
         (const void*)pt_schur_kernel<5, 512>, (const void*)pt_schur_kernel<6, 512>,
         (const void*)pt_schur_kernel<7, 512>, (const void*)pt_schur_kernel<8, 512>,
         (const void*)pt_schur_kernel<9, 512>, (const void*)pt_schur_kernel<10, 512>,
-        (const void*)pt_schur_kernel<12, 512>, (const void*)pt_schur_kernel<16, 256>,
-        (const void*)pt_schur_kernel<20, 256>, (const void*)pt_schur_kernel<24, 256>,
-        (const void*)pt_schur_kernel<48, 256>})
+        (const void*)pt_schur_kernel<12, 512>, (const void*)pt_schur_kernel<16, 512>,
+        (const void*)pt_schur_kernel<24, 512>})
     ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
   return ME_OK;
 }
@@ -1900,27 +1899,26 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   {
     // point blocks + Schur partial tiles (BA_SCHUR family)
     me_ktimer t(c, ME_KT_BA_SCHUR);
-    // NT = this wave's tile count, instantiated tight (an unused tile's
-    // accumulator costs 8 VGPRs).  512 threads (2 waves per SIMD, 256
-    // registers each) while the spill stays small -- measured faster than one
-    // wave per SIMD even with a 120 B spill at 9 tiles (config 4); beyond 12
-    // tiles per wave, 256 threads so the accumulators live in AGPRs.
-    const int pw8 = (g.npairs + 7) / 8, pw4 = (g.npairs + 3) / 4;
+    // NT = this wave's tile count, instantiated tight: an unused tile's
+    // accumulator costs 8 VGPRs, and at 512 threads (2 waves per SIMD) the
+    // budget is 256 registers -- up to 5 tiles nothing spills, 9 tiles (config
+    // 4) spill 120 B.  (A 256-thread, AGPR-accumulator variant measured slower
+    // at 9-17 tiles than the small spill, and beyond 12 tiles per wave it spills
+    // more than the 512-thread instances.)
+    const int pw8 = (g.npairs + 7) / 8;
     const dim3 grd(g.ksplit);
-#define ME_SCHUR(N, B) hipLaunchKernelGGL((pt_schur_kernel<N, B>), grd, dim3(B), P.schur_lds, s, g, P.b, P.o)
-    if (pw8 <= 3) ME_SCHUR(3, 512);
-    else if (pw8 <= 4) ME_SCHUR(4, 512);
-    else if (pw8 <= 5) ME_SCHUR(5, 512);
-    else if (pw8 <= 6) ME_SCHUR(6, 512);
-    else if (pw8 <= 7) ME_SCHUR(7, 512);
-    else if (pw8 <= 8) ME_SCHUR(8, 512);
-    else if (pw8 <= 9) ME_SCHUR(9, 512);
-    else if (pw8 <= 10) ME_SCHUR(10, 512);
-    else if (pw8 <= 12) ME_SCHUR(12, 512);
-    else if (pw4 <= 16) ME_SCHUR(16, 256);
-    else if (pw4 <= 20) ME_SCHUR(20, 256);
-    else if (pw4 <= 24) ME_SCHUR(24, 256);
-    else ME_SCHUR(48, 256);
+#define ME_SCHUR(N) hipLaunchKernelGGL((pt_schur_kernel<N, 512>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o)
+    if (pw8 <= 3) ME_SCHUR(3);
+    else if (pw8 <= 4) ME_SCHUR(4);
+    else if (pw8 <= 5) ME_SCHUR(5);
+    else if (pw8 <= 6) ME_SCHUR(6);
+    else if (pw8 <= 7) ME_SCHUR(7);
+    else if (pw8 <= 8) ME_SCHUR(8);
+    else if (pw8 <= 9) ME_SCHUR(9);
+    else if (pw8 <= 10) ME_SCHUR(10);
+    else if (pw8 <= 12) ME_SCHUR(12);
+    else if (pw8 <= 16) ME_SCHUR(16);
+    else ME_SCHUR(24);
 #undef ME_SCHUR
   }
   if (ar) {
