@@ -277,6 +277,27 @@ def test_klt_bit_exact(ctx, oracle):
     assert gst.mean() > 0.8
 
 
+@pytest.mark.parametrize("w,h,shift", [(640, 480, (13.3, -9.6)), (1280, 720, (2.5, 1.25)), (40, 30, (1.5, 0.5)),
+                                       (200, 24, (3.0, 0.0))])
+def test_klt_region_staging_bit_exact(ctx, oracle, w, h, shift):
+    """Large displacements walk the window out of the LDS-staged region
+    (restaging); levels under 32 px read global memory directly."""
+    from uasl_motion_estimation_amd.klt import calcOpticalFlowPyrLK
+
+    rng = np.random.default_rng(int(w + h))
+    big = np.kron(rng.integers(0, 256, ((h + 3) // 4 + 16, (w + 3) // 4 + 16)), np.ones((4, 4)))
+    big = (big + rng.integers(0, 16, big.shape)).clip(0, 255).astype(np.uint8)
+    prev = np.ascontiguousarray(big[32:32 + h, 32:32 + w])
+    ox, oy = int(32 + round(shift[0])), int(32 + round(shift[1]))
+    nxt = np.ascontiguousarray(big[oy:oy + h, ox:ox + w])
+    margin = min(12, w // 4, h // 4)
+    pts = S.grid_features(rng, 300, w, h, margin).astype(np.float32)
+    got, gst = calcOpticalFlowPyrLK(prev, nxt, pts, ctx=ctx)
+    ref, rst = oracle.klt(prev, nxt, pts)
+    assert np.array_equal(gst, rst)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
 # ------------------------------------------------------------------ device-resident BA windows
 def test_ba_device_resident_matches_host_bit_exact(ctx):
     from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions, ba_solve

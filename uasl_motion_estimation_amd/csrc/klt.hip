@@ -78,29 +78,91 @@ __global__ void scharr_levels_kernel(Pyr P) {
   dy[(long)y * w + x] = (int16_t)(3 * (t1p + t1m) + 10 * t1);
 }
 
-__device__ __forceinline__ long wave_sum64(long v) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+// Exact wave-wide sum of per-lane int32 partials: every partial sum is an
+// integer below 2^53 (|b| <= 64 * 7 * 8160 * 4080, A <= 441 * 4080^2), so the
+// FP64 adds are exact and the result equals the int64 sum in any order.
+// Within each 16-lane row: quad xor 1, xor 2, half-mirror, mirror (DPP, VALU
+// latency); then the four row sums by readlane.  All 64 lanes must be active.
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), Ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), Ctrl, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ int descale(long v, int n) { return (int)((v + (1L << (n - 1))) >> n); }
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_sum_exact(int v) {
+  double x = (double)v;
+  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f64<0x141>(x);  // row_half_mirror
+  x += dpp_f64<0x140>(x);  // row_mirror
+  return (readlane_f64(x, 0) + readlane_f64(x, 16)) + (readlane_f64(x, 32) + readlane_f64(x, 48));
+}
 // 32-bit form: every per-pixel product below fits in int32 (|I w| <= 255 * 16384,
 // |DX w| <= 4080 * 16384, |diff * grad| <= 8160 * 4080, 7 pixels per lane), so
-// only the wave-wide sums need 64 bits -- same integers as the 64-bit form.
+// only the wave-wide sums need more than 32 bits -- same integers as the 64-bit form.
 __device__ __forceinline__ int descale32(int v, int n) { return (v + (1 << (n - 1))) >> n; }
 
 constexpr int kMaxWinPx = 7;  // pixels per lane: ceil(21*21/64)
+// Next-image region staged in LDS per wave: 32x32 bytes around the current
+// window (the (win+1)^2 bilinear footprint plus a margin), so the LK
+// iterations read LDS instead of making an L2 round trip each.  When the
+// window walks out of the region it is restaged around the new position;
+// levels narrower or shorter than the region read global memory directly.
+// Same pixel values either way, so results are unchanged bit for bit.
+constexpr int kRegion = 32;
 
+// wave-local ordering of this wave's LDS region (no cross-wave sharing)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// lane = (row lane>>1, half lane&1): 16 bytes of row ry0 + (lane>>1)
+__device__ __forceinline__ void stage_region(uint8_t* reg, const uint8_t* __restrict__ J, int SI, int rx0, int ry0,
+                                             int lane) {
+  const uint8_t* src = J + (long)(ry0 + (lane >> 1)) * SI + rx0 + 16 * (lane & 1);
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w[k] = (uint32_t)src[4 * k] | ((uint32_t)src[4 * k + 1] << 8) | ((uint32_t)src[4 * k + 2] << 16) |
+           ((uint32_t)src[4 * k + 3] << 24);
+  wave_lds_sync();  // earlier reads of the previous region are done
+  *(uint4*)(reg + 16 * lane) = make_uint4(w[0], w[1], w[2], w[3]);
+  wave_lds_sync();
+}
+
+// Every lane loads all of its window pixels unconditionally (pixels past the
+// window alias pixel 0 and are masked afterwards), so the loads of one step
+// issue back to back behind a single wait instead of one round trip per pixel.
 __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict__ pin, float* __restrict__ pout,
                                                   uint8_t* __restrict__ status, int n, int win, int max_iters,
                                                   double eps2, double min_eig) {
+  __shared__ __attribute__((aligned(16))) uint8_t regions[4][kRegion * kRegion];
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= n) return;  // wave-uniform
+  uint8_t* reg = regions[threadIdx.x >> 6];
   const int half = (win - 1) / 2, npx = win * win;
   const double FLT_SCALE = 1.0 / (1 << 20);
   uint8_t st = 1;
   float nx = 0, ny = 0;
   int iv[kMaxWinPx], ixv[kMaxWinPx], iyv[kMaxWinPx];
+  int wy[kMaxWinPx], wx[kMaxWinPx];  // window coordinates of this lane's pixels
+  bool wok[kMaxWinPx];
+#pragma unroll
+  for (int q = 0; q < kMaxWinPx; ++q) {
+    const int k = lane + 64 * q;
+    wok[q] = k < npx;
+    const int kk = wok[q] ? k : 0;
+    wy[q] = kk / win;
+    wx[q] = kk - wy[q] * win;
+  }
   const float px0 = pin[2 * f], py0 = pin[2 * f + 1];
   for (int L = P.nl - 1; L >= 0; --L) {
     const int W = P.w[L], H = P.h[L], SI = P.is[L];
@@ -127,29 +189,38 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const uint8_t* I = P.I[L];
     const int16_t* DX = P.dx[L];
     const int16_t* DY = P.dy[L];
+    int i4[kMaxWinPx][4], x4[kMaxWinPx][4], y4[kMaxWinPx][4];
+#pragma unroll
+    for (int q = 0; q < kMaxWinPx; ++q) {
+      const long o = (long)(iy0 + wy[q]) * W + ix0 + wx[q], oi = (long)(iy0 + wy[q]) * SI + ix0 + wx[q];
+      i4[q][0] = I[oi];
+      i4[q][1] = I[oi + 1];
+      i4[q][2] = I[oi + SI];
+      i4[q][3] = I[oi + SI + 1];
+      x4[q][0] = DX[o];
+      x4[q][1] = DX[o + 1];
+      x4[q][2] = DX[o + W];
+      x4[q][3] = DX[o + W + 1];
+      y4[q][0] = DY[o];
+      y4[q][1] = DY[o + 1];
+      y4[q][2] = DY[o + W];
+      y4[q][3] = DY[o + W + 1];
+    }
     int a11l = 0, a12l = 0, a22l = 0;
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
-      const int k = lane + 64 * q;
-      iv[q] = 0;
-      ixv[q] = 0;
-      iyv[q] = 0;
-      if (k < npx) {
-        const int y = k / win, x = k - y * win;
-        const long o = (long)(iy0 + y) * W + ix0 + x, oi = (long)(iy0 + y) * SI + ix0 + x;
-        const int v = I[oi] * iw00 + I[oi + 1] * iw01 + I[oi + SI] * iw10 + I[oi + SI + 1] * iw11;
-        const int gx = DX[o] * iw00 + DX[o + 1] * iw01 + DX[o + W] * iw10 + DX[o + W + 1] * iw11;
-        const int gy = DY[o] * iw00 + DY[o + 1] * iw01 + DY[o + W] * iw10 + DY[o + W + 1] * iw11;
-        iv[q] = descale32(v, 9);
-        ixv[q] = descale32(gx, 14);
-        iyv[q] = descale32(gy, 14);
-        a11l += ixv[q] * ixv[q];
-        a12l += ixv[q] * iyv[q];
-        a22l += iyv[q] * iyv[q];
-      }
+      const int v = i4[q][0] * iw00 + i4[q][1] * iw01 + i4[q][2] * iw10 + i4[q][3] * iw11;
+      const int gx = x4[q][0] * iw00 + x4[q][1] * iw01 + x4[q][2] * iw10 + x4[q][3] * iw11;
+      const int gy = y4[q][0] * iw00 + y4[q][1] * iw01 + y4[q][2] * iw10 + y4[q][3] * iw11;
+      iv[q] = wok[q] ? descale32(v, 9) : 0;
+      ixv[q] = wok[q] ? descale32(gx, 14) : 0;  // masked pixels contribute nothing below
+      iyv[q] = wok[q] ? descale32(gy, 14) : 0;
+      a11l += ixv[q] * ixv[q];
+      a12l += ixv[q] * iyv[q];
+      a22l += iyv[q] * iyv[q];
     }
-    const long A11 = wave_sum64(a11l), A12 = wave_sum64(a12l), A22 = wave_sum64(a22l);
-    const double a11 = (double)A11 * FLT_SCALE, a12 = (double)A12 * FLT_SCALE, a22 = (double)A22 * FLT_SCALE;
+    const double a11 = wave_sum_exact(a11l) * FLT_SCALE, a12 = wave_sum_exact(a12l) * FLT_SCALE,
+                 a22 = wave_sum_exact(a22l) * FLT_SCALE;
     const double D = a11 * a22 - a12 * a12;
     const double minEig = (a22 + a11 - sqrt((a11 - a22) * (a11 - a22) + 4.0 * a12 * a12)) / (2.0 * win * win);
     if (minEig < min_eig || D < 1.1920928955078125e-07) {
@@ -160,6 +231,8 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     float nxw = nx - (float)half, nyw = ny - (float)half;
     float pdx = 0, pdy = 0;
     const uint8_t* J = P.J[L];
+    const bool staged = W >= kRegion && H >= kRegion && win + 1 <= kRegion;
+    int rx0 = -(1 << 30), ry0 = -(1 << 30);  // no region yet
     for (int j = 0; j < max_iters; ++j) {
       const int jx0 = (int)floorf(nxw), jy0 = (int)floorf(nyw);
       if (jx0 < 0 || jy0 < 0 || jx0 + win >= W || jy0 + win >= H) {
@@ -171,21 +244,42 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       const int jw01 = (int)rintf(c * (1.f - d) * 16384.f);
       const int jw10 = (int)rintf((1.f - c) * d * 16384.f);
       const int jw11 = 16384 - jw00 - jw01 - jw10;
+      int j4[kMaxWinPx][4];
+      if (staged) {
+        if (jx0 < rx0 || jy0 < ry0 || jx0 + win >= rx0 + kRegion || jy0 + win >= ry0 + kRegion) {
+          // centre the region on the window, clamped inside the level
+          rx0 = min(max(jx0 - (kRegion - win - 1) / 2, 0), W - kRegion);
+          ry0 = min(max(jy0 - (kRegion - win - 1) / 2, 0), H - kRegion);
+          stage_region(reg, J, SI, rx0, ry0, lane);
+        }
+        const uint8_t* R0 = reg + (jy0 - ry0) * kRegion + (jx0 - rx0);
+#pragma unroll
+        for (int q = 0; q < kMaxWinPx; ++q) {
+          const uint8_t* r = R0 + wy[q] * kRegion + wx[q];
+          j4[q][0] = r[0];
+          j4[q][1] = r[1];
+          j4[q][2] = r[kRegion];
+          j4[q][3] = r[kRegion + 1];
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < kMaxWinPx; ++q) {
+          const uint8_t* r = J + (long)(jy0 + wy[q]) * SI + jx0 + wx[q];
+          j4[q][0] = r[0];
+          j4[q][1] = r[1];
+          j4[q][2] = r[SI];
+          j4[q][3] = r[SI + 1];
+        }
+      }
       int b1l = 0, b2l = 0;
 #pragma unroll
       for (int q = 0; q < kMaxWinPx; ++q) {
-        const int k = lane + 64 * q;
-        if (k < npx) {
-          const int y = k / win, x = k - y * win;
-          const long o = (long)(jy0 + y) * SI + jx0 + x;
-          const int v = J[o] * jw00 + J[o + 1] * jw01 + J[o + SI] * jw10 + J[o + SI + 1] * jw11;
-          const int diff = descale32(v, 9) - iv[q];
-          b1l += diff * ixv[q];
-          b2l += diff * iyv[q];
-        }
+        const int v = j4[q][0] * jw00 + j4[q][1] * jw01 + j4[q][2] * jw10 + j4[q][3] * jw11;
+        const int diff = descale32(v, 9) - iv[q];
+        b1l += diff * ixv[q];  // ixv = iyv = 0 on masked pixels
+        b2l += diff * iyv[q];
       }
-      const long b1 = wave_sum64(b1l), b2 = wave_sum64(b2l);
-      const double b1d = (double)b1 * FLT_SCALE, b2d = (double)b2 * FLT_SCALE;
+      const double b1d = wave_sum_exact(b1l) * FLT_SCALE, b2d = wave_sum_exact(b2l) * FLT_SCALE;
       const float ddx = (float)((a12 * b2d - a22 * b1d) * Dinv);
       const float ddy = (float)((a12 * b1d - a11 * b2d) * Dinv);
       nxw += ddx;
