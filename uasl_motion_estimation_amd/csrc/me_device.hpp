@@ -170,8 +170,17 @@ struct GroupHist {
     }
     wave_sync();
     float MI = 0.0f;
-    if (gl == 0)
-      for (int t = 0; t < total; ++t) MI += terms[t];
+    if (gl == 0) {  // in-order float sum; the reads of a batch issue together
+      int t = 0;
+      for (; t + 8 <= total; t += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = terms[t + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) MI += v[u];
+      }
+      for (; t < total; ++t) MI += terms[t];
+    }
     return MI;
   }
 };
@@ -182,14 +191,30 @@ __device__ __forceinline__ float group_mi(GroupHist<16>& h, const uint8_t* A, lo
                                           long bstride, int pw, int ph, float invN) {
   h.clear();
   const int npx = pw * ph;
-  for (int p = h.gl; p < npx; p += 16) {
-    const int y = p / pw, x = p - y * pw;
-    int va = A[y * astride + x], vb = B[y * bstride + x];
-    if (BIN) {
-      va = va ? 255 : 0;
-      vb = vb ? 255 : 0;
+  // Pixels in batches of 8 per lane: every load of a batch is issued before
+  // the first histogram update (pixels past the patch alias pixel 0 and are
+  // skipped), one memory round trip per batch instead of one per pixel.
+  constexpr int kB = 8;
+  for (int p0 = h.gl; p0 < npx; p0 += 16 * kB) {
+    int va[kB], vb[kB];
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      const int p = p0 + 16 * u < npx ? p0 + 16 * u : 0;
+      const int y = p / pw, x = p - y * pw;
+      va[u] = A[y * astride + x];
+      vb[u] = B[y * bstride + x];
     }
-    h.add(va, vb);
+#pragma unroll
+    for (int u = 0; u < kB; ++u) {
+      if (p0 + 16 * u < npx) {
+        int a = va[u], b = vb[u];
+        if (BIN) {
+          a = a ? 255 : 0;
+          b = b ? 255 : 0;
+        }
+        h.add(a, b);
+      }
+    }
   }
   return h.mi(invN);
 }

@@ -399,17 +399,36 @@ __device__ __forceinline__ void block_reduce2(const double* __restrict__ x, cons
                                               int square, double* ox, double* oy) {
   static_assert(kRedBlock % B == 0, "block size must divide 1024");
   __shared__ double sx[kRedBlock], sy[kRedBlock];
+  constexpr int K = kRedBlock / B;
+  double ax[K], ay[K];
 #pragma unroll
-  for (int k = 0; k < kRedBlock / B; ++k) {
-    const int v = threadIdx.x + B * k;
-    double ax = 0, ay = 0;
-    for (int i = v; i < n; i += kRedBlock) {
-      double w = x[i];
-      ax += square ? w * w : w;
-      if (y) ay += y[i];
-    }
-    sx[v] = ax;
-    sy[v] = ay;
+  for (int k = 0; k < K; ++k) ax[k] = ay[k] = 0.0;
+  // chunks of 4 strides: the 4K loads of a chunk issue together, then each
+  // virtual thread accumulates its entries in increasing i (the fixed order)
+  for (int c0 = 0; c0 < n; c0 += 4 * kRedBlock) {
+    double wx[K][4], wy[K][4];
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = c0 + threadIdx.x + B * k + kRedBlock * u;
+        wx[k][u] = i < n ? x[i] : 0.0;
+        wy[k][u] = (y && i < n) ? y[i] : 0.0;
+      }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (c0 + threadIdx.x + B * k + kRedBlock * u < n) {
+          ax[k] += square ? wx[k][u] * wx[k][u] : wx[k][u];
+          ay[k] += wy[k][u];
+        }
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    sx[threadIdx.x + B * k] = ax[k];
+    sy[threadIdx.x + B * k] = ay[k];
   }
   __syncthreads();
   for (int s = kRedBlock / 2; s > 0; s >>= 1) {
