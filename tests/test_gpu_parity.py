@@ -396,3 +396,18 @@ def test_ba_duplicate_observations(ctx, oracle):
     assert s["successful_steps"] == rs["successful_steps"]
     np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+def test_ba_config5_window_50(ctx, oracle):
+    """Config 5's 50-keyframe window: 48 variable cameras, a 289-column camera
+    system (19 tiles, the widest Schur instance, S in global memory)."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    bp = S.ba_problem(73, 150, 50, 1280, 720)
+    assert len(bp.cams) - bp.fixed_frames == 48
+    cams, pts, s = ba_solve(bp, SolverOptions.fixed_iterations(3), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=3, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert s["iterations"] == rs["iterations"] and s["successful_steps"] == rs["successful_steps"]
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)

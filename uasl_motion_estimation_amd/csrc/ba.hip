@@ -839,43 +839,53 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
   return r;
 }
 constexpr int kXchDoubles = 192;  // per buffer: pivot rows A (64) | pivot rows Y (64) | column group (64)
-template <int R>
-__device__ __forceinline__ void chol4w_round(double& a, double& y, bool act, int w, int i, int c, int lane,
-                                             int nreal, bool& ok, double* Ablk, int ld, double* X, double* xch) {
+// PB = pivots per round (PB x PB pivot block, factored and inverted
+// redundantly by every lane); round R eliminates columns PB R .. PB R + PB - 1.
+// The per-round cost is a fixed ~690 cycles (barrier + LDS exchange + read
+// latency) plus the uniform PB x PB work, which every lane issues.  Measured
+// on config 3 (7 diagonal blocks): PB = 4 -> 45.4k cycles of diagonal work per
+// solve, PB = 2 (8 rounds per block) -> 56.1k; PB = 4 stays.
+#ifndef ME_CHOL_PB
+#define ME_CHOL_PB 4
+#endif
+template <int PB, int R>
+__device__ __forceinline__ void cholw_round(double& a, double& y, bool act, int i, int c, int nreal, bool& ok,
+                                            double* Ablk, int ld, double* X, double* xch) {
   double* xb = xch + kXchDoubles * (R & 1);
+  constexpr int p0 = PB * R;
   if (act) {
-    if (w == R) {
-      xb[lane] = a;       // A[4R+u][c], u = lane >> 4
-      xb[64 + lane] = y;  // Y[4R+u][c]
+    if (i >= p0 && i < p0 + PB) {
+      xb[16 * (i - p0) + c] = a;       // A[p0+u][c]
+      xb[64 + 16 * (i - p0) + c] = y;  // Y[p0+u][c]
     }
-    if ((c >> 2) == R) xb[128 + 4 * i + (c & 3)] = a;  // A[i][4R+u]
+    if (c >= p0 && c < p0 + PB) xb[128 + PB * i + (c - p0)] = a;  // A[i][p0+u]
   }
   __syncthreads();
   if (!act) return;
-  // uniform 4x4 Cholesky of the pivot block and its inverse M = L44^-1
-  double Lq[4][4], rinv[4];
+  // uniform PB x PB Cholesky of the pivot block and its inverse M = L^-1
+  double Lq[PB][PB], rinv[PB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    double piv = xb[16 * t + 4 * R + t];
+  for (int t = 0; t < PB; ++t) {
+    double piv = xb[16 * t + p0 + t];
 #pragma unroll
     for (int u = 0; u < t; ++u) piv = fma(-Lq[t][u], Lq[t][u], piv);
-    const bool pad = 4 * R + t >= nreal;  // padding / right-hand-side row: never a failure
+    const bool pad = p0 + t >= nreal;  // padding / right-hand-side row: never a failure
     ok = ok && (pad || piv > 0);
     piv = (pad && !(piv > 0)) ? 1.0 : piv;
     const double r = rsqrt_nr(piv);
     rinv[t] = r;
     Lq[t][t] = piv * r;
 #pragma unroll
-    for (int v = t + 1; v < 4; ++v) {
-      double x = xb[16 * v + 4 * R + t];
+    for (int v = t + 1; v < PB; ++v) {
+      double x = xb[16 * v + p0 + t];
 #pragma unroll
       for (int u = 0; u < t; ++u) x = fma(-Lq[v][u], Lq[t][u], x);
       Lq[v][t] = x * r;
     }
   }
-  double M[4][4];
+  double M[PB][PB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < PB; ++t) {
     M[t][t] = rinv[t];
 #pragma unroll
     for (int u = t - 1; u >= 0; --u) {
@@ -885,16 +895,16 @@ __device__ __forceinline__ void chol4w_round(double& a, double& y, bool act, int
       M[t][u] = -x * rinv[t];
     }
   }
-  double ar[4], xa[4], xy[4];
+  double ar[PB], xa[PB], xy[PB];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    ar[u] = xb[128 + 4 * i + u];   // A[i][4R+u]
-    xa[u] = xb[16 * u + c];        // A[4R+u][c] = A[c][4R+u]
-    xy[u] = xb[64 + 16 * u + c];   // Y[4R+u][c]
+  for (int u = 0; u < PB; ++u) {
+    ar[u] = xb[128 + PB * i + u];  // A[i][p0+u]
+    xa[u] = xb[16 * u + c];        // A[p0+u][c] = A[c][p0+u]
+    xy[u] = xb[64 + 16 * u + c];   // Y[p0+u][c]
   }
-  double Lr[4], Lc[4], Xg[4];
+  double Lr[PB], Lc[PB], Xg[PB];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
+  for (int t = 0; t < PB; ++t) {
     double sr = 0.0, sc = 0.0, sx = 0.0;
 #pragma unroll
     for (int u = 0; u <= t; ++u) {
@@ -902,35 +912,46 @@ __device__ __forceinline__ void chol4w_round(double& a, double& y, bool act, int
       sc = fma(xa[u], M[t][u], sc);
       sx = fma(M[t][u], xy[u], sx);
     }
-    Lr[t] = sr;  // L[i][4R+t]
-    Lc[t] = sc;  // L[c][4R+t]
-    Xg[t] = sx;  // X[4R+t][c]
+    Lr[t] = sr;  // L[i][p0+t]
+    Lc[t] = sc;  // L[c][p0+t]
+    Xg[t] = sx;  // X[p0+t][c]
   }
-  if ((c >> 2) == R && c <= i) {
+  if (c >= p0 && c < p0 + PB && c <= i) {
     double v = Lr[0];
 #pragma unroll
-    for (int t = 1; t < 4; ++t)
-      if ((c & 3) == t) v = Lr[t];
-    if (c == i) v = Lq[c & 3][c & 3];
+    for (int t = 1; t < PB; ++t)
+      if (c - p0 == t) v = Lr[t];
+    if (c == i) {
+#pragma unroll
+      for (int t = 0; t < PB; ++t)
+        if (c - p0 == t) v = Lq[t][t];
+    }
     Ablk[i * ld + c] = v;
   }
-  if (w == R) {
+  if (i >= p0 && i < p0 + PB) {
     double v = Xg[0];
 #pragma unroll
-    for (int t = 1; t < 4; ++t)
-      if ((i & 3) == t) v = Xg[t];
+    for (int t = 1; t < PB; ++t)
+      if (i - p0 == t) v = Xg[t];
     X[i * 16 + c] = v;
   }
-  if (w > R) {
+  if (i >= p0 + PB) {
     double av = a, yv = y;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
+    for (int t = 0; t < PB; ++t) {
       av = fma(-Lr[t], Lc[t], av);
       yv = fma(-Lr[t], Xg[t], yv);
     }
     a = av;
     y = yv;
   }
+}
+
+template <int PB, int R>
+__device__ __forceinline__ void chol_rounds(double& a, double& y, bool act, int i, int c, int nreal, bool& ok,
+                                            double* Ablk, int ld, double* X, double* xch) {
+  cholw_round<PB, R>(a, y, act, i, c, nreal, ok, Ablk, ld, X, xch);
+  if constexpr (R + 1 < 16 / PB) chol_rounds<PB, R + 1>(a, y, act, i, c, nreal, ok, Ablk, ld, X, xch);
 }
 
 template <bool kLds>
@@ -1002,10 +1023,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       bool ok = true;
       double* XJw = X + 256 * J;
-      chol4w_round<0>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4w_round<1>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4w_round<2>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
-      chol4w_round<3>(a, y, act, wave, i, c, lane, n - j0, ok, Ablk, ld, XJw, xch);
+      chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Ablk, ld, XJw, xch);
       if (act && !ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
