@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--lib", default=None, help="development A/B only: load this libme_hip.so build")
     ap.add_argument("--vo-matches", type=int, default=2000,
                     help="matches of the StereoVisualOdometry::process line (SURVEY 8f rank 1; 0: off)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="run each frame's KLT, scale LM and BA back to back on one stream (no KLT/back-end overlap)")
     ap.add_argument("--streams", type=int, default=1,
                     help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
                          "thread each), reported as multi_stream; the headline value stays one stream per GPU")
@@ -129,19 +131,89 @@ class _Calls:
         self.ba = (ctx.h, ctypes.byref(self.bp), ctypes.byref(self.bo), ctypes.byref(self.bs))
 
 
+def _calls(ctx, fd, kp, ba_opts):
+    """The frame's argument blocks for this context (built once per context)."""
+    m = fd.__dict__.setdefault("_calls", {})
+    c = m.get(id(ctx))
+    if c is None:
+        c = m[id(ctx)] = _Calls(ctx, fd, kp, ba_opts)
+    return c
+
+
 def gpu_step(ctx, fd, kp, ba_opts, stats):
-    c = getattr(fd, "_calls", None)
-    if c is None or c.klt[0] is not ctx.h:
-        c = fd._calls = _Calls(ctx, fd, kp, ba_opts)
+    """One frame, sequential on the ctx stream: KLT, scale LM, BA."""
+    c = _calls(ctx, fd, kp, ba_opts)
+    ctx.check(ctx.lib.me_klt_track(*c.klt), "klt")
+    back_end(ctx, fd, kp, ba_opts, stats)
+
+
+def back_end(ctx, fd, kp, ba_opts, stats, between=None):
+    """Scale LM + BA of one frame on the ctx stream (blocking, as the
+    reference's optimise()); `between` runs on the host between the two."""
+    c = _calls(ctx, fd, kp, ba_opts)
     lib = ctx.lib
-    ctx.check(lib.me_klt_track(*c.klt), "klt")
     c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
     ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
     stats["scale_iters"] += c.it.value
+    if between is not None:
+        between()
     fd.dba.reset()  # same starting point every time the frame is replayed (device copy)
     ctx.check(lib.me_ba_solve(*c.ba), "me_ba_solve")
     stats["ba_iters"] += c.bs.iterations
     stats["frames"] += 1
+
+
+class _Hip:
+    """HIP events through the runtime (plumbing for the two-stream frame pipeline)."""
+
+    def __init__(self):
+        self.rt = ctypes.CDLL("libamdhip64.so")
+        self.rt.hipEventCreateWithFlags.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint]
+        self.rt.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        self.rt.hipStreamWaitEvent.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint]
+        self.rt.hipEventDestroy.argtypes = [ctypes.c_void_p]
+
+    def event(self):
+        e = ctypes.c_void_p()
+        assert self.rt.hipEventCreateWithFlags(ctypes.byref(e), 2) == 0  # hipEventDisableTiming
+        return e
+
+    def record(self, e, stream):
+        assert self.rt.hipEventRecord(e, stream) == 0
+
+    def wait(self, stream, e):
+        assert self.rt.hipStreamWaitEvent(stream, e, 0) == 0
+
+
+class FramePipeline:
+    """Two-stage frame pipeline on one GPU: the tracker context (its own HIP
+    stream) runs KLT of frame t+1 while the back-end context runs the BA of
+    frame t (issued after frame t's scale LM, whose kernels need the CUs).  Frame t's back end waits (stream-side) on an event
+    recorded after KLT of frame t, so every dependency a VO front end has on
+    its tracks is kept; per frame the work is exactly the sequential
+    gpu_step's (one KLT, one scale LM, one BA)."""
+
+    def __init__(self, ctx, tctx, hip):
+        self.ctx, self.tctx, self.hip = ctx, tctx, hip
+        self.ev = [hip.event(), hip.event()]
+        self.s_main = ctypes.c_void_p(ctx.lib.me_get_stream(ctx.h))
+        self.s_trk = ctypes.c_void_p(tctx.lib.me_get_stream(tctx.h))
+
+    def _klt(self, fd, kp, ba_opts, k):
+        c = _calls(self.tctx, fd, kp, ba_opts)
+        self.tctx.check(self.tctx.lib.me_klt_track(*c.klt), "klt")
+        self.hip.record(self.ev[k & 1], self.s_trk)
+
+    def run(self, frames, n, kp, ba_opts, stats, first=0):
+        if n <= 0:
+            return
+        self._klt(frames[first % len(frames)], kp, ba_opts, 0)
+        for t in range(n):
+            self.hip.wait(self.s_main, self.ev[t & 1])
+            nxt = None
+            if t + 1 < n:  # issued once the scale LM is done: it overlaps the BA's latency-bound kernels
+                nxt = lambda t=t: self._klt(frames[(first + t + 1) % len(frames)], kp, ba_opts, t + 1)  # noqa: E731
+            back_end(self.ctx, frames[(first + t) % len(frames)], kp, ba_opts, stats, between=nxt)
 
 
 def cpu_step(fd, ba_iters, stats):
@@ -368,6 +440,13 @@ def main():
     for i in range(args.warmup):
         gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
     ctx.synchronize()
+    pipe = tctx = None
+    if not args.no_pipeline:
+        tctx = Context(local_rank)  # tracker context: its own HIP stream and scratch
+        pipe = FramePipeline(ctx, tctx, _Hip())
+        pipe.run(frames, max(args.warmup, 2), kp, ba_opts, dict(frames=0, ba_iters=0, scale_iters=0))
+        tctx.synchronize()
+        ctx.synchronize()
     # untimed profile steps with every family timed: per-family device time and
     # the dominant family (by device time) among those with a roofline
     ctx.timing_reset()
@@ -388,8 +467,12 @@ def main():
     torch.cuda.synchronize()
     ctx.synchronize()
     t_start = time.perf_counter()
-    for i in range(args.steps):
-        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+    if pipe is None:
+        for i in range(args.steps):
+            gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+    else:
+        pipe.run(frames, args.steps, kp, ba_opts, stats)
+        tctx.synchronize()
     ctx.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
@@ -449,7 +532,9 @@ def main():
             "config": {"workload": f"config {args.config}: {cfg['width']}x{cfg['height']} stereo, "
                                    f"{cfg['n_feats']} feats, {cfg['window']}-keyframe window, 11x11 MI patches",
                        "frame": f"KLT + MI scale LM + {args.ba_iters} BA LM iterations",
-                       "parallelism": f"{world} independent streams (one per GPU)"},
+                       "parallelism": f"{world} independent streams (one per GPU)",
+                       "pipeline": None if pipe is None else "KLT of frame t+1 overlaps the BA of frame t "
+                                                             "(two HIP streams, event dependency per frame)"},
             "ba_iter_per_s": round(ba_total / t_max, 2),
             "roofline": roofline,
             "mi_roofline": mi_rl,
