@@ -147,16 +147,13 @@ def gpu_step(ctx, fd, kp, ba_opts, stats):
     back_end(ctx, fd, kp, ba_opts, stats)
 
 
-def back_end(ctx, fd, kp, ba_opts, stats, between=None):
-    """Scale LM + BA of one frame on the ctx stream (blocking, as the
-    reference's optimise()); `between` runs on the host between the two."""
+def back_end(ctx, fd, kp, ba_opts, stats):
+    """Scale LM + BA of one frame on the ctx stream (blocking, as the reference's optimise())."""
     c = _calls(ctx, fd, kp, ba_opts)
     lib = ctx.lib
     c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
     ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
     stats["scale_iters"] += c.it.value
-    if between is not None:
-        between()
     fd.dba.reset()  # same starting point every time the frame is replayed (device copy)
     ctx.check(lib.me_ba_solve(*c.ba), "me_ba_solve")
     stats["ba_iters"] += c.bs.iterations
@@ -188,7 +185,10 @@ class _Hip:
 class FramePipeline:
     """Two-stage frame pipeline on one GPU: the tracker context (its own HIP
     stream) runs KLT of frame t+1 while the back-end context runs the BA of
-    frame t (issued after frame t's scale LM, whose kernels need the CUs).  Frame t's back end waits (stream-side) on an event
+    frame t (issued after frame t's scale LM, whose kernels need the CUs).
+    The BA is queued whole (me_ba_solve_async) and its summary collected
+    (me_ba_wait) after the next frame's scale LM is queued behind it, so the
+    host's per-frame work never leaves the back-end stream idle.  Frame t's back end waits (stream-side) on an event
     recorded after KLT of frame t, so every dependency a VO front end has on
     its tracks is kept; per frame the work is exactly the sequential
     gpu_step's (one KLT, one scale LM, one BA)."""
@@ -207,13 +207,29 @@ class FramePipeline:
     def run(self, frames, n, kp, ba_opts, stats, first=0):
         if n <= 0:
             return
+        ctx, lib = self.ctx, self.ctx.lib
         self._klt(frames[first % len(frames)], kp, ba_opts, 0)
+        pend = None
         for t in range(n):
-            self.hip.wait(self.s_main, self.ev[t & 1])
-            nxt = None
+            fd = frames[(first + t) % len(frames)]
+            c = _calls(ctx, fd, kp, ba_opts)
+            self.hip.wait(self.s_main, self.ev[t & 1])  # frame t's back end after its tracks
+            c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
+            ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
+            stats["scale_iters"] += c.it.value
             if t + 1 < n:  # issued once the scale LM is done: it overlaps the BA's latency-bound kernels
-                nxt = lambda t=t: self._klt(frames[(first + t + 1) % len(frames)], kp, ba_opts, t + 1)  # noqa: E731
-            back_end(self.ctx, frames[(first + t) % len(frames)], kp, ba_opts, stats, between=nxt)
+                self._klt(frames[(first + t + 1) % len(frames)], kp, ba_opts, t + 1)
+            if pend is not None:  # frame t-1's BA finished before this scale LM ran (same stream)
+                self._ba_wait(pend, stats)
+            fd.dba.reset()
+            ctx.check(lib.me_ba_solve_async(ctx.h, ctypes.byref(c.bp), ctypes.byref(c.bo)), "me_ba_solve_async")
+            pend = c
+        self._ba_wait(pend, stats)
+
+    def _ba_wait(self, c, stats):
+        self.ctx.check(self.ctx.lib.me_ba_wait(self.ctx.h, ctypes.byref(c.bs)), "me_ba_wait")
+        stats["ba_iters"] += c.bs.iterations
+        stats["frames"] += 1
 
 
 def cpu_step(fd, ba_iters, stats):

@@ -207,6 +207,16 @@ typedef struct {
 
 void me_ba_default_options(me_ba_options* o);
 int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_summary* s);
+/* Asynchronous form of me_ba_solve (same BundleAdjuster<M>::optimise,
+   BundleAdjuster.h:378-476, same results bit for bit): queues every
+   possible iteration (max_num_iterations + 1 linearisations; launches after
+   convergence return at once, so it suits fixed-iteration windows) and the
+   read-back on the ctx stream, and returns without waiting.  The caller keeps
+   *p's arrays alive until me_ba_wait, which blocks on this solve only (not on
+   work queued after it), writes host-problem results back and fills *s.  One
+   solve in flight per ctx: any other BA call on the ctx completes it first. */
+int me_ba_solve_async(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o);
+int me_ba_wait(me_ctx* ctx, me_ba_summary* s);
 /* Cost (Ceres ½Σρ) at the problem's current parameters. */
 int me_ba_cost(me_ctx* ctx, const me_ba_problem* p, double* cost);
 /* Residuals (sigma-scaled, uncorrected) and Jacobian blocks per observation:

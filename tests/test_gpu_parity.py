@@ -411,3 +411,54 @@ def test_ba_config5_window_50(ctx, oracle):
     assert s["iterations"] == rs["iterations"] and s["successful_steps"] == rs["successful_steps"]
     np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+# ------------------------------------------------------------------ asynchronous BA solve
+def test_ba_solve_async_matches_sync_device_and_host(ctx, scale_prob):
+    """me_ba_solve_async + me_ba_wait == me_ba_solve bit for bit, with other
+    work (a scale LM) queued on the ctx between the two calls."""
+    import ctypes
+
+    from uasl_motion_estimation_amd._lib import BASummaryC
+    from uasl_motion_estimation_amd.optimisation import (DeviceBAProblem, SolverOptions, ba_solve, ba_struct,
+                                                         scale_optimise)
+
+    bp = S.ba_problem(41, 300, 10, 640, 480)
+    opts = SolverOptions.fixed_iterations(6)
+    hc, hp, hs = ba_solve(bp.copy(), opts, ctx=ctx)
+    d = DeviceBAProblem(bp, ctx)
+    d.solve_async(opts)
+    sc = scale_optimise(scale_prob, ctx=ctx)  # uses the ctx's own pinned staging meanwhile
+    ds = d.wait()
+    dc, dp = d.download()
+    assert ds == hs and np.array_equal(dc, hc) and np.array_equal(dp, hp)
+    assert sc["scale"] == scale_optimise(scale_prob, ctx=ctx)["scale"]
+    # host-memory problem: results land in the caller's arrays at me_ba_wait
+    keep = []
+    p, cams, pts = ba_struct(bp.copy(), keep)
+    o = opts.to_c()
+    ctx.check(ctx.lib.me_ba_solve_async(ctx.h, ctypes.byref(p), ctypes.byref(o)), "async")
+    s = BASummaryC()
+    ctx.check(ctx.lib.me_ba_wait(ctx.h, ctypes.byref(s)), "wait")
+    assert s.iterations == hs["iterations"] and np.array_equal(cams, hc) and np.array_equal(pts, hp)
+    d.close()
+
+
+def test_ba_async_drained_by_next_call_and_wait_errors(ctx):
+    """A second BA call completes the pending solve; me_ba_wait without a
+    pending solve is ME_ERR_STATE."""
+    from uasl_motion_estimation_amd._lib import MEError
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions, ba_cost
+
+    bp = S.ba_problem(42, 200, 8, 640, 480)
+    opts = SolverOptions.fixed_iterations(4)
+    d = DeviceBAProblem(bp, ctx)
+    ref = d.solve(opts)
+    ref_c = d.download()[0]
+    d.reset()
+    d.solve_async(opts)
+    ba_cost(bp, ctx=ctx)  # another BA entry point: completes the pending solve first
+    assert d.wait() == ref and np.array_equal(d.download()[0], ref_c)
+    with pytest.raises(MEError):
+        d.wait()
+    d.close()

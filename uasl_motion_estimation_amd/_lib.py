@@ -122,7 +122,7 @@ EXPORTS = [
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
-    "me_ba_solve_sharded", "me_ba_covariance",
+    "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait",
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
@@ -187,6 +187,8 @@ def load_library(path: str = LIB_PATH):
         "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
         "me_ba_default_options": (None, [P(BAOptionsC)]),
         "me_ba_solve": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), P(BASummaryC)]),
+        "me_ba_solve_async": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC)]),
+        "me_ba_wait": (c_int, [c_void_p, P(BASummaryC)]),
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
         "me_ba_evaluate": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_double), P(c_double)]),
         "me_ba_reduced_system": (c_int, [c_void_p, P(BAProblemC), c_double, P(c_double), P(c_double)]),

@@ -145,6 +145,8 @@ void me_destroy(me_ctx* c) {
     if (p) hipFree(p);
   for (float* t : c->mi_table)
     if (t) hipFree(t);
+  if (c->ba_async_free) c->ba_async_free(c);
+  if (c->ba_pinned) hipHostFree(c->ba_pinned);
   if (c->pinned) hipHostFree(c->pinned);
   for (auto e : c->event_pool) hipEventDestroy(e);
   for (auto e : c->poll_ev)

@@ -789,7 +789,10 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
 //  * trailing update A_IK -= L_IJ L_KJ^T on the matrix cores.
 // Then the backward solve L^T y = z in wave 0 with the block inverses.
 // The matrix is padded to N = 16 Ts >= n + 1 with an identity block.
-constexpr int kSolveBlock = 512;
+#ifndef ME_SOLVE_BLOCK
+#define ME_SOLVE_BLOCK 512
+#endif
+constexpr int kSolveBlock = ME_SOLVE_BLOCK;
 constexpr int kLoadBatch = 32;
 #define SOLVE_STAMP(i)                                                                      \
   do {                                                                                      \
@@ -1692,7 +1695,11 @@ struct Plan {
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
 int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 
-int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base) {
+int ba_drain(me_ctx* c);
+
+int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base,
+               bool async = false) {
+  ME_TRY(ba_drain(c));  // a pending asynchronous solve owns the BA scratch until it completes
   ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
   ME_CHECK(c, p->n_cams <= kMaxScanCams, "BA: at most %d cameras per window", kMaxScanCams);
   ME_CHECK(c, p->obs_dim == 0 || p->obs_dim == 2 || p->obs_dim == 4, "BA: obs_dim must be 2 or 4 (Observation<M>)");
@@ -1828,7 +1835,19 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   b.diagU = b.bvec + g.n6;
   void* hp;
   const size_t stage = rup((long)std::max(8 * out_doubles, dev ? (size_t)0 : input_span), 64);
-  ME_TRY(me_pinned(c, stage + 2 * rup(sizeof(State), 64), &hp));
+  const size_t hbytes = stage + 2 * rup(sizeof(State), 64);
+  if (async) {  // staging owned by the asynchronous solve (grown only while none is pending)
+    if (c->ba_pinned_size < hbytes) {
+      if (c->ba_pinned) ME_HIP(c, hipHostFree(c->ba_pinned));
+      c->ba_pinned = nullptr;
+      c->ba_pinned_size = 0;
+      ME_HIP(c, hipHostMalloc(&c->ba_pinned, std::max(hbytes, (size_t)4096), hipHostMallocDefault));
+      c->ba_pinned_size = std::max(hbytes, (size_t)4096);
+    }
+    hp = c->ba_pinned;
+  } else {
+    ME_TRY(me_pinned(c, hbytes, &hp));
+  }
   P.host = (double*)hp;
   P.hstate[0] = (State*)((char*)hp + stage);
   P.hstate[1] = (State*)((char*)hp + stage + rup(sizeof(State), 64));
@@ -2015,13 +2034,14 @@ int enqueue_output(Plan& P, me_ba_problem* p) {
   return ME_OK;
 }
 
-int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = false) {
+int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = false, hipEvent_t done = nullptr) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   constexpr size_t nst = sizeof(State) / 8;
   static_assert(sizeof(State) % 8 == 0, "State is read back as doubles");
   if (!output_queued) ME_TRY(enqueue_output(P, p));
-  ME_HIP(c, hipStreamSynchronize(c->stream));
+  if (done) ME_HIP(c, hipEventSynchronize(done));  // asynchronous solve: not the work queued after it
+  else ME_HIP(c, hipStreamSynchronize(c->stream));
   State st;
   std::memcpy(&st, P.host, sizeof(State));
   std::memcpy(P.c->dbg, st.stamps, sizeof(st.stamps));
@@ -2087,7 +2107,81 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
   return finish(P, p, sum, out_q);
 }
 
+// Asynchronous solve: every possible iteration is queued at once (launches
+// after convergence test State::done and return), then the output kernel and
+// read-back behind an event.  The host is free as soon as it is queued.
+struct AsyncSolve {
+  Plan P;
+  me_ba_problem prob;  // copy: cams / pts are written back at completion
+  hipEvent_t ev = nullptr;
+  bool completed = false;
+  int rc = ME_OK;
+  me_ba_summary sum{};
+};
+
+void ba_async_free(me_ctx* c) {
+  auto* A = (AsyncSolve*)c->ba_async;
+  if (!A) return;
+  if (!A->completed) hipEventSynchronize(A->ev);
+  hipEventDestroy(A->ev);
+  delete A;
+  c->ba_async = nullptr;
+  c->ba_async_free = nullptr;
+}
+
+int ba_complete(me_ctx* c) {
+  auto* A = (AsyncSolve*)c->ba_async;
+  if (!A || A->completed) return ME_OK;
+  A->rc = finish(A->P, &A->prob, &A->sum, true, A->ev);
+  A->completed = true;
+  return ME_OK;
+}
+
+// Any other BA call on the ctx first completes the pending solve (its
+// summary stays readable by me_ba_wait until the next asynchronous solve).
+int ba_drain(me_ctx* c) { return ba_complete(c); }
+
 }  // namespace
+
+extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
+  if (!c || !p || !opt) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  ME_TRY(ba_drain(c));
+  ba_async_free(c);
+  auto* A = new AsyncSolve;
+  A->prob = *p;
+  int rc = plan_build(c, p, opt, A->P, 0, true);
+  if (rc == ME_OK) {
+    for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it) rc = enqueue_iteration(A->P, nullptr, nullptr);
+  }
+  if (rc == ME_OK) rc = enqueue_output(A->P, &A->prob);
+  if (rc == ME_OK && hipEventCreateWithFlags(&A->ev, hipEventDisableTiming) != hipSuccess)
+    rc = me_set_error(c, ME_ERR_HIP, "me_ba_solve_async: event creation failed");
+  if (rc == ME_OK && hipEventRecord(A->ev, c->stream) != hipSuccess) {
+    hipEventDestroy(A->ev);
+    rc = me_set_error(c, ME_ERR_HIP, "me_ba_solve_async: event record failed");
+  }
+  if (rc != ME_OK) {
+    hipStreamSynchronize(c->stream);  // nothing queued may outlive the plan
+    delete A;
+    return rc;
+  }
+  c->ba_async = A;
+  c->ba_async_free = ba_async_free;
+  return ME_OK;
+}
+
+extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) {
+  if (!c) return ME_ERR_INVALID;
+  auto* A = (AsyncSolve*)c->ba_async;
+  if (!A) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");
+  ME_HIP(c, hipSetDevice(c->device));
+  ME_TRY(ba_complete(c));
+  const int rc = A->rc;
+  if (s && rc == ME_OK) *s = A->sum;
+  ba_async_free(c);
+  return rc;
+}
 
 extern "C" void me_ba_default_options(me_ba_options* o) {
   o->max_num_iterations = 50;

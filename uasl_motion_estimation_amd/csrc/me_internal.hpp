@@ -37,6 +37,12 @@ struct me_ctx {
   int rand_f = 3, rand_r = 0;
   bool rand_init = false;
   long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
+  // asynchronous BA solve in flight (me_ba_solve_async / me_ba_wait, ba.hip):
+  // its own pinned staging, so later calls on the ctx cannot overwrite it
+  void* ba_async = nullptr;
+  void (*ba_async_free)(me_ctx*) = nullptr;
+  void* ba_pinned = nullptr;
+  size_t ba_pinned_size = 0;
   // MI term tables, one per patch pixel count N (built on first use, mi.hip)
   float* mi_table[256] = {nullptr};
 };

@@ -441,6 +441,19 @@ class DeviceBAProblem:
         self.ctx.check(self.ctx.lib.me_ba_solve(self.ctx.h, byref(p), byref(o), byref(s)), "me_ba_solve")
         return _summary(s)
 
+    def solve_async(self, options: SolverOptions | None = None) -> None:
+        """Queue the whole solve on the ctx stream and return (me_ba_solve_async);
+        wait() blocks on it and returns the summary."""
+        self._async = (self.struct(), (options or SolverOptions()).to_c())
+        p, o = self._async
+        self.ctx.check(self.ctx.lib.me_ba_solve_async(self.ctx.h, byref(p), byref(o)), "me_ba_solve_async")
+
+    def wait(self) -> dict:
+        s = BASummaryC()
+        self.ctx.check(self.ctx.lib.me_ba_wait(self.ctx.h, byref(s)), "me_ba_wait")
+        self._async = None
+        return _summary(s)
+
     def download(self):
         cams = np.zeros((self.n_cams, 6))
         pts = np.zeros((self.n_pts, 3))
