@@ -158,15 +158,29 @@ struct GroupHist {
     }
     const int total = __shfl(pre, G - 1, G);
     int idx = pre - cnt;
+    // four set bits per pass: the four terms' independent chains (division,
+    // log2f table reads, polynomial) overlap instead of running back to back
     while (bits) {
-      const int b = __builtin_ctz(bits);
-      bits &= bits - 1u;
-      const int code = gl * 32 + b;
-      const int i = code / 20, j = code - i * 20;
-      const int cJ = (h[code >> 2] >> ((code & 3) * 8)) & 0xff;
-      const int cL = (h[100 + (i >> 2)] >> ((i & 3) * 8)) & 0xff;
-      const int cR = (h[105 + (j >> 2)] >> ((j & 3) * 8)) & 0xff;
-      terms[idx++] = mi_term(cJ, cL, cR, invN);
+      int code[4];
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        ok[u] = bits != 0u;
+        code[u] = ok[u] ? gl * 32 + __builtin_ctz(bits) : 0;
+        bits &= bits - 1u;
+      }
+      float tv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = code[u] / 20, j = code[u] - i * 20;
+        const int cJ = (h[code[u] >> 2] >> ((code[u] & 3) * 8)) & 0xff;
+        const int cL = (h[100 + (i >> 2)] >> ((i & 3) * 8)) & 0xff;
+        const int cR = (h[105 + (j >> 2)] >> ((j & 3) * 8)) & 0xff;
+        tv[u] = mi_term(cJ, cL > 0 ? cL : 1, cR > 0 ? cR : 1, invN);  // padded slots: any finite value
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (ok[u]) terms[idx++] = tv[u];
     }
     wave_sync();
     float MI = 0.0f;

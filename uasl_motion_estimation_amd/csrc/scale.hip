@@ -23,6 +23,9 @@ using namespace me_dev;
 namespace {
 
 constexpr int kScBlock = 256;
+#ifndef ME_SCALE_EXP
+#define ME_SCALE_EXP 0
+#endif
 
 struct ScaleArgs {
   double K1[9], K2[9], q1[4], t1[3], q2[4], t2[3];
@@ -267,10 +270,18 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
   float mi;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, lx, ly, P);
+#if ME_SCALE_EXP == 2  // timing experiment: projection only, no MI
+    mi = (float)lx;
+#else
     mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN);
+#endif
   } else {
     if (a.weighting) wv = sobel_weight(a.imgR, a.stride, a.cols, a.rows, rx, ry, P);
+#if ME_SCALE_EXP == 2
+    mi = (float)rx;
+#else
     mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN);
+#endif
   }
   if (h.gl == 0) res[row] = (double)mi * wv;
 }
@@ -431,13 +442,28 @@ __device__ __forceinline__ void block_reduce2(const double* __restrict__ x, cons
     sy[threadIdx.x + B * k] = ay[k];
   }
   __syncthreads();
-  for (int s = kRedBlock / 2; s > 0; s >>= 1) {
+  for (int s = kRedBlock / 2; s >= 64; s >>= 1) {
     for (int v = threadIdx.x; v < s; v += B) {
       sx[v] += sx[v + s];
       sy[v] += sy[v + s];
     }
     __syncthreads();
   }
+  // levels 32 .. 1 of the same tree inside wave 0 (x[v] += x[v + s], same
+  // adds in the same order), by shuffles instead of six block barriers
+  if (threadIdx.x < 64) {
+    double x = sx[threadIdx.x], z = sy[threadIdx.x];
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+      x += __shfl_down(x, s, 64);
+      z += __shfl_down(z, s, 64);
+    }
+    if (threadIdx.x == 0) {
+      sx[0] = x;
+      sy[0] = z;
+    }
+  }
+  __syncthreads();
   *ox = sx[0];
   *oy = sy[0];
   __syncthreads();  // sx / sy are reused by the next reduction of a persistent block
@@ -478,9 +504,25 @@ __device__ void lm_propose(ScaleLM* lm, const LMParams& p) {
 // One workgroup: reduce the evaluation of `phase`, then thread 0 runs the
 // reference's scalar control for that phase (optimisation.cpp:29-147,
 // run_GN_step :674-683, run_LM_step :685-730).
+__device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
+                                                  int phase, double sx, double sy, int err);
+
 template <int B>
-__device__ void scale_ctrl_body(ScaleLM* lm, const LMParams& p, int phase, const double* __restrict__ x,
+__device__ void scale_ctrl_body(ScaleLM* lm_g, const LMParams& p, int phase, const double* __restrict__ x,
                                 const double* __restrict__ y, const int* err) {
+  // Thread 0 requests the LM header and the error flag before the reduction,
+  // so their latency overlaps it; the control then runs on a register copy
+  // (no chain of dependent global round trips) and stores the header once.
+  constexpr int kHead = offsetof(ScaleLM, trace) / 8;
+  static_assert(offsetof(ScaleLM, trace) % 8 == 0, "LM header is copied as 8-byte words");
+  unsigned long long hw[kHead];
+  int err_v = 0;
+  if (threadIdx.x == 0) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lm_g);
+#pragma unroll
+    for (int i = 0; i < kHead; ++i) hw[i] = src[i];
+    err_v = *err;
+  }
   double sx = 0, sy = 0;
   if (phase == PH_B) {
     if (!p.test) block_reduce2<B>(x, y, p.n, 0, &sx, &sy);
@@ -488,8 +530,21 @@ __device__ void scale_ctrl_body(ScaleLM* lm, const LMParams& p, int phase, const
     block_reduce2<B>(x, nullptr, p.rows, 1, &sx, &sy);
   }
   if (threadIdx.x != 0) return;
-  if (*err) {  // ROI outside the image (the reference throws cv::Exception) / bad mask
-    lm->err = *err;
+  ScaleLM L;
+  __builtin_memcpy(&L, hw, sizeof(hw));
+  scale_ctrl_decide(&L, lm_g->trace, p, phase, sx, sy, err_v);
+  __builtin_memcpy(hw, &L, sizeof(hw));
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(lm_g);
+#pragma unroll
+  for (int i = 0; i < kHead; ++i) dst[i] = hw[i];
+}
+
+// The reference's scalar control for one phase, on the register copy *lm
+// (trace entries go straight to the device trace array).
+__device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
+                                                  int phase, double sx, double sy, int err) {
+  if (err) {  // ROI outside the image (the reference throws cv::Exception) / bad mask
+    lm->err = err;
     lm->phase = PH_DONE;
     return;
   }
@@ -555,8 +610,8 @@ __device__ void scale_ctrl_body(ScaleLM* lm, const LMParams& p, int phase, const
       lm->nevals += p.n;
       if (p.type == 0 && (e2 - lm->e1) * (e2 - lm->e1) < p.rel_tol) lm->stop = SMALL_DECREASE_FUNCTION;
       if (lm->ntrace < kTraceCap) {
-        lm->trace[2 * lm->ntrace] = lm->e1;
-        lm->trace[2 * lm->ntrace + 1] = lm->scale;
+        trace[2 * lm->ntrace] = lm->e1;
+        trace[2 * lm->ntrace + 1] = lm->scale;
       }
       lm->ntrace++;
       // while (!stop && k++ < max_nb_iter)
@@ -603,7 +658,9 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
   const int t = blockIdx.x * kTracksPerBlock + grp;
+#if ME_SCALE_EXP != 1  // timing experiments only (tools/exp): 1 = no track work
   if (t < a.nL + a.nR) residual_track(a, td, t, h, res, err);
+#endif
   if (!last_block_arrives(cnt)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   scale_ctrl_body<kScBlock>(lm, p, phase, res, nullptr, err);
