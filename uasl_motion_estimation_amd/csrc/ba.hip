@@ -24,7 +24,7 @@ constexpr double kDblEps = 2.220446049250313e-16;
 
 // ---------------------------------------------------------------- helpers
 template <int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* lds /* 4*NV */) {
+__device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* lds /* nw*NV */, int nw_active = 0) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     double x = v[i];
@@ -37,7 +37,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* 
     for (int i = 0; i < NV; ++i) lds[wave * NV + i] = v[i];
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int nw = (blockDim.x + 63) >> 6;
+    const int nw = nw_active ? nw_active : (blockDim.x + 63) >> 6;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       double s = 0;
@@ -337,19 +337,20 @@ __device__ void cam_reduce_body(const Geo& g, const Bufs& b, int sharded, const 
 // contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
 // k + ck, ... of 256 slots of camera c into a partial; the last of the ck
 // workgroups of camera c to finish adds the ck partials in order.
-__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart, int sharded,
-                                                              double* colnorm, double* gc_raw, double* Uraw) {
+// Threads 0 .. kBlock-1 of the block take part (in a wider block the other
+// waves have exited: barriers count only live waves).
+__device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, double* cpart, int sharded,
+                                                  double* colnorm, double* gc_raw, double* Uraw, int ci, int k) {
   __shared__ double lds[4 * 27];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
-  const int ci = blockIdx.x, k = blockIdx.y;
   const int beg = b.c_off[ci], end = b.c_off[ci + 1];
   double v[27];
   for (int i = 0; i < 27; ++i) v[i] = 0;
   for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock)
     for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
   double out[27];
-  block_sum<27>(v, out, lds);
+  block_sum<27>(v, out, lds, kBlock / 64);
   if (threadIdx.x == 0) {
     double* P = cpart + 27 * ((long)ci * g.ck + k);
     for (int u = 0; u < 27; ++u) P[u] = out[u];
@@ -357,6 +358,18 @@ __global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, dou
   if (!last_arrival(b.cnt + ci, g.ck)) return;
   cam_reduce_body(g, b, sharded, cpart, colnorm, gc_raw, Uraw, ci);
 }
+
+__global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart, int sharded,
+                                                              double* colnorm, double* gc_raw, double* Uraw) {
+  cam_assemble_body(g, b, cpart, sharded, colnorm, gc_raw, Uraw, blockIdx.x, blockIdx.y);
+}
+
+// Camera assembly riding in the Schur launch (iterations after the first,
+// when the Jacobi scaling is fixed and the two passes are independent).
+struct CamArgs {
+  double *cpart, *colnorm, *gc_raw, *Uraw;
+  int on;
+};
 
 // Sharded mode: scaling from the all-reduced column norms, then scale the
 // (local) U / g blocks.
@@ -444,10 +457,16 @@ __device__ __forceinline__ int group_max(int x) {
 }
 
 template <int NT, int BLK>
-__global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
+__global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, CamArgs ca) {
   constexpr int SL = BLK / kSchurPts, NW = BLK / 64;  // lanes per landmark, waves
   extern __shared__ double smem[];
   __shared__ double red[8];
+  if (ca.on && (int)blockIdx.x >= g.ksplit) {  // camera-assembly blocks of a fused launch
+    if (threadIdx.x >= kBlock) return;
+    const int q = blockIdx.x - g.ksplit;
+    cam_assemble_body(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
+    return;
+  }
   State* st = b.st;
   if (st->done) return;
   const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
@@ -479,7 +498,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o) {
 #pragma unroll
   for (int u = 0; u < NT; ++u) acc[u] = double4_t{0.0, 0.0, 0.0, 0.0};
   double gm = 0;
-  for (int sc = blockIdx.x; sc < g.nsub; sc += gridDim.x) {
+  for (int sc = blockIdx.x; sc < g.nsub; sc += g.ksplit) {
     const int j = sc * P + gi;
     double* Yp = Y + (size_t)(3 * gi) * Rz;  // this landmark's 3 rows, written by its own lane group only
     for (int i = gl; i < 3 * Rz / 2; i += SL) reinterpret_cast<double2*>(Yp)[i] = double2{0.0, 0.0};
@@ -1690,6 +1709,8 @@ struct Plan {
   size_t schur_lds = 0;
   int use_lds = 0;
   int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
+  int n_enq = 0;      // linearisations queued so far (the first runs the camera assembly on its own)
+  bool sequential = false;  // ME_BA_SEQUENTIAL=1: never fuse (A/B timing)
 };
 
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
@@ -1717,6 +1738,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   P.c = c;
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
+  if (const char* sq = getenv("ME_BA_SEQUENTIAL")) P.sequential = atoi(sq) != 0;
   Geo& g = P.g;
   g.nc = p->n_cams;
   g.np = p->n_pts;
@@ -1922,7 +1944,14 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     else
       hipLaunchKernelGGL(linearize_kernel<2>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
   }
-  if (g.m > 0) {
+  // After the first linearisation the Jacobi scaling is fixed and the Schur
+  // pass no longer needs the camera assembly: its m x ck workgroups then ride
+  // in the Schur launch (one launch fewer per iteration; a second stream with
+  // event fork/join measured slower).
+  const bool fused = P.n_enq > 0 && !ar && g.m > 0 && !P.sequential;
+  ++P.n_enq;
+  CamArgs ca{P.cpart, P.colnorm, P.gc_raw, P.Uraw, fused ? 1 : 0};
+  if (g.m > 0 && !fused) {
     hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart, ar ? 1 : 0,
                        P.colnorm, P.gc_raw, P.Uraw);
     if (ar) {
@@ -1943,8 +1972,8 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     // at 9-17 tiles than the small spill, and beyond 12 tiles per wave it spills
     // more than the 512-thread instances.)
     const int pw8 = (g.npairs + 7) / 8;
-    const dim3 grd(g.ksplit);
-#define ME_SCHUR(N) hipLaunchKernelGGL((pt_schur_kernel<N, 512>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o)
+    const dim3 grd(g.ksplit + (fused ? g.m * g.ck : 0));
+#define ME_SCHUR(N) hipLaunchKernelGGL((pt_schur_kernel<N, 512>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca)
     if (pw8 <= 3) ME_SCHUR(3);
     else if (pw8 <= 4) ME_SCHUR(4);
     else if (pw8 <= 5) ME_SCHUR(5);
