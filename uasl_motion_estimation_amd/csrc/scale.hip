@@ -621,7 +621,15 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
         lm->k++;
       }
       if (more) {
-        lm->phase = PH_A;
+        // The next iteration's compute_residuals(m_state) (optimisation.cpp:51)
+        // sees the same m_state as this tmp_residuals evaluation (:100), and the
+        // function is pure: its residuals are this phase's (written to the same
+        // buffer phase B reads), so phase A's body runs here without a launch.
+        lm->e1 = e2;
+        lm->nevals += p.n;
+        const double mre = e2 / (double)(p.rows * 1);
+        if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
+        lm->phase = PH_B;
       } else {
         if (lm->k == p.max_nb_iter) lm->stop = MAX_ITERATIONS;
         lm->phase = PH_DONE;
@@ -1048,7 +1056,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, dst, P.err, P.lm, lp, phase,
                        use_tmp, P.bar);
   };
-  // LM phases are enqueued in blocks [A, B, C, C, D] (one launch each, the
+  // LM phases are enqueued in blocks [A, B, C, C, D] ([B, C, C, D] after the first; one launch each, the
   // control fused into the last workgroup); the device state after each
   // block is copied to one of two pinned slots behind an event, and the host
   // reads block k's state only after block k + 1 is queued (the GPU never
@@ -1056,8 +1064,10 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   const long max_blocks = 64L * (p.max_nb_iter + 2);
   ScaleLM* slot[2] = {P.hlm, P.hlm2};
   long blk = 0;
+  // Phase A is launched only in the first block: later iterations take their
+  // residuals from the previous phase D (same state, see scale_ctrl_decide).
   auto enqueue_block = [&](int sl) -> int {
-    res(PH_A, 0, P.res);
+    if (blk == 0) res(PH_A, 0, P.res);
     {
       me_ktimer t(c, ME_KT_SCALE_NEQ);
       hipLaunchKernelGGL(scale_neq_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res, P.jj,
@@ -1065,7 +1075,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     }
     res(PH_C, 1, P.res2);
     res(PH_C, 1, P.res2);
-    res(PH_D, 0, P.res2);
+    res(PH_D, 0, P.res);  // the next iteration's phase-A residuals
     ++blk;
     ME_TRY(me_check_launch(c, "scale optimise"));
     ME_HIP(c, hipMemcpyAsync(slot[sl], P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
