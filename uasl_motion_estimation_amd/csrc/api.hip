@@ -147,6 +147,7 @@ void me_destroy(me_ctx* c) {
     if (t) hipFree(t);
   if (c->ba_async_free) c->ba_async_free(c);
   if (c->ba_pinned) hipHostFree(c->ba_pinned);
+  if (c->scale_mirror) hipHostFree(c->scale_mirror);
   if (c->pinned) hipHostFree(c->pinned);
   for (auto e : c->event_pool) hipEventDestroy(e);
   for (auto e : c->poll_ev)

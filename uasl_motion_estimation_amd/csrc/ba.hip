@@ -1893,8 +1893,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     b.pt_idx = p->pt_idx;
     if (mono) b.cam_id = p->cam_id;
   }
-  ME_HIP(c, hipMemsetAsync(b.work, 0, work_bytes, s));
-  ME_HIP(c, hipMemsetAsync(b.cnt, 0, 4 * (size_t)(g.m + 1), s));
+  // cnt | work are adjacent in the arena: one fill clears both
+  ME_HIP(c, hipMemsetAsync(b.cnt, 0, (size_t)((char*)b.work - (char*)b.cnt) + work_bytes, s));
   const double* cams_in = dev ? p->cams : b.cams[0];
   const double* pts_in = dev ? p->pts : b.pts[0];
   const long nthr = std::max({(long)g.nblk_obs * kBlock, (long)g.np, 6L * g.nc, 3L * g.np});

@@ -43,6 +43,7 @@ struct me_ctx {
   void (*ba_async_free)(me_ctx*) = nullptr;
   void* ba_pinned = nullptr;
   size_t ba_pinned_size = 0;
+  void* scale_mirror = nullptr;  // coherent host page the scale LM control writes its state to
   // MI term tables, one per patch pixel count N (built on first use, mi.hip)
   float* mi_table[256] = {nullptr};
 };

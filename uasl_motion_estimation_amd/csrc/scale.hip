@@ -15,6 +15,7 @@
 #include <cstring>
 #include <vector>
 #include <algorithm>
+#include <atomic>
 #include "me_internal.hpp"
 #include "me_device.hpp"
 
@@ -483,6 +484,10 @@ struct LMParams {
   int type, minim, max_nb_iter, test;
   double abs_tol, grad_tol, incr_tol, rel_tol, alpha;
   int rows, n;
+  // Coherent host page (or null): every control update also stores the LM
+  // header there, the word holding `phase` last behind a system-scope fence,
+  // so the host polls it behind an event instead of a D2H copy per block.
+  unsigned long long* mirror;
 };
 
 __device__ __forceinline__ double ldlt1(double JJ, double e) { return fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
@@ -537,6 +542,13 @@ __device__ void scale_ctrl_body(ScaleLM* lm_g, const LMParams& p, int phase, con
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(lm_g);
 #pragma unroll
   for (int i = 0; i < kHead; ++i) dst[i] = hw[i];
+  if (p.mirror) {
+    constexpr int kPhaseWord = offsetof(ScaleLM, phase) / 8;
+#pragma unroll
+    for (int i = 0; i < kHead; ++i)
+      if (i != kPhaseWord) __hip_atomic_store(p.mirror + i, hw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.mirror + kPhaseWord, hw[kPhaseWord], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // The reference's scalar control for one phase, on the register copy *lm
@@ -707,11 +719,39 @@ struct PrepArgs {
   const uint8_t* mask;  // device copy or null
   int mask_len, nL, nR, tot;
   uint32_t lframe;
+  // Zeroing and LM start state folded into this launch (were two fills and an
+  // H2D copy on the stream): res | res2 rows (zero_words doubles), the error
+  // flag | arrival counter block (kErrWords words) and, when lm != null, the
+  // ScaleLM header (optimisation.cpp:29-40: scale, mu, v, phase A, no stop).
+  double* zero;
+  int zero_words;
+  unsigned* err_block;
+  ScaleLM* lm;
+  double scale0, mu0, v0;
 };
 constexpr int kPrepBlock = 1024;
+constexpr int kErrWords = 64;
 __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uint8_t* flags, int* row, int* err) {
   __shared__ int wsum[kPrepBlock / 64];
   const int n = pa.nL + pa.nR, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int i = t; i < pa.zero_words; i += kPrepBlock) pa.zero[i] = 0.0;
+  if (t < kErrWords) pa.err_block[t] = 0u;
+  if (pa.lm && t == 0) {
+    ScaleLM* lm = pa.lm;
+    lm->scale = pa.scale0;
+    lm->tmp_scale = 0.0;
+    lm->mu = pa.mu0;
+    lm->v = pa.v0;
+    lm->e1 = lm->JJ = lm->e = lm->dX = 0.0;
+    lm->nevals = 0;
+    lm->phase = PH_A;
+    lm->k = 0;
+    lm->stop = NO_STOP;
+    lm->ntrace = 0;
+    lm->err = 0;
+    lm->pad = 0;
+  }
+  __syncthreads();  // err cleared before the scan below may set it
   auto mask_at = [&](int idx) { return !pa.mask || (idx < pa.mask_len && pa.mask[idx]); };
   const int chunk = (n + kPrepBlock - 1) / kPrepBlock;
   const int beg = min(n, t * chunk), end = min(n, beg + chunk);
@@ -772,7 +812,8 @@ struct ScaleProblem {
   ScaleLM* hlm2;  // second pinned poll slot
 };
 
-int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
+// lm0 (me_scale_optimise only): the LM start state {scale, mu, v}, written by the prep launch
+int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, const double* lm0 = nullptr) {
   ME_CHECK(c, s->n_left >= 0 && s->n_right >= 0, "scale: negative track count");
   ME_CHECK(c, s->window_size > 0 && s->cols > 0 && s->rows > 0 && s->stride >= s->cols, "scale: bad image / window");
   ME_CHECK(c, (2 * s->window_size + 1) * (2 * s->window_size + 1) <= 255,
@@ -873,9 +914,16 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P) {
   P.err = (int*)(base + oErr);
   P.bar = (unsigned*)(base + oErr + 64);
   P.lm = (ScaleLM*)(base + oLM);
-  // zero: residual rows never owned by a track stay 0; error flag
-  ME_HIP(c, hipMemsetAsync(base + oRes, 0, oRes2 - oRes + up(8 * nr), c->stream));
-  ME_HIP(c, hipMemsetAsync(base + oErr, 0, 256, c->stream));  // error flag | grid barrier
+  // zeroed by the prep launch: residual rows never owned by a track stay 0;
+  // error flag | arrival counter; LM start state
+  pa.zero = P.res;
+  pa.zero_words = (int)((oRes2 - oRes + up(8 * nr)) / 8);
+  pa.err_block = (unsigned*)(base + oErr);
+  static_assert(4 * kErrWords == 256, "error flag | arrival counter block");
+  pa.lm = lm0 ? P.lm : nullptr;
+  pa.scale0 = lm0 ? lm0[0] : 0.0;
+  pa.mu0 = lm0 ? lm0[1] : 0.0;
+  pa.v0 = lm0 ? lm0[2] : 0.0;
   hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
                      (int*)(base + oRow), P.err);
   ME_TRY(me_check_launch(c, "scale_prep_kernel"));
@@ -1026,16 +1074,8 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     p.rel_tol = 0;
   }
   ScaleProblem P;
-  ME_TRY(upload(c, s, p.weighting, P));
-  // initial state
-  ScaleLM* h0 = P.hlm;
-  std::memset(h0, 0, offsetof(ScaleLM, trace));
-  h0->scale = s->scale;
-  h0->mu = p.mu;
-  h0->v = p.v;
-  h0->phase = PH_A;
-  h0->stop = NO_STOP;
-  ME_HIP(c, hipMemcpyAsync(P.lm, h0, offsetof(ScaleLM, trace), hipMemcpyHostToDevice, c->stream));
+  const double lm0[3] = {s->scale, p.mu, p.v};  // initial state (set on the device by the prep launch)
+  ME_TRY(upload(c, s, p.weighting, P, lm0));
   LMParams lp;
   lp.type = p.type;
   lp.minim = p.minim;
@@ -1048,6 +1088,12 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   lp.alpha = p.alpha;
   lp.rows = P.rows;
   lp.n = P.n;
+  if (!c->scale_mirror) ME_HIP(c, hipHostMalloc(&c->scale_mirror, 4096, hipHostMallocCoherent));
+  constexpr size_t kHeadBytes = offsetof(ScaleLM, trace);
+  static_assert(kHeadBytes <= 4096, "LM header mirror page");
+  lp.mirror = (unsigned long long*)c->scale_mirror;
+  volatile ScaleLM* mir = (volatile ScaleLM*)c->scale_mirror;
+  mir->phase = PH_A;  // the start state (the prep launch writes the device copy)
   const ScaleArgs aR = with_invN(P.a, 2 * P.a.w + 1), aN = with_invN(P.a, 2 * P.a.w);
   const int nb = blocks_for(P.n);
   hipStream_t st = c->stream;
@@ -1057,12 +1103,17 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
                        use_tmp, P.bar);
   };
   // LM phases are enqueued in blocks [A, B, C, C, D] ([B, C, C, D] after the first; one launch each, the
-  // control fused into the last workgroup); the device state after each
-  // block is copied to one of two pinned slots behind an event, and the host
-  // reads block k's state only after block k + 1 is queued (the GPU never
-  // drains while the host polls; launches of a finished solve return at once).
+  // control fused into the last workgroup); every control update also lands
+  // in the coherent host mirror, an event marks each block's end, and the
+  // host reads the mirror after block k's event only once block k + 1 is
+  // queued (the GPU never drains while the host polls; launches of a
+  // finished solve return at once).  The mirror may already hold a later
+  // block's state: harmless, the solve only ever moves towards PH_DONE and
+  // nothing is written after it.  (One phase-agnostic kernel per launch,
+  // whatever phase is current, measured slower: 610 vs 641 frames/s -- its
+  // merged register budget spills and the no-op tail queued after PH_DONE
+  // grows.)
   const long max_blocks = 64L * (p.max_nb_iter + 2);
-  ScaleLM* slot[2] = {P.hlm, P.hlm2};
   long blk = 0;
   // Phase A is launched only in the first block: later iterations take their
   // residuals from the previous phase D (same state, see scale_ctrl_decide).
@@ -1078,7 +1129,6 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     res(PH_D, 0, P.res);  // the next iteration's phase-A residuals
     ++blk;
     ME_TRY(me_check_launch(c, "scale optimise"));
-    ME_HIP(c, hipMemcpyAsync(slot[sl], P.lm, offsetof(ScaleLM, trace), hipMemcpyDeviceToHost, st));
     ME_HIP(c, hipEventRecord(c->poll_ev[sl], st));
     return ME_OK;
   };
@@ -1087,15 +1137,31 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   for (;; cur ^= 1) {
     const bool more = blk < max_blocks;
     if (more) ME_TRY(enqueue_block(cur ^ 1));
-    ME_HIP(c, hipEventSynchronize(c->poll_ev[cur]));
-    if (slot[cur]->phase == PH_DONE) break;
+    // Spin on the mirror and the block's event (no sleeping wait: its wake-up
+    // latency exceeded a block's ~60 us and idled the stream).  PH_DONE ends
+    // the wait at once; the finished solve's queued launches return at once.
+    bool done = false;
+    for (;;) {
+      if (mir->phase == PH_DONE) {
+        done = true;
+        break;
+      }
+      const hipError_t q = hipEventQuery(c->poll_ev[cur]);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) ME_HIP(c, q);
+    }
+    if (done || mir->phase == PH_DONE) break;
     if (!more) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
   }
-  ScaleLM& hs = *slot[cur];
+  std::atomic_thread_fence(std::memory_order_acquire);  // phase read before the rest of the header
+  ScaleLM& hs = *P.hlm;
+  std::memcpy(&hs, c->scale_mirror, kHeadBytes);
   if (hs.err) return check_err(c, hs.err);
   const int nt = std::min(std::min(hs.ntrace, kTraceCap), std::max(trace_cap, 0));
-  if (trace && nt > 0)
-    ME_HIP(c, hipMemcpy(trace, P.lm->trace, 16 * (size_t)nt, hipMemcpyDeviceToHost));
+  if (trace && nt > 0) {  // stream-ordered: the solve's tail launches may still be queued
+    ME_HIP(c, hipMemcpyAsync(trace, P.lm->trace, 16 * (size_t)nt, hipMemcpyDeviceToHost, c->stream));
+    ME_HIP(c, hipStreamSynchronize(c->stream));
+  }
   s->scale = hs.scale;
   if (stop_out) *stop_out = hs.stop;
   if (iterations) *iterations = hs.ntrace;

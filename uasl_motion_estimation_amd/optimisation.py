@@ -401,21 +401,31 @@ class DeviceBAProblem:
                       cam_idx=np.ascontiguousarray(bp.cam_idx, np.int32),
                       pt_idx=np.ascontiguousarray(bp.pt_idx, np.int32))
         self.obs_dim = int(getattr(bp, "obs_dim", 4))
-        names = ["cams", "pts", "obs", "cam_idx", "pt_idx", "cams0", "pts0"]
+        names = ["obs", "cam_idx", "pt_idx"]
         if self.obs_dim == 2:
             arrays["cam_id"] = np.ascontiguousarray(bp.cam_id, np.int32)
             names.append("cam_id")
         self.nbytes = {k: v.nbytes for k, v in arrays.items()}
         self.d = {}
+        self._blocks = []
         for k in names:
-            src = arrays[k[:-1]] if k.endswith("0") else arrays[k]
-            self.d[k] = self.ctx.malloc(max(src.nbytes, 16))
-            self.ctx.h2d(self.d[k], src)
+            self.d[k] = self.ctx.malloc(max(arrays[k].nbytes, 16))
+            self._blocks.append(self.d[k])
+            self.ctx.h2d(self.d[k], arrays[k])
+        # cams | pts (solved in place) and cams0 | pts0 (the starting point) are
+        # each one block, so reset() is a single device copy
+        self._poff = (self.nbytes["cams"] + 255) & ~255
+        self._pspan = self._poff + self.nbytes["pts"]
+        for sfx in ("", "0"):
+            base = self.ctx.malloc(max(self._pspan, 16))
+            self._blocks.append(base)
+            self.d["cams" + sfx], self.d["pts" + sfx] = base, base + self._poff
+            self.ctx.h2d(self.d["cams" + sfx], arrays["cams"])
+            self.ctx.h2d(self.d["pts" + sfx], arrays["pts"])
         self.n_cams, self.n_pts, self.n_obs = len(bp.cams), len(bp.pts), len(bp.obs)
 
     def reset(self):
-        self.ctx.d2d(self.d["cams"], self.d["cams0"], self.nbytes["cams"])
-        self.ctx.d2d(self.d["pts"], self.d["pts0"], self.nbytes["pts"])
+        self.ctx.d2d(self.d["cams"], self.d["cams0"], self._pspan)
 
     def struct(self) -> BAProblemC:
         p = BAProblemC()
@@ -462,9 +472,10 @@ class DeviceBAProblem:
         return cams, pts
 
     def close(self):
-        for v in self.d.values():
+        for v in self._blocks:
             self.ctx.free(v)
         self.d = {}
+        self._blocks = []
 
 
 def shard_landmarks(bp, rank: int, world: int):
