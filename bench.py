@@ -291,8 +291,11 @@ def pmc_traffic(family: str):
     (profiles/*_pmc_traffic.json, written by tools_pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench); None if absent."""
     import glob
+    import re
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")))
+    # newest = highest round / version numbers (natural order: v10 after v9)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")),
+                   key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
     if not files:
         return None
     d = json.load(open(files[-1]))

@@ -62,7 +62,7 @@ struct ScaleLM {
   double scale, tmp_scale, mu, v, e1, JJ, e, dX;
   long nevals;
   int phase, k, stop, ntrace, err;
-  int pad;
+  int cur;  // residual buffer holding the residuals at `scale`: 0 = res, 1 = res2 (the other takes candidates)
   double trace[2 * kTraceCap];
 };
 
@@ -551,6 +551,42 @@ __device__ void scale_ctrl_body(ScaleLM* lm_g, const LMParams& p, int phase, con
   }
 }
 
+// Phase D's control (optimisation.cpp:100-146): e2 = the residual sum at the
+// accepted state.
+__device__ __forceinline__ void ctrl_after_eval(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
+                                                double e2) {
+  // (the SMALL_INCREMENT test precedes this evaluation in the reference;
+  // it only reads dX, so it is applied here with the same result)
+  if (!lm->stop && sqrt(lm->dX * lm->dX) <= p.incr_tol) lm->stop = SMALL_INCREMENT;
+  lm->nevals += p.n;
+  if (p.type == 0 && (e2 - lm->e1) * (e2 - lm->e1) < p.rel_tol) lm->stop = SMALL_DECREASE_FUNCTION;
+  if (lm->ntrace < kTraceCap) {
+    trace[2 * lm->ntrace] = lm->e1;
+    trace[2 * lm->ntrace + 1] = lm->scale;
+  }
+  lm->ntrace++;
+  // while (!stop && k++ < max_nb_iter)
+  bool more = false;
+  if (!lm->stop) {
+    more = lm->k < p.max_nb_iter;
+    lm->k++;
+  }
+  if (more) {
+    // The next iteration's compute_residuals(m_state) (optimisation.cpp:51)
+    // sees the same m_state as this tmp_residuals evaluation (:100), and the
+    // function is pure: its residuals are this phase's (written to the same
+    // buffer phase B reads), so phase A's body runs here without a launch.
+    lm->e1 = e2;
+    lm->nevals += p.n;
+    const double mre = e2 / (double)(p.rows * 1);
+    if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
+    lm->phase = PH_B;
+  } else {
+    if (lm->k == p.max_nb_iter) lm->stop = MAX_ITERATIONS;
+    lm->phase = PH_DONE;
+  }
+}
+
 // The reference's scalar control for one phase, on the register copy *lm
 // (trace entries go straight to the device trace array).
 __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
@@ -600,7 +636,12 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
         const double dd = sqrt(e1) - sqrt(e2);
         if (dd * dd < p.rel_tol * sqrt(e1)) lm->stop = SMALL_DECREASE_FUNCTION;
         lm->scale = lm->tmp_scale;
-        lm->phase = PH_D;
+        // Phase D would evaluate the residuals at scale == tmp_scale: the
+        // candidate's residuals (a pure function of the same state, reduced in
+        // the same order), so its control runs here without a launch and the
+        // candidate buffer becomes the current one.
+        lm->cur ^= 1;
+        ctrl_after_eval(lm, trace, p, sx);
       } else {
         lm->mu *= lm->v;
         const double v2 = 2 * lm->v;
@@ -614,40 +655,9 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
       }
       break;
     }
-    case PH_D: {
-      // (the SMALL_INCREMENT test precedes this evaluation in the reference;
-      // it only reads dX, so it is applied here with the same result)
-      if (!lm->stop && sqrt(lm->dX * lm->dX) <= p.incr_tol) lm->stop = SMALL_INCREMENT;
-      const double e2 = sx;
-      lm->nevals += p.n;
-      if (p.type == 0 && (e2 - lm->e1) * (e2 - lm->e1) < p.rel_tol) lm->stop = SMALL_DECREASE_FUNCTION;
-      if (lm->ntrace < kTraceCap) {
-        trace[2 * lm->ntrace] = lm->e1;
-        trace[2 * lm->ntrace + 1] = lm->scale;
-      }
-      lm->ntrace++;
-      // while (!stop && k++ < max_nb_iter)
-      bool more = false;
-      if (!lm->stop) {
-        more = lm->k < p.max_nb_iter;
-        lm->k++;
-      }
-      if (more) {
-        // The next iteration's compute_residuals(m_state) (optimisation.cpp:51)
-        // sees the same m_state as this tmp_residuals evaluation (:100), and the
-        // function is pure: its residuals are this phase's (written to the same
-        // buffer phase B reads), so phase A's body runs here without a launch.
-        lm->e1 = e2;
-        lm->nevals += p.n;
-        const double mre = e2 / (double)(p.rows * 1);
-        if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
-        lm->phase = PH_B;
-      } else {
-        if (lm->k == p.max_nb_iter) lm->stop = MAX_ITERATIONS;
-        lm->phase = PH_DONE;
-      }
+    case PH_D:
+      ctrl_after_eval(lm, trace, p, sx);
       break;
-    }
   }
 }
 
@@ -669,11 +679,17 @@ __device__ __forceinline__ bool last_block_arrives(unsigned* cnt) {
   return slast != 0;
 }
 
-__global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
-                                                                  int* __restrict__ err, ScaleLM* lm, LMParams p,
-                                                                  int phase, int use_tmp, unsigned* cnt) {
-  if (lm->phase != phase) return;
-  lm_scale(a, lm, use_tmp);
+// A residual launch serves phase A (first != 0) or whichever of C (residuals
+// at the candidate, into the buffer not holding the current residuals) and D
+// (at the accepted scale, into the current buffer) is current.
+__global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res0,
+                                                                  double* __restrict__ res1, int* __restrict__ err,
+                                                                  ScaleLM* lm, LMParams p, int first, unsigned* cnt) {
+  const int phase = lm->phase;
+  if (first ? phase != PH_A : (phase != PH_C && phase != PH_D)) return;
+  const int cand = phase == PH_C ? 1 : 0;
+  double* res = (lm->cur ^ cand) ? res1 : res0;
+  lm_scale(a, lm, cand);
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
@@ -688,11 +704,13 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
 }
 
 __global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, TrackDev td,
-                                                                  const double* __restrict__ res,
+                                                                  const double* __restrict__ res0,
+                                                                  const double* __restrict__ res1,
                                                                   double* __restrict__ jj, double* __restrict__ je,
                                                                   int* __restrict__ err, ScaleLM* lm, LMParams p,
                                                                   unsigned* cnt) {
   if (lm->phase != PH_B) return;
+  const double* res = lm->cur ? res1 : res0;
   lm_scale(a, lm, 0);
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   const int grp = threadIdx.x >> 4;
@@ -749,7 +767,7 @@ __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uin
     lm->stop = NO_STOP;
     lm->ntrace = 0;
     lm->err = 0;
-    lm->pad = 0;
+    lm->cur = 0;
   }
   __syncthreads();  // err cleared before the scan below may set it
   auto mask_at = [&](int idx) { return !pa.mask || (idx < pa.mask_len && pa.mask[idx]); };
@@ -1097,36 +1115,42 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   const ScaleArgs aR = with_invN(P.a, 2 * P.a.w + 1), aN = with_invN(P.a, 2 * P.a.w);
   const int nb = blocks_for(P.n);
   hipStream_t st = c->stream;
-  auto res = [&](int phase, int use_tmp, double* dst) {
+  auto res = [&](int first) {
     me_ktimer t(c, ME_KT_SCALE_RES);
-    hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, dst, P.err, P.lm, lp, phase,
-                       use_tmp, P.bar);
+    hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, P.res, P.res2, P.err, P.lm,
+                       lp, first, P.bar);
   };
-  // LM phases are enqueued in blocks [A, B, C, C, D] ([B, C, C, D] after the first; one launch each, the
-  // control fused into the last workgroup); every control update also lands
-  // in the coherent host mirror, an event marks each block's end, and the
-  // host reads the mirror after block k's event only once block k + 1 is
-  // queued (the GPU never drains while the host polls; launches of a
-  // finished solve return at once).  The mirror may already hold a later
-  // block's state: harmless, the solve only ever moves towards PH_DONE and
-  // nothing is written after it.  (One phase-agnostic kernel per launch,
-  // whatever phase is current, measured slower: 610 vs 641 frames/s -- its
-  // merged register budget spills and the no-op tail queued after PH_DONE
-  // grows.)
+  auto neq = [&]() {
+    me_ktimer t(c, ME_KT_SCALE_NEQ);
+    hipLaunchKernelGGL(scale_neq_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res,
+                       (const double*)P.res2, P.jj, P.je, P.err, P.lm, lp, P.bar);
+  };
+  // The LM is enqueued in blocks [A,] B, R, B, R (one launch per LM phase, the
+  // control fused into the last workgroup; R = a residual launch serving
+  // phase C or D, whichever is current; an accepted candidate closes its
+  // iteration in C's control, so a typical iteration is one B and one R);
+  // every control update also lands in the coherent host mirror, an event
+  // marks each block's end, and the host reads the mirror after block k's
+  // event only once block k + 1 is queued (the GPU never drains while the
+  // host polls; launches of a finished solve return at once).  The mirror
+  // may already hold a later block's state: harmless, the solve only ever
+  // moves towards PH_DONE and nothing is written after it.  (One
+  // phase-agnostic kernel per launch, whatever phase is current, measured
+  // slower: 610 vs 641 frames/s -- its merged register budget spills.)
   const long max_blocks = 64L * (p.max_nb_iter + 2);
   long blk = 0;
   // Phase A is launched only in the first block: later iterations take their
-  // residuals from the previous phase D (same state, see scale_ctrl_decide).
+  // residuals from the previous evaluation (same state, see ctrl_after_eval).
+  // While the mirror shows a rejection streak (phase C: every retry is one
+  // more R), the block is R, R, R, R.  Only the launch mix depends on this
+  // (stale) read: every launch still runs the phase that is current.
   auto enqueue_block = [&](int sl) -> int {
-    if (blk == 0) res(PH_A, 0, P.res);
-    {
-      me_ktimer t(c, ME_KT_SCALE_NEQ);
-      hipLaunchKernelGGL(scale_neq_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res, P.jj,
-                         P.je, P.err, P.lm, lp, P.bar);
-    }
-    res(PH_C, 1, P.res2);
-    res(PH_C, 1, P.res2);
-    res(PH_D, 0, P.res);  // the next iteration's phase-A residuals
+    if (blk == 0) res(1);
+    const bool retrying = blk > 0 && mir->phase == PH_C;
+    retrying ? res(0) : neq();
+    res(0);
+    retrying ? res(0) : neq();
+    res(0);
     ++blk;
     ME_TRY(me_check_launch(c, "scale optimise"));
     ME_HIP(c, hipEventRecord(c->poll_ev[sl], st));
