@@ -124,6 +124,8 @@ bool masked_out(const oracle_scale_state* s, int idx) {
 }
 
 long g_mi_evals = 0;
+// logical call counts of the last oracle_scale_optimise (optimisation.cpp:51,75,101,702; rejections :719-727)
+long g_res_calls = 0, g_neq_calls = 0, g_rejections = 0;
 
 }  // namespace
 
@@ -409,6 +411,7 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
   oracle_optim_params p = *p_in;
   oracle_scale_state st = *s_in;
   g_mi_evals = 0;
+  g_res_calls = g_neq_calls = g_rejections = 0;
   int stop = NO_STOP;
   if (test) { p.type = 0; p.max_nb_iter = 300; p.abs_tol = 0; p.incr_tol = 0; p.grad_tol = 0; p.rel_tol = 0; }
   const int ntot = s_in->n_left + s_in->n_right;
@@ -417,13 +420,14 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
   int ntrace = 0;
   do {
     int rows = oracle_scale_residuals(&st, p.weighting, r.data());
+    ++g_res_calls;
     if (rows < 0) return -100 + rows;
     double e1 = sumsq(r, rows);
     double mre = e1 / (double)(rows * 1);
     if (mre < p.abs_tol) stop = SMALL_REPROJ_ERROR;
     double JJ, e;
     if (test) { JJ = 75; e = 1; }
-    else { int rc = oracle_scale_normal_equations(&st, p.weighting, r.data(), &JJ, &e); if (rc < 0) return -100 + rc; }
+    else { int rc = oracle_scale_normal_equations(&st, p.weighting, r.data(), &JJ, &e); ++g_neq_calls; if (rc < 0) return -100 + rc; }
     if (k == 0) p.mu = JJ;
     if (std::sqrt(e * e) < p.grad_tol) stop = SMALL_GRADIENT;
     double dX = 0;
@@ -439,6 +443,7 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
         oracle_scale_state tmp = st;
         tmp.scale += p.alpha * dX;
         int rows2 = oracle_scale_residuals(&tmp, p.weighting, rt.data());
+        ++g_res_calls;
         if (rows2 < 0) return -100 + rows2;
         double e2 = sumsq(rt, rows2);
         double rho = (p.minim ? -1.0 : 1.0) * (e2 - e1);
@@ -450,6 +455,7 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
           st = tmp;
           break;
         } else {
+          ++g_rejections;
           p.mu *= p.v;
           double v2 = 2 * p.v;
           if (v2 <= p.v) { stop = NO_CONVERGENCE; break; }
@@ -459,6 +465,7 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
     }
     if (!stop && std::sqrt(dX * dX) <= p.incr_tol) stop = SMALL_INCREMENT;
     int rows3 = oracle_scale_residuals(&st, p.weighting, rt.data());
+    ++g_res_calls;
     if (rows3 < 0) return -100 + rows3;
     double e2 = sumsq(rt, rows3);
     if (p.type == 0 && (e2 - e1) * (e2 - e1) < p.rel_tol) stop = SMALL_DECREASE_FUNCTION;
@@ -469,6 +476,12 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
   if (iterations) *iterations = ntrace;
   if (mi_evals) *mi_evals = g_mi_evals;
   return stop;
+}
+
+extern "C" void oracle_scale_counters(long* out3) {
+  out3[0] = g_res_calls;
+  out3[1] = g_neq_calls;
+  out3[2] = g_rejections;
 }
 
 // optimisation.cpp:732-747

@@ -331,8 +331,10 @@ def scale_optimise(sp, test=0, **kw):
                                        ctypes.byref(nmi))
     if stop < 0:
         raise RuntimeError(f"oracle_scale_optimise failed {stop}")
+    cnt = (c_long * 3)()
+    lib().oracle_scale_counters(cnt)
     return dict(stop=stop, scale=s.scale, iterations=it.value, trace=trace[:2 * min(it.value, 400)].reshape(-1, 2),
-                mi_evals=nmi.value)
+                mi_evals=nmi.value, res_evals=cnt[0], neq_evals=cnt[1], rejections=cnt[2])
 
 
 def scale_inliers(sp, threshold):

@@ -1,0 +1,169 @@
+"""GPU parity at the BASELINE configurations' full sizes (configs 2-5), and
+the scale optimiser's LM rejection path.
+
+Every case runs the product path (libme_hip.so through the C ABI) and the
+CPU restatement (oracle/) on the same seeded synthetic input:
+  * BA (BundleAdjuster<4>::optimise, BundleAdjuster.h:431-476): same
+    iteration / successful-step counts, cameras and points within 1e-6
+    relative (1e-9 absolute floor) at fixed iteration counts;
+  * scale LM (Optimiser<ScaleState,...>::optimise, optimisation.cpp:29-147,
+    run_LM_step :685-730): same stop condition, iterations, residual /
+    normal-equation evaluation counts and LM rejections; trace and scale
+    within 1e-9 relative;
+  * KLT: positions and status bit-exact.
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+from uasl_motion_estimation_amd import synthetic as S
+from uasl_motion_estimation_amd.optimisation import OptimisationParams
+
+pytestmark = pytest.mark.gpu
+
+
+def _ba_fixed(ctx, oracle, bp, iters):
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    cams, pts, s = ba_solve(bp.copy(), SolverOptions.fixed_iterations(iters), ctx=ctx)
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    assert s["iterations"] == rs["iterations"] == iters, (s, rs)
+    assert s["successful_steps"] == rs["successful_steps"], (s, rs)
+    assert s["status"] == rs["status"] == 2
+    np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(s["final_cost"], rs["final_cost"], rtol=1e-9)
+
+
+def _scale_check(ctx, oracle, sp, params: OptimisationParams, test=False):
+    from uasl_motion_estimation_amd.optimisation import scale_optimise
+
+    got = scale_optimise(sp, params, test=test, ctx=ctx)
+    ref = oracle.scale_optimise(sp, test=int(test), **params.oracle_kw())
+    assert int(got["stop"]) == ref["stop"], (got["stop"], ref)
+    assert got["iterations"] == ref["iterations"]
+    assert (got["res_evals"], got["neq_evals"], got["rejections"]) == \
+        (ref["res_evals"], ref["neq_evals"], ref["rejections"]), (got, ref)
+    n = len(sp.X_left) + len(sp.X_right)
+    assert got["track_evals"] == n * (got["res_evals"] + (0 if test else 2 * got["neq_evals"]))
+    np.testing.assert_allclose(got["scale"], ref["scale"], rtol=1e-9)
+    np.testing.assert_allclose(got["trace"], ref["trace"], rtol=1e-9)
+    return got, ref
+
+
+# ------------------------------------------------------------------ LM rejection path
+@pytest.fixture(scope="module")
+def sp300():
+    return S.scale_problem(3, 640, 480, 300)
+
+
+@pytest.mark.parametrize("scale0,kw,stop", [
+    (1.02, {}, 2),                                   # rejections, then SMALL_INCREMENT after an accepted step
+    (0.9, dict(alpha=5.0, incr_tol=1e-6), 4),        # rejections, then SMALL_DECREASE_FUNCTION
+    (0.9, dict(v=float("inf")), 6),                  # NO_CONVERGENCE (v2 <= v)
+    (1.2, dict(minim=False), 2),                     # maximisation: rho sign flipped
+    (1.02, dict(alpha=20.0), 2),
+])
+def test_scale_lm_rejections(ctx, oracle, sp300, scale0, kw, stop):
+    sp = dataclasses.replace(sp300, scale=scale0)
+    got, ref = _scale_check(ctx, oracle, sp, OptimisationParams(**kw))
+    assert ref["rejections"] > 0 and ref["stop"] == stop
+
+
+def test_scale_lm_fixed_iterations_long_streak(ctx, oracle, sp300):
+    """Tolerances off: the final rejection streak runs until mu overflows and
+    the step is exactly 0 (~33 rejections); most late candidates equal the
+    current state bit for bit and are decided without an evaluation."""
+    got, ref = _scale_check(ctx, oracle, sp300, OptimisationParams.fixed_iterations(10))
+    assert ref["rejections"] >= 30
+
+
+def test_scale_gn_fixed_iterations(ctx, oracle, sp300):
+    """GN with tolerances off runs MAX_NB_ITER + 1 iterations and reports NO_STOP (SURVEY A-2)."""
+    p = dataclasses.replace(OptimisationParams.fixed_iterations(10), type=0)
+    got, ref = _scale_check(ctx, oracle, sp300, p)
+    assert ref["iterations"] == 11 and ref["stop"] == 0
+
+
+# ------------------------------------------------------------------ config-sized scale LM
+def _cfg_scale_problem(c: int, frame: int, render_div: int = 1):
+    """The bench's scale problem of config c, frame `frame` (bench.py make_frames)."""
+    cfg = S.CONFIGS[c]
+    seed = S.SEED0 + c
+    scene, K, stream = S.stereo_stream(seed, cfg["width"], cfg["height"], frame + 2, render_div=render_div)
+    return S.scale_problem(seed + frame, cfg["width"], cfg["height"], cfg["n_feats"], window=cfg["window"], w=5,
+                           frames=stream[: frame + 2], scene=scene)
+
+
+@pytest.fixture(scope="module")
+def sp_cfg3():
+    return [_cfg_scale_problem(3, f) for f in (0, 1)]
+
+
+@pytest.mark.parametrize("frame", [0, 1])
+@pytest.mark.parametrize("mode", ["default", "fixed10"])
+def test_scale_config3_2000_tracks(ctx, oracle, sp_cfg3, frame, mode):
+    sp = sp_cfg3[frame]
+    assert len(sp.X_left) + len(sp.X_right) == 2000 and sp.imgL.shape == (720, 1280)
+    p = OptimisationParams() if mode == "default" else OptimisationParams.fixed_iterations(10)
+    _scale_check(ctx, oracle, sp, p)
+
+
+def test_scale_config2_500_tracks(ctx, oracle):
+    sp = _cfg_scale_problem(2, 0)
+    assert len(sp.X_left) + len(sp.X_right) == 500
+    _scale_check(ctx, oracle, sp, OptimisationParams())
+    _scale_check(ctx, oracle, sp, OptimisationParams.fixed_iterations(10))
+
+
+def test_scale_config4_8000_tracks_4k(ctx, oracle):
+    sp = _cfg_scale_problem(4, 0, render_div=4)
+    assert len(sp.X_left) + len(sp.X_right) == 8000 and sp.imgL.shape == (2160, 3840)
+    _scale_check(ctx, oracle, sp, OptimisationParams.fixed_iterations(10))
+
+
+# ------------------------------------------------------------------ config-sized BA windows
+def test_ba_config3_2000x20_10_iterations(ctx, oracle):
+    c = S.CONFIGS[3]
+    bp = S.ba_problem(S.SEED0 + 3, c["n_feats"], c["window"], c["width"], c["height"])
+    assert len(bp.pts) == 2000 and len(bp.cams) == 20
+    _ba_fixed(ctx, oracle, bp, 10)
+
+
+def test_ba_config3_bench_window(ctx, oracle):
+    """The exact BA window bench.py times first (make_frames: seed * 7 + frame)."""
+    c = S.CONFIGS[3]
+    seed = S.SEED0 + 3
+    _ba_fixed(ctx, oracle, S.ba_problem(seed * 7 + 0, c["n_feats"], c["window"], c["width"], c["height"]), 10)
+
+
+def test_ba_config4_8000x30(ctx, oracle):
+    c = S.CONFIGS[4]
+    bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
+    assert len(bp.pts) == 8000 and len(bp.cams) == 30
+    _ba_fixed(ctx, oracle, bp, 4)
+
+
+def test_ba_config5_2000x50(ctx, oracle):
+    c = S.CONFIGS[5]
+    bp = S.ba_problem(S.SEED0 + 5, c["n_feats"], c["window"], c["width"], c["height"])
+    assert len(bp.pts) == 2000 and len(bp.cams) == 50
+    _ba_fixed(ctx, oracle, bp, 4)
+
+
+# ------------------------------------------------------------------ config-sized KLT
+def test_klt_config3_2000_features(ctx, oracle):
+    from uasl_motion_estimation_amd.klt import calcOpticalFlowPyrLK
+
+    c = S.CONFIGS[3]
+    seed = S.SEED0 + 3
+    scene, K, stream = S.stereo_stream(seed, c["width"], c["height"], 2)
+    rng = np.random.default_rng(seed)
+    pts = S.grid_features(rng, c["n_feats"], c["width"], c["height"], 12).astype(np.float32)
+    got, gst = calcOpticalFlowPyrLK(stream[0].left, stream[1].left, pts, ctx=ctx)
+    ref, rst = oracle.klt(stream[0].left, stream[1].left, pts)
+    assert np.array_equal(gst, rst)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert gst.mean() > 0.8

@@ -16,6 +16,7 @@
 #include <vector>
 #include <algorithm>
 #include <atomic>
+#include <thread>
 #include "me_internal.hpp"
 #include "me_device.hpp"
 
@@ -62,8 +63,38 @@ struct ScaleLM {
   double scale, tmp_scale, mu, v, e1, JJ, e, dX;
   long nevals;
   int phase, k, stop, ntrace, err;
-  int cur;  // residual buffer holding the residuals at `scale`: 0 = res, 1 = res2 (the other takes candidates)
+  int cur;  // residual buffer (of kResBufs) holding the residuals at `scale`; candidates take the next ones
+  // logical call counts of the reference's loop (a skipped launch still counts
+  // the evaluation it stands for): compute_residuals, compute_normal_equations,
+  // rejected LM candidates (run_LM_step's else branch)
+  int nres, nneq, nrej;
+  int gen;     // solve generation (host-chosen): the host ignores a mirror written by an older solve
+  int nbatch;  // candidate batches proposed in the current outer iteration
   double trace[2 * kTraceCap];
+};
+
+// Speculative LM candidates (run_LM_step, optimisation.cpp:688-728).  Until a
+// candidate is accepted, the loop's state (JJ += mu, dX, mu *= v, v *= 2)
+// does not depend on the evaluations, so the control lays out the next
+// candidates in one go and one launch evaluates them all (blockIdx.y =
+// candidate, each into its own residual buffer, each reduced in the fixed
+// order); the control then walks them in order exactly as the sequential loop
+// would: the first with rho > 0 is accepted with the mu of its turn, the ones
+// before it count as rejections, the ones after it never happened.  A
+// candidate whose scale equals the current scale bit for bit is the current
+// state: its residuals are the current ones, e2 == e1, rho = 0, so it is
+// rejected without an evaluation (every late candidate of a rejection streak
+// is one: its step is below the scale's ulp).
+constexpr int kSpecMax = 16;
+constexpr int kResBufs = kSpecMax + 1;  // the current residuals + one per candidate
+struct ScaleSpec {
+  double ts[kSpecMax];   // candidate scale
+  double dX[kSpecMax];   // its increment
+  double mu[kSpecMax];   // mu at its turn (the accepted candidate's mu update starts there)
+  double e2[kSpecMax];   // its residual sum (written by the candidate's last workgroup)
+  int skips[kSpecMax];   // same-state candidates rejected without evaluation just before it
+  double rs_JJ, rs_mu, rs_v, rs_dX;  // loop state once every candidate of the batch is rejected
+  int n, term, tail_skips;           // candidates, terminal stop after them (or NO_STOP), same-state ones after the last
 };
 
 __device__ __forceinline__ bool lm_skip(const ScaleLM* lm, int phase) { return lm && lm->phase != phase; }
@@ -492,62 +523,113 @@ struct LMParams {
 
 __device__ __forceinline__ double ldlt1(double JJ, double e) { return fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
 
-// LM (or GN) step from the current JJ, e, mu (run_LM_step head,
-// optimisation.cpp:688-698): the candidate is evaluated in phase C.
-__device__ void lm_propose(ScaleLM* lm, const LMParams& p) {
-  lm->JJ += lm->mu;
-  lm->dX = ldlt1(lm->JJ, lm->e);
-  if (sqrt(lm->dX * lm->dX) <= p.incr_tol) {
-    lm->stop = SMALL_INCREMENT;
-    lm->phase = PH_D;
-  } else {
-    lm->tmp_scale = lm->scale + p.alpha * lm->dX;
-    lm->phase = PH_C;
+// The accepted-state evaluation (phase D) and the loop tail, defined below.
+__device__ __forceinline__ void ctrl_after_eval(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
+                                                double e2);
+
+// Lays out the next batch of LM candidates from the register state *lm
+// (after phase B, or after a batch whose candidates were all rejected):
+// run_LM_step's loop (optimisation.cpp:688-728) run ahead under the
+// assumption that every candidate is rejected.  A batch with no candidate to
+// evaluate ends in its terminal stop and closes the iteration here.
+__device__ void lm_propose_batch(ScaleLM* lm, ScaleSpec* __restrict__ sp, double* __restrict__ trace,
+                                 const LMParams& p) {
+  const int cap = lm->nbatch == 0 ? 4 : kSpecMax;  // an accept usually comes early; streaks get wide batches
+  lm->nbatch++;
+  double JJ = lm->JJ, mu = lm->mu, v = lm->v, dX = lm->dX;
+  const unsigned long long cur_bits = __double_as_longlong(lm->scale);
+  int n = 0, skips = 0, term = NO_STOP;
+  while (n < cap) {
+    JJ += mu;                 // JJ.diagonal() += mu (:690)
+    dX = ldlt1(JJ, lm->e);    // (:692)
+    if (sqrt(dX * dX) <= p.incr_tol) {  // (:694-697)
+      term = SMALL_INCREMENT;
+      break;
+    }
+    const double ts = lm->scale + p.alpha * dX;  // tmp_state.update(alpha dX) (:699-700)
+    if (__double_as_longlong(ts) != cur_bits) {
+      sp->ts[n] = ts;
+      sp->dX[n] = dX;
+      sp->mu[n] = mu;
+      sp->skips[n] = skips;
+      skips = 0;
+      ++n;
+    } else {
+      ++skips;  // the current state: e2 == e1, rho = 0, rejected
+    }
+    mu *= v;  // rejection (:719-727)
+    const double v2 = 2 * v;
+    if (v2 <= v) {
+      term = NO_CONVERGENCE;
+      break;
+    }
+    v = v2;
   }
+  sp->n = n;
+  sp->term = term;
+  sp->tail_skips = skips;
+  sp->rs_JJ = JJ;
+  sp->rs_mu = mu;
+  sp->rs_v = v;
+  sp->rs_dX = dX;
+  if (n > 0) {
+    lm->phase = PH_C;
+    return;
+  }
+  // nothing to evaluate: every candidate was the current state, up to the stop
+  const long sk = skips;
+  lm->nres += (int)sk;
+  lm->nrej += (int)sk;
+  lm->nevals += sk * p.n;
+  lm->JJ = JJ;
+  lm->mu = mu;
+  lm->v = v;
+  lm->dX = dX;
+  lm->stop = term;
+  // tmp_residuals at the unchanged state (:101): the current residuals, e2 == e1
+  ctrl_after_eval(lm, trace, p, lm->e1);
 }
 
-// One workgroup: reduce the evaluation of `phase`, then thread 0 runs the
-// reference's scalar control for that phase (optimisation.cpp:29-147,
-// run_GN_step :674-683, run_LM_step :685-730).
-__device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
-                                                  int phase, double sx, double sy, int err);
-
-template <int B>
-__device__ void scale_ctrl_body(ScaleLM* lm_g, const LMParams& p, int phase, const double* __restrict__ x,
-                                const double* __restrict__ y, const int* err) {
-  // Thread 0 requests the LM header and the error flag before the reduction,
-  // so their latency overlaps it; the control then runs on a register copy
-  // (no chain of dependent global round trips) and stores the header once.
-  constexpr int kHead = offsetof(ScaleLM, trace) / 8;
-  static_assert(offsetof(ScaleLM, trace) % 8 == 0, "LM header is copied as 8-byte words");
-  unsigned long long hw[kHead];
-  int err_v = 0;
-  if (threadIdx.x == 0) {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lm_g);
-#pragma unroll
-    for (int i = 0; i < kHead; ++i) hw[i] = src[i];
-    err_v = *err;
+// Phase C's control: walk the evaluated batch in the sequential loop's order.
+__device__ void lm_walk_batch(ScaleLM* lm, ScaleSpec* __restrict__ sp, double* __restrict__ trace,
+                              const LMParams& p) {
+  const int n = sp->n;
+  const double e1 = lm->e1;
+  for (int j = 0; j < n; ++j) {
+    const long sk = sp->skips[j];
+    lm->nres += (int)sk + 1;
+    lm->nrej += (int)sk;
+    lm->nevals += (sk + 1) * p.n;
+    const double e2 = sp->e2[j];
+    const double rho = (p.minim ? -1.0 : 1.0) * (e2 - e1);  // (:705-706)
+    if (rho > 0) {  // (:708-717)
+      lm->mu = sp->mu[j] * fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
+      lm->v = 2;
+      const double dd = sqrt(e1) - sqrt(e2);
+      if (dd * dd < p.rel_tol * sqrt(e1)) lm->stop = SMALL_DECREASE_FUNCTION;
+      lm->scale = sp->ts[j];
+      lm->dX = sp->dX[j];
+      // The reference's tmp_residuals (:101) are at scale == ts[j]: candidate
+      // j's residuals (same state, same order), whose buffer becomes current.
+      lm->cur = (lm->cur + 1 + j) % kResBufs;
+      ctrl_after_eval(lm, trace, p, e2);
+      return;
+    }
+    lm->nrej++;
   }
-  double sx = 0, sy = 0;
-  if (phase == PH_B) {
-    if (!p.test) block_reduce2<B>(x, y, p.n, 0, &sx, &sy);
+  const long sk = sp->tail_skips;
+  lm->nres += (int)sk;
+  lm->nrej += (int)sk;
+  lm->nevals += sk * p.n;
+  lm->JJ = sp->rs_JJ;
+  lm->mu = sp->rs_mu;
+  lm->v = sp->rs_v;
+  lm->dX = sp->rs_dX;
+  if (sp->term != NO_STOP) {
+    lm->stop = sp->term;
+    ctrl_after_eval(lm, trace, p, e1);  // unchanged state: e2 == e1
   } else {
-    block_reduce2<B>(x, nullptr, p.rows, 1, &sx, &sy);
-  }
-  if (threadIdx.x != 0) return;
-  ScaleLM L;
-  __builtin_memcpy(&L, hw, sizeof(hw));
-  scale_ctrl_decide(&L, lm_g->trace, p, phase, sx, sy, err_v);
-  __builtin_memcpy(hw, &L, sizeof(hw));
-  unsigned long long* dst = reinterpret_cast<unsigned long long*>(lm_g);
-#pragma unroll
-  for (int i = 0; i < kHead; ++i) dst[i] = hw[i];
-  if (p.mirror) {
-    constexpr int kPhaseWord = offsetof(ScaleLM, phase) / 8;
-#pragma unroll
-    for (int i = 0; i < kHead; ++i)
-      if (i != kPhaseWord) __hip_atomic_store(p.mirror + i, hw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(p.mirror + kPhaseWord, hw[kPhaseWord], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    lm_propose_batch(lm, sp, trace, p);
   }
 }
 
@@ -559,6 +641,7 @@ __device__ __forceinline__ void ctrl_after_eval(ScaleLM* lm, double* __restrict_
   // it only reads dX, so it is applied here with the same result)
   if (!lm->stop && sqrt(lm->dX * lm->dX) <= p.incr_tol) lm->stop = SMALL_INCREMENT;
   lm->nevals += p.n;
+  lm->nres++;
   if (p.type == 0 && (e2 - lm->e1) * (e2 - lm->e1) < p.rel_tol) lm->stop = SMALL_DECREASE_FUNCTION;
   if (lm->ntrace < kTraceCap) {
     trace[2 * lm->ntrace] = lm->e1;
@@ -578,6 +661,7 @@ __device__ __forceinline__ void ctrl_after_eval(ScaleLM* lm, double* __restrict_
     // buffer phase B reads), so phase A's body runs here without a launch.
     lm->e1 = e2;
     lm->nevals += p.n;
+    lm->nres++;
     const double mre = e2 / (double)(p.rows * 1);
     if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
     lm->phase = PH_B;
@@ -588,9 +672,9 @@ __device__ __forceinline__ void ctrl_after_eval(ScaleLM* lm, double* __restrict_
 }
 
 // The reference's scalar control for one phase, on the register copy *lm
-// (trace entries go straight to the device trace array).
-__device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restrict__ trace, const LMParams& p,
-                                                  int phase, double sx, double sy, int err) {
+// (trace entries and candidate batches go straight to device memory).
+__device__ void scale_ctrl_decide(ScaleLM* lm, ScaleSpec* __restrict__ sp, double* __restrict__ trace,
+                                  const LMParams& p, int phase, double sx, double sy, int err) {
   if (err) {  // ROI outside the image (the reference throws cv::Exception) / bad mask
     lm->err = err;
     lm->phase = PH_DONE;
@@ -600,6 +684,7 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
     case PH_A: {
       lm->e1 = sx;
       lm->nevals += p.n;
+      lm->nres++;
       const double mre = sx / (double)(p.rows * 1);
       if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
       lm->phase = PH_B;
@@ -611,6 +696,7 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
         JJ = sx;
         e = sy;
         lm->nevals += 2 * (long)p.n;
+        lm->nneq++;
       }
       if (lm->k == 0) lm->mu = JJ;
       if (sqrt(e * e) < p.grad_tol) lm->stop = SMALL_GRADIENT;
@@ -622,42 +708,44 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
         lm->scale += p.alpha * lm->dX;
         lm->phase = PH_D;
       } else {
-        lm_propose(lm, p);
+        lm->nbatch = 0;
+        lm_propose_batch(lm, sp, trace, p);
       }
       break;
     }
-    case PH_C: {
-      const double e1 = lm->e1, e2 = sx;
-      lm->nevals += p.n;
-      const double rho = (p.minim ? -1.0 : 1.0) * (e2 - e1);
-      if (rho > 0) {
-        lm->mu *= fmax(1.0 / 3.0, 1 - pow(2 * rho - 1, 3));
-        lm->v = 2;
-        const double dd = sqrt(e1) - sqrt(e2);
-        if (dd * dd < p.rel_tol * sqrt(e1)) lm->stop = SMALL_DECREASE_FUNCTION;
-        lm->scale = lm->tmp_scale;
-        // Phase D would evaluate the residuals at scale == tmp_scale: the
-        // candidate's residuals (a pure function of the same state, reduced in
-        // the same order), so its control runs here without a launch and the
-        // candidate buffer becomes the current one.
-        lm->cur ^= 1;
-        ctrl_after_eval(lm, trace, p, sx);
-      } else {
-        lm->mu *= lm->v;
-        const double v2 = 2 * lm->v;
-        if (v2 <= lm->v) {
-          lm->stop = NO_CONVERGENCE;
-          lm->phase = PH_D;
-        } else {
-          lm->v = v2;
-          lm_propose(lm, p);
-        }
-      }
+    case PH_C:
+      lm_walk_batch(lm, sp, trace, p);
       break;
-    }
     case PH_D:
       ctrl_after_eval(lm, trace, p, sx);
       break;
+  }
+}
+
+// Thread 0 of the deciding workgroup: LM header -> registers, the phase's
+// control, header back (and into the coherent host mirror, the word holding
+// `phase` last behind a system-scope release).
+__device__ void scale_ctrl_run(ScaleLM* lm_g, ScaleSpec* __restrict__ sp, const LMParams& p, int phase, double sx,
+                               double sy, int err_v) {
+  constexpr int kHead = offsetof(ScaleLM, trace) / 8;
+  static_assert(offsetof(ScaleLM, trace) % 8 == 0, "LM header is copied as 8-byte words");
+  unsigned long long hw[kHead];
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(lm_g);
+#pragma unroll
+  for (int i = 0; i < kHead; ++i) hw[i] = src[i];
+  ScaleLM L;
+  __builtin_memcpy(&L, hw, sizeof(hw));
+  scale_ctrl_decide(&L, sp, lm_g->trace, p, phase, sx, sy, err_v);
+  __builtin_memcpy(hw, &L, sizeof(hw));
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(lm_g);
+#pragma unroll
+  for (int i = 0; i < kHead; ++i) dst[i] = hw[i];
+  if (p.mirror) {
+    constexpr int kPhaseWord = offsetof(ScaleLM, phase) / 8;
+#pragma unroll
+    for (int i = 0; i < kHead; ++i)
+      if (i != kPhaseWord) __hip_atomic_store(p.mirror + i, hw[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(p.mirror + kPhaseWord, hw[kPhaseWord], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -668,28 +756,37 @@ __device__ __forceinline__ void scale_ctrl_decide(ScaleLM* lm, double* __restric
 // launch per LM phase instead of two; a launch whose phase is not the current
 // one returns at once (every workgroup reads the phase before the last one can
 // change it).
-__device__ __forceinline__ bool last_block_arrives(unsigned* cnt) {
+__device__ __forceinline__ bool last_block_arrives(unsigned* cnt, unsigned target) {
   __shared__ int slast;
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    slast = k == gridDim.x - 1;
+    slast = k == target - 1;
   }
   __syncthreads();
   return slast != 0;
 }
 
-// A residual launch serves phase A (first != 0) or whichever of C (residuals
-// at the candidate, into the buffer not holding the current residuals) and D
-// (at the accepted scale, into the current buffer) is current.
-__global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res0,
-                                                                  double* __restrict__ res1, int* __restrict__ err,
-                                                                  ScaleLM* lm, LMParams p, int first, unsigned* cnt) {
+// Residual buffer b of kResBufs (rows_pad doubles each).
+__device__ __forceinline__ double* res_buf(double* base, int rows_pad, int b) { return base + (long)b * rows_pad; }
+
+// A residual launch serves phase A (first != 0: the residuals at the start
+// state), phase C (blockIdx.y = candidate j of the batch, at ts[j], into its
+// own buffer) or phase D (GN only: the new state, into the current buffer).
+// Counters: cnt[1 + j] gathers candidate j's workgroups, its last one reduces
+// the candidate and arrives on cnt[0]; the last candidate runs the control.
+__global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, TrackDev td, double* __restrict__ resb,
+                                                                  int rows_pad, int* __restrict__ err, ScaleLM* lm,
+                                                                  ScaleSpec* __restrict__ sp, LMParams p, int first,
+                                                                  unsigned* cnt) {
   const int phase = lm->phase;
   if (first ? phase != PH_A : (phase != PH_C && phase != PH_D)) return;
-  const int cand = phase == PH_C ? 1 : 0;
-  double* res = (lm->cur ^ cand) ? res1 : res0;
-  lm_scale(a, lm, cand);
+  const int j = blockIdx.y;
+  const int ncand = phase == PH_C ? sp->n : 1;
+  if (j >= ncand) return;
+  const int cur = lm->cur;
+  double* res = res_buf(resb, rows_pad, phase == PH_C ? (cur + 1 + j) % kResBufs : cur);
+  a.scale = phase == PH_C ? sp->ts[j] : lm->scale;
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
@@ -697,30 +794,42 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
 #if ME_SCALE_EXP != 1  // timing experiments only (tools/exp): 1 = no track work
   if (t < a.nL + a.nR) residual_track(a, td, t, h, res, err);
 #endif
-  if (!last_block_arrives(cnt)) return;
+  if (!last_block_arrives(cnt + 1 + j, gridDim.x)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  scale_ctrl_body<kScBlock>(lm, p, phase, res, nullptr, err);
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double sx, sy;
+  block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + 1 + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (phase == PH_C) {
+    if (threadIdx.x == 0) sp->e2[j] = sx;
+    if (!last_block_arrives(cnt, ncand)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) scale_ctrl_run(lm, sp, p, phase, sx, 0.0, *err);
 }
 
 __global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, TrackDev td,
-                                                                  const double* __restrict__ res0,
-                                                                  const double* __restrict__ res1,
+                                                                  const double* __restrict__ resb, int rows_pad,
                                                                   double* __restrict__ jj, double* __restrict__ je,
-                                                                  int* __restrict__ err, ScaleLM* lm, LMParams p,
+                                                                  int* __restrict__ err, ScaleLM* lm,
+                                                                  ScaleSpec* __restrict__ sp, LMParams p,
                                                                   unsigned* cnt) {
   if (lm->phase != PH_B) return;
-  const double* res = lm->cur ? res1 : res0;
-  lm_scale(a, lm, 0);
+  const double* res = resb + (long)lm->cur * rows_pad;
+  a.scale = lm->scale;
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
   const int t = blockIdx.x * kTracksPerBlock + grp;
   if (!p.test && t < a.nL + a.nR) neq_track(a, td, t, h, res, jj, je, err);
-  if (!last_block_arrives(cnt)) return;
+  if (!last_block_arrives(cnt + 1, gridDim.x)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  scale_ctrl_body<kScBlock>(lm, p, PH_B, jj, je, err);
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double sx = 0, sy = 0;
+  if (!p.test) block_reduce2<kScBlock>(jj, je, p.n, 0, &sx, &sy);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    scale_ctrl_run(lm, sp, p, PH_B, sx, sy, *err);
+  }
 }
 
 // Track flags / residual rows (optimisation.cpp:157-194) from the raw track
@@ -738,21 +847,21 @@ struct PrepArgs {
   int mask_len, nL, nR, tot;
   uint32_t lframe;
   // Zeroing and LM start state folded into this launch (were two fills and an
-  // H2D copy on the stream): res | res2 rows (zero_words doubles), the error
+  // H2D copy on the stream): unowned residual rows of zero_bufs buffers, the error
   // flag | arrival counter block (kErrWords words) and, when lm != null, the
   // ScaleLM header (optimisation.cpp:29-40: scale, mu, v, phase A, no stop).
   double* zero;
-  int zero_words;
+  int zero_bufs, rows_pad;
   unsigned* err_block;
   ScaleLM* lm;
   double scale0, mu0, v0;
+  int gen;
 };
 constexpr int kPrepBlock = 1024;
 constexpr int kErrWords = 64;
 __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uint8_t* flags, int* row, int* err) {
   __shared__ int wsum[kPrepBlock / 64];
   const int n = pa.nL + pa.nR, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int i = t; i < pa.zero_words; i += kPrepBlock) pa.zero[i] = 0.0;
   if (t < kErrWords) pa.err_block[t] = 0u;
   if (pa.lm && t == 0) {
     ScaleLM* lm = pa.lm;
@@ -768,6 +877,9 @@ __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uin
     lm->ntrace = 0;
     lm->err = 0;
     lm->cur = 0;
+    lm->nres = lm->nneq = lm->nrej = 0;
+    lm->gen = pa.gen;
+    lm->nbatch = 0;
   }
   __syncthreads();  // err cleared before the scan below may set it
   auto mask_at = [&](int idx) { return !pa.mask || (idx < pa.mask_len && pa.mask[idx]); };
@@ -794,8 +906,15 @@ __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uin
   }
   if (lane == 63) wsum[wv] = x;
   __syncthreads();
-  int base = 0;
-  for (int k = 0; k < wv; ++k) base += wsum[k];
+  int base = 0, owned = 0;
+  for (int k = 0; k < kPrepBlock / 64; ++k) {
+    if (k < wv) base += wsum[k];
+    owned += wsum[k];
+  }
+  // rows no track owns (a mask selecting more rows than triangulated tracks)
+  // are never written by an evaluation: zero them in every residual buffer
+  for (int b = 0; b < pa.zero_bufs; ++b)
+    for (int i = owned + t; i < pa.tot; i += kPrepBlock) pa.zero[(long)b * pa.rows_pad + i] = 0.0;
   int r = base + x - cnt;
   for (int i = beg; i < end; ++i) {
     if (flags[i] & 1) {
@@ -817,21 +936,21 @@ struct ScaleProblem {
   TrackDev td;
   int n;        // tracks
   int rows;     // residual rows (tot_nb_elements)
-  double* res;  // device residual vector (rows)
-  double* res2;
+  double* res;  // device residual vectors: kResBufs buffers of rows_pad doubles (buffer 0 = the one-shot entry points')
+  int rows_pad;
   double* jj;
   double* je;
   double* red;  // 4 doubles
   int* err;
   unsigned* bar;  // arrival counter of the fused phase + control kernels
   ScaleLM* lm;
-  char* host;   // pinned: input staging | LM state
-  ScaleLM* hlm;
-  ScaleLM* hlm2;  // second pinned poll slot
+  ScaleSpec* spec;
+  char* host;   // pinned: input staging | read-back
 };
 
 // lm0 (me_scale_optimise only): the LM start state {scale, mu, v}, written by the prep launch
-int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, const double* lm0 = nullptr) {
+int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, const double* lm0 = nullptr,
+           int gen = 0) {
   ME_CHECK(c, s->n_left >= 0 && s->n_right >= 0, "scale: negative track count");
   ME_CHECK(c, s->window_size > 0 && s->cols > 0 && s->rows > 0 && s->stride >= s->cols, "scale: bad image / window");
   ME_CHECK(c, (2 * s->window_size + 1) * (2 * s->window_size + 1) <= 255,
@@ -870,23 +989,23 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
   a.nrows = tot;
   const size_t nn = (size_t)(n > 0 ? n : 1), nr = (size_t)(tot > 0 ? tot : 1);
   // device layout: [XL 4nL | XR 4nR][tri nL | tri nR][last nL | last nR][mask][flags n][row n]
-  //                [res rows][res2 rows][jj n][je n][red 8][err][ScaleLM]
+  //                [res: kResBufs x rows_pad][jj n][je n][red 8][err][ScaleLM][ScaleSpec]
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const bool dev = s->tracks_mem == ME_DEVICE;
   const size_t bX = 32 * nn, bTri = nn, bLast = 4 * nn, bMask = has_mask ? (size_t)s->mask_len : 1;
   const size_t oX = 0, oTri = oX + up(bX), oLast = oTri + up(bTri), oMask = oLast + up(bLast);
   const size_t in_span = oMask + up(bMask);
-  const size_t oFl = in_span, oRow = oFl + up(nn), oRes = oRow + up(4 * nn), oRes2 = oRes + up(8 * nr);
-  const size_t oJJ = oRes2 + up(8 * nr), oJE = oJJ + up(8 * nn), oRed = oJE + up(8 * nn), oErr = oRed + 256;
-  const size_t oLM = oErr + 256, total = oLM + up(sizeof(ScaleLM));
+  const size_t rows_pad = up(8 * nr) / 8;
+  const size_t nbufs = lm0 ? kResBufs : 1;
+  const size_t oFl = in_span, oRow = oFl + up(nn), oRes = oRow + up(4 * nn);
+  const size_t oJJ = oRes + nbufs * 8 * rows_pad, oJE = oJJ + up(8 * nn), oRed = oJE + up(8 * nn), oErr = oRed + 256;
+  const size_t oLM = oErr + 256, oSpec = oLM + up(sizeof(ScaleLM)), total = oSpec + up(sizeof(ScaleSpec));
   void* d;
   ME_TRY(me_scratch(c, SLOT_SC_TRACKS, total, &d));
   char* base = (char*)d;
   void* ph;
-  ME_TRY(me_pinned(c, up(in_span) + 2 * up(sizeof(ScaleLM)) + 256, &ph));
+  ME_TRY(me_pinned(c, up(in_span) + 256, &ph));
   P.host = (char*)ph;
-  P.hlm = (ScaleLM*)(P.host + up(in_span));  // separate from the input staging (async H2D)
-  P.hlm2 = (ScaleLM*)(P.host + up(in_span) + up(sizeof(ScaleLM)));
   PrepArgs pa;
   pa.mask = has_mask ? (const uint8_t*)(base + oMask) : nullptr;
   pa.mask_len = has_mask ? s->mask_len : 0;
@@ -925,23 +1044,26 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
   P.td.flags = (const uint8_t*)(base + oFl);
   P.td.row = (const int*)(base + oRow);
   P.res = (double*)(base + oRes);
-  P.res2 = (double*)(base + oRes2);
+  P.rows_pad = (int)rows_pad;
   P.jj = (double*)(base + oJJ);
   P.je = (double*)(base + oJE);
   P.red = (double*)(base + oRed);
   P.err = (int*)(base + oErr);
   P.bar = (unsigned*)(base + oErr + 64);
   P.lm = (ScaleLM*)(base + oLM);
+  P.spec = (ScaleSpec*)(base + oSpec);
   // zeroed by the prep launch: residual rows never owned by a track stay 0;
   // error flag | arrival counter; LM start state
   pa.zero = P.res;
-  pa.zero_words = (int)((oRes2 - oRes + up(8 * nr)) / 8);
+  pa.zero_bufs = (int)nbufs;
+  pa.rows_pad = (int)rows_pad;
   pa.err_block = (unsigned*)(base + oErr);
   static_assert(4 * kErrWords == 256, "error flag | arrival counter block");
   pa.lm = lm0 ? P.lm : nullptr;
   pa.scale0 = lm0 ? lm0[0] : 0.0;
   pa.mu0 = lm0 ? lm0[1] : 0.0;
   pa.v0 = lm0 ? lm0[2] : 0.0;
+  pa.gen = gen;
   hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
                      (int*)(base + oRow), P.err);
   ME_TRY(me_check_launch(c, "scale_prep_kernel"));
@@ -1093,7 +1215,6 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   }
   ScaleProblem P;
   const double lm0[3] = {s->scale, p.mu, p.v};  // initial state (set on the device by the prep launch)
-  ME_TRY(upload(c, s, p.weighting, P, lm0));
   LMParams lp;
   lp.type = p.type;
   lp.minim = p.minim;
@@ -1104,26 +1225,34 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   lp.incr_tol = p.incr_tol;
   lp.rel_tol = p.rel_tol;
   lp.alpha = p.alpha;
-  lp.rows = P.rows;
-  lp.n = P.n;
   if (!c->scale_mirror) ME_HIP(c, hipHostMalloc(&c->scale_mirror, 4096, hipHostMallocCoherent));
   constexpr size_t kHeadBytes = offsetof(ScaleLM, trace);
   static_assert(kHeadBytes <= 4096, "LM header mirror page");
   lp.mirror = (unsigned long long*)c->scale_mirror;
   volatile ScaleLM* mir = (volatile ScaleLM*)c->scale_mirror;
+  // Solve generation: launches of an earlier solve abandoned on an error path
+  // may still be queued ahead of this one and write the mirror; their header
+  // carries the older generation and is ignored (the device copy is reset by
+  // this solve's prep launch, which runs after them in stream order).
+  const int gen = ++c->scale_gen;
+  mir->gen = gen;
   mir->phase = PH_A;  // the start state (the prep launch writes the device copy)
+  ME_TRY(upload(c, s, p.weighting, P, lm0, gen));
+  lp.rows = P.rows;
+  lp.n = P.n;
   const ScaleArgs aR = with_invN(P.a, 2 * P.a.w + 1), aN = with_invN(P.a, 2 * P.a.w);
   const int nb = blocks_for(P.n);
   hipStream_t st = c->stream;
   auto res = [&](int first) {
     me_ktimer t(c, ME_KT_SCALE_RES);
-    hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aR, P.td, P.res, P.res2, P.err, P.lm,
-                       lp, first, P.bar);
+    // grid y: candidates of a batch (phase A / D use y = 0 only)
+    hipLaunchKernelGGL(scale_res_ctrl_kernel, dim3(nb, first ? 1 : kSpecMax), dim3(kScBlock), 0, st, aR, P.td, P.res,
+                       P.rows_pad, P.err, P.lm, P.spec, lp, first, P.bar);
   };
   auto neq = [&]() {
     me_ktimer t(c, ME_KT_SCALE_NEQ);
     hipLaunchKernelGGL(scale_neq_ctrl_kernel, dim3(nb), dim3(kScBlock), 0, st, aN, P.td, (const double*)P.res,
-                       (const double*)P.res2, P.jj, P.je, P.err, P.lm, lp, P.bar);
+                       P.rows_pad, P.jj, P.je, P.err, P.lm, P.spec, lp, P.bar);
   };
   // The LM is enqueued in blocks [A,] B, R, B, R (one launch per LM phase, the
   // control fused into the last workgroup; R = a residual launch serving
@@ -1139,6 +1268,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   // slower: 610 vs 641 frames/s -- its merged register budget spills.)
   const long max_blocks = 64L * (p.max_nb_iter + 2);
   long blk = 0;
+  auto mine = [&]() { return mir->gen == gen; };
   // Phase A is launched only in the first block: later iterations take their
   // residuals from the previous evaluation (same state, see ctrl_after_eval).
   // While the mirror shows a rejection streak (phase C: every retry is one
@@ -1146,7 +1276,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   // (stale) read: every launch still runs the phase that is current.
   auto enqueue_block = [&](int sl) -> int {
     if (blk == 0) res(1);
-    const bool retrying = blk > 0 && mir->phase == PH_C;
+    const bool retrying = blk > 0 && mine() && mir->phase == PH_C;
     retrying ? res(0) : neq();
     res(0);
     retrying ? res(0) : neq();
@@ -1156,29 +1286,41 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     ME_HIP(c, hipEventRecord(c->poll_ev[sl], st));
     return ME_OK;
   };
-  ME_TRY(enqueue_block(0));
+  // Error exits after launches were queued drain the stream first, so no
+  // launch of this solve is left to run behind the caller's next call.
+  auto drain = [&](int rc) {
+    (void)hipStreamSynchronize(st);
+    return rc;
+  };
+  if (int rc = enqueue_block(0)) return drain(rc);
   int cur = 0;
+  // Spin budget before the poll loop yields the core between polls: a solve
+  // queued behind other work on the stream (e.g. a pipelined BA) would
+  // otherwise burn a host core for that work's whole duration.
+  constexpr int kSpinsBeforeYield = 4096;
   for (;; cur ^= 1) {
     const bool more = blk < max_blocks;
-    if (more) ME_TRY(enqueue_block(cur ^ 1));
+    if (more)
+      if (int rc = enqueue_block(cur ^ 1)) return drain(rc);
     // Spin on the mirror and the block's event (no sleeping wait: its wake-up
     // latency exceeded a block's ~60 us and idled the stream).  PH_DONE ends
     // the wait at once; the finished solve's queued launches return at once.
     bool done = false;
-    for (;;) {
-      if (mir->phase == PH_DONE) {
+    for (int spins = 0;; ++spins) {
+      if (mine() && mir->phase == PH_DONE) {
         done = true;
         break;
       }
       const hipError_t q = hipEventQuery(c->poll_ev[cur]);
       if (q == hipSuccess) break;
-      if (q != hipErrorNotReady) ME_HIP(c, q);
+      if (q != hipErrorNotReady) return drain(me_set_error(c, ME_ERR_HIP, "scale optimise: %s", hipGetErrorString(q)));
+      if (spins >= kSpinsBeforeYield) std::this_thread::yield();
     }
-    if (done || mir->phase == PH_DONE) break;
-    if (!more) return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
+    if (done || (mine() && mir->phase == PH_DONE)) break;
+    if (!more) return drain(me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate"));
   }
   std::atomic_thread_fence(std::memory_order_acquire);  // phase read before the rest of the header
-  ScaleLM& hs = *P.hlm;
+  ScaleLM hs;
   std::memcpy(&hs, c->scale_mirror, kHeadBytes);
   if (hs.err) return check_err(c, hs.err);
   const int nt = std::min(std::min(hs.ntrace, kTraceCap), std::max(trace_cap, 0));
@@ -1190,6 +1332,17 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   if (stop_out) *stop_out = hs.stop;
   if (iterations) *iterations = hs.ntrace;
   if (mi_evals) *mi_evals = hs.nevals;
+  c->scale_counters[0] = hs.nres;
+  c->scale_counters[1] = hs.nneq;
+  c->scale_counters[2] = hs.nrej;
+  return ME_OK;
+}
+
+extern "C" int me_scale_last_counters(me_ctx* c, long* res_evals, long* neq_evals, long* rejections) {
+  if (!c) return ME_ERR_INVALID;
+  if (res_evals) *res_evals = c->scale_counters[0];
+  if (neq_evals) *neq_evals = c->scale_counters[1];
+  if (rejections) *rejections = c->scale_counters[2];
   return ME_OK;
 }
 

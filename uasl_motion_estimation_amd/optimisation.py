@@ -52,6 +52,20 @@ class OptimisationParams:
     alpha: float = 1.0
     weighting: bool = False
 
+    @staticmethod
+    def fixed_iterations(n: int = 10) -> "OptimisationParams":
+        """The bench frame's scale LM (10 iterations, no time or
+        tolerance stop): LM, MAX_NB_ITER = n, abs/grad/incr/rel tolerances 0.
+        The reference loop still ends early by SMALL_INCREMENT once mu has
+        grown until the step is exactly 0 (optimisation.cpp:694-697)."""
+        return OptimisationParams(MAX_NB_ITER=n, abs_tol=0.0, grad_tol=0.0, incr_tol=0.0, rel_tol=0.0)
+
+    def oracle_kw(self) -> dict:
+        """The same parameters as keyword arguments of tests/oracle.py's optim_params."""
+        return dict(type=int(self.type), minim=int(self.minim), max_nb_iter=int(self.MAX_NB_ITER), v=self.v,
+                    tau=self.tau, mu=self.mu, abs_tol=self.abs_tol, grad_tol=self.grad_tol, incr_tol=self.incr_tol,
+                    rel_tol=self.rel_tol, alpha=self.alpha, weighting=int(self.weighting))
+
     def to_c(self) -> OptimParamsC:
         p = OptimParamsC()
         p.type, p.minim, p.max_nb_iter = int(self.type), int(self.minim), int(self.MAX_NB_ITER)
@@ -154,8 +168,11 @@ def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx
     ctx.check(ctx.lib.me_scale_optimise(ctx.h, byref(s), byref(p), int(test), byref(stop), byref(it), _p(trace), 400,
                                         byref(nmi)), "me_scale_optimise")
     n = min(it.value, 400)
+    nres, nneq, nrej = c_long(), c_long(), c_long()
+    ctx.check(ctx.lib.me_scale_last_counters(ctx.h, byref(nres), byref(nneq), byref(nrej)), "me_scale_last_counters")
     return dict(stop=StopCondition(stop.value), scale=s.scale, iterations=it.value,
-                trace=trace[:2 * n].reshape(-1, 2), track_evals=nmi.value)
+                trace=trace[:2 * n].reshape(-1, 2), track_evals=nmi.value, res_evals=nres.value,
+                neq_evals=nneq.value, rejections=nrej.value)
 
 
 def scale_inliers(sp, threshold: float, weighting=False, ctx: Context | None = None) -> np.ndarray:

@@ -309,14 +309,28 @@ class StereoFrame:
     t: np.ndarray
 
 
-def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: int = 0):
+def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: int = 0, render_div: int = 1):
+    """Stereo keyframes of the synthetic trajectory.  render_div > 1 renders
+    each image at 1/render_div resolution and replicates pixels (4K test
+    inputs in seconds instead of minutes; the geometry -- intrinsics, poses,
+    depth_at -- stays at full resolution)."""
     scene = make_scene(seed)
     K = intrinsics(width, height)
     lut = tone_map()
     frames = []
+    d = max(1, int(render_div))
+    w_r, h_r = -(-width // d), -(-height // d)
+    K_r = intrinsics(w_r, h_r)
+
+    def rend(R, t, shift=0.0):
+        if d == 1:
+            return render(scene, K, R, t, width, height, shift=shift)
+        img = render(scene, K_r, R, t, w_r, h_r, shift=shift)
+        return np.ascontiguousarray(np.kron(img, np.ones((d, d), np.uint8))[:height, :width])
+
     for (R, t) in trajectory(n_frames, first_id):
-        L = render(scene, K, R, t, width, height)
-        Rraw = render(scene, K, R, t, width, height, shift=BASELINE)
+        L = rend(R, t)
+        Rraw = rend(R, t, shift=BASELINE)
         frames.append(StereoFrame(L, lut[Rraw], R, t))
     return scene, K, frames
 
