@@ -39,7 +39,11 @@ def parse():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--frames", type=int, default=4, help="distinct synthetic frames cycled per rank")
     ap.add_argument("--ba-iters", type=int, default=10)
-    ap.add_argument("--cpu-frames", type=int, default=48, help="frames of the bounded CPU-baseline sample (~10 s)")
+    ap.add_argument("--scale-iters", type=int, default=10,
+                    help="MAX_NB_ITER of the frame's scale LM; tolerances off (SURVEY 8d frame definition)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="runs of the 1-thread CPU-baseline sample (median)")
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="processes of the all-cores CPU figure (0: the host cores this process may use, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lib", default=None, help="development A/B only: load this libme_hip.so build")
     ap.add_argument("--vo-matches", type=int, default=2000,
@@ -60,6 +64,22 @@ def parse():
 
 class FrameData:
     pass
+
+
+SCALE_ITERS = 10  # the frame's scale-LM MAX_NB_ITER (set from --scale-iters)
+
+
+def scale_counters(ctx, stats):
+    """Per-solve LM counters (me_scale_last_counters) into the frame statistics."""
+    v = [ctypes.c_long() for _ in range(4)]
+    ctx.check(ctx.lib.me_scale_last_counters(ctx.h, *[ctypes.byref(x) for x in v]), "me_scale_last_counters")
+    stats["scale_res_evals"] += v[0].value
+    stats["scale_rejections"] += v[2].value
+    stats["scale_executed"] += v[3].value
+
+
+def new_stats():
+    return dict(frames=0, ba_iters=0, scale_iters=0, scale_res_evals=0, scale_rejections=0, scale_executed=0)
 
 
 def make_frames(cfg: dict, seed: int, n_frames: int):
@@ -121,7 +141,7 @@ class _Calls:
         self.keep = []
         self.sc = scale_struct(fd.scale, self.keep, ME_DEVICE, (fd.d_curL, fd.d_curR), fd.dscale.d)
         self.scale0 = self.sc.scale
-        self.sp = OptimisationParams().to_c()
+        self.sp = OptimisationParams.fixed_iterations(SCALE_ITERS).to_c()
         self.stop, self.it, self.nmi = ctypes.c_int(), ctypes.c_int(), ctypes.c_long()
         self.scale = (ctx.h, ctypes.byref(self.sc), ctypes.byref(self.sp), 0, ctypes.byref(self.stop),
                       ctypes.byref(self.it), None, 0, ctypes.byref(self.nmi))
@@ -154,6 +174,7 @@ def back_end(ctx, fd, kp, ba_opts, stats):
     c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
     ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
     stats["scale_iters"] += c.it.value
+    scale_counters(ctx, stats)
     fd.dba.reset()  # same starting point every time the frame is replayed (device copy)
     ctx.check(lib.me_ba_solve(*c.ba), "me_ba_solve")
     stats["ba_iters"] += c.bs.iterations
@@ -217,6 +238,7 @@ class FramePipeline:
             c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
             ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
             stats["scale_iters"] += c.it.value
+            scale_counters(ctx, stats)
             if t + 1 < n:  # issued once the scale LM is done: it overlaps the BA's latency-bound kernels
                 self._klt(frames[(first + t + 1) % len(frames)], kp, ba_opts, t + 1)
             if pend is not None:  # frame t-1's BA finished before this scale LM ran (same stream)
@@ -232,15 +254,84 @@ class FramePipeline:
         stats["frames"] += 1
 
 
-def cpu_step(fd, ba_iters, stats):
+def cpu_payload(fd):
+    """The host inputs of one frame (what the oracle leg needs; picklable)."""
+    return (fd.prev, fd.cur.left, fd.klt_pts, fd.scale, fd.ba)
+
+
+def cpu_frame(payload, ba_iters, scale_iters):
+    """One frame on the CPU restatement (oracle/, 1 thread): KLT, scale LM, BA.
+    Returns its outputs (the parity leg compares them with the GPU's)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle as O  # CPU baseline leg only
+    from uasl_motion_estimation_amd.optimisation import OptimisationParams
 
-    O.klt(fd.prev, fd.cur.left, fd.klt_pts)
-    O.scale_optimise(fd.scale)
-    _, _, s = O.ba_solve(fd.ba, max_num_iterations=ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
-                         parameter_tolerance=0.0)
-    stats["ba_iters"] += s["iterations"]
+    prev, cur, pts, sp, bp = payload
+    kp, kst = O.klt(prev, cur, pts)
+    sc = O.scale_optimise(sp, **OptimisationParams.fixed_iterations(scale_iters).oracle_kw())
+    cams, pps, s = O.ba_solve(bp, max_num_iterations=ba_iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                              parameter_tolerance=0.0)
+    return dict(klt=kp, klt_status=kst, scale=sc, cams=cams, pts=pps, ba=s)
+
+
+def _cpu_worker(args):
+    """All-cores leg: one process runs its frames back to back (spawned before
+    this bench touched the GPU)."""
+    payloads, ba_iters, scale_iters = args
+    t0 = time.perf_counter()
+    for pl in payloads:
+        cpu_frame(pl, ba_iters, scale_iters)
+    return len(payloads), time.perf_counter() - t0
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        avail = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, avail
+
+
+def gpu_outputs(ctx, fd):
+    """Outputs of the last timed replay of a frame, read back after the timed
+    region: KLT points/status (device buffers), the scale LM result (the
+    frame's argument block) and the BA window (device-resident problem)."""
+    n = len(fd.klt_pts)
+    kp = np.zeros((n, 2), np.float32)
+    kst = np.zeros(n, np.uint8)
+    ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, kp.ctypes.data, ctypes.c_void_p(fd.d_pts_out), kp.nbytes))
+    ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, kst.ctypes.data, ctypes.c_void_p(fd.d_status), kst.nbytes))
+    c = fd._calls[id(ctx)]
+    cams, pts = fd.dba.download()
+    return dict(klt=kp, klt_status=kst, scale=dict(stop=c.stop.value, iterations=c.it.value, scale=c.sc.scale),
+                cams=cams, pts=pts, ba=dict(iterations=c.bs.iterations, successful_steps=c.bs.successful_steps))
+
+
+def compare(g, o):
+    """Parity bars of the tests (tests/test_gpu_configs.py) on one frame."""
+    klt = bool(np.array_equal(g["klt_status"], o["klt_status"])
+               and np.array_equal(g["klt"].view(np.uint32), np.asarray(o["klt"], np.float32).view(np.uint32)))
+    gs, os_ = g["scale"], o["scale"]
+    scale = (gs["stop"] == os_["stop"] and gs["iterations"] == os_["iterations"]
+             and abs(gs["scale"] - os_["scale"]) <= 1e-9 * abs(os_["scale"]))
+
+    def rel(a, b):
+        return float(np.max(np.abs(a - b) / (np.abs(b) + 1e-3)))  # 1e-6 rel with a 1e-9 floor ~ this at |b| >= 1e-3
+
+    ba_ok = (g["ba"]["iterations"] == o["ba"]["iterations"]
+             and g["ba"]["successful_steps"] == o["ba"]["successful_steps"]
+             and np.allclose(g["cams"], o["cams"], rtol=1e-6, atol=1e-9)
+             and np.allclose(g["pts"], o["pts"], rtol=1e-6, atol=1e-9))
+    return dict(klt_bit_exact=klt, scale_match=bool(scale), ba_match=bool(ba_ok),
+                ba_max_rel=max(rel(g["cams"], o["cams"]), rel(g["pts"], o["pts"])))
 
 
 # Algorithmic work per launch of each kernel family (DESIGN.md §5): (bound,
@@ -386,12 +477,12 @@ def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
         f = make_frames(cfg, seed + 7919 * (k + 1), args.frames)
         upload_images(c, f)
         fr.append(f)
-    stats = [dict(frames=0, ba_iters=0, scale_iters=0) for _ in range(S_)]
+    stats = [new_stats() for _ in range(S_)]
     for k in range(S_):
         for i in range(args.warmup):
             gpu_step(ctxs[k], fr[k][i % len(fr[k])], kp, ba_opts, stats[k])
         ctxs[k].synchronize()
-    stats = [dict(frames=0, ba_iters=0, scale_iters=0) for _ in range(S_)]
+    stats = [new_stats() for _ in range(S_)]
     errs = []
 
     def run(k):
@@ -418,10 +509,20 @@ def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
 
 
 def main():
+    global SCALE_ITERS
     args = parse()
+    SCALE_ITERS = args.scale_iters
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    pool = None
+    model, ncpu, avail = host_cpu()
+    cpu_workers = args.cpu_workers or min(16, avail)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_workers > 1:
+        # all-cores CPU leg: worker processes started before anything touches the GPU
+        import multiprocessing as mp
+
+        pool = mp.get_context("spawn").Pool(cpu_workers)
     import torch
 
     dist = None
@@ -455,7 +556,7 @@ def main():
 
     fam_names = ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_POINTS", "BA_SCHUR", "BA_SOLVE", "BA_STEP",
                  "KLT", "PYR")
-    stats = dict(frames=0, ba_iters=0, scale_iters=0)
+    stats = new_stats()
     for i in range(args.warmup):
         gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
     ctx.synchronize()
@@ -463,25 +564,40 @@ def main():
     if not args.no_pipeline:
         tctx = Context(local_rank)  # tracker context: its own HIP stream and scratch
         pipe = FramePipeline(ctx, tctx, _Hip())
-        pipe.run(frames, max(args.warmup, 2), kp, ba_opts, dict(frames=0, ba_iters=0, scale_iters=0))
+        pipe.run(frames, max(args.warmup, 2), kp, ba_opts, new_stats())
         tctx.synchronize()
         ctx.synchronize()
     # untimed profile steps with every family timed: per-family device time and
     # the dominant family (by device time) among those with a roofline
     ctx.timing_reset()
     ctx.timing(True)
+    pstats = new_stats()
     for i in range(args.profile_steps):
-        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
+        gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, pstats)
     ctx.synchronize()
     ctx.timing(False)
     prof = {f: ctx.timing_read(f) for f in fam_names}
     rl = {f: alg_work(f, cfg, frames) for f in fam_names if prof[f][0] > 0}
+    npf = max(1, pstats["frames"])
+    # per-frame device-time budget of every family (the latency-bound ones included)
+    budget = {f: {"launches_per_frame": round(prof[f][0] / npf, 2), "us_per_launch": round(1e3 * prof[f][1] / prof[f][0], 2),
+                  "us_per_frame": round(1e3 * prof[f][1] / npf, 1)} for f in fam_names if prof[f][0] > 0}
+    # the MI that runs in the frame (scale LM residual launches, speculative candidates included):
+    # 262 algorithmic bytes per executed track evaluation
+    mi_in_frame = None
+    if prof["SCALE_RES"][0] > 0:
+        b = 262.0 * cfg["n_feats"] * pstats["scale_executed"]
+        a_gbs = b / (prof["SCALE_RES"][1] * 1e-3) / 1e9
+        mi_in_frame = {"bound": "hbm", "achieved": round(a_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                       "frac": round(a_gbs / PEAK_HBM_GBS, 5), "kernel": "scale_res_ctrl_kernel",
+                       "track_evaluations_per_frame": round(cfg["n_feats"] * pstats["scale_executed"] / npf, 1),
+                       "us_per_frame": budget["SCALE_RES"]["us_per_frame"]}
     dom = max((f for f in rl if rl[f] is not None), key=lambda f: prof[f][1])
     # timed region: HIP events on the ctx stream around the dominant family only
     ctx.timing_reset()
     if args.timing != "none":
         ctx.timing(True, None if args.timing == "all" else [dom])
-    stats = dict(frames=0, ba_iters=0, scale_iters=0)
+    stats = new_stats()
     barrier()
     torch.cuda.synchronize()
     ctx.synchronize()
@@ -511,6 +627,8 @@ def main():
     value = frames_total / t_max
     bound, amount, unit, peak = rl[dom]
     n_l, ms_l = fams[dom] if fams[dom][0] > 0 else prof[dom]
+    if dom == "SCALE_RES":  # executed evaluations per launch (speculative candidate batches)
+        amount = 262.0 * cfg["n_feats"] * (stats if fams[dom][0] > 0 else pstats)["scale_executed"] / n_l
     avg_ms = ms_l / n_l
     scale_u = 1e9 if unit == "GB/s" else 1e12
     achieved = amount / (avg_ms * 1e-3) / scale_u
@@ -522,18 +640,48 @@ def main():
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
     vo_line = stereo_vo_line(ctx, args.vo_matches, cpu=rank == 0 and world == 1 and not args.no_cpu_baseline) \
         if args.vo_matches > 0 else None
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cstats = dict(ba_iters=0)
-        t1 = time.perf_counter()
-        nf = max(1, args.cpu_frames)
-        for i in range(nf):
-            cpu_step(frames[i % len(frames)], args.ba_iters, cstats)
-        ct = time.perf_counter() - t1
-        cpu = {"value": round(nf / ct, 4), "unit": "frames/s", "cores": 1, "kind": "port",
-               "sample": f"{nf} config-{args.config} frames (KLT + MI scale LM + {args.ba_iters}-iteration BA) on the "
-                         f"oracle restatement, 1 thread; {ct:.1f} s",
-               "ba_iter_per_s": round(cstats['ba_iters'] / ct, 3)}
+        # parity of the timed frames: the last timed replay of each distinct
+        # frame (read back after the timed region) against the oracle
+        outs = [cpu_frame(cpu_payload(fd), args.ba_iters, args.scale_iters) for fd in frames]
+        cmp = [compare(gpu_outputs(ctx, fd), o) for fd, o in zip(frames, outs)]
+        parity = {"frames_checked": len(cmp), "klt_bit_exact": all(c["klt_bit_exact"] for c in cmp),
+                  "scale_match": all(c["scale_match"] for c in cmp), "ba_match": all(c["ba_match"] for c in cmp),
+                  "ba_max_rel_diff": float("%.3g" % max(c["ba_max_rel"] for c in cmp))}
+        parity["ok"] = parity["klt_bit_exact"] and parity["scale_match"] and parity["ba_match"]
+        # 1 thread: median of cpu_runs runs over the distinct frames (one warm-up frame first)
+        pls = [cpu_payload(fd) for fd in frames]
+        cpu_frame(pls[0], args.ba_iters, args.scale_iters)
+        rates, tot_t, tot_f, ba_it = [], 0.0, 0, 0
+        for _ in range(max(1, args.cpu_runs)):
+            t1 = time.perf_counter()
+            for pl in pls:
+                ba_it += cpu_frame(pl, args.ba_iters, args.scale_iters)["ba"]["iterations"]
+            dt = time.perf_counter() - t1
+            rates.append(len(pls) / dt)
+            tot_t += dt
+            tot_f += len(pls)
+        cpu = {"value": round(float(np.median(rates)), 4), "unit": "frames/s", "cores": 1, "kind": "port",
+               "sample": f"median of {len(rates)} runs x {len(pls)} config-{args.config} frames (KLT + MI scale LM "
+                         f"(<= {args.scale_iters} it.) + {args.ba_iters}-iteration BA) on the oracle restatement, "
+                         f"1 thread, after 1 warm-up frame; {tot_t:.1f} s",
+               "runs_frames_per_s": [round(r, 4) for r in rates],
+               "ba_iter_per_s": round(ba_it / tot_t, 3), "cpu_model": model, "nproc": ncpu,
+               "cores_available": avail}
+        if pool is not None:
+            per = [(pls * 2, args.ba_iters, args.scale_iters)] * cpu_workers
+            t1 = time.perf_counter()
+            res = pool.map(_cpu_worker, per)
+            wall = time.perf_counter() - t1
+            nf_all = sum(r[0] for r in res)
+            cpu["all_cores"] = {"value": round(nf_all / wall, 3), "unit": "frames/s", "cores": cpu_workers,
+                                "sample": f"{cpu_workers} processes x {2 * len(pls)} frames (independent frames, "
+                                          f"one process per core: an upper bound for a multi-threaded CPU path); "
+                                          f"{wall:.1f} s"}
+    if pool is not None:
+        pool.close()
+        pool.join()
     if rank == 0:
         out = {
             "metric": "frames/sec + BA iter/sec, 2000 feats x 20-keyframe window, 1/2/4/8 MI355X",
@@ -550,17 +698,24 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"config {args.config}: {cfg['width']}x{cfg['height']} stereo, "
                                    f"{cfg['n_feats']} feats, {cfg['window']}-keyframe window, 11x11 MI patches",
-                       "frame": f"KLT + MI scale LM + {args.ba_iters} BA LM iterations",
+                       "frame": f"KLT + MI scale LM (LM, MAX_NB_ITER {args.scale_iters}, tolerances off) + "
+                                f"{args.ba_iters} BA LM iterations",
                        "parallelism": f"{world} independent streams (one per GPU)",
                        "pipeline": None if pipe is None else "KLT of frame t+1 overlaps the BA of frame t "
                                                              "(two HIP streams, event dependency per frame)"},
             "ba_iter_per_s": round(ba_total / t_max, 2),
+            "scale_lm_per_frame": {k: round(stats[k2] / max(1, stats["frames"]), 3) for k, k2 in
+                                   (("iterations", "scale_iters"), ("residual_evaluations", "scale_res_evals"),
+                                    ("rejections", "scale_rejections"), ("executed_evaluations", "scale_executed"))},
+            "parity": parity,
             "roofline": roofline,
             "mi_roofline": mi_rl,
             "multi_stream": multi,
             "stereo_vo": vo_line,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
+            "kernel_budget_per_frame": budget,
+            "mi_in_frame": mi_in_frame,
             "gen_s": round(gen_s, 1),
         }
         print(json.dumps(out))

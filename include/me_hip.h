@@ -158,8 +158,9 @@ int me_scale_optimise(me_ctx* ctx, me_scale_state* s, const me_optim_params* p, 
    terms (optimisation.cpp:29-147, :685-730): compute_residuals calls,
    compute_normal_equations calls and rejected LM candidates (the else branch
    of run_LM_step, :719-727).  An evaluation the device skips because its
-   result is already known (same state) still counts. */
-int me_scale_last_counters(me_ctx* ctx, long* res_evals, long* neq_evals, long* rejections);
+   result is already known (same state) still counts.  executed = residual
+   evaluations the device actually ran (speculative candidates included). */
+int me_scale_last_counters(me_ctx* ctx, long* res_evals, long* neq_evals, long* rejections, long* executed);
 /* Optimiser::compute_inliers (optimisation.cpp:732-747): row indices. */
 int me_scale_inliers(me_ctx* ctx, const me_scale_state* s, int weighting, double threshold, int* idx, int cap,
                      int* n_out);

@@ -184,7 +184,7 @@ def load_library(path: str = LIB_PATH):
         "me_scale_jacobian": (c_int, [c_void_p, P(ScaleStateC), c_int, P(c_double)]),
         "me_scale_optimise": (c_int, [c_void_p, P(ScaleStateC), P(OptimParamsC), c_int, P(c_int), P(c_int),
                                       P(c_double), c_int, P(c_long)]),
-        "me_scale_last_counters": (c_int, [c_void_p, P(c_long), P(c_long), P(c_long)]),
+        "me_scale_last_counters": (c_int, [c_void_p, P(c_long), P(c_long), P(c_long), P(c_long)]),
         "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
         "me_ba_default_options": (None, [P(BAOptionsC)]),
         "me_ba_solve": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), P(BASummaryC)]),

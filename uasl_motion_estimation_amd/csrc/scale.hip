@@ -70,6 +70,7 @@ struct ScaleLM {
   int nres, nneq, nrej;
   int gen;     // solve generation (host-chosen): the host ignores a mirror written by an older solve
   int nbatch;  // candidate batches proposed in the current outer iteration
+  int nexec;   // residual evaluations actually run on the device (A, every evaluated candidate, GN's D)
   double trace[2 * kTraceCap];
 };
 
@@ -685,6 +686,7 @@ __device__ void scale_ctrl_decide(ScaleLM* lm, ScaleSpec* __restrict__ sp, doubl
       lm->e1 = sx;
       lm->nevals += p.n;
       lm->nres++;
+      lm->nexec++;
       const double mre = sx / (double)(p.rows * 1);
       if (mre < p.abs_tol) lm->stop = SMALL_REPROJ_ERROR;
       lm->phase = PH_B;
@@ -714,9 +716,11 @@ __device__ void scale_ctrl_decide(ScaleLM* lm, ScaleSpec* __restrict__ sp, doubl
       break;
     }
     case PH_C:
+      lm->nexec += sp->n;
       lm_walk_batch(lm, sp, trace, p);
       break;
     case PH_D:
+      lm->nexec++;
       ctrl_after_eval(lm, trace, p, sx);
       break;
   }
@@ -880,6 +884,7 @@ __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uin
     lm->nres = lm->nneq = lm->nrej = 0;
     lm->gen = pa.gen;
     lm->nbatch = 0;
+    lm->nexec = 0;
   }
   __syncthreads();  // err cleared before the scan below may set it
   auto mask_at = [&](int idx) { return !pa.mask || (idx < pa.mask_len && pa.mask[idx]); };
@@ -1335,14 +1340,17 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   c->scale_counters[0] = hs.nres;
   c->scale_counters[1] = hs.nneq;
   c->scale_counters[2] = hs.nrej;
+  c->scale_counters[3] = hs.nexec;
   return ME_OK;
 }
 
-extern "C" int me_scale_last_counters(me_ctx* c, long* res_evals, long* neq_evals, long* rejections) {
+extern "C" int me_scale_last_counters(me_ctx* c, long* res_evals, long* neq_evals, long* rejections,
+                                      long* executed) {
   if (!c) return ME_ERR_INVALID;
   if (res_evals) *res_evals = c->scale_counters[0];
   if (neq_evals) *neq_evals = c->scale_counters[1];
   if (rejections) *rejections = c->scale_counters[2];
+  if (executed) *executed = c->scale_counters[3];
   return ME_OK;
 }
 

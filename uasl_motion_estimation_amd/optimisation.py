@@ -168,11 +168,12 @@ def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx
     ctx.check(ctx.lib.me_scale_optimise(ctx.h, byref(s), byref(p), int(test), byref(stop), byref(it), _p(trace), 400,
                                         byref(nmi)), "me_scale_optimise")
     n = min(it.value, 400)
-    nres, nneq, nrej = c_long(), c_long(), c_long()
-    ctx.check(ctx.lib.me_scale_last_counters(ctx.h, byref(nres), byref(nneq), byref(nrej)), "me_scale_last_counters")
+    nres, nneq, nrej, nexe = c_long(), c_long(), c_long(), c_long()
+    ctx.check(ctx.lib.me_scale_last_counters(ctx.h, byref(nres), byref(nneq), byref(nrej), byref(nexe)),
+              "me_scale_last_counters")
     return dict(stop=StopCondition(stop.value), scale=s.scale, iterations=it.value,
                 trace=trace[:2 * n].reshape(-1, 2), track_evals=nmi.value, res_evals=nres.value,
-                neq_evals=nneq.value, rejections=nrej.value)
+                neq_evals=nneq.value, rejections=nrej.value, executed_evals=nexe.value)
 
 
 def scale_inliers(sp, threshold: float, weighting=False, ctx: Context | None = None) -> np.ndarray:
