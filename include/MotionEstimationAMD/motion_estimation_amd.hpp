@@ -9,6 +9,11 @@
 //   me::nonMaxSupScanline3x3      <- include/MotionEstimation/core/feature_types.h:270
 //   me::optimisation::BundleAdjuster<M> (StereoBundleAdjuster = <4>, MonoBundleAdjuster = <2>)
 //                                 <- BundleAdjuster<M> (include/MotionEstimation/optimisation/BundleAdjuster.h:182-528)
+//   me::optimisation::Optimiser<ScaleState, std::vector<std::pair<ImageView, ImageView>>>, ScaleState
+//                                 <- include/MotionEstimation/optimisation/optimisation.h:20-125
+//   me::StereoVisualOdometry      <- include/MotionEstimation/vo/StereoVisualOdometry.h:18-60
+//   me::amd::flatten_scale_state  the reference-side glue of INTEGRATION.md §3 (templated on the
+//                                 reference's own ScaleState / m_obs / mask types)
 // Errors: the reference asserts on empty input (mutual_information.cpp:57);
 // here invalid input throws std::invalid_argument, device/runtime failures
 // throw std::runtime_error.  BundleAdjuster misuse reports through std::cerr
@@ -63,6 +68,7 @@ struct ImageView {
   int rows = 0, cols = 0;
   int step = 0;  // bytes per row
   bool empty() const { return !data || rows <= 0 || cols <= 0; }
+  const uint8_t* ptr() const { return data; }  // cv::Mat::ptr()
 };
 
 }  // namespace amd
@@ -250,4 +256,405 @@ using StereoBundleAdjuster = BundleAdjuster<4>;
 using MonoBundleAdjuster = BundleAdjuster<2>;
 
 }  // namespace optimisation
+}  // namespace me
+
+// ===========================================================================
+// ScaleState optimiser (A4-A9), the stacked state MI (A7), StereoVO (A19),
+// KLT (A12).
+// ===========================================================================
+namespace me {
+namespace amd {
+
+// Host arrays behind a flattened me_scale_state (kept alive by the caller
+// for as long as the struct is used).
+struct ScaleStateBuffers {
+  std::vector<double> XL, XR;
+  std::vector<uint8_t> triL, triR, mask;
+  std::vector<uint32_t> lastL, lastR;
+};
+
+namespace detail {
+template <class M>
+inline int row_stride(const M& m) {
+  return static_cast<int>(static_cast<size_t>(m.step));  // cv::Mat::step (MStep -> size_t) or ImageView::step
+}
+template <class Track>
+inline void flatten_tracks(const std::vector<Track>& v, std::vector<double>& X, std::vector<uint8_t>& tri,
+                           std::vector<uint32_t>& last) {
+  X.resize(4 * v.size());
+  tri.resize(v.size());
+  last.resize(v.size());
+  for (size_t i = 0; i < v.size(); ++i) {
+    const auto pt = v[i].get3DLocation();  // ptH3D (cv::Matx41d)
+    for (int k = 0; k < 4; ++k) X[4 * i + k] = pt(k);
+    tri[i] = v[i].isTriangulated() ? 1 : 0;
+    last[i] = v[i].getLastFrameIdx();
+  }
+}
+template <class Pose>
+inline void flatten_pose(const Pose& p, double q[4], double t[3]) {
+  q[0] = p.orientation.w();
+  q[1] = p.orientation.x();
+  q[2] = p.orientation.y();
+  q[3] = p.orientation.z();
+  for (int k = 0; k < 3; ++k) t[k] = p.position[k];
+}
+}  // namespace detail
+
+// The flattening step of the reference-side binding: a
+// ScaleState (optimisation.h:76-98) + its observations m_obs
+// (vector<pair<cv::Mat, cv::Mat>>) + the optional mask (Eigen::VectorXi) ->
+// me_scale_state.  Templated on the reference's own types; it uses only the
+// members they have:
+//   state.pts.{first,second}[i].get3DLocation()(k) / .isTriangulated() / .getLastFrameIdx()
+//     (WBA_Ptf, feature_types.h:121-197)
+//   state.poses.{first,second}: [0].ID, .size(), .back().orientation.w()..z(), .back().position[k]
+//     (CamPose_qd, feature_types.h:202-230; Quat::w() etc., rotation_utils.h:183-186)
+//   state.K.{first,second}(r, c) (cv::Matx33d), state.scale, state.baseline, state.window_size
+//   obs[f].first / .second: .ptr(), .step, .cols, .rows (cv::Mat, CV_8U)
+//   mask.size(), mask(i) (Eigen::VectorXi)
+// The frame is m_obs[poses.first.size() - 1] (optimisation.cpp:174), the
+// residual bounds use m_obs[0].first.cols and m_obs[1].first.rows (:155), and
+// lframe = poses.first[0].ID + poses.first.size() - 1 (:165).
+template <class State, class Obs, class Mask>
+inline void flatten_scale_state(const State& st, const Obs& obs, const Mask& mask, me_scale_state* s,
+                                ScaleStateBuffers& buf) {
+  if (st.poses.first.empty() || st.poses.second.empty())
+    throw std::invalid_argument("flatten_scale_state: empty pose window");
+  const size_t f = st.poses.first.size() - 1;
+  if (obs.size() < 2 || obs.size() <= f)
+    throw std::invalid_argument("flatten_scale_state: m_obs must hold the window's image pairs (>= 2)");
+  *s = me_scale_state{};
+  detail::flatten_tracks(st.pts.first, buf.XL, buf.triL, buf.lastL);
+  detail::flatten_tracks(st.pts.second, buf.XR, buf.triR, buf.lastR);
+  s->n_left = (int)st.pts.first.size();
+  s->n_right = (int)st.pts.second.size();
+  s->X_left = buf.XL.data();
+  s->X_right = buf.XR.data();
+  s->tri_left = buf.triL.data();
+  s->tri_right = buf.triR.data();
+  s->last_left = buf.lastL.data();
+  s->last_right = buf.lastR.data();
+  s->lframe = (uint32_t)(st.poses.first[0].ID + st.poses.first.size() - 1);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      s->K1[3 * r + c] = st.K.first(r, c);
+      s->K2[3 * r + c] = st.K.second(r, c);
+    }
+  detail::flatten_pose(st.poses.first.back(), s->q1, s->t1);
+  detail::flatten_pose(st.poses.second.back(), s->q2, s->t2);
+  s->scale = st.scale;
+  s->baseline = st.baseline;
+  s->window_size = st.window_size;
+  const auto& L = obs[f].first;
+  const auto& R = obs[f].second;
+  if (L.rows != R.rows || L.cols != R.cols || detail::row_stride(L) != detail::row_stride(R))
+    throw std::invalid_argument("flatten_scale_state: left / right images differ in shape or stride");
+  s->imgL = static_cast<const uint8_t*>(L.ptr());
+  s->imgR = static_cast<const uint8_t*>(R.ptr());
+  s->stride = detail::row_stride(L);
+  s->cols = L.cols;
+  s->rows = L.rows;
+  s->bb_cols = obs[0].first.cols;
+  s->bb_rows = obs[1].first.rows;
+  buf.mask.resize((size_t)mask.size());
+  for (int i = 0; i < (int)mask.size(); ++i) buf.mask[i] = mask(i) ? 1 : 0;
+  s->mask = buf.mask.empty() ? nullptr : buf.mask.data();
+  s->mask_len = (int)buf.mask.size();
+  s->img_mem = ME_HOST;
+  s->tracks_mem = ME_HOST;
+}
+
+}  // namespace amd
+
+// ---- reference-shaped value types (plain, no OpenCV / Eigen) -------------
+using ptH3D = std::array<double, 4>;  // cv::Matx41d: pt(k) is pt[k] here
+struct Point2f {
+  float x = 0.f, y = 0.f;
+};
+template <class T>
+struct StereoOdoMatches {  // feature_types.h:101-109 (f1, f2 previous L/R, f3, f4 current L/R)
+  T f1, f2, f3, f4;
+  float m_score = -1.f;
+};
+using StereoOdoMatchesf = StereoOdoMatches<Point2f>;
+enum StopCondition { NO_STOP, SMALL_GRADIENT, SMALL_INCREMENT, MAX_ITERATIONS, SMALL_DECREASE_FUNCTION,
+                     SMALL_REPROJ_ERROR, NO_CONVERGENCE };  // rotation_utils.h:20
+
+// Quat / CamPose_qd / WBA_Ptf reduced to the members the scale optimiser reads.
+struct Quat {
+  double m_w = 1, m_x = 0, m_y = 0, m_z = 0;
+  double w() const { return m_w; }
+  double x() const { return m_x; }
+  double y() const { return m_y; }
+  double z() const { return m_z; }
+};
+struct CamPose_qd {
+  int ID = 0;
+  Quat orientation;
+  std::array<double, 3> position{{0, 0, 0}};
+};
+struct Matx33d {
+  std::array<double, 9> val{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+  double operator()(int r, int c) const { return val[3 * r + c]; }
+};
+struct WBA_Ptf {  // the 3-D location and the frame bookkeeping of WBA_Point<Point2f>
+  struct Loc {
+    ptH3D v{{0, 0, 0, 1}};
+    double operator()(int k) const { return v[k]; }
+  } pt;
+  unsigned last_frame = (unsigned)-1;
+  bool isTriangulated() const { return !(pt.v[0] == 0 && pt.v[1] == 0 && pt.v[2] == 0 && pt.v[3] == 1); }
+  unsigned getLastFrameIdx() const { return last_frame; }
+  Loc get3DLocation() const { return pt; }
+};
+struct VectorXi {  // Eigen::VectorXi
+  std::vector<int> v;
+  int size() const { return (int)v.size(); }
+  int operator()(int i) const { return v[i]; }
+};
+
+namespace optimisation {
+
+enum class OptimType { GN, LM };
+
+// OptimisationParams (optimisation.h:22-32), same defaults
+struct OptimisationParams {
+  int MAX_NB_ITER;
+  double v, tau, mu;
+  double abs_tol, grad_tol, incr_tol, rel_tol;
+  double alpha;
+  OptimType type;
+  bool minim;
+  bool weighting;
+  OptimisationParams(OptimType type_ = OptimType::LM, bool min = true, int it = 20, double v_ = 2, double t = 1e-3,
+                     double m = 1e-20, double e1 = 1e-4, double e2 = 1e-4, double e3 = 1e-3, double e4 = 1e-4,
+                     double a = 1.0)
+      : MAX_NB_ITER(it), v(v_), tau(t), mu(m), abs_tol(e1), grad_tol(e2), incr_tol(e3), rel_tol(e4), alpha(a),
+        type(type_), minim(min), weighting(false) {}
+  me_optim_params to_c() const {
+    me_optim_params p;
+    me_optim_default_params(&p);
+    p.type = (int)type;
+    p.minim = minim;
+    p.max_nb_iter = MAX_NB_ITER;
+    p.v = v;
+    p.tau = tau;
+    p.mu = mu;
+    p.abs_tol = abs_tol;
+    p.grad_tol = grad_tol;
+    p.incr_tol = incr_tol;
+    p.rel_tol = rel_tol;
+    p.alpha = alpha;
+    p.weighting = weighting;
+    return p;
+  }
+};
+
+using ImagePairs = std::vector<std::pair<amd::ImageView, amd::ImageView>>;
+
+// ScaleState (optimisation.h:76-98)
+struct ScaleState {
+  std::pair<std::vector<WBA_Ptf>, std::vector<WBA_Ptf>> pts;
+  std::pair<Matx33d, Matx33d> K;
+  std::pair<std::vector<CamPose_qd>, std::vector<CamPose_qd>> poses;
+  double scale = 1.0;
+  double baseline = 0.0;
+  int window_size = 0;
+  int nb_params = 1;
+  // double ScaleState::compute_residuals(std::vector<std::pair<cv::Mat,cv::Mat>>&) (optimisation.cpp:230-278):
+  // the MI of the stacked 2w x 2w pairs (evident intent; see me_scale_state_mi in me_hip.h)
+  double compute_residuals(const ImagePairs& m_obs,
+                           amd::Context& ctx = amd::Context::thread_default()) const {
+    amd::ScaleStateBuffers buf;
+    me_scale_state s;
+    amd::flatten_scale_state(*this, m_obs, VectorXi{}, &s, buf);
+    double mi = 0;
+    ctx.check(me_scale_state_mi(ctx.get(), &s, &mi, nullptr), "ScaleState::compute_residuals");
+    return mi;
+  }
+  void update(double dX) { scale += dX; }  // optimisation.h:90-93
+};
+
+template <class S, class T>
+class Optimiser;
+
+// Optimiser<ScaleState, vector<pair<Mat,Mat>>> (optimisation.h:100-125,
+// optimisation.cpp:29-228,435-747) over me_scale_*: the same public
+// members; MatrixXd results are std::vector<double> (residual column) and a
+// double (the 1x1 Jacobian product).  Device errors throw (the reference
+// would throw cv::Exception on an out-of-image ROI).
+template <>
+class Optimiser<ScaleState, ImagePairs> {
+ public:
+  Optimiser(const ImagePairs& observations, const OptimisationParams& params = OptimisationParams(),
+            amd::Context& ctx = amd::Context::thread_default())
+      : m_obs(observations), m_params(params), m_ctx(&ctx) {}
+
+  StopCondition optimise(ScaleState& state, const bool test = false, const VectorXi& mask = VectorXi()) {
+    m_state = state;
+    m_mask = mask;
+    amd::ScaleStateBuffers buf;
+    me_scale_state s;
+    amd::flatten_scale_state(m_state, m_obs, m_mask, &s, buf);
+    const me_optim_params p = m_params.to_c();
+    int stop = 0, iters = 0;
+    long evals = 0;
+    m_ctx->check(me_scale_optimise(m_ctx->get(), &s, &p, test ? 1 : 0, &stop, &iters, nullptr, 0, &evals),
+                 "Optimiser::optimise");
+    m_state.scale = s.scale;
+    m_iterations = iters;
+    m_stop = static_cast<StopCondition>(stop);
+    state = m_state;
+    return m_stop;
+  }
+  std::vector<double> compute_residuals(const ScaleState& state) {
+    amd::ScaleStateBuffers buf;
+    me_scale_state s;
+    amd::flatten_scale_state(state, m_obs, m_mask, &s, buf);
+    std::vector<double> res((size_t)(s.n_left + s.n_right) + 1);
+    int rows = 0;
+    m_ctx->check(me_scale_residuals(m_ctx->get(), &s, m_params.weighting, res.data(), &rows),
+                 "Optimiser::compute_residuals");
+    res.resize((size_t)rows);
+    return res;
+  }
+  std::vector<int> compute_inliers(const double threshold) {
+    amd::ScaleStateBuffers buf;
+    me_scale_state s;
+    amd::flatten_scale_state(m_state, m_obs, VectorXi{}, &s, buf);  // the mask is cleared (:735-736)
+    std::vector<int> idx((size_t)(s.n_left + s.n_right) + 1);
+    int n = 0;
+    m_ctx->check(me_scale_inliers(m_ctx->get(), &s, m_params.weighting, threshold, idx.data(), (int)idx.size(), &n),
+                 "Optimiser::compute_inliers");
+    idx.resize((size_t)std::min<int>(n, (int)idx.size()));
+    return idx;
+  }
+  double getJacobian() {
+    amd::ScaleStateBuffers buf;
+    me_scale_state s;
+    amd::flatten_scale_state(m_state, m_obs, m_mask, &s, buf);
+    double JJ = 0;
+    m_ctx->check(me_scale_jacobian(m_ctx->get(), &s, m_params.weighting, &JJ), "Optimiser::getJacobian");
+    return JJ;
+  }
+  int iterations() const { return m_iterations; }
+
+ private:
+  ScaleState m_state;
+  ImagePairs m_obs;
+  VectorXi m_mask;
+  OptimisationParams m_params;
+  StopCondition m_stop = NO_STOP;
+  amd::Context* m_ctx;
+  int m_iterations = 0;
+};
+
+}  // namespace optimisation
+
+// StereoVisualOdometry (StereoVisualOdometry.h:18-60, StereoVisualOdometry.cpp:34-342)
+// over me_vo_process.  cv::Mat results are row-major arrays: getMotion() 4x4,
+// getPts3D() homogeneous points, the state six values (Euler angles,
+// translation).  The RANSAC triples come from the context's glibc rand()
+// stream (srand() reseeds it, as the reference's unseeded rand()).
+class StereoVisualOdometry {
+ public:
+  enum class Method { GN, LM };
+  struct parameters {  // VisualOdometry::parameters (VisualOdometry.h:19-33) + Stereo (:24-33), same defaults
+    Method method;
+    double step_size, eps, e1, e2, e3, e4;
+    int max_iter, nb_fixed_frames;
+    bool ransac;
+    int n_ransac;
+    double inlier_threshold;
+    double baseline;
+    bool weighting;
+    double fu1, fv1, fu2, fv2, cu1, cu2, cv1, cv2;
+    parameters()
+        : method(Method::GN), step_size(1.0), eps(1e-9), e1(1e-3), e2(1e-12), e3(1e-12), e4(1e-15), max_iter(100),
+          nb_fixed_frames(2), ransac(true), n_ransac(200), inlier_threshold(2.0), baseline(1.0), weighting(false),
+          fu1(1.0), fv1(1.0), fu2(1.0), fv2(1.0), cu1(0.0), cu2(0.0), cv1(0.0), cv2(0.0) {}
+  };
+  explicit StereoVisualOdometry(parameters param = parameters(), amd::Context& ctx = amd::Context::thread_default(),
+                                int max_outer = 10000)
+      : m_param(param), m_ctx(&ctx), m_max_outer(max_outer) {}
+
+  void srand(unsigned seed) { m_ctx->check(me_vo_srand(m_ctx->get(), seed), "srand"); }
+
+  // bool process(const std::vector<StereoOdoMatchesf>&, cv::Mat init = zeros(6,1))
+  bool process(const std::vector<StereoOdoMatchesf>& matches, const std::array<double, 6>& init = {}) {
+    if (matches.size() < 6) return false;  // StereoVisualOdometry.cpp:40-42
+    const int n = (int)matches.size();
+    std::vector<float> m(8 * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+      const StereoOdoMatchesf& q = matches[i];
+      const float v[8] = {q.f1.x, q.f1.y, q.f2.x, q.f2.y, q.f3.x, q.f3.y, q.f4.x, q.f4.y};
+      std::copy(v, v + 8, &m[8 * (size_t)i]);
+    }
+    me_vo_params p;
+    me_vo_default_params(&p);
+    p.method = (int)m_param.method;
+    p.step_size = m_param.step_size;
+    p.eps = m_param.eps;
+    p.e1 = m_param.e1;
+    p.e2 = m_param.e2;
+    p.e3 = m_param.e3;
+    p.e4 = m_param.e4;
+    p.max_iter = m_param.max_iter;
+    p.nb_fixed_frames = m_param.nb_fixed_frames;
+    p.ransac = m_param.ransac;
+    p.n_ransac = m_param.n_ransac;
+    p.inlier_threshold = m_param.inlier_threshold;
+    p.baseline = m_param.baseline;
+    p.weighting = m_param.weighting;
+    p.fu1 = m_param.fu1;
+    p.fv1 = m_param.fv1;
+    p.fu2 = m_param.fu2;
+    p.fv2 = m_param.fv2;
+    p.cu1 = m_param.cu1;
+    p.cu2 = m_param.cu2;
+    p.cv1 = m_param.cv1;
+    p.cv2 = m_param.cv2;
+    m_pts3D.assign((size_t)n, ptH3D{{0, 0, 0, 0}});
+    m_inliers.assign((size_t)n, 0);
+    int nin = 0, ok = 0;
+    m_ctx->check(me_vo_process(m_ctx->get(), m.data(), n, init.data(), &p, m_max_outer, m_motion.data(),
+                               m_state.data(), m_pts3D[0].data(), m_inliers.data(), &nin, &ok),
+                 "StereoVisualOdometry::process");
+    m_inliers.resize((size_t)nin);
+    return ok != 0;
+  }
+  const std::array<double, 16>& getMotion() const { return m_motion; }
+  const std::array<double, 6>& getState() const { return m_state; }
+  const std::vector<ptH3D>& getPts3D() const { return m_pts3D; }
+  const std::vector<int>& getInliers_idx() const { return m_inliers; }
+  parameters getParams() const { return m_param; }
+
+ private:
+  parameters m_param;
+  amd::Context* m_ctx;
+  int m_max_outer;
+  std::array<double, 16> m_motion{};
+  std::array<double, 6> m_state{};
+  std::vector<ptH3D> m_pts3D;
+  std::vector<int> m_inliers;
+};
+
+// Pyramidal LK tracking of n points from prev to next (A12, no reference
+// counterpart: the application's feature tracker).  status[i] = 1 tracked.
+inline void calcOpticalFlowPyrLK(const amd::ImageView& prev, const amd::ImageView& next,
+                                 const std::vector<Point2f>& pts_in, std::vector<Point2f>& pts_out,
+                                 std::vector<uint8_t>& status, amd::Context& ctx = amd::Context::thread_default()) {
+  if (prev.rows != next.rows || prev.cols != next.cols || prev.step != next.step)
+    throw std::invalid_argument("calcOpticalFlowPyrLK: images differ in shape");
+  pts_out.resize(pts_in.size());
+  status.assign(pts_in.size(), 0);
+  if (pts_in.empty()) return;
+  me_klt_params kp;
+  me_klt_default_params(&kp);
+  ctx.check(me_klt_track(ctx.get(), ME_HOST, prev.data, next.data, prev.cols, prev.rows, prev.step,
+                         &pts_in[0].x, &pts_out[0].x, status.data(), (int)pts_in.size(), &kp),
+            "calcOpticalFlowPyrLK");
+}
+
 }  // namespace me

@@ -161,6 +161,18 @@ int me_scale_optimise(me_ctx* ctx, me_scale_state* s, const me_optim_params* p, 
    result is already known (same state) still counts.  executed = residual
    evaluations the device actually ran (speculative candidates included). */
 int me_scale_last_counters(me_ctx* ctx, long* res_evals, long* neq_evals, long* rejections, long* executed);
+/* double ScaleState::compute_residuals(std::vector<std::pair<cv::Mat,cv::Mat>>&)
+   (include/MotionEstimation/optimisation/optimisation.h:86, src/optimisation/optimisation.cpp:230-278):
+   one mutual information over the stacked 2w x 2w patch pairs of the left
+   tracks (triangulated, seen in the last keyframe, both reprojections inside
+   Rect(w, w, cols - 2w, rows - 2w)).  The reference's stacking
+   (`left_img(Range..) = imgs[i].first`, :273-274) rebinds a temporary ROI
+   header and copies no pixels, so its stacked images are uninitialised and
+   its result undefined; this computes the evident intent (the MI of the
+   stacked patches), parity unpinned.  n_patches (optional) receives the
+   number of stacked pairs; none -> ME_ERR_INVALID (the reference's
+   computeMutualInformation asserts on empty input). */
+int me_scale_state_mi(me_ctx* ctx, const me_scale_state* s, double* mi_out, int* n_patches);
 /* Optimiser::compute_inliers (optimisation.cpp:732-747): row indices. */
 int me_scale_inliers(me_ctx* ctx, const me_scale_state* s, int weighting, double threshold, int* idx, int cap,
                      int* n_out);

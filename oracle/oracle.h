@@ -77,6 +77,9 @@ int oracle_scale_jacobian(const oracle_scale_state* s, int weighting, double* JJ
 int oracle_scale_optimise(oracle_scale_state* s, const oracle_optim_params* p, int test,
                           int* iterations, double* trace, int trace_cap, long* mi_evals);
 int oracle_scale_inliers(const oracle_scale_state* s, double threshold, int* idx, int cap);
+/* ScaleState::compute_residuals (optimisation.cpp:230-278), evident intent (parity unpinned) */
+int oracle_scale_state_mi(const oracle_scale_state* s, double* out, int* npairs);
+void oracle_scale_counters(long* out3);
 
 /* ---- A13-A17: windowed stereo BA (BundleAdjuster.h + Ceres LM semantics) ---- */
 typedef struct {

@@ -478,6 +478,45 @@ extern "C" int oracle_scale_optimise(oracle_scale_state* s_in, const oracle_opti
   return stop;
 }
 
+// ScaleState::compute_residuals (optimisation.cpp:230-278), evident intent:
+// the 2w x 2w patch pairs of the left tracks stacked into one tall image pair
+// (rows = pairs * 2w), then computeMutualInformation on it.  The reference's
+// `left_img(Range..) = imgs[i].first` (:273-274) copies nothing (it rebinds a
+// temporary header), so the literal reference reads uninitialised memory:
+// parity unpinned.  Returns 0, -1 (no pair: computeMutualInformation asserts,
+// mutual_information.cpp:57) or -2 (ROI outside the image: cv::Exception).
+extern "C" int oracle_scale_state_mi(const oracle_scale_state* s, double* out, int* npairs) {
+  const int w = s->window_size, P = 2 * w;
+  RectI bb{w, w, s->bb_cols - 2 * w, s->bb_rows - 2 * w};  // :232 (no -1)
+  std::vector<uint8_t> L, R;
+  int n = 0;
+  for (int i = 0; i < s->n_left; ++i) {
+    if (!s->tri_left[i] || s->last_left[i] != s->lframe) continue;  // :246-248
+    double T[16], Y[4], f[3], Z[4], f2[3];
+    pose_T(s->q1, s->t1, T);
+    mul44x41(T, s->X_left + 4 * i, Y);
+    proj_scaled_K(s->K1, s->scale, Y, f);
+    P2f fl = to_euclid_f(f);
+    for (int c = 0; c < 4; ++c) Z[c] = s->scale * Y[c];
+    Z[0] = Z[0] - s->baseline;
+    proj_K(s->K2, Z, f2);
+    P2f fr = to_euclid_f(f2);
+    if (!(contains(bb, fl) && contains(bb, fr))) continue;  // :257
+    int lx = roi0(fl.x, w), ly = roi0(fl.y, w), rx = roi0(fr.x, w), ry = roi0(fr.y, w);
+    if (!roi_ok(lx, ly, P, P, s->cols, s->rows) || !roi_ok(rx, ry, P, P, s->cols, s->rows)) return -2;
+    for (int y = 0; y < P; ++y)
+      for (int x = 0; x < P; ++x) {
+        L.push_back(s->imgL[(long)(ly + y) * s->stride + lx + x]);
+        R.push_back(s->imgR[(long)(ry + y) * s->stride + rx + x]);
+      }
+    ++n;
+  }
+  if (npairs) *npairs = n;
+  if (n == 0) return -1;
+  *out = (double)oracle_mutual_information(L.data(), P, R.data(), P, P, n * P);  // :277
+  return 0;
+}
+
 extern "C" void oracle_scale_counters(long* out3) {
   out3[0] = g_res_calls;
   out3[1] = g_neq_calls;

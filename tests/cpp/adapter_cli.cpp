@@ -6,6 +6,9 @@
 //   adapter_cli ba  <in.bin> <out.bin>   BundleAdjuster<M>-style solve (M = 4 or 2, optional covariance)
 //   adapter_cli mi  <in.bin> <out.bin>   computeMutualInformation / computeEntropy
 //   adapter_cli nms <in.bin> <out.bin>   nonMaxSupScanline3x3
+//   adapter_cli scale <in.bin> <out.bin> Optimiser<ScaleState,...>: compute_residuals, optimise, compute_inliers,
+//                                        getJacobian, ScaleState::compute_residuals (via flatten_scale_state)
+//   adapter_cli vo  <in.bin> <out.bin>   StereoVisualOdometry::process / getMotion / getInliers_idx
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -123,11 +126,127 @@ int run_nms(Reader& in, FILE* out) {
   fwrite(mask.data(), 1, mask.size(), out);
   return 0;
 }
+// payload: nL nR w lframe fixed10 has_mask rows cols | K1 K2 q1 t1 q2 t2 scale baseline threshold |
+//          XL XR | triL triR (u8) | lastL lastR (u32) | [mask u8 nL+nR] | imgL imgR
+int run_scale(Reader& in, FILE* out) {
+  using namespace me::optimisation;
+  const int nL = in.get<int32_t>(), nR = in.get<int32_t>(), w = in.get<int32_t>(), lframe = in.get<int32_t>();
+  const int fixed10 = in.get<int32_t>(), has_mask = in.get<int32_t>(), rows = in.get<int32_t>(),
+            cols = in.get<int32_t>();
+  ScaleState st;
+  in.get(st.K.first.val.data(), 9);
+  in.get(st.K.second.val.data(), 9);
+  me::CamPose_qd p1, p2;
+  double q[4];
+  in.get(q, 4);
+  p1.orientation = me::Quat{q[0], q[1], q[2], q[3]};
+  in.get(p1.position.data(), 3);
+  in.get(q, 4);
+  p2.orientation = me::Quat{q[0], q[1], q[2], q[3]};
+  in.get(p2.position.data(), 3);
+  st.scale = in.get<double>();
+  st.baseline = in.get<double>();
+  const double thr = in.get<double>();
+  st.window_size = w;
+  // a two-keyframe window ending at lframe: poses.first[0].ID + size - 1 == lframe (optimisation.cpp:165)
+  me::CamPose_qd p0;
+  p0.ID = lframe - 1;
+  p1.ID = p2.ID = lframe;
+  st.poses.first = {p0, p1};
+  st.poses.second = {p0, p2};
+  std::vector<double> XL(4 * (size_t)nL), XR(4 * (size_t)nR);
+  in.get(XL.data(), XL.size());
+  in.get(XR.data(), XR.size());
+  std::vector<uint8_t> tL(nL), tR(nR);
+  in.get(tL.data(), nL);
+  in.get(tR.data(), nR);
+  std::vector<uint32_t> lL(nL), lR(nR);
+  in.get(lL.data(), nL);
+  in.get(lR.data(), nR);
+  me::VectorXi mask;
+  if (has_mask) {
+    std::vector<uint8_t> m(nL + nR);
+    in.get(m.data(), m.size());
+    mask.v.assign(m.begin(), m.end());
+  }
+  auto fill = [](std::vector<me::WBA_Ptf>& v, const std::vector<double>& X, const std::vector<uint32_t>& last) {
+    v.resize(last.size());
+    for (size_t i = 0; i < v.size(); ++i) {
+      for (int k = 0; k < 4; ++k) v[i].pt.v[k] = X[4 * i + k];
+      v[i].last_frame = last[i];
+    }
+  };
+  fill(st.pts.first, XL, lL);
+  fill(st.pts.second, XR, lR);
+  std::vector<uint8_t> L((size_t)rows * cols), R((size_t)rows * cols);
+  in.get(L.data(), L.size());
+  in.get(R.data(), R.size());
+  const me::amd::ImageView vl{L.data(), rows, cols, cols}, vr{R.data(), rows, cols, cols};
+  const ImagePairs obs{{vl, vr}, {vl, vr}};
+  OptimisationParams params;
+  if (fixed10) {  // the bench frame: MAX_NB_ITER 10, tolerances off
+    params.MAX_NB_ITER = 10;
+    params.abs_tol = params.grad_tol = params.incr_tol = params.rel_tol = 0;
+  }
+  const ScaleState st0 = st;
+  Optimiser<ScaleState, ImagePairs> opt(obs, params);
+  const std::vector<double> res0 = opt.compute_residuals(st0);
+  const int32_t stop = (int32_t)opt.optimise(st, false, mask);
+  const int32_t iters = opt.iterations();
+  const std::vector<int> inl = opt.compute_inliers(thr);
+  const double jac = opt.getJacobian();
+  const double smi = st0.compute_residuals(obs);
+  fwrite(&stop, 4, 1, out);
+  fwrite(&iters, 4, 1, out);
+  fwrite(&st.scale, 8, 1, out);
+  const int32_t nres = (int32_t)res0.size(), ninl = (int32_t)inl.size();
+  fwrite(&nres, 4, 1, out);
+  fwrite(res0.data(), 8, res0.size(), out);
+  fwrite(&ninl, 4, 1, out);
+  fwrite(inl.data(), 4, inl.size(), out);
+  fwrite(&jac, 8, 1, out);
+  fwrite(&smi, 8, 1, out);
+  return 0;
+}
+
+// payload: n seed | baseline fu1 fv1 fu2 fv2 cu1 cu2 cv1 cv2 | matches n x 8 floats
+int run_vo(Reader& in, FILE* out) {
+  const int n = in.get<int32_t>();
+  const unsigned seed = (unsigned)in.get<int32_t>();
+  me::StereoVisualOdometry::parameters prm;
+  prm.baseline = in.get<double>();
+  prm.fu1 = in.get<double>();
+  prm.fv1 = in.get<double>();
+  prm.fu2 = in.get<double>();
+  prm.fv2 = in.get<double>();
+  prm.cu1 = in.get<double>();
+  prm.cu2 = in.get<double>();
+  prm.cv1 = in.get<double>();
+  prm.cv2 = in.get<double>();
+  std::vector<me::StereoOdoMatchesf> m((size_t)n);
+  for (auto& q : m) {
+    float v[8];
+    in.get(v, 8);
+    q.f1 = {v[0], v[1]};
+    q.f2 = {v[2], v[3]};
+    q.f3 = {v[4], v[5]};
+    q.f4 = {v[6], v[7]};
+  }
+  me::StereoVisualOdometry vo(prm);
+  vo.srand(seed);
+  const int32_t ok = vo.process(m) ? 1 : 0;
+  fwrite(&ok, 4, 1, out);
+  fwrite(vo.getMotion().data(), 8, 16, out);
+  const int32_t ninl = (int32_t)vo.getInliers_idx().size();
+  fwrite(&ninl, 4, 1, out);
+  fwrite(vo.getInliers_idx().data(), 4, vo.getInliers_idx().size(), out);
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc != 4) {
-    std::fprintf(stderr, "usage: %s ba|mi|nms in.bin out.bin\n", argv[0]);
+    std::fprintf(stderr, "usage: %s ba|mi|nms|scale|vo in.bin out.bin\n", argv[0]);
     return 2;
   }
   Reader in = read_file(argv[2]);
@@ -138,6 +257,8 @@ int main(int argc, char** argv) {
     if (!std::strcmp(argv[1], "ba")) rc = run_ba(in, out);
     else if (!std::strcmp(argv[1], "mi")) rc = run_mi(in, out);
     else if (!std::strcmp(argv[1], "nms")) rc = run_nms(in, out);
+    else if (!std::strcmp(argv[1], "scale")) rc = run_scale(in, out);
+    else if (!std::strcmp(argv[1], "vo")) rc = run_vo(in, out);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "adapter_cli: %s\n", e.what());
     rc = 1;

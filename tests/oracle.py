@@ -121,6 +121,8 @@ def lib():
         L.oracle_scale_optimise.argtypes = [P(OScaleState), P(OOptimParams), c_int, P(c_int), P(c_double), c_int,
                                             P(c_long)]
         L.oracle_scale_inliers.argtypes = [P(OScaleState), c_double, P(c_int), c_int]
+        L.oracle_scale_state_mi.argtypes = [P(OScaleState), P(c_double), P(c_int)]
+        L.oracle_scale_counters.argtypes = [P(c_long)]
         L.oracle_ba_default_options.argtypes = [P(OBAOptions)]
         L.oracle_ba_evaluate.argtypes = [P(OBAProblem), P(c_double), P(c_double), P(c_double)]
         L.oracle_ba_cost.restype = c_double
@@ -335,6 +337,16 @@ def scale_optimise(sp, test=0, **kw):
     lib().oracle_scale_counters(cnt)
     return dict(stop=stop, scale=s.scale, iterations=it.value, trace=trace[:2 * min(it.value, 400)].reshape(-1, 2),
                 mi_evals=nmi.value, res_evals=cnt[0], neq_evals=cnt[1], rejections=cnt[2])
+
+
+def scale_state_mi(sp):
+    """ScaleState::compute_residuals (optimisation.cpp:230-278), evident intent."""
+    s, keep = scale_state(sp)
+    out, n = c_double(), c_int()
+    rc = lib().oracle_scale_state_mi(ctypes.byref(s), ctypes.byref(out), ctypes.byref(n))
+    if rc < 0:
+        raise RuntimeError(f"oracle_scale_state_mi failed {rc}")
+    return out.value, n.value
 
 
 def scale_inliers(sp, threshold):

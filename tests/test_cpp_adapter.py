@@ -115,3 +115,78 @@ def test_cpp_mono_bundle_adjuster_with_covariance(tmp_path, oracle):
     after.cams, after.pts = rc, rp
     rcov = oracle.ba_covariance(after)
     np.testing.assert_allclose(cov, rcov, rtol=1e-5, atol=1e-8 * np.abs(rcov).max())
+
+
+def _scale_payload(sp, fixed10, thr, mask=None):
+    nL, nR = len(sp.X_left), len(sp.X_right)
+    rows, cols = sp.imgL.shape
+    b = struct.pack("<8i", nL, nR, sp.window_size, int(sp.lframe), int(fixed10), int(mask is not None), rows, cols)
+    b += np.asarray(sp.K1, np.float64).tobytes() + np.asarray(sp.K2, np.float64).tobytes()
+    b += np.asarray(sp.q1, np.float64).tobytes() + np.asarray(sp.t1, np.float64).tobytes()
+    b += np.asarray(sp.q2, np.float64).tobytes() + np.asarray(sp.t2, np.float64).tobytes()
+    b += struct.pack("<ddd", sp.scale, sp.baseline, thr)
+    b += np.ascontiguousarray(sp.X_left, np.float64).tobytes() + np.ascontiguousarray(sp.X_right, np.float64).tobytes()
+    b += np.asarray(sp.tri_left, np.uint8).tobytes() + np.asarray(sp.tri_right, np.uint8).tobytes()
+    b += np.asarray(sp.last_left, np.uint32).tobytes() + np.asarray(sp.last_right, np.uint32).tobytes()
+    if mask is not None:
+        b += np.asarray(mask, np.uint8).tobytes()
+    return b + np.ascontiguousarray(sp.imgL).tobytes() + np.ascontiguousarray(sp.imgR).tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fixed10,masked", [(0, False), (1, False), (0, True)])
+def test_cpp_scale_optimiser_matches_oracle(tmp_path, oracle, fixed10, masked):
+    """Optimiser<ScaleState, vector<pair<Mat,Mat>>> through the C++ mirror:
+    the ScaleState is flattened by me::amd::flatten_scale_state, the template
+    the reference-side binding instantiates on its own ScaleState."""
+    import dataclasses
+
+    from uasl_motion_estimation_amd.optimisation import OptimisationParams
+
+    sp = S.scale_problem(20261022, 640, 480, 400)
+    mask = None
+    if masked:  # keep every row the reference can index (A-6): mask out a few tracks on both sides
+        mask = np.ones(len(sp.X_left) + len(sp.X_right), np.uint8)
+        mask[::17] = 0
+        mask[len(sp.X_left):] = 1
+    thr = 1.2
+    _, out = _run("scale", _scale_payload(sp, fixed10, thr, mask), tmp_path)
+    stop, iters, scale = struct.unpack_from("<iid", out)
+    off = 16
+    (nres,) = struct.unpack_from("<i", out, off)
+    res0 = np.frombuffer(out, np.float64, nres, off + 4)
+    off += 4 + 8 * nres
+    (ninl,) = struct.unpack_from("<i", out, off)
+    inl = np.frombuffer(out, np.int32, ninl, off + 4)
+    off += 4 + 4 * ninl
+    jac, smi = struct.unpack_from("<dd", out, off)
+
+    params = OptimisationParams.fixed_iterations(10) if fixed10 else OptimisationParams()
+    spm = dataclasses.replace(sp, mask=mask)
+    assert np.array_equal(res0, oracle.scale_residuals(sp))
+    ref = oracle.scale_optimise(spm, **params.oracle_kw())
+    assert stop == ref["stop"] and iters == ref["iterations"]
+    np.testing.assert_allclose(scale, ref["scale"], rtol=1e-9)
+    after = dataclasses.replace(sp, scale=scale)
+    assert np.array_equal(inl, oracle.scale_inliers(after, thr))
+    np.testing.assert_allclose(jac, oracle.scale_jacobian(dataclasses.replace(after, mask=mask)), rtol=1e-12)
+    rmi, _ = oracle.scale_state_mi(sp)
+    assert np.float32(smi) == np.float32(rmi)
+
+
+@pytest.mark.gpu
+def test_cpp_stereo_vo_matches_oracle(tmp_path, oracle):
+    m, p = S.vo_matches(12, 300, noise=0.005)
+    b = struct.pack("<ii", len(m), 1)
+    b += struct.pack("<9d", p["baseline"], p["fu1"], p["fv1"], p["fu2"], p["fv2"], p["cu1"], p["cu2"], p["cv1"],
+                     p["cv2"])
+    b += np.ascontiguousarray(m, np.float32).tobytes()
+    _, out = _run("vo", b, tmp_path)
+    (ok,) = struct.unpack_from("<i", out)
+    motion = np.frombuffer(out, np.float64, 16, 4).reshape(4, 4)
+    (ninl,) = struct.unpack_from("<i", out, 4 + 128)
+    inl = np.frombuffer(out, np.int32, ninl, 8 + 128)
+    rc, rM, rinl = oracle.vo_process(m, p)
+    assert rc in (0, 1) and bool(ok) == bool(rc)
+    assert np.array_equal(inl, rinl)
+    np.testing.assert_allclose(motion, rM, rtol=1e-6, atol=1e-9)

@@ -167,3 +167,26 @@ def test_klt_config3_2000_features(ctx, oracle):
     assert np.array_equal(gst, rst)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     assert gst.mean() > 0.8
+
+
+# ------------------------------------------------------------------ A7: ScaleState::compute_residuals
+@pytest.mark.parametrize("which", ["cfg1", "cfg3"])
+def test_scale_state_mi_matches_oracle(ctx, oracle, which, sp300, sp_cfg3):
+    """Evident intent of optimisation.cpp:230-278 (parity unpinned: the
+    reference's stacking copies nothing): float MI of the stacked pairs, bit-exact."""
+    from uasl_motion_estimation_amd.optimisation import scale_state_mi
+
+    sp = sp300 if which == "cfg1" else sp_cfg3[1]
+    mi, n = scale_state_mi(sp, ctx=ctx)
+    rmi, rn = oracle.scale_state_mi(sp)
+    assert n == rn > 0
+    assert np.float32(mi).view(np.uint32) == np.float32(rmi).view(np.uint32)
+
+
+def test_scale_state_mi_empty_is_an_error(ctx, sp300):
+    from uasl_motion_estimation_amd import MEError
+    from uasl_motion_estimation_amd.optimisation import scale_state_mi
+
+    sp = dataclasses.replace(sp300, tri_left=np.zeros_like(sp300.tri_left))
+    with pytest.raises(MEError):
+        scale_state_mi(sp, ctx=ctx)

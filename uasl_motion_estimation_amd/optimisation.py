@@ -176,6 +176,18 @@ def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx
                 neq_evals=nneq.value, rejections=nrej.value, executed_evals=nexe.value)
 
 
+def scale_state_mi(sp, ctx: Context | None = None):
+    """ScaleState::compute_residuals(m_obs) (optimisation.cpp:230-278): the MI
+    of the stacked left-track patch pairs (the evident intent; the reference's
+    stacking copies nothing, see include/me_hip.h).  Returns (mi, n_patches)."""
+    ctx = ctx or default_context()
+    keep = []
+    s = scale_struct(sp, keep)
+    mi, n = c_double(), c_int()
+    ctx.check(ctx.lib.me_scale_state_mi(ctx.h, byref(s), byref(mi), byref(n)), "me_scale_state_mi")
+    return mi.value, n.value
+
+
 def scale_inliers(sp, threshold: float, weighting=False, ctx: Context | None = None) -> np.ndarray:
     ctx = ctx or default_context()
     keep = []
