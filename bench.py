@@ -53,6 +53,12 @@ def parse():
     ap.add_argument("--streams", type=int, default=1,
                     help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
                          "thread each), reported as multi_stream; the headline value stays one stream per GPU")
+    ap.add_argument("--sharded-ba", type=int, default=1,
+                    help="config-4 landmark-sharded BA line (SURVEY 8e): over RCCL across the ranks when --gpus > 1, "
+                         "two contexts on one GPU (host exchange, the crossover point) at N = 1; 0: off")
+    ap.add_argument("--sharded-reps", type=int, default=3)
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise the RCCL process group even at one rank (exercises the RCCL exchange path)")
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
@@ -461,6 +467,104 @@ def stereo_vo_line(ctx, n: int, reps: int = 5, cpu: bool = True):
     return out
 
 
+def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
+    """Config-4 window (8000 landmarks x 30 keyframes, args.ba_iters LM
+    iterations) solved (a) unsharded on this GPU and (b) landmark-sharded: over
+    RCCL across the world's ranks (one GPU each, torch.distributed all-reduce of
+    S, b and the LM scalars on device buffers) or, at N = 1, over two contexts
+    of this GPU with a host exchange.  Every shard is resident in HBM (reset by
+    a device copy); timing: barrier + MAX over ranks."""
+    import threading
+
+    import torch
+
+    from uasl_motion_estimation_amd import synthetic as S
+    from uasl_motion_estimation_amd._lib import Context
+    from uasl_motion_estimation_amd.optimisation import (DeviceBAProblem, SolverOptions, ThreadAllReduce,
+                                                         shard_landmarks, torch_allreduce)
+
+    c = S.CONFIGS[4]
+    bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
+    opts = SolverOptions.fixed_iterations(args.ba_iters)
+    reps = max(1, args.sharded_reps)
+    full = DeviceBAProblem(bp, ctx)
+    full.solve(opts)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        full.reset()
+        s1 = full.solve(opts)
+    t_single = (time.perf_counter() - t0) / reps
+    full.close()
+    out = {"workload": f"config 4 BA: {len(bp.pts)} landmarks x {len(bp.cams)} keyframes, {len(bp.obs)} observations, "
+                       f"{args.ba_iters} LM iterations", "single_gpu_ms": round(1e3 * t_single, 3),
+           "single_gpu_ba_iter_per_s": round(s1["iterations"] / t_single, 1)}
+    if dist is not None:
+        local, (lo, hi) = shard_landmarks(bp, rank, world)
+        d = DeviceBAProblem(local, ctx)
+        ar = torch_allreduce()
+        stream = torch.cuda.Stream()  # kernels and RCCL ordered on one (non-default) stream
+        with torch.cuda.stream(stream):
+            ctx.set_stream(stream.cuda_stream)
+            try:
+                d.solve_sharded(ar, opts)
+                barrier()
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    d.reset()
+                    ss = d.solve_sharded(ar, opts)
+                torch.cuda.synchronize()
+                el = (time.perf_counter() - t0) / reps
+            finally:
+                ctx.set_stream(None)
+        d.close()
+        tt = torch.tensor([el], device=f"cuda:{local_rank}", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        out.update({"mode": f"landmark-sharded over {dist.get_backend()} (RCCL), {dist.get_world_size()} ranks, "
+                            f"one GPU each", "ranks": dist.get_world_size(), "sharded_ms": round(1e3 * el, 3),
+                    "sharded_ba_iter_per_s": round(ss["iterations"] / el, 1),
+                    "speedup_vs_single_gpu": round(t_single / el, 3), "landmarks_rank0": hi - lo if rank == 0 else None})
+        return out
+    # N = 1: two contexts on this GPU, threads + host exchange (the crossover point)
+    ranks = 2
+    ctxs = [Context(local_rank) for _ in range(ranks)]
+    shards = [DeviceBAProblem(shard_landmarks(bp, r, ranks)[0], ctxs[r]) for r in range(ranks)]
+    res, errs = [None] * ranks, []
+
+    def run(r, ar):
+        try:
+            for _ in range(reps):
+                shards[r].reset()
+                res[r] = shards[r].solve_sharded(ar.callback(r, ctxs[r]), opts)
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+
+    def timed():
+        ar = ThreadAllReduce(ranks)
+        th = [threading.Thread(target=run, args=(r, ar)) for r in range(ranks)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        return (time.perf_counter() - t0) / reps
+
+    timed()
+    el = timed()
+    for sh in shards:
+        sh.close()
+    for cc in ctxs:
+        cc.close()
+    if errs:
+        raise errs[0]
+    out.update({"mode": "landmark-sharded over 2 contexts of one GPU (threads, host-staged exchange)", "ranks": ranks,
+                "sharded_ms": round(1e3 * el, 3), "sharded_ba_iter_per_s": round(res[0]["iterations"] / el, 1),
+                "speedup_vs_single_gpu": round(t_single / el, 3)})
+    return out
+
+
 def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
     """S independent stereo streams on this GPU, each sequential (its own
     context = HIP stream + scratch, its own host thread; ctypes releases the
@@ -526,11 +630,15 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    if world > 1 or args.dist:
+        from datetime import timedelta
+
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        if "MASTER_ADDR" not in os.environ:  # --dist at one rank without a launcher
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29511", RANK="0", WORLD_SIZE="1")
+        dist.init_process_group("nccl", timeout=timedelta(seconds=180))
     from uasl_motion_estimation_amd import synthetic as S
     from uasl_motion_estimation_amd._lib import Context, KT
     from uasl_motion_estimation_amd.klt import klt_params
@@ -638,6 +746,12 @@ def main():
                 "timed_live": fams[dom][0] > 0}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
+    sharded = None
+    if args.sharded_ba:
+        try:
+            sharded = sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier)
+        except Exception as e:  # reported, never fatal to the headline line
+            sharded = {"error": f"{type(e).__name__}: {e}"}
     vo_line = stereo_vo_line(ctx, args.vo_matches, cpu=rank == 0 and world == 1 and not args.no_cpu_baseline) \
         if args.vo_matches > 0 else None
     cpu = parity = None
@@ -711,6 +825,7 @@ def main():
             "roofline": roofline,
             "mi_roofline": mi_rl,
             "multi_stream": multi,
+            "sharded_ba": sharded,
             "stereo_vo": vo_line,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},

@@ -133,3 +133,32 @@ def test_gpu_sharded_solve_matches_single_device(ctx, jacobi):
         assert s["iterations"] == ref_s["iterations"]
         pts[lo:hi] = p
     np.testing.assert_allclose(pts, ref_p, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_ba_solve_distributed_world2_on_device0(tmp_path, oracle):
+    """ba_solve_distributed (torch.distributed glue + me_ba_solve_sharded) in
+    two processes on device 0 over gloo (host-staged exchange): the gathered
+    landmarks and the cameras match the oracle's unsharded solve."""
+    import subprocess
+    import sys
+
+    iters = 6
+    port = str(_free_port())
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_ba_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", port, str(tmp_path), str(iters)],
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=240)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    c = S.CONFIGS[2]
+    bp = S.ba_problem(S.SEED0 + 2, c["n_feats"], c["window"], c["width"], c["height"])
+    rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=iters, function_tolerance=0.0, gradient_tolerance=0.0,
+                                 parameter_tolerance=0.0)
+    pts = np.full_like(rp, np.nan)
+    for r in range(2):
+        d = np.load(tmp_path / f"rank{r}.npz")
+        assert str(d["backend"]) == "gloo" and int(d["world"]) == 2
+        assert int(d["iterations"]) == rs["iterations"] and int(d["successful"]) == rs["successful_steps"]
+        np.testing.assert_allclose(d["cams"], rc, rtol=1e-6, atol=1e-9)
+        pts[int(d["lo"]):int(d["hi"])] = d["pts"]
+    np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)

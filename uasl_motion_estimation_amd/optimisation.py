@@ -481,6 +481,28 @@ class DeviceBAProblem:
         self.ctx.check(self.ctx.lib.me_ba_solve(self.ctx.h, byref(p), byref(o), byref(s)), "me_ba_solve")
         return _summary(s)
 
+    def solve_sharded(self, allreduce, options: SolverOptions | None = None) -> dict:
+        """me_ba_solve_sharded on this device-resident shard (a rank's landmark
+        range, see shard_landmarks): ``allreduce(dev_ptr, n)`` sums n doubles
+        across ranks in place (n < 0: max)."""
+        p = self.struct()
+        o = (options or SolverOptions()).to_c()
+        s = BASummaryC()
+
+        def _cb(ptr, n, user):
+            try:
+                allreduce(ctypes.cast(ptr, ctypes.c_void_p).value, int(n))
+                return 0
+            except Exception:  # pragma: no cover
+                import traceback
+                traceback.print_exc()
+                return -1
+
+        cb = ALLREDUCE_FN(_cb)
+        self.ctx.check(self.ctx.lib.me_ba_solve_sharded(self.ctx.h, byref(p), byref(o), cb, None, byref(s)),
+                       "me_ba_solve_sharded")
+        return _summary(s)
+
     def solve_async(self, options: SolverOptions | None = None) -> None:
         """Queue the whole solve on the ctx stream and return (me_ba_solve_async);
         wait() blocks on it and returns the summary."""
@@ -531,6 +553,33 @@ def shard_landmarks(bp, rank: int, world: int):
     return local, (lo, hi)
 
 
+class ThreadAllReduce:
+    """Exchange between contexts driven by threads of one process (several
+    contexts on one device, or one per device without a process group):
+    device buffer -> host, summed (or max) over the ranks at a barrier, -> device."""
+
+    def __init__(self, world: int):
+        import threading
+
+        self.world = world
+        self.barrier = threading.Barrier(world)
+        self.bufs = [None] * world
+
+    def callback(self, rank: int, ctx: Context):
+        def _ar(ptr, n):
+            ctx.synchronize()
+            a = np.zeros(abs(n))
+            ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, a.ctypes.data, ptr, 8 * abs(n)))
+            self.bufs[rank] = a
+            self.barrier.wait()
+            tot = np.max(self.bufs, axis=0) if n < 0 else np.sum(self.bufs, axis=0)
+            self.barrier.wait()
+            ctx.check(ctx.lib.me_memcpy_h2d(ctx.h, ptr, np.ascontiguousarray(tot).ctypes.data, 8 * abs(n)))
+            ctx.synchronize()
+
+        return _ar
+
+
 class _DeviceDoubles:
     """Zero-copy view of a device buffer for torch.as_tensor (CUDA array interface)."""
 
@@ -540,33 +589,65 @@ class _DeviceDoubles:
 
 
 def torch_allreduce(group=None):
-    """all-reduce callback over torch.distributed (RCCL on MI355X, gloo on CPU
-    tests): sums n doubles in place, or takes the max for n < 0."""
+    """all-reduce callback over torch.distributed on device buffers (RCCL on
+    MI355X): sums n doubles in place, or takes the max for n < 0."""
     import torch
     import torch.distributed as dist
 
+    dev = torch.device("cuda", torch.cuda.current_device())
+
     def _ar(ptr: int, n: int):
-        t = torch.as_tensor(_DeviceDoubles(ptr, abs(n)), device="cuda")
+        t = torch.as_tensor(_DeviceDoubles(ptr, abs(n)), device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM if n > 0 else dist.ReduceOp.MAX, group=group)
 
     return _ar
 
 
-def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context | None = None, group=None):
-    """Landmark-sharded BA over torch.distributed: each rank solves the same
-    camera system from the all-reduced S, b (one exchange per LM iteration)
-    and updates its own landmarks.  Returns (cams, local pts, (lo, hi), summary)."""
+def host_staged_allreduce(group=None):
+    """all-reduce callback for a CPU backend (gloo): device buffer -> host,
+    dist.all_reduce, -> device, ordered on torch's current stream (the
+    solver's stream inside ba_solve_distributed)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    def _ar(ptr: int, n: int):
+        t = torch.as_tensor(_DeviceDoubles(ptr, abs(n)), device=dev)
+        h = t.cpu()  # synchronises the stream the solver enqueued on
+        dist.all_reduce(h, op=dist.ReduceOp.SUM if n > 0 else dist.ReduceOp.MAX, group=group)
+        t.copy_(h)
+
+    return _ar
+
+
+def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context | None = None, group=None,
+                         allreduce=None):
+    """Landmark-sharded BA over torch.distributed: each rank holds
+    the cameras and a contiguous, observation-balanced landmark range; the
+    reduced camera system S, b (and the scalar LM quantities) are summed
+    across ranks once per LM iteration, every rank solves the same camera
+    step and updates its own landmarks.  The exchange runs on device buffers
+    through RCCL for the nccl backend, host-staged for gloo (or the given
+    ``allreduce(dev_ptr, n)`` callback).  Returns (cams, local pts, (lo, hi), summary)."""
     import torch
     import torch.distributed as dist
 
     ctx = ctx or default_context()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     local, rng = shard_landmarks(bp, rank, world)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)  # order kernels and RCCL on one stream
-    try:
-        cams, pts, summ = ba_solve_sharded(local, torch_allreduce(group), options, ctx)
-    finally:
-        ctx.set_stream(None)
+    if allreduce is None:
+        allreduce = host_staged_allreduce(group) if dist.get_backend(group) == "gloo" else torch_allreduce(group)
+    # kernels and the exchange ordered on one stream: a dedicated torch stream
+    # (the default stream's handle is 0, which me_set_stream reads as "the
+    # ctx-owned stream", and that one is not ordered with torch's)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        ctx.set_stream(stream.cuda_stream)
+        try:
+            cams, pts, summ = ba_solve_sharded(local, allreduce, options, ctx)
+        finally:
+            ctx.set_stream(None)
     return cams, pts, rng, summ
 
 
