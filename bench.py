@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--sharded-reps", type=int, default=3)
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at one rank (exercises the RCCL exchange path)")
+    ap.add_argument("--pipeline-frames", type=int, default=24,
+                    help="keyframes of the end-to-end windowed VO line (config 5 shape: KLT -> MI stereo matching -> "
+                         "WBA_Point tracks -> scale LM -> sliding-window BA); 0: off")
+    ap.add_argument("--pipeline-config", type=int, default=5)
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
@@ -565,6 +569,62 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     return out
 
 
+def pipeline_line(args, ctx, cpu: bool):
+    """End-to-end windowed stereo VO (uasl_motion_estimation_amd/pipeline.py)
+    on one synthetic stream of the pipeline config: every keyframe runs KLT,
+    MI stereo matching, the WBA_Point bookkeeping, the scale LM and the
+    sliding-window BA (10 LM iterations).  Images are uploaded before the
+    timed loop; the host bookkeeping (numpy) is inside it.  With cpu=True the
+    same loop runs on the oracle backend (1 thread) and its track IDs, feature
+    positions and poses are compared with the GPU's."""
+    from uasl_motion_estimation_amd import pipeline as PL
+
+    c = args.pipeline_config
+    n = args.pipeline_frames
+    t0 = time.perf_counter()
+    fr, K, p0, v, truth = PL.synthetic_sequence(c, n)
+    gen = time.perf_counter() - t0
+    be = PL.GPUBackend(ctx)
+    cfg = PL.PipelineConfig.from_config(c)
+    for t in range(n):
+        be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
+    ctx.synchronize()
+    vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=cpu)
+    ts = []
+    for t in range(n):
+        t1 = time.perf_counter()
+        vo.process(t, fr[t].left, fr[t].right)
+        ts.append(time.perf_counter() - t1)
+    be.close()
+    warm = min(4, n // 2)
+    steady = ts[warm:]
+    last = vo.results[-1]
+    out = {"workload": f"config {c}: {cfg.width}x{cfg.height} stereo, {cfg.n_feats} features, {cfg.window}-keyframe "
+                       f"sliding window, {n} keyframes (KLT + MI stereo match + tracks + scale LM + "
+                       f"{cfg.ba_iters}-iteration BA per keyframe)",
+           "frames_per_s": round(len(steady) / sum(steady), 2), "ms_per_frame": round(1e3 * np.mean(steady), 3),
+           "frames_timed": len(steady), "window_landmarks_last": last.n_window_pts,
+           "window_observations_last": last.n_window_obs, "tracks_created": int(vo.latest_id),
+           "pose_drift_m_last": round(float(np.abs(vo.poses[n - 1][:3] - truth[n - 1][:3]).max()), 4),
+           "render_s": round(gen, 1)}
+    if cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from pipeline_oracle import OracleBackend  # CPU baseline / parity leg only
+
+        ov = PL.WindowedStereoVO(cfg, OracleBackend(), K, p0, v, log_events=True)
+        t1 = time.perf_counter()
+        for t in range(n):
+            ov.process(t, fr[t].left, fr[t].right)
+        ct = time.perf_counter() - t1
+        pose_rel = max(float(np.max(np.abs(vo.poses[t] - ov.poses[t]) / (np.abs(ov.poses[t]) + 1e-3)))
+                       for t in range(n))
+        out["cpu_baseline"] = {"frames_per_s": round(n / ct, 3), "cores": 1, "kind": "port",
+                               "sample": f"the same {n} keyframes on the oracle backend, 1 thread; {ct:.1f} s"}
+        out["parity"] = {"events_bit_exact": vo.events == ov.events, "track_ids_equal": bool(np.array_equal(vo.ids, ov.ids)),
+                         "pose_max_rel_diff": float("%.3g" % pose_rel)}
+    return out
+
+
 def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
     """S independent stereo streams on this GPU, each sequential (its own
     context = HIP stream + scratch, its own host thread; ctypes releases the
@@ -746,6 +806,9 @@ def main():
                 "timed_live": fams[dom][0] > 0}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
+    pipe_line = None
+    if args.pipeline_frames > 0 and rank == 0:
+        pipe_line = pipeline_line(args, ctx, cpu=world == 1 and not args.no_cpu_baseline)
     sharded = None
     if args.sharded_ba:
         try:
@@ -826,6 +889,7 @@ def main():
             "mi_roofline": mi_rl,
             "multi_stream": multi,
             "sharded_ba": sharded,
+            "pipeline": pipe_line,
             "stereo_vo": vo_line,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
