@@ -440,7 +440,12 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
 // Partials (workgroup x tile) are summed in fixed order by s_assemble:
 // deterministic, no atomics.  Operand map of the MFMA: lane l holds
 // A[l&15][l>>4] and B[l>>4][l&15]; result register i holds D[(l>>4)+4i][l&15].
-constexpr int kSchurPts = 16;                       // landmarks per sub-chunk (48 rows of Y)
+// Landmarks per sub-chunk: 32 (96 rows of Y, 16 lanes per landmark) while the
+// Y block fits the LDS budget, else 16 (48 rows, 32 lanes per landmark).  Each
+// Schur workgroup leaves one set of partial tiles that s_assemble sums, so
+// twice the landmarks per workgroup halve that traffic.
+constexpr int kSchurPts = 16, kSchurPtsWide = 32;
+constexpr size_t kSchurLdsCap = 150 * 1024;
 __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
 
 template <int W>
@@ -456,9 +461,9 @@ __device__ __forceinline__ int group_max(int x) {
   return x;
 }
 
-template <int NT, int BLK>
+template <int NT, int BLK, int PTS>
 __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, CamArgs ca) {
-  constexpr int SL = BLK / kSchurPts, NW = BLK / 64;  // lanes per landmark, waves
+  constexpr int SL = BLK / PTS, NW = BLK / 64;  // lanes per landmark, waves
   extern __shared__ double smem[];
   __shared__ double red[8];
   if (ca.on && (int)blockIdx.x >= g.ksplit) {  // camera-assembly blocks of a fused launch
@@ -747,10 +752,16 @@ constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // lin_finalize_kernel instead (one launch less per iteration): the assembly
 // blocks do not read what it writes, and the camera solve that follows
 // reads both.
-__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal) {
+// Only the lower block triangle of S (16 x 16 tile rows >= tile columns) is
+// assembled unless `full`: the camera solve reads nothing else, and the upper
+// tiles would re-read the same partials transposed (43% of the traffic at
+// config 3).
+__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal,
+                                                            int full) {
   __shared__ double part[kSaGroups][kSaElems];
   static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
   if (blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x < 2) b.ssync[threadIdx.x] = 0u;  // the camera solve that follows starts its steps at 0
     lin_finalize_body(g, b, o, gc_raw, use_scal, &part[0][0]);
     return;
   }
@@ -767,8 +778,10 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
     r = idx - n * n;
     c = n;  // Y^T z: column n6 of the partial tiles
   }
+  // upper block triangle: never read by the solve (no early return: the block barrier follows)
+  const bool skip = !full && r >= 0 && c < n && (r >> 4) < (c >> 4);
   double acc = 0.0;
-  if (r >= 0 && !st->fail) {
+  if (r >= 0 && !skip && !st->fail) {
     int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
     if (I > J) {  // the partials hold the upper block triangle: S is symmetric
       int t = I; I = J; J = t;
@@ -781,7 +794,7 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
   }
   part[grp][e] = acc;
   __syncthreads();
-  if (grp != 0) return;
+  if (grp != 0 || skip) return;
   double sum = 0.0;
 #pragma unroll
   for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
@@ -824,7 +837,14 @@ constexpr int kLoadBatch = 32;
 
 __host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
 // dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
-__host__ __device__ inline size_t solve_small_doubles(int Ts) { return 256 * (size_t)Ts + 16 * (size_t)Ts + 2 * 192; }
+#ifndef ME_CHOL_PB
+#define ME_CHOL_PB 4
+#endif
+constexpr int kXchDoubles = 48 * ME_CHOL_PB;  // per buffer: pivot rows A (16 PB) | pivot rows Y (16 PB) | column group (16 PB)
+constexpr int kDiagLd = 17;  // staged diagonal block (global-memory form): 16 x 17 doubles
+__host__ __device__ inline size_t solve_small_doubles(int Ts) {
+  return 256 * (size_t)Ts + 16 * (size_t)Ts + 2 * (size_t)kXchDoubles + 16 * kDiagLd;
+}
 __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
 
 // wave-local ordering of LDS (and, for the global fallback, L1) traffic
@@ -852,7 +872,7 @@ __device__ __forceinline__ double quad_bcast(double x) {
 // chain, and splitting the updates over 4 SIMDs removes the single-wave
 // issue bottleneck of the previous one-wave version.
 #ifndef ME_RSQ_NR
-#define ME_RSQ_NR 2
+#define ME_RSQ_NR 1
 #endif
 __device__ __forceinline__ double rsqrt_nr(double p) {
   double r = __builtin_amdgcn_rsq(p);
@@ -860,84 +880,98 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
   if (ME_RSQ_NR > 1) r = r * fma(-0.5 * p * r, r, 1.5);
   return r;
 }
-constexpr int kXchDoubles = 192;  // per buffer: pivot rows A (64) | pivot rows Y (64) | column group (64)
 // PB = pivots per round (PB x PB pivot block, factored and inverted
 // redundantly by every lane); round R eliminates columns PB R .. PB R + PB - 1.
 // The per-round cost is a fixed ~690 cycles (barrier + LDS exchange + read
 // latency) plus the uniform PB x PB work, which every lane issues.  Measured
 // on config 3 (7 diagonal blocks): PB = 4 -> 45.4k cycles of diagonal work per
 // solve, PB = 2 (8 rounds per block) -> 56.1k; PB = 4 stays.
-#ifndef ME_CHOL_PB
-#define ME_CHOL_PB 4
+#ifdef ME_ROUND_STAMPS  // timing experiment only (tools/abl): per-round phase times of the diagonal factor
+__device__ unsigned long long g_round_stamps[8];
+#define RSTAMP(k, dep)                                                                                 \
+  do {                                                                                                 \
+    if (threadIdx.x == 0) {                                                                            \
+      asm volatile("" ::"v"(dep));                                                                     \
+      unsigned long long tt_;                                                                          \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt_)::"memory");                     \
+      if ((k) > 0) atomicAdd(&g_round_stamps[(k)-1], tt_ - rs_prev_);                                 \
+      rs_prev_ = tt_;                                                                                  \
+    }                                                                                                  \
+  } while (0)
+#else
+#define RSTAMP(k, dep) \
+  do {                 \
+  } while (0)
 #endif
 template <int PB, int R>
 __device__ __forceinline__ void cholw_round(double& a, double& y, bool act, int i, int c, int nreal, bool& ok,
                                             double* Ablk, int ld, double* X, double* xch) {
   double* xb = xch + kXchDoubles * (R & 1);
   constexpr int p0 = PB * R;
+#ifdef ME_ROUND_STAMPS
+  unsigned long long rs_prev_ = 0;
+#endif
+  RSTAMP(0, a);
   if (act) {
     if (i >= p0 && i < p0 + PB) {
-      xb[16 * (i - p0) + c] = a;       // A[p0+u][c]
-      xb[64 + 16 * (i - p0) + c] = y;  // Y[p0+u][c]
+      xb[16 * (i - p0) + c] = a;            // A[p0+u][c]
+      xb[16 * PB + 16 * (i - p0) + c] = y;  // Y[p0+u][c]
     }
-    if (c >= p0 && c < p0 + PB) xb[128 + PB * i + (c - p0)] = a;  // A[i][p0+u]
+    if (c >= p0 && c < p0 + PB) xb[32 * PB + PB * i + (c - p0)] = a;  // A[i][p0+u]
   }
   __syncthreads();
   if (!act) return;
-  // uniform PB x PB Cholesky of the pivot block and its inverse M = L^-1
-  double Lq[PB][PB], rinv[PB];
+  RSTAMP(1, a);
+  // Uniform PB x PB Cholesky of the pivot block (every lane, redundantly),
+  // interleaved with the forward substitutions that need its columns as
+  // they appear: this lane's row of the panel, L[i][p0+t]; the row the update
+  // pairs it with, L[c][p0+t]; and the pivot rows of X = L^-1, X[p0+t][c].
+  // No inverse of the pivot block is formed, and the rank-PB update is summed
+  // as the columns arrive, so after the last pivot only one substitution step
+  // and one update term remain on the round's dependency chain.
+  double Lq[PB][PB], ar[PB], xa[PB], xy[PB];
+#pragma unroll
+  for (int u = 0; u < PB; ++u) {
+    ar[u] = xb[32 * PB + PB * i + u];  // A[i][p0+u]
+    xa[u] = xb[16 * u + c];            // A[p0+u][c] = A[c][p0+u]
+    xy[u] = xb[16 * PB + 16 * u + c];  // Y[p0+u][c]
+#pragma unroll
+    for (int v = u; v < PB; ++v) Lq[v][u] = xb[16 * v + p0 + u];  // A[p0+v][p0+u] (lower)
+  }
+  double Lr[PB], Lc[PB], Xg[PB];
+  double av = a, yv = y;
 #pragma unroll
   for (int t = 0; t < PB; ++t) {
-    double piv = xb[16 * t + p0 + t];
+    double piv = Lq[t][t];
 #pragma unroll
     for (int u = 0; u < t; ++u) piv = fma(-Lq[t][u], Lq[t][u], piv);
     const bool pad = p0 + t >= nreal;  // padding / right-hand-side row: never a failure
     ok = ok && (pad || piv > 0);
     piv = (pad && !(piv > 0)) ? 1.0 : piv;
     const double r = rsqrt_nr(piv);
-    rinv[t] = r;
     Lq[t][t] = piv * r;
 #pragma unroll
     for (int v = t + 1; v < PB; ++v) {
-      double x = xb[16 * v + p0 + t];
+      double x = Lq[v][t];
 #pragma unroll
       for (int u = 0; u < t; ++u) x = fma(-Lq[v][u], Lq[t][u], x);
       Lq[v][t] = x * r;
     }
-  }
-  double M[PB][PB];
+    double sr = ar[t], sc = xa[t], sx = xy[t];
 #pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    M[t][t] = rinv[t];
-#pragma unroll
-    for (int u = t - 1; u >= 0; --u) {
-      double x = 0.0;
-#pragma unroll
-      for (int v = u; v < t; ++v) x = fma(Lq[t][v], M[v][u], x);
-      M[t][u] = -x * rinv[t];
+    for (int u = 0; u < t; ++u) {
+      sr = fma(-Lr[u], Lq[t][u], sr);
+      sc = fma(-Lc[u], Lq[t][u], sc);
+      sx = fma(-Lq[t][u], Xg[u], sx);
     }
+    Lr[t] = sr * r;  // L[i][p0+t]
+    Lc[t] = sc * r;  // L[c][p0+t]
+    Xg[t] = sx * r;  // X[p0+t][c]
+    av = fma(-Lr[t], Lc[t], av);
+    yv = fma(-Lr[t], Xg[t], yv);
   }
-  double ar[PB], xa[PB], xy[PB];
-#pragma unroll
-  for (int u = 0; u < PB; ++u) {
-    ar[u] = xb[128 + PB * i + u];  // A[i][p0+u]
-    xa[u] = xb[16 * u + c];        // A[p0+u][c] = A[c][p0+u]
-    xy[u] = xb[64 + 16 * u + c];   // Y[p0+u][c]
-  }
-  double Lr[PB], Lc[PB], Xg[PB];
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    double sr = 0.0, sc = 0.0, sx = 0.0;
-#pragma unroll
-    for (int u = 0; u <= t; ++u) {
-      sr = fma(ar[u], M[t][u], sr);
-      sc = fma(xa[u], M[t][u], sc);
-      sx = fma(M[t][u], xy[u], sx);
-    }
-    Lr[t] = sr;  // L[i][p0+t]
-    Lc[t] = sc;  // L[c][p0+t]
-    Xg[t] = sx;  // X[p0+t][c]
-  }
+  RSTAMP(2, Lq[PB - 1][PB - 1]);
+  RSTAMP(3, Lr[PB - 1] + Lc[PB - 1] + Xg[PB - 1]);
   if (c >= p0 && c < p0 + PB && c <= i) {
     double v = Lr[0];
 #pragma unroll
@@ -958,15 +992,10 @@ __device__ __forceinline__ void cholw_round(double& a, double& y, bool act, int 
     X[i * 16 + c] = v;
   }
   if (i >= p0 + PB) {
-    double av = a, yv = y;
-#pragma unroll
-    for (int t = 0; t < PB; ++t) {
-      av = fma(-Lr[t], Lc[t], av);
-      yv = fma(-Lr[t], Xg[t], yv);
-    }
     a = av;
     y = yv;
   }
+  RSTAMP(4, a + y);
 }
 
 template <int PB, int R>
@@ -976,11 +1005,152 @@ __device__ __forceinline__ void chol_rounds(double& a, double& y, bool act, int 
   if constexpr (R + 1 < 16 / PB) chol_rounds<PB, R + 1>(a, y, act, i, c, nreal, ok, Ablk, ld, X, xch);
 }
 
-template <bool kLds>
-__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip) {
+// Global-memory form (windows whose [S; -b^T] does not fit the LDS, config 4
+// and 5): block 0 factors the diagonal blocks and panels as below, and the
+// trailing update of each block step is spread over `nworkers` further
+// workgroups of the same launch.  Hand-offs through b.ssync (zeroed by
+// s_assemble before every solve): block 0 publishes step J (epoch J + 1)
+// once the panel of J is stored (every thread: agent-scope release fence,
+// barrier, release store); a worker waits for the epoch (acquire, barrier),
+// updates its tiles of step J and counts itself done (fence, barrier,
+// release add); block 0 waits for all workers before the next diagonal
+// block.  Every spin is bounded: a missing partner ends the solve as a
+// failed step, never a hang.
+constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
+// Hand-off form (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms
+// row 1): every store of A is write-through (sc1), every storing wave drains
+// (vmcnt 0) before the workgroup barrier, ONE lane then stores the epoch / adds
+// to the counter (agent-scope atomic), the consumer polls with an sc1 load and
+// reads A only with sc1 loads after its barrier -- no release fence (an L2
+// write-back) and no acquire (an L1 invalidate) per hand-off.
+template <bool SC1>
+__device__ __forceinline__ double a_ld(const double* p) {
+  if (!SC1) return *p;
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool SC1>
+__device__ __forceinline__ void a_st(double* p, double v) {
+  if (!SC1) {
+    *p = v;
+    return;
+  }
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_and_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+  __syncthreads();
+}
+constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
+constexpr int kSolveMwMinTs = 16;             // block steps from which the trailing workers are used
+
+template <bool SC1>
+__device__ void trailing_tiles(double* A, int ld, int Ts, int J, int first, int stride, int lane) {
+  const int j0 = 16 * J;
+  const int rem = Ts - J - 1;
+  const int npairs = rem * (rem + 1) / 2;
+  for (int p = first; p < npairs; p += stride) {
+    int I = 0, q = p;
+    while (q > I) {
+      q -= I + 1;
+      ++I;
+    }
+    const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
+    double av[4], bv[4];
+    double4_t acc;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cc = j0 + 4 * s + (lane >> 4);
+      av[s] = -a_ld<SC1>(&A[(long)(i0 + (lane & 15)) * ld + cc]);
+      bv[s] = a_ld<SC1>(&A[(long)(k0 + (lane & 15)) * ld + cc]);
+      acc[s] = a_ld<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a_st<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)], acc[s]);
+  }
+}
+
+// One trailing tile of block step J: A_IK -= L_IJ L_KJ^T (16 x 16, v_mfma_f64_16x16x4f64).
+template <bool SC1>
+__device__ __forceinline__ void trailing_tile(double* A, int ld, int J, int I, int K, int lane) {
+  const int j0 = 16 * J, i0 = 16 * I, k0 = 16 * K;
+  double av[4], bv[4];
+  double4_t acc;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int cc = j0 + 4 * s + (lane >> 4);
+    av[s] = -a_ld<SC1>(&A[(long)(i0 + (lane & 15)) * ld + cc]);
+    bv[s] = a_ld<SC1>(&A[(long)(k0 + (lane & 15)) * ld + cc]);
+    acc[s] = a_ld<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)]);
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) a_st<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)], acc[s]);
+}
+
+// Workers of the multi-workgroup solve.  Tile (I, K), 1 <= K <= I < Ts, is
+// owned by one wave of one worker for the whole solve (linear index
+// (I-1) I / 2 + K - 1, dealt round-robin over the workers' waves), so its
+// successive updates are ordered by that wave's program order.  Per block step
+// J (after block 0 publishes the panel of J): the tiles of column J + 1 first
+// -- block 0 factors that column next -- then the worker signals, then its
+// other tiles, which overlap block 0's diagonal block and panel of J + 1.
+__device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
+  __shared__ unsigned sep;
+  const State* st = b.st;
+  if (st->done || st->fail || b.scal[R_COUNT] != 0.0) return;  // block 0 returns for the same reasons
+  const int Ts = g.Ts, ld = solve_ld(Ts);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int slot0 = (blockIdx.x - 1) * nw + wave, nslots = nworkers * nw;
+  const int ntiles = (Ts - 1) * Ts / 2;
+  for (int J = 0; J + 1 < Ts; ++J) {
+    if (tid == 0) {
+      unsigned e = 0;
+      long k = 0;
+      for (; k < kSolveSpin; ++k) {
+        e = __hip_atomic_load(b.ssync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e >= (unsigned)(J + 1)) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      sep = k == kSolveSpin ? kSolveTerm : e;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
+    __syncthreads();
+    if (sep >= kSolveTerm) return;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int t = slot0; t < ntiles; t += nslots) {
+        int I = 1, r = t;
+        while (r >= I) {  // t = (I-1) I / 2 + (K-1)
+          r -= I;
+          ++I;
+        }
+        const int K = r + 1;
+        if (pass == 0 ? K == J + 1 : K > J + 1) trailing_tile<true>(b.Abuf, ld, J, I, K, lane);
+      }
+      if (pass == 0) {
+        drain_and_barrier();
+        if (tid == 0) __hip_atomic_fetch_add(b.ssync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// kMode: 0 = [S; -b^T] in LDS, one workgroup; 1 = in global memory, one workgroup;
+// 2 = in global memory, trailing updates on `nworkers` more workgroups (sc1 hand-offs)
+template <int kMode>
+__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int nworkers) {
   extern __shared__ double smem[];
   __shared__ double red[64];
   __shared__ int sfail;
+  constexpr bool kLds = kMode == 0, kSc1 = kMode == 2;
+  if (kMode == 2 && blockIdx.x > 0) {
+    cam_solve_worker(g, b, nworkers);
+    return;
+  }
   State* st = b.st;
   const int n = g.n6, Ts = g.Ts, N = 16 * Ts;
   const int ld = solve_ld(Ts);
@@ -995,6 +1165,16 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int done = st->done;
   const int fail_in = st->fail || b.scal[R_COUNT] != 0.0;
   const double radius = st->radius;
+  // the candidate-camera inputs (current cameras, Jacobi scales) are requested
+  // now; they are consumed after the factorisation, which hides their latency
+  const int cur = st->cur;
+  const int ncp = 6 * g.nc;
+  const bool pre = ncp <= nt;
+  double x_pre = 0.0, cs_pre = 1.0;
+  if (pre && tid < ncp) {
+    x_pre = b.cams[cur][tid];
+    if (tid >= 6 * g.nf) cs_pre = b.csc[tid - 6 * g.nf];
+  }
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
   for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
     double v[kLoadBatch];
@@ -1004,8 +1184,13 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       const int r = wave + nw * t, c = lane + 64 * uu;
       v[k] = 0.0;
       if (q < NQ && r < N && c < n && (c >> 4) <= (r >> 4)) {
-        if (r < n) v[k] = b.S[r * n + c];
-        else if (r == n) v[k] = -b.bvec[c];
+        if (r < n) {
+          v[k] = b.S[r * n + c];
+          // LM diagonal (Ceres: clamp(diag(U)) / radius), loaded in the same round
+          if (r == c) v[k] += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
+        } else if (r == n) {
+          v[k] = -b.bvec[c];
+        }
       } else if (q < NQ && c == n && r < n && (r >> 4) == (n >> 4)) {
         v[k] = -b.bvec[r];  // the diagonal block must stay symmetric
       }
@@ -1015,7 +1200,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     for (int k = 0; k < kLoadBatch; ++k) {
       const int q = q0 + k, t = q / CC, uu = q - t * CC;
       const int r = wave + nw * t, c = lane + 64 * uu;
-      if (q < NQ && r < N && c < N && (c >> 4) <= (r >> 4)) A[r * ld + c] = (r == c && r >= n) ? 1.0 : v[k];
+      if (q < NQ && r < N && c < N && (c >> 4) <= (r >> 4)) a_st<kSc1>(&A[r * ld + c], (r == c && r >= n) ? 1.0 : v[k]);
     }
   }
   if (done) return;
@@ -1027,8 +1212,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     if (tid == 0) st->fail = 1;
     return;
   }
-  for (int r = tid; r < n; r += nt) A[r * ld + r] += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
-  __syncthreads();
   SOLVE_STAMP(0);
   for (int J = 0; J < Ts; ++J) {
     const int j0 = 16 * J;
@@ -1038,14 +1221,23 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       const bool act = wave < 4;
       const int i = 4 * wave + (lane >> 4), c = lane & 15;
       double* Ablk = A + (long)j0 * ld + j0;
+      // global-memory form: the rounds write the block's L into LDS (a round's
+      // barrier would otherwise wait for its global stores), copied back after
+      double* Lblk = kLds ? Ablk : xch + 2 * kXchDoubles;
+      const int lld = kLds ? ld : kDiagLd;
       double a = 0.0, y = 0.0;
       if (act) {
-        a = Ablk[i * ld + c];
+        a = a_ld<kSc1>(&Ablk[i * ld + c]);
         y = (c == i) ? 1.0 : 0.0;
       }
       bool ok = true;
       double* XJw = X + 256 * J;
-      chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Ablk, ld, XJw, xch);
+      if (!(skip & 1)) {
+        chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Lblk, lld, XJw, xch);
+      } else {  // timing diagnostics (ME_SOLVE_SKIP & 1): the rounds' barriers only
+        for (int r = 0; r < 16 / ME_CHOL_PB; ++r) __syncthreads();
+      }
+      if (!kLds && act && c <= i) a_st<kSc1>(&Ablk[i * ld + c], Lblk[i * kDiagLd + c]);
       if (act && !ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
@@ -1055,61 +1247,60 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     // (b) panel on the matrix cores: L_IJ = A_IJ X_J^T
     {
       const double* XJ = X + 256 * J;
-      for (int I = J + 1 + wave; I < Ts; I += nw) {
+      for (int I = J + 1 + wave; I < ((skip & 2) ? 0 : Ts); I += nw) {
         const int i0 = 16 * I;
         double av[4], bv[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          av[s] = A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s + (lane >> 4)];
+          av[s] = a_ld<kSc1>(&A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s + (lane >> 4)]);
           bv[s] = XJ[(lane & 15) * 16 + 4 * s + (lane >> 4)];
         }
         double4_t acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) A[(long)(i0 + (lane >> 4) + 4 * q) * ld + j0 + (lane & 15)] = acc[q];
+        for (int q = 0; q < 4; ++q) a_st<kSc1>(&A[(long)(i0 + (lane >> 4) + 4 * q) * ld + j0 + (lane & 15)], acc[q]);
       }
     }
     __syncthreads();
     SOLVE_STAMP(2);
     SOLVE_START(3);
     // (c) trailing update on the matrix cores: A_IK -= L_IJ L_KJ^T, J < K <= I
-    const int rem = Ts - J - 1;
-    const int npairs = rem * (rem + 1) / 2;
-    for (int p = wave; p < npairs; p += nw) {
-      int I = 0, q = p;
-      while (q > I) {
-        q -= I + 1;
-        ++I;
+    if (kMode == 2 && nworkers > 0) {
+      if (J + 1 < Ts) {  // hand the step to the workers and wait for all of them
+        drain_and_barrier();  // the panel's (and diagonal copy-back's) sc1 stores have left
+        if (tid == 0) {
+          __hip_atomic_store(b.ssync, (unsigned)(J + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned want = (unsigned)nworkers * (unsigned)(J + 1);
+          long k = 0;
+          for (; k < kSolveSpin; ++k) {
+            if (__hip_atomic_load(b.ssync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (k == kSolveSpin) sfail = 1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
+        __syncthreads();
       }
-      const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
-      double av[4], bv[4];
-      double4_t acc;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int cc = j0 + 4 * s + (lane >> 4);
-        av[s] = -A[(long)(i0 + (lane & 15)) * ld + cc];
-        bv[s] = A[(long)(k0 + (lane & 15)) * ld + cc];
-        acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)];
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)] = acc[s];
+    } else {
+      if (!(skip & 4)) trailing_tiles<kSc1>(A, ld, Ts, J, wave, nw, lane);
+      __syncthreads();
     }
-    __syncthreads();
     SOLVE_STAMP(3);
   }
   if (sfail) {
-    if (tid == 0) st->fail = 1;
+    if (tid == 0) {
+      st->fail = 1;
+      if (kMode == 2 && nworkers > 0) __hip_atomic_store(b.ssync, kSolveTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     return;
   }
   SOLVE_START(5);
   // backward solve L^T y = z (z = row n of L), block by block: wave 0 forms
   // y_J = X_J^T z_J, then every wave updates the entries above the block
-  for (int c = tid; c < N; c += nt) u[c] = c < n ? A[(long)n * ld + c] : 0.0;
+  for (int c = tid; c < N; c += nt) u[c] = c < n ? a_ld<kSc1>(&A[(long)n * ld + c]) : 0.0;
   __syncthreads();
-  for (int J = (n - 1) >> 4; J >= 0; --J) {
+  for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
     const int j0 = 16 * J;
     if (wave == 0) {
       const double* XJ = X + 256 * J;
@@ -1131,8 +1322,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         double a0 = 0.0, a1 = 0.0;
 #pragma unroll
         for (int m = 0; m < 16; m += 2) {
-          a0 = fma(A[(long)(j0 + m) * ld + cc], yj[m], a0);
-          a1 = fma(A[(long)(j0 + m + 1) * ld + cc], yj[m + 1], a1);
+          a0 = fma(a_ld<kSc1>(&A[(long)(j0 + m) * ld + cc]), yj[m], a0);
+          a1 = fma(a_ld<kSc1>(&A[(long)(j0 + m + 1) * ld + cc]), yj[m + 1], a1);
         }
         u[cc] -= a0 + a1;
       }
@@ -1142,23 +1333,23 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   SOLVE_STAMP(5);
   for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
   // candidate cameras
-  const int cur = st->cur;
   const double* x = b.cams[cur];
   double* xc = b.cams[1 - cur];
   double s2 = 0, xn2 = 0;
-  for (int i = tid; i < 6 * g.nc; i += nt) {
+  for (int i = tid; i < ncp; i += nt) {
+    const double xi = pre ? x_pre : x[i];
     const int ci = i / 6 - g.nf;
     if (ci < 0) {
-      xc[i] = x[i];
+      xc[i] = xi;
       continue;
     }
-    const double d = u[i - 6 * g.nf] * b.csc[i - 6 * g.nf];
+    const double d = u[i - 6 * g.nf] * (pre ? cs_pre : b.csc[i - 6 * g.nf]);
     b.dc[i - 6 * g.nf] = d;
-    const double v = x[i] + d;
+    const double v = xi + d;
     xc[i] = v;
-    const double dd = v - x[i];
+    const double dd = v - xi;
     s2 += dd * dd;
-    xn2 += x[i] * x[i];
+    xn2 += xi * xi;
   }
   double v2[2] = {s2, xn2}, out[2];
   block_sum<2>(v2, out, red);
@@ -1711,6 +1902,8 @@ struct Plan {
   int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
   int n_enq = 0;      // linearisations queued so far (the first runs the camera assembly on its own)
   bool sequential = false;  // ME_BA_SEQUENTIAL=1: never fuse (A/B timing)
+  bool full_S = false;      // assemble both block triangles of S (reduced-system / covariance read-back)
+  int solve_workers = -1;   // global-memory camera solve: trailing-update workgroups (-1: by size; ME_SOLVE_WORKERS)
 };
 
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
@@ -1738,6 +1931,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   P.c = c;
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
+  if (const char* sw = getenv("ME_SOLVE_WORKERS")) P.solve_workers = atoi(sw);  // A/B timing (0: one workgroup)
   if (const char* sq = getenv("ME_BA_SEQUENTIAL")) P.sequential = atoi(sq) != 0;
   Geo& g = P.g;
   g.nc = p->n_cams;
@@ -1751,7 +1945,12 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.T = g.Rpad / 16;
   g.Ts = (g.n6 + 1 + 15) / 16;
   g.npairs = g.T * (g.T + 1) / 2;
-  g.spts = kSchurPts;
+  // wide sub-chunks pay off once the tile count is large (config 4: 66 pairs,
+  // -2% BA time); at config 3 (28 pairs) the longer per-workgroup chain costs
+  // more than the halved partial traffic saves (1.23 vs 1.19 ms per 10 iterations)
+  g.spts = (g.npairs > 40 && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap) ? kSchurPtsWide : kSchurPts;
+  if (const char* e = getenv("ME_SCHUR_PTS"))  // A/B timing only
+    if (atoi(e) == kSchurPts) g.spts = kSchurPts;
   g.nsub = (int)std::max(1L, ((long)g.np + g.spts - 1) / g.spts);
   g.ksplit = std::min(g.nsub, 256);  // Schur workgroups = partial slices summed by s_assemble
   ME_CHECK(c, g.npairs <= 8 * 24, "BA: %d variable cameras exceed the Schur tile budget", g.m);
@@ -1836,7 +2035,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * (size_t)g.n6, &P.gc_glob);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
-  add(4 * (size_t)(g.m + 1), &b.cnt);  // last-arrival counters: per camera (cam_assemble) | pt_step
+  add(4 * (size_t)(g.m + 1 + 2), &b.cnt);  // last-arrival counters: per camera (cam_assemble) | pt_step | solve sync
   const size_t work_bytes = 4 * (2 * (size_t)g.np + (size_t)g.nblk_obs * g.nc + 4);
   add(work_bytes, &b.work);
   const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
@@ -1853,6 +2052,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     *it.second = ptr;
     ptr += it.first;
   }
+  b.ssync = b.cnt + g.m + 1;
   b.bvec = b.S + (size_t)g.n6 * g.n6;
   b.diagU = b.bvec + g.n6;
   void* hp;
@@ -1910,17 +2110,14 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
   if (!P.use_lds) P.solve_lds = 8 * solve_small_doubles(g.Ts);
   ME_CHECK(c, P.solve_lds <= 150 * 1024, "BA: %d variable cameras exceed the camera-solve workspace", g.m);
-  ME_HIP(c, hipFuncSetAttribute(P.use_lds ? (const void*)cam_solve_kernel<true> : (const void*)cam_solve_kernel<false>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
+  for (const void* k : {(const void*)cam_solve_kernel<0>, (const void*)cam_solve_kernel<1>, (const void*)cam_solve_kernel<2>})
+    ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
-  ME_CHECK(c, P.schur_lds <= 150 * 1024, "BA: %d variable cameras exceed the Schur workspace", g.m);
-  for (const void* k :
-       {(const void*)pt_schur_kernel<3, 512>, (const void*)pt_schur_kernel<4, 512>,
-        (const void*)pt_schur_kernel<5, 512>, (const void*)pt_schur_kernel<6, 512>,
-        (const void*)pt_schur_kernel<7, 512>, (const void*)pt_schur_kernel<8, 512>,
-        (const void*)pt_schur_kernel<9, 512>, (const void*)pt_schur_kernel<10, 512>,
-        (const void*)pt_schur_kernel<12, 512>, (const void*)pt_schur_kernel<16, 512>,
-        (const void*)pt_schur_kernel<24, 512>})
+  ME_CHECK(c, P.schur_lds <= kSchurLdsCap, "BA: %d variable cameras exceed the Schur workspace", g.m);
+#define ME_SCHUR_K(N) (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>
+  for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5), ME_SCHUR_K(6), ME_SCHUR_K(7), ME_SCHUR_K(8),
+                        ME_SCHUR_K(9), ME_SCHUR_K(10), ME_SCHUR_K(12), ME_SCHUR_K(16), ME_SCHUR_K(24)})
+#undef ME_SCHUR_K
     ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
   return ME_OK;
 }
@@ -1973,7 +2170,13 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     // more than the 512-thread instances.)
     const int pw8 = (g.npairs + 7) / 8;
     const dim3 grd(g.ksplit + (fused ? g.m * g.ck : 0));
-#define ME_SCHUR(N) hipLaunchKernelGGL((pt_schur_kernel<N, 512>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca)
+#define ME_SCHUR(N)                                                                                          \
+  do {                                                                                                       \
+    if (g.spts == kSchurPtsWide)                                                                             \
+      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsWide>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca); \
+    else                                                                                                     \
+      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPts>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca);     \
+  } while (0)
     if (pw8 <= 3) ME_SCHUR(3);
     else if (pw8 <= 4) ME_SCHUR(4);
     else if (pw8 <= 5) ME_SCHUR(5);
@@ -2002,7 +2205,7 @@ int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
   const double* gc = ar ? P.gc_glob : P.gc_raw;
   if (g.m > 0)
     hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kSaElems) + 1), dim3(kBlock), 0,
-                       c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
+                       c->stream, g, P.b, P.o, gc, ar ? 1 : 0, P.full_S ? 1 : 0);
   else
     hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
   return me_check_launch(c, "BA assemble");
@@ -2027,10 +2230,23 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_SOLVE);
-    if (P.use_lds)
-      hipLaunchKernelGGL(cam_solve_kernel<true>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip);
-    else
-      hipLaunchKernelGGL(cam_solve_kernel<false>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip);
+    if (P.use_lds) {
+      hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip, 0);
+    } else {
+      // Trailing-update workers pay once the block steps are many and wide:
+      // config 5 (19 steps) 372 -> 274 us per solve; config 4 (11 steps) is
+      // faster on one workgroup (118 vs 131 us: the per-step hand-offs).
+      const int np0 = (g.Ts - 1) * g.Ts / 2;
+      const int nwk = P.solve_workers >= 0 ? P.solve_workers
+                      : g.Ts >= kSolveMwMinTs
+                          ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
+                          : 0;
+      if (nwk > 0)
+        hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o,
+                           P.diag_skip, nwk);
+      else
+        hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip, 0);
+    }
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
@@ -2231,6 +2447,17 @@ extern "C" int me_ba_solve(me_ctx* c, me_ba_problem* p, const me_ba_options* o, 
   return solve_impl(c, p, o, nullptr, nullptr, s);
 }
 
+#ifdef ME_ROUND_STAMPS
+extern "C" int me_round_stamps(unsigned long long* out, int reset) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_round_stamps), sizeof(g_round_stamps));
+  if (reset) {
+    unsigned long long z[8] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_round_stamps), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
+
 extern "C" int me_ba_solve_sharded(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn ar,
                                    void* user, me_ba_summary* s) {
   if (!ar) return me_set_error(c, ME_ERR_INVALID, "me_ba_solve_sharded: null allreduce");
@@ -2298,6 +2525,7 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
   ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
+  P.full_S = true;
   const Geo& g = P.g;
   ME_TRY(enqueue_linearize(P, nullptr, nullptr));
   ME_TRY(enqueue_assemble(P, nullptr));
@@ -2327,6 +2555,7 @@ extern "C" int me_ba_covariance(me_ctx* c, const me_ba_problem* p, double* cov, 
   ME_CHECK(c, p->mem == ME_HOST, "BA: evaluation helpers take host arrays");
   int rc = plan_build(c, p, &o, P, 0);
   if (rc < 0) return rc;
+  P.full_S = true;
   const Geo& g = P.g;
   hipLaunchKernelGGL(cov_prep_kernel, dim3(1), dim3(1), 0, c->stream, P.b);
   ME_TRY(enqueue_linearize(P, nullptr, nullptr));

@@ -116,6 +116,7 @@ struct Bufs {
   State* st;
   int* work;          // plan build: cnt_p[np] | fill_p[np] | blk_cam[nblk_obs*nc] | flags[4] (zeroed)
   unsigned* cnt;      // last-arrival counters: m (cam_assemble, per camera) + 1 (pt_step); re-armed by the last
+  unsigned* ssync;    // camera solve, global-memory form: {step epoch, worker step count} (zeroed by s_assemble)
   double* out;        // State | cams[cur] | pts[cur] for the single read-back
 };
 
