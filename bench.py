@@ -804,6 +804,13 @@ def main():
                 "frac": round(achieved / peak, 5), "traffic": pmc_traffic(dom), "kernel": dom,
                 "kernels": FAMILY_KERNELS.get(dom), "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount,
                 "timed_live": fams[dom][0] > 0}
+    if "BA_SOLVE" in budget:  # the frame's largest kernel has no HBM/MFMA roofline: a latency budget
+        b = budget["BA_SOLVE"]
+        roofline["solve"] = {"kernel": "cam_solve_kernel", "bound": "latency (dependent blocked-Cholesky chain)",
+                             "us_per_lm_iteration": b["us_per_launch"], "launches_per_frame": b["launches_per_frame"],
+                             "us_per_frame": b["us_per_frame"],
+                             "share_of_step": round(b["us_per_frame"] * 1e-3 / (t_max * 1e3 / max(frames_total, 1)
+                                                                                  * max(world, 1)), 4)}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
     pipe_line = None

@@ -745,17 +745,18 @@ __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) 
 // S = U - sum over the Schur workgroups' partial tiles, b = g - Y^T z, diag(U)
 // (sharded mode: the local pieces, no LM diagonal).  256 threads = 32
 // elements x 8 partial groups: group k sums partials k, k + 8, ... in order,
-// then the 8 group sums are added in order (deterministic); consecutive
-// threads read consecutive doubles of a tile row.
+// then the 8 group sums are added in order (deterministic).  The threads walk
+// the partial tiles in their own layout (the upper block triangle, tile pair
+// p = (I <= J), row-major 16 x 16), so consecutive threads read consecutive
+// doubles of every partial; the sums land in the lower block triangle of S
+// (transposed for I < J; the diagonal tiles as they are), the column n6 of
+// the tiles in b.  `full` also writes the upper block triangle (reduced-system
+// / covariance read-back); the camera solve reads only the lower one.
 constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // The grid's last workgroup runs the linearisation bookkeeping of
 // lin_finalize_kernel instead (one launch less per iteration): the assembly
 // blocks do not read what it writes, and the camera solve that follows
 // reads both.
-// Only the lower block triangle of S (16 x 16 tile rows >= tile columns) is
-// assembled unless `full`: the camera solve reads nothing else, and the upper
-// tiles would re-read the same partials transposed (43% of the traffic at
-// config 3).
 __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal,
                                                             int full) {
   __shared__ double part[kSaGroups][kSaElems];
@@ -770,43 +771,47 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
   const int n = g.n6;
   const int e = threadIdx.x % kSaElems, grp = threadIdx.x / kSaElems;
   const int idx = blockIdx.x * kSaElems + e;
-  int r = -1, c = -1;
-  if (idx < n * n) {
-    r = idx / n;
-    c = idx - r * n;
-  } else if (idx < n * n + n) {
-    r = idx - n * n;
-    c = n;  // Y^T z: column n6 of the partial tiles
-  }
-  // upper block triangle: never read by the solve (no early return: the block barrier follows)
-  const bool skip = !full && r >= 0 && c < n && (r >> 4) < (c >> 4);
-  double acc = 0.0;
-  if (r >= 0 && !skip && !st->fail) {
-    int I = r >> 4, J = c >> 4, rr = r & 15, cc = c & 15;
-    if (I > J) {  // the partials hold the upper block triangle: S is symmetric
-      int t = I; I = J; J = t;
-      t = rr; rr = cc; cc = t;
+  int gr = -1, gc = -1;  // position in the (padded) system [S | b]
+  bool diag = false;
+  if (idx < g.npairs * 256) {
+    int p = idx >> 8, I = 0;
+    while (p >= g.T - I) {  // tile pair p -> (I, J): row I holds T - I pairs
+      p -= g.T - I;
+      ++I;
     }
-    const int p = I * g.T - I * (I - 1) / 2 + (J - I);
-    const double* src = b.Spart + (long)p * 256 + rr * 16 + cc;
+    const int J = I + p;
+    diag = I == J;
+    gr = 16 * I + ((idx >> 4) & 15);
+    gc = 16 * J + (idx & 15);
+  }
+  // S entries (gr, gc < n) and the right-hand side (gc == n); the padding is skipped
+  const bool use = gr >= 0 && gr < n && gc <= n;
+  double acc = 0.0;
+  if (use && !st->fail) {
+    const double* src = b.Spart + idx;
     const long stride = (long)g.npairs * 256;
     for (int q = grp; q < g.ksplit; q += kSaGroups) acc += src[q * stride];
   }
   part[grp][e] = acc;
   __syncthreads();
-  if (grp != 0 || skip) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
+  if (grp != 0 || !use) return;
   double sum = 0.0;
 #pragma unroll
   for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
-  if (idx < n * n) {
+  if (gc < n) {
     double v = 0;
-    if (r / 6 == c / 6) v = b.U[36 * (r / 6) + (r % 6) * 6 + (c % 6)];
-    b.S[idx] = st->fail ? 0.0 : v - sum;
-  } else if (idx < n * n + n) {
-    b.bvec[r] = st->fail ? 0.0 : b.gcs[r] - sum;
-    b.diagU[r] = b.U[36 * (r / 6) + (r % 6) * 7];
-  } else if (idx == n * n + n) {
-    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
+    if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];  // U blocks are symmetric
+    v = st->fail ? 0.0 : v - sum;
+    if (diag) {
+      b.S[(long)gr * n + gc] = v;
+    } else {
+      b.S[(long)gc * n + gr] = v;
+      if (full) b.S[(long)gr * n + gc] = v;
+    }
+  } else {
+    b.bvec[gr] = st->fail ? 0.0 : b.gcs[gr] - sum;
+    b.diagU[gr] = b.U[36 * (gr / 6) + (gr % 6) * 7];
   }
 }
 
@@ -2204,7 +2209,7 @@ int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
   const Geo& g = P.g;
   const double* gc = ar ? P.gc_glob : P.gc_raw;
   if (g.m > 0)
-    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.n6 * g.n6 + g.n6 + 1, kSaElems) + 1), dim3(kBlock), 0,
+    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.npairs * 256, kSaElems) + 1), dim3(kBlock), 0,
                        c->stream, g, P.b, P.o, gc, ar ? 1 : 0, P.full_S ? 1 : 0);
   else
     hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
