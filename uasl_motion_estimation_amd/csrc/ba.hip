@@ -11,6 +11,7 @@
 #include <vector>
 #include "me_internal.hpp"
 #include "ba_kernels.hpp"
+#include "solve_diag.hpp"
 #include "me_device.hpp"
 
 using me_dev::wave_sync;
@@ -852,12 +853,6 @@ __host__ __device__ inline size_t solve_small_doubles(int Ts) {
 }
 __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
 
-// wave-local ordering of LDS (and, for the global fallback, L1) traffic
-__device__ __forceinline__ void solve_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 template <int S>
 __device__ __forceinline__ double quad_bcast(double x) {
   constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
@@ -876,15 +871,6 @@ __device__ __forceinline__ double quad_bcast(double x) {
 // LDS round trip ~105, barrier ~80 -- so the round is bound by the pivot
 // chain, and splitting the updates over 4 SIMDs removes the single-wave
 // issue bottleneck of the previous one-wave version.
-#ifndef ME_RSQ_NR
-#define ME_RSQ_NR 1
-#endif
-__device__ __forceinline__ double rsqrt_nr(double p) {
-  double r = __builtin_amdgcn_rsq(p);
-  r = r * fma(-0.5 * p * r, r, 1.5);
-  if (ME_RSQ_NR > 1) r = r * fma(-0.5 * p * r, r, 1.5);
-  return r;
-}
 // PB = pivots per round (PB x PB pivot block, factored and inverted
 // redundantly by every lane); round R eliminates columns PB R .. PB R + PB - 1.
 // The per-round cost is a fixed ~690 cycles (barrier + LDS exchange + read
@@ -1047,6 +1033,9 @@ __device__ __forceinline__ void drain_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
   __syncthreads();
 }
+#ifndef ME_SOLVE_LOOKAHEAD
+#define ME_SOLVE_LOOKAHEAD 1
+#endif
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
 constexpr int kSolveMwMinTs = 16;             // block steps from which the trailing workers are used
 
@@ -1060,6 +1049,46 @@ __device__ void trailing_tiles(double* A, int ld, int Ts, int J, int first, int 
     while (q > I) {
       q -= I + 1;
       ++I;
+    }
+    const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
+    double av[4], bv[4];
+    double4_t acc;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int cc = j0 + 4 * s + (lane >> 4);
+      av[s] = -a_ld<SC1>(&A[(long)(i0 + (lane & 15)) * ld + cc]);
+      bv[s] = a_ld<SC1>(&A[(long)(k0 + (lane & 15)) * ld + cc]);
+      acc[s] = a_ld<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)]);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) a_st<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)], acc[s]);
+  }
+}
+
+// Trailing tiles of block step J split for the lookahead of the one-workgroup
+// solve: `col` = the tiles of column J + 1 only (they feed the next diagonal
+// block), else every other tile (the deferred part, overlapped with the next
+// diagonal block).  Tiles are dealt round-robin over (first, stride).
+template <bool SC1>
+__device__ void trailing_split(double* A, int ld, int Ts, int J, bool col, int first, int stride, int lane) {
+  const int rem = Ts - J - 1;
+  const int cnt = col ? rem : rem * (rem - 1) / 2;
+  const int j0 = 16 * J;
+  for (int p = first; p < cnt; p += stride) {
+    int I, q;
+    if (col) {
+      I = p;
+      q = 0;
+    } else {  // p = I (I - 1) / 2 + q - 1, 1 <= q <= I
+      I = 1;
+      q = p;
+      while (q >= I) {
+        q -= I;
+        ++I;
+      }
+      ++q;
     }
     const int i0 = 16 * (J + 1 + I), k0 = 16 * (J + 1 + q);
     double av[4], bv[4];
@@ -1152,6 +1181,15 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   __shared__ double red[64];
   __shared__ int sfail;
   constexpr bool kLds = kMode == 0, kSc1 = kMode == 2;
+  // lookahead: the trailing update of step J outside column J + 1 overlaps the
+  // next diagonal block (config 3: 44.2 -> 42.0 us).  Measured and dropped:
+  // the panel fused with the column-(J+1) update in one phase (transposed
+  // panel tiles as MFMA operands, no barrier between; 43.8 us) and a one-wave
+  // backward solve without workgroup barriers (unchanged).
+  constexpr bool kLook = ME_DIAG_MFMA && ME_SOLVE_LOOKAHEAD && kMode != 2;
+  // Measured and dropped (config 3): panel fused with the column-(J+1) update
+  // in one phase (transposed panel tiles as MFMA operands, no barrier between;
+  // 43.8 vs 42.0 us) and a one-wave backward solve without barriers (no change)
   if (kMode == 2 && blockIdx.x > 0) {
     cam_solve_worker(g, b, nworkers);
     return;
@@ -1223,7 +1261,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     SOLVE_START(1);
     // (a) diagonal block + its inverse (waves 0-3; every wave joins the barriers)
     {
-      const bool act = wave < 4;
+      const bool act = !ME_DIAG_MFMA && wave < 4;  // four-wave form
       const int i = 4 * wave + (lane >> 4), c = lane & 15;
       double* Ablk = A + (long)j0 * ld + j0;
       // global-memory form: the rounds write the block's L into LDS (a round's
@@ -1237,13 +1275,42 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       bool ok = true;
       double* XJw = X + 256 * J;
-      if (!(skip & 1)) {
-        chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Lblk, lld, XJw, xch);
-      } else {  // timing diagnostics (ME_SOLVE_SKIP & 1): the rounds' barriers only
-        for (int r = 0; r < 16 / ME_CHOL_PB; ++r) __syncthreads();
+      if (ME_DIAG_MFMA) {
+        // lookahead: the trailing tiles of step J - 1 outside column J run on
+        // waves 1-3 and 5-7 while wave 0 factors this block (wave 4 shares
+        // wave 0's SIMD and stays out of its way)
+        const bool sib = nw > 4 && wave == 4;  // wave 0's SIMD sibling
+        if (kLook && J > 0 && wave != 0 && !sib && !(skip & 4))
+          trailing_split<kSc1>(A, ld, Ts, J - 1, false, wave - 1 - (nw > 4 && wave > 4), nw - 1 - (nw > 4), lane);
+        if (wave == 0 && !(skip & 1)) {
+          const int q = lane >> 4;
+          double4_t A4, Y4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            A4[r] = a_ld<kSc1>(&Ablk[(q + 4 * r) * ld + c]);
+            Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+          }
+          diag_round_mfma<0>(A4, Y4, q, c, n - j0, ok, Lblk, lld, XJw, xch);
+          diag_round_mfma<1>(A4, Y4, q, c, n - j0, ok, Lblk, lld, XJw, xch);
+          diag_round_mfma<2>(A4, Y4, q, c, n - j0, ok, Lblk, lld, XJw, xch);
+          diag_round_mfma<3>(A4, Y4, q, c, n - j0, ok, Lblk, lld, XJw, xch);
+          if (!kLds) {
+            solve_wave_sync();
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (c <= q + 4 * r) a_st<kSc1>(&Ablk[(q + 4 * r) * ld + c], Lblk[(q + 4 * r) * kDiagLd + c]);
+          }
+          if (!ok) sfail = 1;  // benign race: every writer stores 1
+        }
+      } else {
+        if (!(skip & 1)) {
+          chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Lblk, lld, XJw, xch);
+        } else {  // timing diagnostics (ME_SOLVE_SKIP & 1): the rounds' barriers only
+          for (int r = 0; r < 16 / ME_CHOL_PB; ++r) __syncthreads();
+        }
+        if (!kLds && act && c <= i) a_st<kSc1>(&Ablk[i * ld + c], Lblk[i * kDiagLd + c]);
+        if (act && !ok) sfail = 1;  // benign race: every writer stores 1
       }
-      if (!kLds && act && c <= i) a_st<kSc1>(&Ablk[i * ld + c], Lblk[i * kDiagLd + c]);
-      if (act && !ok) sfail = 1;  // benign race: every writer stores 1
     }
     __syncthreads();
     SOLVE_STAMP(1);
@@ -1266,8 +1333,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 #pragma unroll
         for (int q = 0; q < 4; ++q) a_st<kSc1>(&A[(long)(i0 + (lane >> 4) + 4 * q) * ld + j0 + (lane & 15)], acc[q]);
       }
+      __syncthreads();
     }
-    __syncthreads();
     SOLVE_STAMP(2);
     SOLVE_START(3);
     // (c) trailing update on the matrix cores: A_IK -= L_IJ L_KJ^T, J < K <= I
@@ -1288,7 +1355,12 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         __syncthreads();
       }
     } else {
-      if (!(skip & 4)) trailing_tiles<kSc1>(A, ld, Ts, J, wave, nw, lane);
+      if (!(skip & 4)) {
+        if (kLook)
+          trailing_split<kSc1>(A, ld, Ts, J, true, wave, nw, lane);  // column J + 1 now, the rest with the next block
+        else
+          trailing_tiles<kSc1>(A, ld, Ts, J, wave, nw, lane);
+      }
       __syncthreads();
     }
     SOLVE_STAMP(3);
