@@ -396,14 +396,13 @@ def pmc_traffic(family: str):
 
     # newest = highest round / version numbers (natural order: v10 after v9)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")),
-                   key=lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))])
-    if not files:
-        return None
-    d = json.load(open(files[-1]))
+                   key=lambda f: ([int(x) for x in re.findall(r"\d+", os.path.basename(f))], os.path.basename(f)))
     ks = FAMILY_KERNELS.get(family, [])
-    if not ks or any(k not in d for k in ks):
-        return None
-    return float(sum(d[k]["traffic_bytes"] for k in ks))
+    for f in reversed(files):  # the newest summary that profiled this family's kernels
+        d = json.load(open(f))
+        if ks and all(k in d for k in ks):
+            return float(sum(d[k]["traffic_bytes"] for k in ks))
+    return None
 
 
 def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):

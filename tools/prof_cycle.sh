@@ -13,7 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
 python3 "$GRAFT_REPO_ROOT/tools_kstats.py" "$(ls $OUT/stats/run_kernel_stats.csv $OUT/stats/*/run_kernel_stats.csv 2>/dev/null | head -1)" 40 > "$OUT/kernel_stats.txt" || true
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $C --output-format csv -d "$OUT/pmc/$C" -o run -- \
-    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 4 --warmup 1 --mi-pairs 0 $ARGS > "$OUT/pmc_$C.log" 2>&1 || exit 1
+    python3 "$GRAFT_REPO_ROOT/bench.py" --steps 4 --warmup 1 $ARGS > "$OUT/pmc_$C.log" 2>&1 || exit 1
 done
 cd "$GRAFT_REPO_ROOT"
 ls -R "$OUT" | head -30
