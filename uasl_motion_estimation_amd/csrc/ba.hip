@@ -445,7 +445,7 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
 // Y block fits the LDS budget, else 16 (48 rows, 32 lanes per landmark).  Each
 // Schur workgroup leaves one set of partial tiles that s_assemble sums, so
 // twice the landmarks per workgroup halve that traffic.
-constexpr int kSchurPts = 16, kSchurPtsWide = 32;
+constexpr int kSchurPts = 16, kSchurPtsWide = 32, kSchurPtsSmall = 8;
 constexpr size_t kSchurLdsCap = 150 * 1024;
 __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
 
@@ -462,6 +462,20 @@ __device__ __forceinline__ int group_max(int x) {
   return x;
 }
 
+#ifdef ME_SCHUR_STAMPS  // timing experiment only (tools/abl): workgroup 0's phase times in st->stamps[6..11]
+#define SCHUR_T(i)                                                                     \
+  do {                                                                                 \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                         \
+      const long long tt_ = (long long)__builtin_amdgcn_s_memtime();                   \
+      if ((i) > 0) st->stamps[5 + (i)] += tt_ - sch_prev_;                             \
+      sch_prev_ = tt_;                                                                 \
+    }                                                                                  \
+  } while (0)
+#else
+#define SCHUR_T(i) \
+  do {             \
+  } while (0)
+#endif
 template <int NT, int BLK, int PTS>
 __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, CamArgs ca) {
   constexpr int SL = BLK / PTS, NW = BLK / 64;  // lanes per landmark, waves
@@ -475,6 +489,11 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   }
   State* st = b.st;
   if (st->done) return;
+#ifdef ME_SCHUR_STAMPS
+  long long sch_prev_ = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) st->stamps[12] += 1;
+#endif
+  SCHUR_T(0);
   const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
   const double radius = st->radius;
   // all allowed steps taken: this pass only evaluates the gradient for the
@@ -534,7 +553,8 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         for (int i = 0; i < 9; ++i) V[i] = X0[i];
         for (int q = q0 + SL; q < end; q += SL)
           for (int i = 0; i < 9; ++i) V[i] += b.obsx[(long)q * kObsxStride + i];
-        for (int i = 0; i < 9; ++i) V[i] = group_sum<SL>(V[i]);
+        SCHUR_T(1);  // loads of phase A issued and returned (first use)
+      for (int i = 0; i < 9; ++i) V[i] = group_sum<SL>(V[i]);
         if (!scaled) {
           pv[0] = g.jacobi ? 1.0 / (1.0 + sqrt(V[0])) : 1.0;
           pv[1] = g.jacobi ? 1.0 / (1.0 + sqrt(V[3])) : 1.0;
@@ -577,6 +597,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         for (int i = 0; i < 9; ++i) b.Lp[9 * (long)j + i] = L[i];
         for (int a = 0; a < 3; ++a) b.zp[3 * (long)j + a] = z[a];
       }
+      SCHUR_T(2);  // group sums, point block
       // (B) this lane's slots -> the landmark's rows of Y (first slot of each camera run only;
       // duplicate residual blocks of one camera are summed in CSR order)
       int lo = 1 << 29, hi = -1;
@@ -629,33 +650,68 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
       band[3 * gi + 2] = 0;
     }
     __syncthreads();
-    // (C) partial tiles on the matrix cores.  The K-step's camera band is
-    // wave-uniform (scalar registers, scalar branches); the operands of all its
-    // live tiles are read before the first MFMA of the step.
-    for (int ks = 0; ks < (final_pass ? 0 : nks); ++ks) {
-      const int pa = (4 * ks) / 3, pb = min((4 * ks + 3) / 3, P - 1);
-      const int lo = __builtin_amdgcn_readfirstlane(min(band[3 * pa], band[3 * pb]));
-      const int hi = __builtin_amdgcn_readfirstlane(max(band[3 * pa + 1], band[3 * pb + 1]));
-      const int live = __builtin_amdgcn_readfirstlane(band[3 * pa + 2] | band[3 * pb + 2]);
-      const double* Yr = Y + (size_t)(4 * ks + (lane >> 4)) * Rz + (lane & 15);
-      bool hit[NT];
-      double av[NT], bv[NT];
+    SCHUR_T(3);  // Y rows in LDS (barrier)
+    // (C) partial tiles on the matrix cores.  First the band test of every
+    // K-step at once (lane ks of each wave tests step ks, one ballot per tile:
+    // wave-uniform hit masks in scalar registers), then the steps run with the
+    // next step's operands requested before this step's MFMAs -- no LDS round
+    // trip between a step's band test and its operands.
+    if (!final_pass) {
+      unsigned long long hm[NT];
+      {
+        int lo = 1 << 29, hi = -1, live = 0;
+        if (lane < nks) {
+          const int pa = (4 * lane) / 3, pb = min((4 * lane + 3) / 3, P - 1);
+          lo = min(band[3 * pa], band[3 * pb]);
+          hi = max(band[3 * pa + 1], band[3 * pb + 1]);
+          live = band[3 * pa + 2] | band[3 * pb + 2];
+        }
 #pragma unroll
-      for (int u = 0; u < NT; ++u) {
-        const int I = tI[u], J = tJ[u];
-        // a tile is touched by these rows iff both its column blocks meet the camera band or the z column
-        const bool hitI = (hi >= 16 * I && lo <= 16 * I + 15) || (live && I == g.T - 1);
-        const bool hitJ = (hi >= 16 * J && lo <= 16 * J + 15) || (live && J == g.T - 1);
-        hit[u] = I >= 0 && hitI && hitJ;
-        av[u] = hit[u] ? Yr[16 * I] : 0.0;
-        bv[u] = hit[u] ? Yr[16 * J] : 0.0;
+        for (int u = 0; u < NT; ++u) {
+          const int I = tI[u], J = tJ[u];
+          // a tile is touched by these rows iff both its column blocks meet the camera band or the z column
+          const bool hitI = (hi >= 16 * I && lo <= 16 * I + 15) || (live && I == g.T - 1);
+          const bool hitJ = (hi >= 16 * J && lo <= 16 * J + 15) || (live && J == g.T - 1);
+          hm[u] = __ballot(lane < nks && I >= 0 && hitI && hitJ);
+        }
       }
+      auto operands = [&](int ks, double* a, double* bb) {
+        const double* Yr = Y + (size_t)(4 * ks + (lane >> 4)) * Rz + (lane & 15);
 #pragma unroll
-      for (int u = 0; u < NT; ++u)
-        if (hit[u]) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bv[u], acc[u], 0, 0, 0);
+        for (int u = 0; u < NT; ++u) {
+          const bool h = (hm[u] >> ks) & 1ull;
+          a[u] = h ? Yr[16 * tI[u]] : 0.0;
+          bb[u] = h ? Yr[16 * tJ[u]] : 0.0;
+        }
+      };
+      auto contract = [&](int ks, const double* a, const double* bb) {
+#pragma unroll
+        for (int u = 0; u < NT; ++u)
+          if ((hm[u] >> ks) & 1ull) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], bb[u], acc[u], 0, 0, 0);
+      };
+      double av[NT], bv[NT];
+      if constexpr (NT <= 6) {  // double-buffered operands (a few tiles per wave: the registers are there)
+        double an[NT], bn[NT];
+        operands(0, av, bv);
+        for (int ks = 0; ks < nks; ++ks) {
+          if (ks + 1 < nks) operands(ks + 1, an, bn);
+          contract(ks, av, bv);
+#pragma unroll
+          for (int u = 0; u < NT; ++u) {
+            av[u] = an[u];
+            bv[u] = bn[u];
+          }
+        }
+      } else {
+        for (int ks = 0; ks < nks; ++ks) {
+          operands(ks, av, bv);
+          contract(ks, av, bv);
+        }
+      }
     }
     __syncthreads();
   }
+  SCHUR_T(4);  // MFMA contraction (barrier)
   if (need_lin) {
     const double r = block_max(gm, red);
     if (tid == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
@@ -669,6 +725,10 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[((lane >> 4) + 4 * i) * 16 + (lane & 15)] = acc[u][i];
   }
+#ifdef ME_SCHUR_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+#endif
+  SCHUR_T(5);  // gradient max + partial stores
 }
 
 // Linearisation bookkeeping + iteration start: reduce the cost / gradient
@@ -2025,7 +2085,15 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   // wide sub-chunks pay off once the tile count is large (config 4: 66 pairs,
   // -2% BA time); at config 3 (28 pairs) the longer per-workgroup chain costs
   // more than the halved partial traffic saves (1.23 vs 1.19 ms per 10 iterations)
-  g.spts = (g.npairs > 40 && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap) ? kSchurPtsWide : kSchurPts;
+  // landmarks per Schur sub-chunk: 32 while the Y block fits the LDS (half the
+  // partial tiles for s_assemble); else 16, or 8 for many tiles (the
+  // contraction is MFMA-bound per workgroup: twice the workgroups spread it
+  // over more CUs; config 5: BA 5.2 -> 4.96 ms per 10 iterations, config 3
+  // slower with 8)
+  if (g.npairs > 40 && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap)
+    g.spts = kSchurPtsWide;
+  else
+    g.spts = g.npairs > 100 ? kSchurPtsSmall : kSchurPts;
   if (const char* e = getenv("ME_SCHUR_PTS"))  // A/B timing only
     if (atoi(e) == kSchurPts) g.spts = kSchurPts;
   g.nsub = (int)std::max(1L, ((long)g.np + g.spts - 1) / g.spts);
@@ -2191,7 +2259,9 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
   ME_CHECK(c, P.schur_lds <= kSchurLdsCap, "BA: %d variable cameras exceed the Schur workspace", g.m);
-#define ME_SCHUR_K(N) (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>
+#define ME_SCHUR_K(N)                                                                                   \
+  (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>, \
+      (const void*)pt_schur_kernel<N, 512, kSchurPtsSmall>
   for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5), ME_SCHUR_K(6), ME_SCHUR_K(7), ME_SCHUR_K(8),
                         ME_SCHUR_K(9), ME_SCHUR_K(10), ME_SCHUR_K(12), ME_SCHUR_K(16), ME_SCHUR_K(24)})
 #undef ME_SCHUR_K
@@ -2251,6 +2321,8 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   do {                                                                                                       \
     if (g.spts == kSchurPtsWide)                                                                             \
       hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsWide>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca); \
+    else if (g.spts == kSchurPtsSmall)                                                                       \
+      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsSmall>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca); \
     else                                                                                                     \
       hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPts>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca);     \
   } while (0)
