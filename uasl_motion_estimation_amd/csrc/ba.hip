@@ -685,6 +685,9 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         }
       };
       auto contract = [&](int ks, const double* a, const double* bb) {
+#ifdef ME_SCHUR_NO_MFMA  // timing experiment only: operands read, no contraction
+        return;
+#endif
 #pragma unroll
         for (int u = 0; u < NT; ++u)
           if ((hm[u] >> ks) & 1ull) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], bb[u], acc[u], 0, 0, 0);

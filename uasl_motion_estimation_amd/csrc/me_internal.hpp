@@ -45,6 +45,7 @@ struct me_ctx {
   size_t ba_pinned_size = 0;
   void* scale_mirror = nullptr;  // coherent host page the scale LM control writes its state to
   int scale_gen = 0;             // generation of the last scale LM solve (mirror ownership)
+  int scale_lm_cap = -1;         // co-resident workgroups of the persistent scale LM kernel (-1: not queried)
   long scale_counters[4] = {0, 0, 0, 0};  // last solve: residual / normal-equation evaluations, LM rejections, executed residual evaluations
   // MI term tables, one per patch pixel count N (built on first use, mi.hip)
   float* mi_table[256] = {nullptr};

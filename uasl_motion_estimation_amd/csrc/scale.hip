@@ -371,7 +371,10 @@ __device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHi
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) {
     jj[t] = J * J * wv;
-    je[t] = J * res[row];
+    // coherent load: in the persistent LM the row may have been written by
+    // another workgroup in the previous phase (no kernel boundary between)
+    je[t] = J * __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(res + row),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
 }
 
@@ -520,6 +523,7 @@ struct LMParams {
   // header there, the word holding `phase` last behind a system-scope fence,
   // so the host polls it behind an event instead of a D2H copy per block.
   unsigned long long* mirror;
+  int mirror_done_only;  // persistent solve: the mirror is written once, at PH_DONE
 };
 
 __device__ __forceinline__ double ldlt1(double JJ, double e) { return fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
@@ -744,7 +748,7 @@ __device__ void scale_ctrl_run(ScaleLM* lm_g, ScaleSpec* __restrict__ sp, const 
   unsigned long long* dst = reinterpret_cast<unsigned long long*>(lm_g);
 #pragma unroll
   for (int i = 0; i < kHead; ++i) dst[i] = hw[i];
-  if (p.mirror) {
+  if (p.mirror && (!p.mirror_done_only || L.phase == PH_DONE)) {
     constexpr int kPhaseWord = offsetof(ScaleLM, phase) / 8;
 #pragma unroll
     for (int i = 0; i < kHead; ++i)
@@ -836,6 +840,163 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, T
   }
 }
 
+// The whole LM in ONE launch (default; ME_SCALE_BLOCKS=1 keeps the per-phase
+// launches): grid (nb, kCandY) workgroups, co-resident (cooperative launch),
+// walk the phases together.  Per phase each workgroup does its tracks' work --
+// phase A / D residuals and phase B normal equations on the y = 0 row, phase C
+// candidates j = y, y + kCandY, ... -- and arrives on the phase's counters as
+// the per-phase kernels do (the last arrival reduces in the fixed order and
+// runs the control); the control publishes the phase count on `epoch`
+// (agent-scope release) and every workgroup waits for it (bounded spin, then
+// acquire) before reading the next phase.  No launch and no host round trip
+// per phase; the host waits for PH_DONE only.  A partner that never arrives
+// sets error bit kErrSpin and the grid drains.
+//
+// Register budget: the track work runs out of line on a device copy of the
+// parameters (written by the prep launch), re-read in every phase with
+// scalar loads; inlined into the phase loop, its invariants (the kernel
+// arguments) are hoisted across the loop and the kernel needs >400 registers.
+constexpr int kCandY = 2;
+constexpr int kEpochWord = 40;  // P.bar[kEpochWord]: phases completed (zeroed by the prep launch with the counters)
+constexpr long kPhaseSpin = 1L << 22;
+constexpr int kErrSpin = 8;
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* q) {
+  const unsigned long long v = (unsigned long long)q;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+  return (T*)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ double uniform_d(double x) {
+  return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(x)),
+                          __builtin_amdgcn_readfirstlane(__double2loint(x)));
+}
+// One track per 16-lane group: residual / normal-equation terms at `scale`
+// (two functions: one combined needs 287 registers per lane).
+__device__ __noinline__ void lm_res_tracks(const ScaleArgs* ga, double scale, const TrackDev* gtd, double* res,
+                                           int* err) {
+  __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
+  ScaleArgs a = *uniform_ptr(ga);
+  a.scale = uniform_d(scale);
+  const TrackDev td = *uniform_ptr(gtd);
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  const int t = blockIdx.x * kTracksPerBlock + grp;
+  if (t < a.nL + a.nR) residual_track(a, td, t, h, uniform_ptr(res), uniform_ptr(err));
+}
+__device__ __noinline__ void lm_neq_tracks(const ScaleArgs* ga, double scale, const TrackDev* gtd,
+                                           const double* res, double* jj, double* je, int* err) {
+  __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
+  ScaleArgs a = *uniform_ptr(ga);
+  a.scale = uniform_d(scale);
+  const TrackDev td = *uniform_ptr(gtd);
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  const int t = blockIdx.x * kTracksPerBlock + grp;
+  if (t < a.nL + a.nR)
+    neq_track(a, td, t, h, uniform_ptr(res), uniform_ptr(jj), uniform_ptr(je), uniform_ptr(err));
+}
+__device__ __forceinline__ void lm_publish(unsigned* epoch, unsigned v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __hip_atomic_store(epoch, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR, const ScaleArgs* gaN,
+                                                            const TrackDev* gtd, double* __restrict__ resb,
+                                                            int rows_pad, double* __restrict__ jj,
+                                                            double* __restrict__ je, int* __restrict__ err,
+                                                            ScaleLM* lm, ScaleSpec* __restrict__ sp, LMParams p,
+                                                            unsigned* cnt, unsigned* epoch, int max_phases) {
+  __shared__ int s_phase, s_n, s_cur, s_quit;
+  __shared__ double s_scale, s_ts[kSpecMax];
+  const unsigned nwg = gridDim.x;
+  // the LM state is read with coherent (agent-scope atomic) loads: no
+  // acquire fence -- an L2 invalidate -- per workgroup and phase
+  auto ld_i = [](const int* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ld_d = [](const double* q) {
+    return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(q),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  };
+  for (int ph = 0; ph < max_phases; ++ph) {
+    if (threadIdx.x == 0) {
+      s_phase = ld_i(&lm->phase);
+      s_cur = ld_i(&lm->cur);
+      s_scale = ld_d(&lm->scale);
+      const int n = s_phase == PH_C ? ld_i(&sp->n) : 0;
+      s_n = n;
+      for (int j = 0; j < n; ++j) s_ts[j] = ld_d(&sp->ts[j]);
+    }
+    __syncthreads();
+    const int phase = s_phase;
+    if (phase == PH_DONE) return;
+    const int cur = s_cur;
+    if (phase == PH_B) {
+      if (blockIdx.y == 0) {
+        const double* res = resb + (long)cur * rows_pad;
+        if (!p.test) lm_neq_tracks(gaN, s_scale, gtd, res, jj, je, err);
+        if (last_block_arrives(cnt + 1, nwg)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          double sx = 0, sy = 0;
+          if (!p.test) block_reduce2<kScBlock>(jj, je, p.n, 0, &sx, &sy);
+          if (threadIdx.x == 0) {
+            __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            scale_ctrl_run(lm, sp, p, PH_B, sx, sy, *err);
+            lm_publish(epoch, (unsigned)ph + 1);
+          }
+        }
+      }
+    } else if (phase == PH_A || phase == PH_D) {
+      if (blockIdx.y == 0) {
+        double* res = res_buf(resb, rows_pad, cur);
+        lm_res_tracks(gaR, s_scale, gtd, res, err);
+        if (last_block_arrives(cnt + 1, nwg)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          double sx, sy;
+          block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
+          if (threadIdx.x == 0) {
+            __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            scale_ctrl_run(lm, sp, p, phase, sx, 0.0, *err);
+            lm_publish(epoch, (unsigned)ph + 1);
+          }
+        }
+      }
+    } else {  // PH_C: the batch's candidates
+      const int n = s_n;
+      for (int j = blockIdx.y; j < n; j += gridDim.y) {
+        double* res = res_buf(resb, rows_pad, (cur + 1 + j) % kResBufs);
+        lm_res_tracks(gaR, s_ts[j], gtd, res, err);
+        if (last_block_arrives(cnt + 1 + j, nwg)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          double sx, sy;
+          block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
+          if (threadIdx.x == 0) {
+            __hip_atomic_store(cnt + 1 + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sp->e2[j] = sx;
+          }
+          if (last_block_arrives(cnt, (unsigned)n)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (threadIdx.x == 0) {
+              __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              scale_ctrl_run(lm, sp, p, PH_C, 0.0, 0.0, *err);
+              lm_publish(epoch, (unsigned)ph + 1);
+            }
+          }
+        }
+      }
+    }
+    // wait for the phase's control (bounded), then read the next phase
+    if (threadIdx.x == 0) {
+      long k = 0;
+      for (; k < kPhaseSpin; ++k) {
+        if (__hip_atomic_load(epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (unsigned)ph) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_quit = k == kPhaseSpin;
+      if (s_quit) atomicOr(err, kErrSpin);
+    }
+    __syncthreads();
+    if (s_quit) return;
+  }
+}
+
 // Track flags / residual rows (optimisation.cpp:157-194) from the raw track
 // arrays: bit0 = owns a residual row (triangulated and unmasked; the right
 // loop tests mask(pts.second.size()+i), SURVEY A-6), bit1 = seen in the last
@@ -860,13 +1021,21 @@ struct PrepArgs {
   ScaleLM* lm;
   double scale0, mu0, v0;
   int gen;
+  // device copy of the persistent LM kernel's parameters (residual and
+  // normal-equation ScaleArgs, TrackDev), or null
+  ScaleArgs args[2];
+  TrackDev td;
+  unsigned long long* args_out;
 };
+constexpr int kArgsWords = (2 * sizeof(ScaleArgs) + sizeof(TrackDev)) / 8;
+static_assert((2 * sizeof(ScaleArgs) + sizeof(TrackDev)) % 8 == 0, "parameter copy in 8-byte words");
 constexpr int kPrepBlock = 1024;
 constexpr int kErrWords = 64;
 __global__ __launch_bounds__(kPrepBlock) void scale_prep_kernel(PrepArgs pa, uint8_t* flags, int* row, int* err) {
   __shared__ int wsum[kPrepBlock / 64];
   const int n = pa.nL + pa.nR, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   if (t < kErrWords) pa.err_block[t] = 0u;
+  if (pa.args_out && t < kArgsWords) pa.args_out[t] = reinterpret_cast<const unsigned long long*>(pa.args)[t];
   if (pa.lm && t == 0) {
     ScaleLM* lm = pa.lm;
     lm->scale = pa.scale0;
@@ -950,8 +1119,15 @@ struct ScaleProblem {
   unsigned* bar;  // arrival counter of the fused phase + control kernels
   ScaleLM* lm;
   ScaleSpec* spec;
+  const ScaleArgs* dargs;  // device copy: residual, normal-equation parameters (persistent LM)
+  const TrackDev* dtd;
   char* host;   // pinned: input staging | read-back
 };
+
+ScaleArgs with_invN(ScaleArgs a, int P) {
+  a.invN = (float)(1.0 / (double)(P * P));
+  return a;
+}
 
 // lm0 (me_scale_optimise only): the LM start state {scale, mu, v}, written by the prep launch
 int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, const double* lm0 = nullptr,
@@ -1004,7 +1180,8 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
   const size_t nbufs = lm0 ? kResBufs : 1;
   const size_t oFl = in_span, oRow = oFl + up(nn), oRes = oRow + up(4 * nn);
   const size_t oJJ = oRes + nbufs * 8 * rows_pad, oJE = oJJ + up(8 * nn), oRed = oJE + up(8 * nn), oErr = oRed + 256;
-  const size_t oLM = oErr + 256, oSpec = oLM + up(sizeof(ScaleLM)), total = oSpec + up(sizeof(ScaleSpec));
+  const size_t oLM = oErr + 256, oSpec = oLM + up(sizeof(ScaleLM)), oArgs = oSpec + up(sizeof(ScaleSpec));
+  const size_t total = oArgs + up(8 * (size_t)kArgsWords);
   void* d;
   ME_TRY(me_scratch(c, SLOT_SC_TRACKS, total, &d));
   char* base = (char*)d;
@@ -1069,9 +1246,6 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
   pa.mu0 = lm0 ? lm0[1] : 0.0;
   pa.v0 = lm0 ? lm0[2] : 0.0;
   pa.gen = gen;
-  hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
-                     (int*)(base + oRow), P.err);
-  ME_TRY(me_check_launch(c, "scale_prep_kernel"));
   if (s->img_mem == ME_DEVICE) {
     a.imgL = s->imgL;
     a.imgR = s->imgR;
@@ -1085,6 +1259,16 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
     a.imgL = (const uint8_t*)dl;
     a.imgR = (const uint8_t*)dr;
   }
+  // the prep launch runs last: it also writes the device copy of the final parameters
+  P.dargs = (const ScaleArgs*)(base + oArgs);
+  P.dtd = (const TrackDev*)(base + oArgs + 2 * sizeof(ScaleArgs));
+  pa.args[0] = with_invN(a, 2 * a.w + 1);  // residual patches (2w+1)^2
+  pa.args[1] = with_invN(a, 2 * a.w);      // normal-equation patches (2w)^2
+  pa.td = P.td;
+  pa.args_out = lm0 ? (unsigned long long*)(base + oArgs) : nullptr;
+  hipLaunchKernelGGL(scale_prep_kernel, dim3(1), dim3(kPrepBlock), 0, c->stream, pa, (uint8_t*)(base + oFl),
+                     (int*)(base + oRow), P.err);
+  ME_TRY(me_check_launch(c, "scale_prep_kernel"));
   return ME_OK;
 }
 
@@ -1093,13 +1277,10 @@ int blocks_for(int n) { return n > 0 ? (n + kTracksPerBlock - 1) / kTracksPerBlo
 int check_err(me_ctx* c, int e) {
   if (e & 2) return me_set_error(c, ME_ERR_INVALID, "scale: mask selects fewer rows than triangulated tracks");
   if (e & 1) return me_set_error(c, ME_ERR_INVALID, "scale: ROI outside the image (reference: cv::Exception)");
+  if (e & kErrSpin) return me_set_error(c, ME_ERR_STATE, "scale: LM workgroups timed out waiting for a phase");
   return ME_OK;
 }
 
-ScaleArgs with_invN(ScaleArgs a, int P) {
-  a.invN = (float)(1.0 / (double)(P * P));
-  return a;
-}
 
 // one evaluation (no LM state): residual rows at a.scale, reduce, read back
 int eval_once_residuals(ScaleProblem& P, double* e_out) {
@@ -1234,6 +1415,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   constexpr size_t kHeadBytes = offsetof(ScaleLM, trace);
   static_assert(kHeadBytes <= 4096, "LM header mirror page");
   lp.mirror = (unsigned long long*)c->scale_mirror;
+  lp.mirror_done_only = 0;
   volatile ScaleLM* mir = (volatile ScaleLM*)c->scale_mirror;
   // Solve generation: launches of an earlier solve abandoned on an error path
   // may still be queued ahead of this one and write the mirror; their header
@@ -1297,32 +1479,77 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     (void)hipStreamSynchronize(st);
     return rc;
   };
-  if (int rc = enqueue_block(0)) return drain(rc);
-  int cur = 0;
   // Spin budget before the poll loop yields the core between polls: a solve
   // queued behind other work on the stream (e.g. a pipelined BA) would
   // otherwise burn a host core for that work's whole duration.
   constexpr int kSpinsBeforeYield = 4096;
-  for (;; cur ^= 1) {
-    const bool more = blk < max_blocks;
-    if (more)
-      if (int rc = enqueue_block(cur ^ 1)) return drain(rc);
-    // Spin on the mirror and the block's event (no sleeping wait: its wake-up
-    // latency exceeded a block's ~60 us and idled the stream).  PH_DONE ends
-    // the wait at once; the finished solve's queued launches return at once.
-    bool done = false;
+  // The persistent launch needs its grid co-resident: used while it takes at
+  // most half of what fits on the device (the rest stays free for concurrent
+  // work, e.g. a KLT on another stream); ME_SCALE_BLOCKS=1 forces the
+  // per-phase launches.
+  static const bool blocks_env = getenv("ME_SCALE_BLOCKS") && atoi(getenv("ME_SCALE_BLOCKS")) != 0;
+  if (c->scale_lm_cap < 0) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scale_lm_kernel, kScBlock, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = cus = 0;
+    }
+    c->scale_lm_cap = per_cu * cus;
+  }
+  const bool persist = !blocks_env && 2L * nb * kCandY <= c->scale_lm_cap;
+  if (persist) {
+    lp.mirror_done_only = 1;
+    {
+      me_ktimer t(c, ME_KT_SCALE_RES);
+      const int max_phases = 256 * (p.max_nb_iter + 2);
+      hipLaunchKernelGGL(scale_lm_kernel, dim3(nb, kCandY), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
+                         P.res, P.rows_pad, P.jj, P.je, P.err, P.lm, P.spec, lp, P.bar, P.bar + kEpochWord,
+                         max_phases);
+    }
+    if (int rc = me_check_launch(c, "scale_lm_kernel")) return drain(rc);
+    ME_HIP(c, hipEventRecord(c->poll_ev[0], st));
+    // PH_DONE in the mirror (written once, by the final control) ends the
+    // wait; the event covers a launch that ends without it (error / timeout)
     for (int spins = 0;; ++spins) {
-      if (mine() && mir->phase == PH_DONE) {
-        done = true;
-        break;
-      }
-      const hipError_t q = hipEventQuery(c->poll_ev[cur]);
+      if (mine() && mir->phase == PH_DONE) break;
+      const hipError_t q = hipEventQuery(c->poll_ev[0]);
       if (q == hipSuccess) break;
       if (q != hipErrorNotReady) return drain(me_set_error(c, ME_ERR_HIP, "scale optimise: %s", hipGetErrorString(q)));
       if (spins >= kSpinsBeforeYield) std::this_thread::yield();
     }
-    if (done || (mine() && mir->phase == PH_DONE)) break;
-    if (!more) return drain(me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate"));
+    if (!(mine() && mir->phase == PH_DONE)) {
+      ME_HIP(c, hipMemcpyAsync(P.host + 32, P.err, 4, hipMemcpyDeviceToHost, st));
+      ME_HIP(c, hipStreamSynchronize(st));
+      int e;
+      std::memcpy(&e, P.host + 32, 4);
+      if (int rc = check_err(c, e)) return rc;
+      return me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate");
+    }
+  } else {
+    if (int rc = enqueue_block(0)) return drain(rc);
+    int cur = 0;
+    for (;; cur ^= 1) {
+      const bool more = blk < max_blocks;
+      if (more)
+        if (int rc = enqueue_block(cur ^ 1)) return drain(rc);
+      // Spin on the mirror and the block's event (no sleeping wait: its wake-up
+      // latency exceeded a block's ~60 us and idled the stream).  PH_DONE ends
+      // the wait at once; the finished solve's queued launches return at once.
+      bool done = false;
+      for (int spins = 0;; ++spins) {
+        if (mine() && mir->phase == PH_DONE) {
+          done = true;
+          break;
+        }
+        const hipError_t q = hipEventQuery(c->poll_ev[cur]);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return drain(me_set_error(c, ME_ERR_HIP, "scale optimise: %s", hipGetErrorString(q)));
+        if (spins >= kSpinsBeforeYield) std::this_thread::yield();
+      }
+      if (done || (mine() && mir->phase == PH_DONE)) break;
+      if (!more) return drain(me_set_error(c, ME_ERR_STATE, "scale optimise did not terminate"));
+    }
   }
   std::atomic_thread_fence(std::memory_order_acquire);  // phase read before the rest of the header
   ScaleLM hs;
