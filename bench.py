@@ -50,6 +50,12 @@ def parse():
                     help="matches of the StereoVisualOdometry::process line (SURVEY 8f rank 1; 0: off)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="run each frame's KLT, scale LM and BA back to back on one stream (no KLT/back-end overlap)")
+    ap.add_argument("--overlap", choices=("frontend", "klt"), default="frontend",
+                    help="two-stream pipeline: the front end (KLT + scale LM) of frame t+1 beside frame t's BA "
+                         "(frontend), or only KLT of frame t+1 beside the scale LM + BA of frame t (klt)")
+    ap.add_argument("--front-cus", type=int, default=8,
+                    help="frontend overlap: the tracker context's stream runs on CUs i with i %% 16 < F and the "
+                         "back-end stream on the others (me_set_cu_mask; every XCD keeps CUs of both); 0: shared CUs")
     ap.add_argument("--streams", type=int, default=1,
                     help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
                          "thread each), reported as multi_stream; the headline value stays one stream per GPU")
@@ -214,30 +220,53 @@ class _Hip:
 
 
 class FramePipeline:
-    """Two-stage frame pipeline on one GPU: the tracker context (its own HIP
-    stream) runs KLT of frame t+1 while the back-end context runs the BA of
-    frame t (issued after frame t's scale LM, whose kernels need the CUs).
-    The BA is queued whole (me_ba_solve_async) and its summary collected
-    (me_ba_wait) after the next frame's scale LM is queued behind it, so the
-    host's per-frame work never leaves the back-end stream idle.  Frame t's back end waits (stream-side) on an event
-    recorded after KLT of frame t, so every dependency a VO front end has on
-    its tracks is kept; per frame the work is exactly the sequential
-    gpu_step's (one KLT, one scale LM, one BA)."""
+    """Two-stream frame pipeline on one GPU.
 
-    def __init__(self, ctx, tctx, hip):
-        self.ctx, self.tctx, self.hip = ctx, tctx, hip
+    overlap="frontend" (default): the front end of frame t+1 (KLT, then the
+    MI scale LM, both on the tracker context's HIP stream) runs while the back
+    end of frame t (the windowed BA, queued whole with me_ba_solve_async on
+    the back-end context's stream) runs beside it -- the usual VO split of a
+    tracking front end and a BA back end (the BA of keyframe t refines the
+    window; frame t+1's motion estimate starts from frame t's front-end pose).
+    Frame t's BA waits (stream-side) on an event recorded after frame t's
+    scale LM, so every dependency the back end has on its front end is kept;
+    per frame the work is exactly the sequential gpu_step's (one KLT, one
+    scale LM, one BA).
+
+    overlap="klt": only KLT of frame t+1 runs on the tracker stream; the scale
+    LM stays on the back-end stream between the BAs (round-1 pipeline)."""
+
+    def __init__(self, ctx, tctx, hip, overlap="frontend"):
+        self.ctx, self.tctx, self.hip, self.overlap = ctx, tctx, hip, overlap
         self.ev = [hip.event(), hip.event()]
         self.s_main = ctypes.c_void_p(ctx.lib.me_get_stream(ctx.h))
         self.s_trk = ctypes.c_void_p(tctx.lib.me_get_stream(tctx.h))
+
+    @property
+    def scale_ctx(self):
+        """The context whose argument blocks hold the frames' scale-LM results."""
+        return self.tctx if self.overlap == "frontend" else self.ctx
 
     def _klt(self, fd, kp, ba_opts, k):
         c = _calls(self.tctx, fd, kp, ba_opts)
         self.tctx.check(self.tctx.lib.me_klt_track(*c.klt), "klt")
         self.hip.record(self.ev[k & 1], self.s_trk)
 
+    def _scale(self, cx, fd, kp, ba_opts, stats):
+        c = _calls(cx, fd, kp, ba_opts)
+        c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
+        cx.check(cx.lib.me_scale_optimise(*c.scale), "me_scale_optimise")
+        stats["scale_iters"] += c.it.value
+        scale_counters(cx, stats)
+
     def run(self, frames, n, kp, ba_opts, stats, first=0):
         if n <= 0:
             return
+        # the contexts' streams may have been re-created (me_set_cu_mask) since the last run
+        self.s_main = ctypes.c_void_p(self.ctx.lib.me_get_stream(self.ctx.h))
+        self.s_trk = ctypes.c_void_p(self.tctx.lib.me_get_stream(self.tctx.h))
+        if self.overlap == "frontend":
+            return self._run_frontend(frames, n, kp, ba_opts, stats, first)
         ctx, lib = self.ctx, self.ctx.lib
         self._klt(frames[first % len(frames)], kp, ba_opts, 0)
         pend = None
@@ -245,14 +274,30 @@ class FramePipeline:
             fd = frames[(first + t) % len(frames)]
             c = _calls(ctx, fd, kp, ba_opts)
             self.hip.wait(self.s_main, self.ev[t & 1])  # frame t's back end after its tracks
-            c.sc.scale = c.scale0  # every replay of the frame starts from the same scale
-            ctx.check(lib.me_scale_optimise(*c.scale), "me_scale_optimise")
-            stats["scale_iters"] += c.it.value
-            scale_counters(ctx, stats)
+            self._scale(ctx, fd, kp, ba_opts, stats)
             if t + 1 < n:  # issued once the scale LM is done: it overlaps the BA's latency-bound kernels
                 self._klt(frames[(first + t + 1) % len(frames)], kp, ba_opts, t + 1)
             if pend is not None:  # frame t-1's BA finished before this scale LM ran (same stream)
                 self._ba_wait(pend, stats)
+            fd.dba.reset()
+            ctx.check(lib.me_ba_solve_async(ctx.h, ctypes.byref(c.bp), ctypes.byref(c.bo)), "me_ba_solve_async")
+            pend = c
+        self._ba_wait(pend, stats)
+
+    def _run_frontend(self, frames, n, kp, ba_opts, stats, first):
+        ctx, lib = self.ctx, self.ctx.lib
+        pend = None
+        for t in range(n):
+            fd = frames[(first + t) % len(frames)]
+            # front end of frame t on the tracker stream: KLT, scale LM (blocking
+            # host call), while frame t-1's BA runs on the back-end stream
+            self._klt(fd, kp, ba_opts, t)
+            self._scale(self.tctx, fd, kp, ba_opts, stats)
+            self.hip.record(self.ev[t & 1], self.s_trk)
+            if pend is not None:
+                self._ba_wait(pend, stats)
+            c = _calls(ctx, fd, kp, ba_opts)
+            self.hip.wait(self.s_main, self.ev[t & 1])  # frame t's back end after its front end
             fd.dba.reset()
             ctx.check(lib.me_ba_solve_async(ctx.h, ctypes.byref(c.bp), ctypes.byref(c.bo)), "me_ba_solve_async")
             pend = c
@@ -310,7 +355,7 @@ def host_cpu():
     return model, os.cpu_count() or 1, avail
 
 
-def gpu_outputs(ctx, fd):
+def gpu_outputs(ctx, fd, sctx=None):
     """Outputs of the last timed replay of a frame, read back after the timed
     region: KLT points/status (device buffers), the scale LM result (the
     frame's argument block) and the BA window (device-resident problem)."""
@@ -320,8 +365,9 @@ def gpu_outputs(ctx, fd):
     ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, kp.ctypes.data, ctypes.c_void_p(fd.d_pts_out), kp.nbytes))
     ctx.check(ctx.lib.me_memcpy_d2h(ctx.h, kst.ctypes.data, ctypes.c_void_p(fd.d_status), kst.nbytes))
     c = fd._calls[id(ctx)]
+    cs = fd._calls[id(sctx or ctx)]  # the context that ran the frame's scale LM
     cams, pts = fd.dba.download()
-    return dict(klt=kp, klt_status=kst, scale=dict(stop=c.stop.value, iterations=c.it.value, scale=c.sc.scale),
+    return dict(klt=kp, klt_status=kst, scale=dict(stop=cs.stop.value, iterations=cs.it.value, scale=cs.sc.scale),
                 cams=cams, pts=pts, ba=dict(iterations=c.bs.iterations, successful_steps=c.bs.successful_steps))
 
 
@@ -728,12 +774,24 @@ def main():
         gpu_step(ctx, frames[i % len(frames)], kp, ba_opts, stats)
     ctx.synchronize()
     pipe = tctx = None
+    ncu = torch.cuda.get_device_properties(local_rank).multi_processor_count
+
+    def cu_split(on):
+        """Frontend overlap: disjoint CU sets for the two streams (only around the pipelined
+        runs; the side measurements use the whole device).  The latency-bound BA kernels and
+        the persistent scale LM otherwise share every CU's issue slots and slow each other."""
+        if pipe is None or args.overlap != "frontend" or not 0 < args.front_cus < 16:
+            return
+        tctx.set_cu_mask([i for i in range(ncu) if i % 16 < args.front_cus] if on else None)
+        ctx.set_cu_mask([i for i in range(ncu) if i % 16 >= args.front_cus] if on else None)
     if not args.no_pipeline:
         tctx = Context(local_rank)  # tracker context: its own HIP stream and scratch
-        pipe = FramePipeline(ctx, tctx, _Hip())
+        pipe = FramePipeline(ctx, tctx, _Hip(), args.overlap)
+        cu_split(True)
         pipe.run(frames, max(args.warmup, 2), kp, ba_opts, new_stats())
         tctx.synchronize()
         ctx.synchronize()
+        cu_split(False)
     # untimed profile steps with every family timed: per-family device time and
     # the dominant family (by device time) among those with a roofline
     ctx.timing_reset()
@@ -759,12 +817,17 @@ def main():
                        "frac": round(a_gbs / PEAK_HBM_GBS, 5), "kernel": "scale_res_ctrl_kernel",
                        "track_evaluations_per_frame": round(cfg["n_feats"] * pstats["scale_executed"] / npf, 1),
                        "us_per_frame": budget["SCALE_RES"]["us_per_frame"]}
-    dom = max((f for f in rl if rl[f] is not None), key=lambda f: prof[f][1])
+    # the persistent scale LM (one launch per frame) is the whole LM control loop with its
+    # phase waits, not one kernel's pass over its data: reported as mi_in_frame, not as the roofline kernel
+    persistent_scale = "SCALE_RES" in budget and budget["SCALE_RES"]["launches_per_frame"] <= 1.5
+    dom = max((f for f in rl if rl[f] is not None and not (f == "SCALE_RES" and persistent_scale)),
+              key=lambda f: prof[f][1])
     # timed region: HIP events on the ctx stream around the dominant family only
     ctx.timing_reset()
     if args.timing != "none":
         ctx.timing(True, None if args.timing == "all" else [dom])
     stats = new_stats()
+    cu_split(True)
     barrier()
     torch.cuda.synchronize()
     ctx.synchronize()
@@ -778,6 +841,7 @@ def main():
     ctx.synchronize()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t_start
+    cu_split(False)
     barrier()
     ctx.timing(False)
     fams = {f: ctx.timing_read(f) for f in fam_names}
@@ -828,7 +892,7 @@ def main():
         # parity of the timed frames: the last timed replay of each distinct
         # frame (read back after the timed region) against the oracle
         outs = [cpu_frame(cpu_payload(fd), args.ba_iters, args.scale_iters) for fd in frames]
-        cmp = [compare(gpu_outputs(ctx, fd), o) for fd, o in zip(frames, outs)]
+        cmp = [compare(gpu_outputs(ctx, fd, pipe.scale_ctx if pipe else None), o) for fd, o in zip(frames, outs)]
         parity = {"frames_checked": len(cmp), "klt_bit_exact": all(c["klt_bit_exact"] for c in cmp),
                   "scale_match": all(c["scale_match"] for c in cmp), "ba_match": all(c["ba_match"] for c in cmp),
                   "ba_max_rel_diff": float("%.3g" % max(c["ba_max_rel"] for c in cmp))}
@@ -884,8 +948,11 @@ def main():
                        "frame": f"KLT + MI scale LM (LM, MAX_NB_ITER {args.scale_iters}, tolerances off) + "
                                 f"{args.ba_iters} BA LM iterations",
                        "parallelism": f"{world} independent streams (one per GPU)",
-                       "pipeline": None if pipe is None else "KLT of frame t+1 overlaps the BA of frame t "
-                                                             "(two HIP streams, event dependency per frame)"},
+                       "pipeline": None if pipe is None else (
+                           ("front end (KLT + scale LM) of frame t+1 overlaps the BA of frame t" + (
+                               f" on disjoint CUs ({args.front_cus} of every 16 for the front end)"
+                               if 0 < args.front_cus < 16 else "")) if args.overlap == "frontend" else "KLT of frame t+1 overlaps the BA of frame t") +
+                           " (two HIP streams, event dependency per frame)"},
             "ba_iter_per_s": round(ba_total / t_max, 2),
             "scale_lm_per_frame": {k: round(stats[k2] / max(1, stats["frames"]), 3) for k, k2 in
                                    (("iterations", "scale_iters"), ("residual_evaluations", "scale_res_evals"),

@@ -53,6 +53,13 @@ const char* me_last_error(const me_ctx* ctx);
    NULL restores the ctx-owned stream. */
 int me_set_stream(me_ctx* ctx, void* hip_stream);
 void* me_get_stream(me_ctx* ctx);
+/* Restrict the ctx-owned stream to a set of compute units (bit i of mask[i/32]
+   = CU i; nwords = 0 restores all CUs): the stream is re-created with
+   hipExtStreamCreateWithCUMask after the old one drains.  Lets two contexts
+   of one GPU (e.g. a tracking front end and a BA back end) run side by side
+   on disjoint CUs instead of sharing every CU's issue slots.  No reference
+   counterpart (the reference runs one CPU thread). */
+int me_set_cu_mask(me_ctx* ctx, const uint32_t* mask, int nwords);
 int me_synchronize(me_ctx* ctx);
 int me_malloc(me_ctx* ctx, void** dptr, size_t bytes);
 int me_free(me_ctx* ctx, void* dptr);

@@ -190,3 +190,47 @@ def test_scale_state_mi_empty_is_an_error(ctx, sp300):
     sp = dataclasses.replace(sp300, tri_left=np.zeros_like(sp300.tri_left))
     with pytest.raises(MEError):
         scale_state_mi(sp, ctx=ctx)
+
+
+# ------------------------------------------------------------------ CU-partitioned concurrent front end / back end
+def test_cu_masked_frontend_backend_overlap(oracle, sp_cfg3):
+    """bench.py's frontend overlap: a tracker context whose stream is restricted
+    to half the CUs (me_set_cu_mask) runs the config-3 scale LM while a
+    back-end context on the other half runs the config-3 BA queued with
+    me_ba_solve_async -- both concurrently on the device, both equal to the
+    oracle; then the masks are lifted and the BA replays bit-identically."""
+    import ctypes
+
+    import torch
+
+    from uasl_motion_estimation_amd._lib import BASummaryC, Context
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions
+
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    front, back = Context(0), Context(0)
+    try:
+        front.set_cu_mask([i for i in range(ncu) if i % 16 < 8])
+        back.set_cu_mask([i for i in range(ncu) if i % 16 >= 8])
+        c = S.CONFIGS[3]
+        bp = S.ba_problem(S.SEED0 + 3, c["n_feats"], c["window"], c["width"], c["height"])
+        d = DeviceBAProblem(bp, back)
+        st, opts = d.struct(), SolverOptions.fixed_iterations(10).to_c()
+        back.check(back.lib.me_ba_solve_async(back.h, ctypes.byref(st), ctypes.byref(opts)), "me_ba_solve_async")
+        _scale_check(front, oracle, sp_cfg3[0], OptimisationParams.fixed_iterations(10))  # while the BA runs
+        s = BASummaryC()
+        back.check(back.lib.me_ba_wait(back.h, ctypes.byref(s)), "me_ba_wait")
+        cams, pts = d.download()
+        rc, rp, rs = oracle.ba_solve(bp, max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                                     parameter_tolerance=0.0)
+        assert s.iterations == rs["iterations"] == 10 and s.successful_steps == rs["successful_steps"]
+        np.testing.assert_allclose(cams, rc, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+        back.set_cu_mask(None)  # all CUs again: same device results
+        d.reset()
+        back.check(back.lib.me_ba_solve(back.h, ctypes.byref(st), ctypes.byref(opts), ctypes.byref(s)), "me_ba_solve")
+        cams2, pts2 = d.download()
+        assert np.array_equal(cams, cams2) and np.array_equal(pts, pts2)
+        d.close()
+    finally:
+        front.close()
+        back.close()

@@ -116,7 +116,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 # every symbol include/me_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
-    "me_get_stream", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
+    "me_get_stream", "me_set_cu_mask", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_timing_enable", "me_timing_read", "me_timing_reset",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
@@ -160,6 +160,7 @@ def load_library(path: str = LIB_PATH):
         "me_last_error": (ctypes.c_char_p, [c_void_p]),
         "me_set_stream": (c_int, [c_void_p, c_void_p]),
         "me_get_stream": (c_void_p, [c_void_p]),
+        "me_set_cu_mask": (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
         "me_synchronize": (c_int, [c_void_p]),
         "me_malloc": (c_int, [c_void_p, P(c_void_p), c_size_t]),
         "me_free": (c_int, [c_void_p, c_void_p]),
@@ -271,6 +272,16 @@ class Context:
     def set_stream(self, stream_handle: int | None):
         self.check(self.lib.me_set_stream(self.h, c_void_p(stream_handle) if stream_handle else None),
                    "me_set_stream")
+
+    def set_cu_mask(self, cus):
+        """Restrict the ctx-owned stream to the compute units in `cus` (an
+        iterable of CU indices; None or empty: all CUs) -- me_set_cu_mask."""
+        cus = sorted(set(cus or ()))
+        nw = (cus[-1] // 32 + 1) if cus else 0
+        words = (ctypes.c_uint32 * max(nw, 1))()
+        for i in cus:
+            words[i // 32] |= 1 << (i % 32)
+        self.check(self.lib.me_set_cu_mask(self.h, words, nw), "me_set_cu_mask")
 
     def stream_ptr(self) -> int:
         """The context's HIP stream (me_get_stream) as an integer handle."""

@@ -1,3 +1,4 @@
+#include <vector>
 // api.hip — context, memory and timing entry points of the C ABI (me_hip.h).
 #include "me_internal.hpp"
 #include <cstring>
@@ -164,6 +165,29 @@ int me_set_stream(me_ctx* c, void* s) {
   return ME_OK;
 }
 void* me_get_stream(me_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int me_set_cu_mask(me_ctx* c, const uint32_t* mask, int nwords) {
+  if (!c || nwords < 0 || (nwords > 0 && !mask)) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  int on = 0;
+  for (int i = 0; i < nwords * 32 && i < c->num_cu; ++i) on += (mask[i / 32] >> (i % 32)) & 1u;
+  if (nwords > 0 && on == 0) return me_set_error(c, ME_ERR_INVALID, "me_set_cu_mask: no compute unit enabled");
+  ME_HIP(c, hipStreamSynchronize(c->own_stream));
+  hipStream_t s = nullptr;
+  if (nwords > 0) {
+    std::vector<uint32_t> m(mask, mask + nwords);
+    ME_HIP(c, hipExtStreamCreateWithCUMask(&s, (uint32_t)nwords, m.data()));
+  } else {
+    ME_HIP(c, hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  }
+  const bool own = c->stream == c->own_stream;
+  ME_HIP(c, hipStreamDestroy(c->own_stream));
+  c->own_stream = s;
+  if (own) c->stream = s;
+  c->cu_active = nwords > 0 ? on : 0;
+  c->scale_lm_cap = -1;  // co-residency of the persistent scale LM re-queried for the new CU set
+  return ME_OK;
+}
 
 int me_synchronize(me_ctx* c) {
   ME_HIP(c, hipStreamSynchronize(c->stream));

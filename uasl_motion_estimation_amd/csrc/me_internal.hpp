@@ -16,6 +16,7 @@ struct me_timer_pair {
 struct me_ctx {
   int device = 0;
   int num_cu = 256;  // compute units of the device (grid sizing of streaming kernels)
+  int cu_active = 0;  // compute units enabled for the own stream (0: all; me_set_cu_mask)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;

@@ -1495,6 +1495,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
       (void)hipGetLastError();
       per_cu = cus = 0;
     }
+    if (c->cu_active > 0) cus = std::min(cus, c->cu_active);  // own stream restricted by me_set_cu_mask
     c->scale_lm_cap = per_cu * cus;
   }
   const bool persist = !blocks_env && 2L * nb * kCandY <= c->scale_lm_cap;
