@@ -294,12 +294,14 @@ class FramePipeline:
             self._klt(fd, kp, ba_opts, t)
             self._scale(self.tctx, fd, kp, ba_opts, stats)
             self.hip.record(self.ev[t & 1], self.s_trk)
-            if pend is not None:
-                self._ba_wait(pend, stats)
             c = _calls(ctx, fd, kp, ba_opts)
             self.hip.wait(self.s_main, self.ev[t & 1])  # frame t's back end after its front end
             fd.dba.reset()
+            # queued behind frame t-1's BA (two solves may be queued per context): the
+            # back-end stream never waits for the host to build this plan
             ctx.check(lib.me_ba_solve_async(ctx.h, ctypes.byref(c.bp), ctypes.byref(c.bo)), "me_ba_solve_async")
+            if pend is not None:
+                self._ba_wait(pend, stats)
             pend = c
         self._ba_wait(pend, stats)
 

@@ -239,8 +239,13 @@ int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_sum
    convergence return at once, so it suits fixed-iteration windows) and the
    read-back on the ctx stream, and returns without waiting.  The caller keeps
    *p's arrays alive until me_ba_wait, which blocks on this solve only (not on
-   work queued after it), writes host-problem results back and fills *s.  One
-   solve in flight per ctx: any other BA call on the ctx completes it first. */
+   work queued after it), writes host-problem results back and fills *s.  Up
+   to two solves may be queued per ctx (each in its own scratch and staging):
+   window t+1 can be queued behind window t before t is waited, so the device
+   never idles while the host builds the next plan; me_ba_wait completes the
+   oldest.  A third me_ba_solve_async before a wait is ME_ERR_STATE.  Any other
+   BA call on the ctx completes the queued solves first (their summaries stay
+   readable by me_ba_wait). */
 int me_ba_solve_async(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o);
 int me_ba_wait(me_ctx* ctx, me_ba_summary* s);
 /* Cost (Ceres ½Σρ) at the problem's current parameters. */

@@ -462,3 +462,32 @@ def test_ba_async_drained_by_next_call_and_wait_errors(ctx):
     with pytest.raises(MEError):
         d.wait()
     d.close()
+
+
+def test_ba_async_two_queued_windows(ctx):
+    """Two windows queued back to back (the second in the other scratch /
+    staging set while the first is in flight) give the synchronous results bit
+    for bit, waited oldest first; a third queued solve before a wait is
+    ME_ERR_STATE."""
+    from uasl_motion_estimation_amd._lib import MEError
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions
+
+    opts = SolverOptions.fixed_iterations(5)
+    probs = [S.ba_problem(51, 400, 12, 640, 480), S.ba_problem(52, 300, 10, 640, 480)]
+    ds = [DeviceBAProblem(bp, ctx) for bp in probs]
+    ref = []
+    for d in ds:
+        ref.append((d.solve(opts), *d.download()))
+        d.reset()
+    for _ in range(2):  # twice: the sets alternate
+        ds[0].solve_async(opts)
+        ds[1].solve_async(opts)
+        with pytest.raises(MEError):
+            ds[0].solve_async(opts)
+        for d, (rs, rc, rp) in zip(ds, ref):
+            assert d.wait() == rs
+            c, p = d.download()
+            assert np.array_equal(c, rc) and np.array_equal(p, rp)
+            d.reset()
+    for d in ds:
+        d.close()

@@ -147,7 +147,8 @@ void me_destroy(me_ctx* c) {
   for (float* t : c->mi_table)
     if (t) hipFree(t);
   if (c->ba_async_free) c->ba_async_free(c);
-  if (c->ba_pinned) hipHostFree(c->ba_pinned);
+  for (void* h : c->ba_pinned)
+    if (h) hipHostFree(h);
   if (c->scale_mirror) hipHostFree(c->scale_mirror);
   if (c->pinned) hipHostFree(c->pinned);
   for (auto e : c->event_pool) hipEventDestroy(e);

@@ -2051,9 +2051,12 @@ int blocks(long n, int bs) { return (int)std::max(1L, (n + bs - 1) / bs); }
 
 int ba_drain(me_ctx* c);
 
+// async >= 0: the plan of a queued asynchronous solve, built in scratch and
+// staging set `async` (0 or 1) while the other set may still be in flight;
+// every other plan first completes the queued solves (they own the scratch)
 int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base,
-               bool async = false) {
-  ME_TRY(ba_drain(c));  // a pending asynchronous solve owns the BA scratch until it completes
+               int async = -1) {
+  if (async < 0) ME_TRY(ba_drain(c));
   ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
   ME_CHECK(c, p->n_cams <= kMaxScanCams, "BA: at most %d cameras per window", kMaxScanCams);
   ME_CHECK(c, p->obs_dim == 0 || p->obs_dim == 2 || p->obs_dim == 4, "BA: obs_dim must be 2 or 4 (Observation<M>)");
@@ -2206,15 +2209,15 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   void* hp;
   const size_t stage = rup((long)std::max(8 * out_doubles, dev ? (size_t)0 : input_span), 64);
   const size_t hbytes = stage + 2 * rup(sizeof(State), 64);
-  if (async) {  // staging owned by the asynchronous solve (grown only while none is pending)
-    if (c->ba_pinned_size < hbytes) {
-      if (c->ba_pinned) ME_HIP(c, hipHostFree(c->ba_pinned));
-      c->ba_pinned = nullptr;
-      c->ba_pinned_size = 0;
-      ME_HIP(c, hipHostMalloc(&c->ba_pinned, std::max(hbytes, (size_t)4096), hipHostMallocDefault));
-      c->ba_pinned_size = std::max(hbytes, (size_t)4096);
+  if (async >= 0) {  // staging owned by the asynchronous solve (set `async` is free: its last solve was waited)
+    if (c->ba_pinned_size[async] < hbytes) {
+      if (c->ba_pinned[async]) ME_HIP(c, hipHostFree(c->ba_pinned[async]));
+      c->ba_pinned[async] = nullptr;
+      c->ba_pinned_size[async] = 0;
+      ME_HIP(c, hipHostMalloc(&c->ba_pinned[async], std::max(hbytes, (size_t)4096), hipHostMallocDefault));
+      c->ba_pinned_size[async] = std::max(hbytes, (size_t)4096);
     }
-    hp = c->ba_pinned;
+    hp = c->ba_pinned[async];
   } else {
     ME_TRY(me_pinned(c, hbytes, &hp));
   }
@@ -2258,17 +2261,23 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   P.use_lds = P.solve_lds <= 150 * 1024 ? 1 : 0;
   if (!P.use_lds) P.solve_lds = 8 * solve_small_doubles(g.Ts);
   ME_CHECK(c, P.solve_lds <= 150 * 1024, "BA: %d variable cameras exceed the camera-solve workspace", g.m);
-  for (const void* k : {(const void*)cam_solve_kernel<0>, (const void*)cam_solve_kernel<1>, (const void*)cam_solve_kernel<2>})
-    ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.solve_lds));
   P.schur_lds = schur_lds_bytes(g.spts, g.Rpad);
   ME_CHECK(c, P.schur_lds <= kSchurLdsCap, "BA: %d variable cameras exceed the Schur workspace", g.m);
+  // dynamic-LDS ceilings of the solve and Schur kernels: set once per context
+  // at the cap every plan stays under (not per solve: ~36 runtime calls of
+  // host time in front of every queued solve)
+  if (!c->ba_lds_attr) {
+    for (const void* k : {(const void*)cam_solve_kernel<0>, (const void*)cam_solve_kernel<1>, (const void*)cam_solve_kernel<2>})
+      ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
 #define ME_SCHUR_K(N)                                                                                   \
   (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>, \
       (const void*)pt_schur_kernel<N, 512, kSchurPtsSmall>
-  for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5), ME_SCHUR_K(6), ME_SCHUR_K(7), ME_SCHUR_K(8),
-                        ME_SCHUR_K(9), ME_SCHUR_K(10), ME_SCHUR_K(12), ME_SCHUR_K(16), ME_SCHUR_K(24)})
+    for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5), ME_SCHUR_K(6), ME_SCHUR_K(7), ME_SCHUR_K(8),
+                          ME_SCHUR_K(9), ME_SCHUR_K(10), ME_SCHUR_K(12), ME_SCHUR_K(16), ME_SCHUR_K(24)})
 #undef ME_SCHUR_K
-    ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.schur_lds));
+      ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSchurLdsCap));
+    c->ba_lds_attr = 1;
+  }
   return ME_OK;
 }
 
@@ -2506,48 +2515,76 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
 
 // Asynchronous solve: every possible iteration is queued at once (launches
 // after convergence test State::done and return), then the output kernel and
-// read-back behind an event.  The host is free as soon as it is queued.
+// read-back behind an event.  The host is free as soon as it is queued.  Up
+// to two solves may be queued on a ctx (each in its own scratch / staging
+// set), so a caller can queue window t+1 behind window t without waiting:
+// the device never idles while the host builds the next plan.
 struct AsyncSolve {
   Plan P;
   me_ba_problem prob;  // copy: cams / pts are written back at completion
   hipEvent_t ev = nullptr;
+  int set = 0;  // scratch / staging set
   bool completed = false;
   int rc = ME_OK;
   me_ba_summary sum{};
 };
+constexpr int kBaQueue = 2;
+struct AsyncQueue {
+  AsyncSolve* q[kBaQueue] = {nullptr, nullptr};  // FIFO: q[0] oldest
+  int n = 0;
+};
 
-void ba_async_free(me_ctx* c) {
-  auto* A = (AsyncSolve*)c->ba_async;
-  if (!A) return;
-  if (!A->completed) hipEventSynchronize(A->ev);
-  hipEventDestroy(A->ev);
-  delete A;
-  c->ba_async = nullptr;
-  c->ba_async_free = nullptr;
-}
-
-int ba_complete(me_ctx* c) {
-  auto* A = (AsyncSolve*)c->ba_async;
-  if (!A || A->completed) return ME_OK;
+int ba_complete_one(me_ctx* c, AsyncSolve* A) {
+  if (A->completed) return ME_OK;
   A->rc = finish(A->P, &A->prob, &A->sum, true, A->ev);
   A->completed = true;
   return ME_OK;
 }
 
-// Any other BA call on the ctx first completes the pending solve (its
-// summary stays readable by me_ba_wait until the next asynchronous solve).
-int ba_drain(me_ctx* c) { return ba_complete(c); }
+void ba_async_free(me_ctx* c) {
+  auto* Q = (AsyncQueue*)c->ba_async;
+  if (!Q) return;
+  for (int i = 0; i < Q->n; ++i) {
+    AsyncSolve* A = Q->q[i];
+    if (!A->completed) hipEventSynchronize(A->ev);
+    hipEventDestroy(A->ev);
+    delete A;
+  }
+  delete Q;
+  c->ba_async = nullptr;
+  c->ba_async_free = nullptr;
+}
+
+AsyncQueue* ba_queue(me_ctx* c) {
+  if (!c->ba_async) {
+    c->ba_async = new AsyncQueue;
+    c->ba_async_free = ba_async_free;
+  }
+  return (AsyncQueue*)c->ba_async;
+}
+
+// Any other BA call on the ctx first completes the queued solves (their
+// summaries stay readable by me_ba_wait, oldest first).
+int ba_drain(me_ctx* c) {
+  auto* Q = (AsyncQueue*)c->ba_async;
+  if (!Q) return ME_OK;
+  for (int i = 0; i < Q->n; ++i) ME_TRY(ba_complete_one(c, Q->q[i]));
+  return ME_OK;
+}
 
 }  // namespace
 
 extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
-  ME_TRY(ba_drain(c));
-  ba_async_free(c);
+  AsyncQueue* Q = ba_queue(c);
+  if (Q->n >= kBaQueue)
+    return me_set_error(c, ME_ERR_STATE, "me_ba_solve_async: %d solves already queued on this context (me_ba_wait first)",
+                        kBaQueue);
   auto* A = new AsyncSolve;
   A->prob = *p;
-  int rc = plan_build(c, p, opt, A->P, 0, true);
+  A->set = Q->n == 0 ? 0 : 1 - Q->q[0]->set;
+  int rc = plan_build(c, p, opt, A->P, A->set, A->set);
   if (rc == ME_OK) {
     for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it) rc = enqueue_iteration(A->P, nullptr, nullptr);
   }
@@ -2563,20 +2600,23 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
     delete A;
     return rc;
   }
-  c->ba_async = A;
-  c->ba_async_free = ba_async_free;
+  Q->q[Q->n++] = A;
   return ME_OK;
 }
 
 extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) {
   if (!c) return ME_ERR_INVALID;
-  auto* A = (AsyncSolve*)c->ba_async;
-  if (!A) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");
+  auto* Q = (AsyncQueue*)c->ba_async;
+  if (!Q || Q->n == 0) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");
   ME_HIP(c, hipSetDevice(c->device));
-  ME_TRY(ba_complete(c));
+  AsyncSolve* A = Q->q[0];
+  ME_TRY(ba_complete_one(c, A));
   const int rc = A->rc;
   if (s && rc == ME_OK) *s = A->sum;
-  ba_async_free(c);
+  hipEventDestroy(A->ev);
+  delete A;
+  for (int i = 1; i < Q->n; ++i) Q->q[i - 1] = Q->q[i];
+  Q->q[--Q->n] = nullptr;
   return rc;
 }
 

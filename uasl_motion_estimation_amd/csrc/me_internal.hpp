@@ -42,8 +42,9 @@ struct me_ctx {
   // its own pinned staging, so later calls on the ctx cannot overwrite it
   void* ba_async = nullptr;
   void (*ba_async_free)(me_ctx*) = nullptr;
-  void* ba_pinned = nullptr;
-  size_t ba_pinned_size = 0;
+  void* ba_pinned[2] = {nullptr, nullptr};  // staging of the (at most two) queued asynchronous BA solves
+  size_t ba_pinned_size[2] = {0, 0};
+  int ba_lds_attr = 0;  // dynamic-LDS ceilings of the BA kernels set (plan_build)
   void* scale_mirror = nullptr;  // coherent host page the scale LM control writes its state to
   int scale_gen = 0;             // generation of the last scale LM solve (mirror ownership)
   int scale_lm_cap = -1;         // co-resident workgroups of the persistent scale LM kernel (-1: not queried)
