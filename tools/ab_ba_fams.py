@@ -4,12 +4,15 @@ import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: F401
+if os.environ.get("LIB"):
+    from uasl_motion_estimation_amd import _lib as _l
+    _l.load_library(os.environ["LIB"])
 from uasl_motion_estimation_amd import synthetic as S
 from uasl_motion_estimation_amd._lib import Context
 from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions
 ctx = Context(0)
 fams = ("BA_LINEARIZE", "BA_SCHUR", "BA_SOLVE", "BA_STEP")
-for c in (3, 4, 5):
+for c in [int(x) for x in os.environ.get("CONFIGS", "3,4,5").split(",")]:
     cfg = S.CONFIGS[c]
     bp = S.ba_problem(S.SEED0 * 7 + c, cfg["n_feats"], cfg["window"], cfg["width"], cfg["height"])
     d = DeviceBAProblem(bp, ctx)

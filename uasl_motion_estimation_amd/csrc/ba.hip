@@ -214,12 +214,18 @@ constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups ove
 // Per observation: corrected residual / Jacobian, cost, and the unscaled
 // per-observation normal-equation pieces W_o = Jc^T Jp (6x3), V_o = Jp^T Jp
 // (6 unique), g_o = Jp^T r, so the per-point stage only sums.
-template <int OD>
-__global__ __launch_bounds__(kBlock) void linearize_kernel(Geo g, Bufs b) {
-  __shared__ double lds[4];
+// Workgroup size by window: one-wave workgroups spread a small window's
+// observations over every CU (config 3: 22k observations = 344 workgroups,
+// 13.6 -> 11.0 us), 256 threads for large ones (config 4: 100k observations,
+// 34.4 us vs 38.6 with one-wave workgroups)
+constexpr int kLinSmall = 64, kLinSmallMaxObs = 64 * 512;
+__host__ __device__ inline int lin_block(int no) { return no <= kLinSmallMaxObs ? kLinSmall : kBlock; }
+template <int OD, int BLK>
+__global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
+  __shared__ double lds[BLK / 64];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
-  const int o = blockIdx.x * kBlock + threadIdx.x;
+  const int o = blockIdx.x * BLK + threadIdx.x;
   double cost = 0;
   if (o < g.no) {
     const int cur = st->cur;
@@ -531,12 +537,13 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
       // (A) every load of the landmark and of this lane's first CSR slot in one round
       const int beg = b.p_off[j], end = b.p_off[j + 1];
       const int q0 = beg + gl;
-      int ci0 = -1, cprev0 = -1;
+      int ci0 = -1, cprev0 = -1, cnext0 = -2;
       double w0[18], cs0[6], X0[9];
       for (int i = 0; i < 9; ++i) X0[i] = 0.0;
       if (q0 < end) {
         ci0 = b.p_cam[q0];
         if (q0 > beg) cprev0 = b.p_cam[q0 - 1];
+        if (q0 + 1 < end) cnext0 = b.p_cam[q0 + 1];  // duplicate test of phase B, requested with the rest
         if (need_lin)
           for (int i = 0; i < 9; ++i) X0[i] = b.obsx[(long)q0 * kObsxStride + i];
         if (ci0 >= 0) {
@@ -623,8 +630,9 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         lo = min(lo, 6 * ci);
         hi = max(hi, 6 * ci + 5);
         if (cp == ci) continue;  // not the first slot of its camera run
-        for (int r = q + 1; r < end && b.p_cam[r] == ci; ++r)
-          for (int i = 0; i < 18; ++i) w[i] += b.Wo[18 * (long)r + i];
+        if (q != q0 || cnext0 == ci)  // (the first slot's next camera came with phase A's loads)
+          for (int r = q + 1; r < end && b.p_cam[r] == ci; ++r)
+            for (int i = 0; i < 18; ++i) w[i] += b.Wo[18 * (long)r + i];
         for (int a = 0; a < 6; ++a) {
           const int col = 6 * ci + a;
           const double wa[3] = {w[3 * a] * cs[a] * pv[0], w[3 * a + 1] * cs[a] * pv[1], w[3 * a + 2] * cs[a] * pv[2]};
@@ -745,10 +753,10 @@ __device__ void lin_finalize_body(const Geo& g, const Bufs& b, const Opts& o, co
   if (st->need_lin) {
     double c = 0, m = 0;
     if (!use_scal) {
-      for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
-      for (int i = threadIdx.x; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+      for (int i = threadIdx.x; i < g.nblk_lin; i += blockDim.x) c += b.part[R_COST * g.pstride + i];
+      for (int i = threadIdx.x; i < g.ksplit; i += blockDim.x) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
     }
-    for (int i = threadIdx.x; i < g.n6; i += kFinBlock) m = fmax(m, fabs(gc_raw[i]));
+    for (int i = threadIdx.x; i < g.n6; i += blockDim.x) m = fmax(m, fabs(gc_raw[i]));
     double v[1] = {c}, out[1];
     block_sum<1>(v, out, lds);
     const double mm = block_max(m, lds + 8);
@@ -794,7 +802,7 @@ __global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) 
   if (st->done) return;
   double c = 0, m = 0;
   if (st->need_lin) {
-    for (int i = threadIdx.x; i < g.nblk_obs; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
+    for (int i = threadIdx.x; i < g.nblk_lin; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
     for (int i = threadIdx.x; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
   }
   double v[1] = {c}, out[1];
@@ -852,9 +860,24 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
   const bool use = gr >= 0 && gr < n && gc <= n;
   double acc = 0.0;
   if (use && !st->fail) {
+    // partials grp, grp + 8, ... added in order; their loads issued 8 at a
+    // time (independent addresses: one memory latency per batch, not per add)
     const double* src = b.Spart + idx;
     const long stride = (long)g.npairs * 256;
-    for (int q = grp; q < g.ksplit; q += kSaGroups) acc += src[q * stride];
+#ifndef ME_SA_BATCH
+#define ME_SA_BATCH 8
+#endif
+    for (int q0 = grp; q0 < g.ksplit; q0 += ME_SA_BATCH * kSaGroups) {
+      double v[ME_SA_BATCH];
+#pragma unroll
+      for (int k = 0; k < ME_SA_BATCH; ++k) {
+        const int q = q0 + k * kSaGroups;
+        v[k] = q < g.ksplit ? src[q * stride] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < ME_SA_BATCH; ++k)
+        if (q0 + k * kSaGroups < g.ksplit) acc += v[k];
+    }
   }
   part[grp][e] = acc;
   __syncthreads();
@@ -1565,7 +1588,7 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
   __shared__ double lds[32];
   State* st = b.st;
   double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_step; i += kFinBlock) {
+  for (int i = threadIdx.x; i < g.nblk_step; i += blockDim.x) {
     v[0] += b.part[R_MODEL * g.pstride + i];
     v[1] += b.part[R_CAND * g.pstride + i];
     v[2] += b.part[R_STEP2 * g.pstride + i];
@@ -1583,6 +1606,8 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
   }
 }
 
+// (64-thread workgroups measured slower: 17.2 -> 21.6 us at config 3, the
+// last arrival then reduces 4x the partials)
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 
 template <int OD>
@@ -2106,12 +2131,13 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.ksplit = std::min(g.nsub, 256);  // Schur workgroups = partial slices summed by s_assemble
   ME_CHECK(c, g.npairs <= 8 * 24, "BA: %d variable cameras exceed the Schur tile budget", g.m);
   g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
+  g.nblk_lin = (int)std::max(1L, rup(std::max(g.no, 1), lin_block(g.no)) / lin_block(g.no));
   g.nblk_pts = (int)std::max(1L, rup(std::max(g.np, 1), kPtBlock) / kPtBlock);
   g.jacobi = opt->jacobi_scaling ? 1 : 0;
   g.ck = (int)std::min(64L, std::max(1L, rup(std::max(g.no, 1), (long)std::max(g.m, 1) * kBlock) /
                                              ((long)std::max(g.m, 1) * kBlock)));
   g.nblk_step = (int)std::max(1L, rup(std::max(g.np, 1), kStepPts) / kStepPts);
-  g.pstride = std::max({g.nblk_obs, g.nblk_pts, g.nblk_step, g.ksplit});
+  g.pstride = std::max({g.nblk_obs, g.nblk_lin, g.nblk_pts, g.nblk_step, g.ksplit});
   std::memcpy(g.K0, p->K0, sizeof(g.K0));
   std::memcpy(g.K1, p->K1, sizeof(g.K1));
   g.baseline = baseline;
@@ -2295,10 +2321,15 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   hipStream_t s = c->stream;
   {
     me_ktimer t(c, ME_KT_BA_LINEARIZE);
-    if (g.od == 4)
-      hipLaunchKernelGGL(linearize_kernel<4>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+    const bool small = lin_block(g.no) == kLinSmall;
+    if (g.od == 4 && small)
+      hipLaunchKernelGGL((linearize_kernel<4, kLinSmall>), dim3(g.nblk_lin), dim3(kLinSmall), 0, s, g, P.b);
+    else if (g.od == 4)
+      hipLaunchKernelGGL((linearize_kernel<4, kBlock>), dim3(g.nblk_lin), dim3(kBlock), 0, s, g, P.b);
+    else if (small)
+      hipLaunchKernelGGL((linearize_kernel<2, kLinSmall>), dim3(g.nblk_lin), dim3(kLinSmall), 0, s, g, P.b);
     else
-      hipLaunchKernelGGL(linearize_kernel<2>, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, P.b);
+      hipLaunchKernelGGL((linearize_kernel<2, kBlock>), dim3(g.nblk_lin), dim3(kBlock), 0, s, g, P.b);
   }
   // After the first linearisation the Jacobi scaling is fixed and the Schur
   // pass no longer needs the camera assembly: its m x ck workgroups then ride

@@ -67,7 +67,7 @@ struct State {
 enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 
 struct Geo {
-  int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_pts, nblk_step, pstride, jacobi,
+  int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_lin, nblk_pts, nblk_step, pstride, jacobi,
       ck;
   int od;                  // residual rows per observation: 4 StereoReprojectionError, 2 Standard/StereoRight
   double K0[9], K1[9];
