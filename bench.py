@@ -73,6 +73,8 @@ def parse():
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
                          "each timed launch adds two event records to the stream), every family, or none")
+    ap.add_argument("--timing-every", type=int, default=8,
+                    help="time every k-th launch of the timed family inside the timed region (HIP events)")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every family timed, to pick the dominant family")
     return ap.parse_args()
@@ -828,6 +830,9 @@ def main():
     ctx.timing_reset()
     if args.timing != "none":
         ctx.timing(True, None if args.timing == "all" else [dom])
+        # every k-th launch of the family: a live average over the timed region whose event
+        # records perturb the stream k times less (--timing-every 1: every launch)
+        ctx.timing_sample(args.timing_every)
     stats = new_stats()
     cu_split(True)
     barrier()
@@ -846,6 +851,7 @@ def main():
     cu_split(False)
     barrier()
     ctx.timing(False)
+    ctx.timing_sample(1)
     fams = {f: ctx.timing_read(f) for f in fam_names}
     t_max = elapsed
     frames_total = stats["frames"]
@@ -868,7 +874,7 @@ def main():
     roofline = {"bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 5), "traffic": pmc_traffic(dom), "kernel": dom,
                 "kernels": FAMILY_KERNELS.get(dom), "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount,
-                "timed_live": fams[dom][0] > 0}
+                "timed_live": fams[dom][0] > 0, "timed_launches": n_l, "sampled_every": args.timing_every}
     if "BA_SOLVE" in budget:  # the frame's largest kernel has no HBM/MFMA roofline: a latency budget
         b = budget["BA_SOLVE"]
         roofline["solve"] = {"kernel": "cam_solve_kernel", "bound": "latency (dependent blocked-Cholesky chain)",

@@ -78,6 +78,10 @@ enum { ME_KT_MI = 0, ME_KT_SCALE_RES = 1, ME_KT_SCALE_NEQ = 2, ME_KT_BA_LINEARIZ
 int me_timing_enable(me_ctx* ctx, int family_mask);
 int me_timing_read(me_ctx* ctx, int kernel, long* launches, double* total_ms);
 int me_timing_reset(me_ctx* ctx);
+/* Time only every k-th launch of each timed family (k >= 1; 1 = every launch,
+   the default): a live measurement of the average launch duration whose
+   event records perturb the stream k times less. */
+int me_timing_sample(me_ctx* ctx, int every);
 
 /* ---- A1/A2: mutual information ---------------------------------------
  * Replaces float me::computeMutualInformation(const cv::Mat&, const cv::Mat&)

@@ -117,7 +117,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 EXPORTS = [
     "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
     "me_get_stream", "me_set_cu_mask", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
-    "me_timing_enable", "me_timing_read", "me_timing_reset",
+    "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
@@ -168,6 +168,7 @@ def load_library(path: str = LIB_PATH):
         "me_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
         "me_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
         "me_timing_enable": (c_int, [c_void_p, c_int]),
+        "me_timing_sample": (c_int, [c_void_p, c_int]),
         "me_timing_read": (c_int, [c_void_p, c_int, P(c_long), P(c_double)]),
         "me_timing_reset": (c_int, [c_void_p]),
         "me_mi_scores": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
@@ -317,6 +318,10 @@ class Context:
         if on:
             mask = 0xFFFF if families is None else sum(1 << KT[f] for f in families)
         self.check(self.lib.me_timing_enable(self.h, mask))
+
+    def timing_sample(self, every: int):
+        """Time every `every`-th launch of each timed family (me_timing_sample)."""
+        self.check(self.lib.me_timing_sample(self.h, int(every)))
 
     def timing_reset(self):
         self.check(self.lib.me_timing_reset(self.h))

@@ -73,7 +73,7 @@ static hipEvent_t pool_get(me_ctx* c) {
 }
 
 me_ktimer::me_ktimer(me_ctx* ctx, int kernel) : c(ctx), k(kernel) {
-  if (c && (c->timing >> kernel & 1)) {
+  if (c && (c->timing >> kernel & 1) && c->kt_seen[kernel]++ % c->timing_every == 0) {
     a = pool_get(c);
     b = pool_get(c);
     if (a) hipEventRecord(a, c->stream);
@@ -224,6 +224,11 @@ int me_timing_enable(me_ctx* c, int family_mask) {
   c->timing = family_mask & ME_KT_ALL;
   return ME_OK;
 }
+int me_timing_sample(me_ctx* c, int every) {
+  if (!c || every < 1) return ME_ERR_INVALID;
+  c->timing_every = every;
+  return ME_OK;
+}
 int me_timing_read(me_ctx* c, int k, long* launches, double* ms) {
   if (k < 0 || k >= ME_KT_COUNT) return ME_ERR_INVALID;
   drain_timers(c);
@@ -236,6 +241,7 @@ int me_timing_reset(me_ctx* c) {
   for (int i = 0; i < ME_KT_COUNT; ++i) {
     c->launches[i] = 0;
     c->total_ms[i] = 0;
+    c->kt_seen[i] = 0;
   }
   return ME_OK;
 }

@@ -1122,6 +1122,9 @@ __device__ __forceinline__ void drain_and_barrier() {
 #ifndef ME_SOLVE_LOOKAHEAD
 #define ME_SOLVE_LOOKAHEAD 1
 #endif
+#ifndef ME_SOLVE_PIPE
+#define ME_SOLVE_PIPE 1
+#endif
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
 constexpr int kSolveMwMinTs = 16;             // block steps from which the trailing workers are used
 
@@ -1273,6 +1276,9 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // panel tiles as MFMA operands, no barrier between; 43.8 us) and a one-wave
   // backward solve without workgroup barriers (unchanged).
   constexpr bool kLook = ME_DIAG_MFMA && ME_SOLVE_LOOKAHEAD && kMode != 2;
+  // LDS-resident system: wave 0 alone on the critical path (see below)
+  constexpr bool kPipe = kLook && kLds && ME_SOLVE_PIPE;
+  __shared__ unsigned pflag, pdone;
   // Measured and dropped (config 3): panel fused with the column-(J+1) update
   // in one phase (transposed panel tiles as MFMA operands, no barrier between;
   // 43.8 vs 42.0 us) and a one-wave backward solve without barriers (no change)
@@ -1333,7 +1339,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     }
   }
   if (done) return;
-  if (tid == 0) sfail = fail_in;
+  if (tid == 0) {
+    sfail = fail_in;
+    pflag = 0u;
+    pdone = 0u;
+  }
   if ((skip & 256) && tid == 0) st->stamps[15] += 1;
   SOLVE_START(0);
   __syncthreads();
@@ -1342,6 +1352,81 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     return;
   }
   SOLVE_STAMP(0);
+  if constexpr (kPipe) {
+    // Wave 0 walks the critical path alone: per block step J it forms the
+    // panel tile L_{J+1,J} = A_{J+1,J} X_J^T, publishes it (LDS flag), applies
+    // step J to the diagonal tile (J+1, J+1) and factors diagonal block J+1 --
+    // no workgroup barrier between.  Meanwhile the workers (waves other than
+    // 0 and its SIMD sibling 4) form the other panel tiles of J, update
+    // column J + 1 below the diagonal tile (after the flag), and, once every
+    // worker's panel tiles are stored (LDS counter), the rest of step J's
+    // trailing tiles.  One barrier per step joins both.  Same operations on
+    // the same operands as the phased loop below: identical results.
+    const bool worker = wave != 0 && !(nw > 4 && wave == 4);
+    const int nwk = nw - 1 - (nw > 4 ? 1 : 0);
+    const int widx = wave - 1 - (nw > 4 && wave > 4 ? 1 : 0);
+    auto diag_block = [&](int Jd) {
+      const int jd0 = 16 * Jd;
+      double* Ablk = A + (long)jd0 * ld + jd0;
+      double* XJw = X + 256 * Jd;
+      const int q = lane >> 4, c = lane & 15;
+      bool ok = true;
+      double4_t A4, Y4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        A4[r] = Ablk[(q + 4 * r) * ld + c];
+        Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+      }
+      diag_round_mfma<0>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+      diag_round_mfma<1>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+      diag_round_mfma<2>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+      diag_round_mfma<3>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+      if (!ok) sfail = 1;  // benign race: every writer stores 1
+    };
+    auto panel_tile = [&](int J, int I) {  // L_IJ = A_IJ X_J^T on the matrix cores
+      const int j0 = 16 * J, i0 = 16 * I;
+      const double* XJ = X + 256 * J;
+      double av[4], bv[4];
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        av[s4] = A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)];
+        bv[s4] = XJ[(lane & 15) * 16 + 4 * s4 + (lane >> 4)];
+      }
+      double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) A[(long)(i0 + (lane >> 4) + 4 * q4) * ld + j0 + (lane & 15)] = acc[q4];
+    };
+    auto lds_wait = [&](volatile unsigned* f, unsigned want) {
+      long k = 0;
+      for (; k < kSolveSpin && *f < want; ++k) __builtin_amdgcn_s_sleep(1);
+      if (k == kSolveSpin) sfail = 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    if (wave == 0) diag_block(0);
+    __syncthreads();
+    for (int J = 0; J + 1 < Ts; ++J) {
+      if (sfail) break;
+      if (wave == 0) {
+        panel_tile(J, J + 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) pflag = (unsigned)(J + 1);
+        trailing_tile<false>(A, ld, J, J + 1, J + 1, lane);  // step J on the diagonal tile
+        solve_wave_sync();
+        diag_block(J + 1);
+      } else if (worker) {
+        for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) atomicAdd(&pdone, 1u);
+        lds_wait(&pflag, (unsigned)(J + 1));
+        for (int I = J + 2 + widx; I < Ts; I += nwk) trailing_tile<false>(A, ld, J, I, J + 1, lane);
+        lds_wait(&pdone, (unsigned)(nwk * (J + 1)));
+        trailing_split<false>(A, ld, Ts, J, false, widx, nwk, lane);  // tiles (I, K), J + 2 <= K <= I
+      }
+      __syncthreads();
+    }
+  } else
   for (int J = 0; J < Ts; ++J) {
     const int j0 = 16 * J;
     SOLVE_START(1);

@@ -32,6 +32,8 @@ struct me_ctx {
   std::vector<hipEvent_t> event_pool;
   long launches[ME_KT_COUNT] = {0};
   double total_ms[ME_KT_COUNT] = {0};
+  long kt_seen[ME_KT_COUNT] = {0};  // launches of each family since the last reset (sampling)
+  int timing_every = 1;             // time every k-th launch of a timed family (me_timing_sample)
   hipEvent_t poll_ev[2] = {nullptr, nullptr};  // device-state read-back events of iterative solves
   // glibc-compatible rand() stream of the RANSAC sampling (vo.hip)
   int32_t rand_st[31] = {0};
