@@ -1704,17 +1704,60 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   const int j = blockIdx.x * kStepPts + (threadIdx.x / kStepG);
   double mc = 0, cc = 0, s2 = 0, xn2 = 0;
   if (j < g.np && !st->fail) {  // uniform within a 16-lane group
+    // Every load of the point and of this lane's first CSR slot is requested
+    // in three dependent rounds (point data + offsets | slot: camera, obs
+    // index, W | camera step / scales, linearisation, observation, candidate
+    // camera) before any arithmetic; further slots (points with more than 16
+    // observations) load in the loops.  Same operations in the same order.
+    const int cur = st->cur;
+    double psv[3], gpv[3], Lv[9], xv[3];
+    for (int a = 0; a < 3; ++a) {
+      psv[a] = b.psc[3 * (long)j + a];
+      gpv[a] = b.gps[3 * (long)j + a];
+      xv[a] = b.pts[cur][3 * (long)j + a];
+    }
+    for (int i = 0; i < 9; ++i) Lv[i] = b.Lp[9 * (long)j + i];
     const int beg = b.p_off[j], end = b.p_off[j + 1];
+    const int q0 = beg + gl;
+    const bool has0 = q0 < end;
+    int ci0 = -1, o0 = 0;
+    double W0[18];
+    if (has0) {
+      ci0 = b.p_cam[q0];
+      o0 = b.p_obs[q0];
+      for (int i = 0; i < 18; ++i) W0[i] = b.Wo[18 * (long)q0 + i];  // (unused for a fixed camera)
+    }
+    const double* cams_c = b.cams[1 - cur];
+    double ys0[6], dc0[6], Lo0[kLinStride], f0[4];
+    int cam0 = 0, right0 = 0;
+    if (has0) {
+      if (ci0 >= 0)
+        for (int a = 0; a < 6; ++a) {
+          ys0[a] = b.csc[6 * ci0 + a] * b.yc[6 * ci0 + a];
+          dc0[a] = b.dc[6 * ci0 + a];
+        }
+      for (int k = 0; k < kLinStride; ++k) Lo0[k] = b.lin[(long)o0 * kLinStride + k];
+      cam0 = b.cam_idx[o0];
+      for (int k = 0; k < OD; ++k) f0[k] = b.obs[(long)OD * o0 + k];
+      if (OD == 2) right0 = b.cam_id[o0] != 0;
+    }
+    double cv0[6];
+    if (has0)
+      for (int a = 0; a < 6; ++a) cv0[a] = cams_c[6 * cam0 + a];
     // (1) sum over the point's slots of W_q^T (Dc y_c)
     double t[3] = {0.0, 0.0, 0.0};
-    for (int q = beg + gl; q < end; q += kStepG) {
-      const int ci = b.p_cam[q];
+    for (int q = q0; q < end; q += kStepG) {
+      const bool first = q == q0;
+      const int ci = first ? ci0 : b.p_cam[q];
       if (ci < 0) continue;
-      const double* W = b.Wo + 18 * (long)q;
-      const double* y = b.yc + 6 * ci;
-      const double* cs = b.csc + 6 * ci;
-      double ys[6];
-      for (int a = 0; a < 6; ++a) ys[a] = cs[a] * y[a];
+      double ys[6], W[18];
+      if (first) {
+        for (int a = 0; a < 6; ++a) ys[a] = ys0[a];
+        for (int i = 0; i < 18; ++i) W[i] = W0[i];
+      } else {
+        for (int a = 0; a < 6; ++a) ys[a] = b.csc[6 * ci + a] * b.yc[6 * ci + a];
+        for (int i = 0; i < 18; ++i) W[i] = b.Wo[18 * (long)q + i];
+      }
       for (int c = 0; c < 3; ++c) {
         double s = 0;
         for (int a = 0; a < 6; ++a) s += W[a * 3 + c] * ys[a];
@@ -1723,46 +1766,61 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     }
     for (int c = 0; c < 3; ++c) t[c] = group_sum<kStepG>(t[c]);
     // (2) point step y_p = -(V + D/r)^-1 (g_p + sum) in the scaled space, candidate point
-    const double* ps = b.psc + 3 * (long)j;
     double rhs[3];
-    for (int c = 0; c < 3; ++c) rhs[c] = -b.gps[3 * (long)j + c] - t[c] * ps[c];
-    const double* L = b.Lp + 9 * (long)j;
+    for (int c = 0; c < 3; ++c) rhs[c] = -gpv[c] - t[c] * psv[c];
     double u[3], yp[3];
-    fwd3(L, rhs, u);
-    bwd3(L, u, yp);
-    const int cur = st->cur;
-    const double* x = b.pts[cur] + 3 * (long)j;
+    fwd3(Lv, rhs, u);
+    bwd3(Lv, u, yp);
     double d[3], xc[3];
     for (int a = 0; a < 3; ++a) {
-      d[a] = yp[a] * ps[a];
-      xc[a] = fmin(fmax(x[a] + d[a], g.lo[a]), g.hi[a]);
+      d[a] = yp[a] * psv[a];
+      xc[a] = fmin(fmax(xv[a] + d[a], g.lo[a]), g.hi[a]);
     }
     if (gl == 0) {
       for (int a = 0; a < 3; ++a) {
         b.dp[3 * (long)j + a] = d[a];
         b.pts[1 - cur][3 * (long)j + a] = xc[a];
-        const double dd = xc[a] - x[a];
+        const double dd = xc[a] - xv[a];
         s2 += dd * dd;
-        xn2 += x[a] * x[a];
+        xn2 += xv[a] * xv[a];
       }
     }
     // (3) model cost change and candidate cost of the point's observations
-    const double* cams_c = b.cams[1 - cur];
-    for (int q = beg + gl; q < end; q += kStepG) {
-      const int o = b.p_obs[q];
-      const double* Lo = b.lin + (long)o * kLinStride;
-      const int ci = b.cam_idx[o] - g.nf;
+    for (int q = q0; q < end; q += kStepG) {
+      const bool first = q == q0;
+      double Lo[kLinStride], dcv[6], cv[6], f[4];
+      int ci, right = 0;
+      if (first) {
+        for (int k = 0; k < kLinStride; ++k) Lo[k] = Lo0[k];
+        ci = cam0 - g.nf;
+        if (ci >= 0)
+          for (int i = 0; i < 6; ++i) dcv[i] = dc0[i];
+        for (int a = 0; a < 6; ++a) cv[a] = cv0[a];
+        for (int k = 0; k < OD; ++k) f[k] = f0[k];
+        right = right0;
+      } else {
+        const int o = b.p_obs[q];
+        for (int k = 0; k < kLinStride; ++k) Lo[k] = b.lin[(long)o * kLinStride + k];
+        const int cam = b.cam_idx[o];
+        ci = cam - g.nf;
+        if (ci >= 0)
+          for (int i = 0; i < 6; ++i) dcv[i] = b.dc[6 * ci + i];
+        for (int a = 0; a < 6; ++a) cv[a] = cams_c[6 * cam + a];
+        for (int k = 0; k < OD; ++k) f[k] = b.obs[(long)OD * o + k];
+        if (OD == 2) right = b.cam_id[o] != 0;
+      }
       for (int k = 0; k < 4; ++k) {
         double jd = 0;
-        if (ci >= 0) {
-          const double* dc = b.dc + 6 * ci;
-          for (int i = 0; i < 6; ++i) jd += Lo[4 + k * 6 + i] * dc[i];
-        }
+        if (ci >= 0)
+          for (int i = 0; i < 6; ++i) jd += Lo[4 + k * 6 + i] * dcv[i];
         jd += Lo[28 + k * 3 + 0] * d[0] + Lo[28 + k * 3 + 1] * d[1] + Lo[28 + k * 3 + 2] * d[2];
         mc -= jd * (Lo[k] + jd / 2.0);
       }
       double r[4];
-      obs_residual<OD>(g, b, o, cams_c + 6 * b.cam_idx[o], xc, r, nullptr, nullptr);
+      if (OD == 4)
+        stereo_residual(g, cv, xc, f, r, nullptr, nullptr);
+      else
+        mono_residual(g, cv, xc, f, right, r, nullptr, nullptr);
       const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
       double rho0, sc;
       huber(s, &rho0, &sc);
@@ -2210,8 +2268,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     g.spts = kSchurPtsWide;
   else
     g.spts = g.npairs > 100 ? kSchurPtsSmall : kSchurPts;
-  if (const char* e = getenv("ME_SCHUR_PTS"))  // A/B timing only
-    if (atoi(e) == kSchurPts) g.spts = kSchurPts;
+  if (const char* e = getenv("ME_SCHUR_PTS")) {  // A/B timing only
+    const int v = atoi(e);
+    if (v == kSchurPts || v == kSchurPtsSmall || (v == kSchurPtsWide && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap))
+      g.spts = v;
+  }
   g.nsub = (int)std::max(1L, ((long)g.np + g.spts - 1) / g.spts);
   g.ksplit = std::min(g.nsub, 256);  // Schur workgroups = partial slices summed by s_assemble
   ME_CHECK(c, g.npairs <= 8 * 24, "BA: %d variable cameras exceed the Schur tile budget", g.m);
