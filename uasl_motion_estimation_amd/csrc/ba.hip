@@ -701,17 +701,43 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
           if ((hm[u] >> ks) & 1ull) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], bb[u], acc[u], 0, 0, 0);
       };
       double av[NT], bv[NT];
-      if constexpr (NT <= 6) {  // double-buffered operands (a few tiles per wave: the registers are there)
-        double an[NT], bn[NT];
-        operands(0, av, bv);
-        for (int ks = 0; ks < nks; ++ks) {
-          if (ks + 1 < nks) operands(ks + 1, an, bn);
-          contract(ks, av, bv);
+      if constexpr (NT <= 6) {
+        // A few tiles per wave: the K-steps unrolled with ping-pong operand
+        // registers, every operand read issued unconditionally (clamped tile
+        // index) and only the MFMAs skipped by the band masks.  Straight-line
+        // LDS reads let each MFMA wait for its own operands only (lgkmcnt(N));
+        // conditional reads made the compiler wait for all of them (lgkmcnt(0)
+        // before every step's first MFMA: the next step's reads were never
+        // overlapped).  Scheduling barriers keep one step of reads in flight.
+        constexpr int NKS = 3 * PTS / 4;
+        static_assert(NKS % 2 == 0, "K-steps are taken in pairs");
+        int cI[NT], cJ[NT];
+#pragma unroll
+        for (int u = 0; u < NT; ++u) {
+          cI[u] = 16 * max(tI[u], 0);
+          cJ[u] = 16 * max(tJ[u], 0);
+        }
+        const double* Y0 = Y + (size_t)(lane >> 4) * Rz + (lane & 15);
+        const size_t kstride = 4 * (size_t)Rz;
+        auto reads = [&](const double* Yr, double* a, double* bb) {
 #pragma unroll
           for (int u = 0; u < NT; ++u) {
-            av[u] = an[u];
-            bv[u] = bn[u];
+            a[u] = Yr[cI[u]];
+            bb[u] = Yr[cJ[u]];
           }
+        };
+        double an[NT], bn[NT];
+        reads(Y0, av, bv);
+#pragma unroll 1
+        for (int ks = 0; ks < NKS; ks += 2) {
+          reads(Y0 + (ks + 1) * kstride, an, bn);
+          __builtin_amdgcn_sched_barrier(0);
+          contract(ks, av, bv);
+          __builtin_amdgcn_sched_barrier(0);
+          reads(Y0 + min(ks + 2, NKS - 1) * kstride, av, bv);  // (the last pair re-reads a valid row, unused)
+          __builtin_amdgcn_sched_barrier(0);
+          contract(ks + 1, an, bn);
+          __builtin_amdgcn_sched_barrier(0);
         }
       } else {
         for (int ks = 0; ks < nks; ++ks) {
