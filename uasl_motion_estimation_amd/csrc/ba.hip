@@ -855,20 +855,39 @@ constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // lin_finalize_kernel instead (one launch less per iteration): the assembly
 // blocks do not read what it writes, and the camera solve that follows
 // reads both.
-__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal,
-                                                            int full) {
-  __shared__ double part[kSaGroups][kSaElems];
-  static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
-  if (blockIdx.x == gridDim.x - 1) {
-    if (threadIdx.x < 2) b.ssync[threadIdx.x] = 0u;  // the camera solve that follows starts its steps at 0
-    lin_finalize_body(g, b, o, gc_raw, use_scal, &part[0][0]);
+template <bool SC1>
+__device__ __forceinline__ double a_ld(const double* p) {
+  if (!SC1) return *p;
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool SC1>
+__device__ __forceinline__ void a_st(double* p, double v) {
+  if (!SC1) {
+    *p = v;
     return;
   }
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_and_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+  __syncthreads();
+}
+
+// Assembly of elements blk * EL .. blk * EL + EL - 1 by NTH = 8 EL threads
+// (8 partial groups of EL elements).  No early return: the fused form's
+// workgroup signals after every thread's stores have drained.  SC1: stores
+// written through for a consumer workgroup of the same launch.
+template <int NTH, bool SC1>
+__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full) {
+  constexpr int EL = NTH / kSaGroups;
+  __shared__ double part[kSaGroups][EL];
   const State* st = b.st;
-  if (st->done || st->final_pass) return;  // final pass: no step follows, S is not needed
+  const bool live = !(st->done || st->final_pass);  // final pass: no step follows, S is not needed
   const int n = g.n6;
-  const int e = threadIdx.x % kSaElems, grp = threadIdx.x / kSaElems;
-  const int idx = blockIdx.x * kSaElems + e;
+  const int e = threadIdx.x % EL, grp = threadIdx.x / EL;
+  const int idx = blk * EL + e;
   int gr = -1, gc = -1;  // position in the (padded) system [S | b]
   bool diag = false;
   if (idx < g.npairs * 256) {
@@ -883,9 +902,10 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
     gc = 16 * J + (idx & 15);
   }
   // S entries (gr, gc < n) and the right-hand side (gc == n); the padding is skipped
-  const bool use = gr >= 0 && gr < n && gc <= n;
+  const bool use = live && gr >= 0 && gr < n && gc <= n;
+  const bool fail = st->fail;
   double acc = 0.0;
-  if (use && !st->fail) {
+  if (use && !fail) {
     // partials grp, grp + 8, ... added in order; their loads issued 8 at a
     // time (independent addresses: one memory latency per batch, not per add)
     const double* src = b.Spart + idx;
@@ -907,25 +927,39 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
   }
   part[grp][e] = acc;
   __syncthreads();
-  if (blockIdx.x == 0 && threadIdx.x == 0) b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
-  if (grp != 0 || !use) return;
-  double sum = 0.0;
+  if (grp == 0 && use) {
+    double sum = 0.0;
 #pragma unroll
-  for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
-  if (gc < n) {
-    double v = 0;
-    if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];  // U blocks are symmetric
-    v = st->fail ? 0.0 : v - sum;
-    if (diag) {
-      b.S[(long)gr * n + gc] = v;
+    for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
+    if (gc < n) {
+      double v = 0;
+      if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];  // U blocks are symmetric
+      v = fail ? 0.0 : v - sum;
+      if (diag) {
+        a_st<SC1>(&b.S[(long)gr * n + gc], v);
+      } else {
+        a_st<SC1>(&b.S[(long)gc * n + gr], v);
+        if (full) b.S[(long)gr * n + gc] = v;
+      }
     } else {
-      b.S[(long)gc * n + gr] = v;
-      if (full) b.S[(long)gr * n + gc] = v;
+      a_st<SC1>(&b.bvec[gr], fail ? 0.0 : b.gcs[gr] - sum);
+      a_st<SC1>(&b.diagU[gr], b.U[36 * (gr / 6) + (gr % 6) * 7]);
     }
-  } else {
-    b.bvec[gr] = st->fail ? 0.0 : b.gcs[gr] - sum;
-    b.diagU[gr] = b.U[36 * (gr / 6) + (gr % 6) * 7];
   }
+}
+
+__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal,
+                                                            int full) {
+  static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
+  if (blockIdx.x == gridDim.x - 1) {
+    __shared__ double lds[16];
+    if (threadIdx.x < 2) b.ssync[threadIdx.x] = 0u;  // the camera solve that follows starts its steps at 0
+    lin_finalize_body(g, b, o, gc_raw, use_scal, lds);
+    return;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && !(b.st->done || b.st->final_pass))
+    b.scal[R_COUNT] = b.st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
+  s_assemble_body<kBlock, false>(g, b, blockIdx.x, full);
 }
 
 // One workgroup: S (assembled by s_assemble_kernel, all-reduced in sharded
@@ -1126,25 +1160,6 @@ constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 // to the counter (agent-scope atomic), the consumer polls with an sc1 load and
 // reads A only with sc1 loads after its barrier -- no release fence (an L2
 // write-back) and no acquire (an L1 invalidate) per hand-off.
-template <bool SC1>
-__device__ __forceinline__ double a_ld(const double* p) {
-  if (!SC1) return *p;
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
-template <bool SC1>
-__device__ __forceinline__ void a_st(double* p, double v) {
-  if (!SC1) {
-    *p = v;
-    return;
-  }
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_and_barrier() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
-  __syncthreads();
-}
 #ifndef ME_SOLVE_LOOKAHEAD
 #define ME_SOLVE_LOOKAHEAD 1
 #endif
@@ -1291,7 +1306,14 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
 // kMode: 0 = [S; -b^T] in LDS, one workgroup; 1 = in global memory, one workgroup;
 // 2 = in global memory, trailing updates on `nworkers` more workgroups (sc1 hand-offs)
 template <int kMode>
-__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int nworkers) {
+// Fused assembly (nasm > 0; single GPU, modes 0 and 1): workgroups 1..nasm
+// assemble S | b | diag(U) from the Schur partials (s_assemble_body, written
+// through) and count themselves done on b.cnt[g.m + 3]; workgroup 0 runs the
+// linearisation bookkeeping (lin_finalize) and, unless the solve has ended,
+// waits for the count (bounded), re-arms it and reads S with sc1 loads.  One
+// launch per LM iteration fewer than s_assemble_kernel + cam_solve_kernel.
+__global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int nworkers, int nasm,
+                                                                const double* gc_raw) {
   extern __shared__ double smem[];
   __shared__ double red[64];
   __shared__ int sfail;
@@ -1312,7 +1334,33 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     cam_solve_worker(g, b, nworkers);
     return;
   }
+  unsigned* asm_cnt = b.cnt + g.m + 3;
+  if (kMode != 2 && nasm > 0 && blockIdx.x > 0) {
+    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0);
+    drain_and_barrier();  // every wave's written-through stores have left
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
   State* st = b.st;
+  const bool fused = kMode != 2 && nasm > 0;
+  if (fused) {
+    lin_finalize_body(g, b, o, gc_raw, 0, red);
+    if (threadIdx.x == 0) {
+      const int live = !st->done;
+      b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // (what s_assemble's first block wrote; read by decide)
+      long k = 0;
+      if (live) {
+        for (; k < kSolveSpin; ++k) {
+          if (__hip_atomic_load(asm_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nasm) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (k == kSolveSpin) st->fail = 1;  // a missing assembler: a failed step, never a hang
+        __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
+    __syncthreads();
+  }
   const int n = g.n6, Ts = g.Ts, N = 16 * Ts;
   const int ld = solve_ld(Ts);
   const int tid = threadIdx.x, nt = blockDim.x;
@@ -1324,7 +1372,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
-  const int fail_in = st->fail || b.scal[R_COUNT] != 0.0;
+  const int fail_in = st->fail || (!fused && b.scal[R_COUNT] != 0.0);
   const double radius = st->radius;
   // the candidate-camera inputs (current cameras, Jacobi scales) are requested
   // now; they are consumed after the factorisation, which hides their latency
@@ -1336,6 +1384,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     x_pre = b.cams[cur][tid];
     if (tid >= 6 * g.nf) cs_pre = b.csc[tid - 6 * g.nf];
   }
+  // the system written through by this launch's assemblers is read through (sc1)
+  auto ld_sys = [&](const double* p) { return fused ? a_ld<true>(p) : *p; };
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
   for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
     double v[kLoadBatch];
@@ -1346,14 +1396,14 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       v[k] = 0.0;
       if (q < NQ && r < N && c < n && (c >> 4) <= (r >> 4)) {
         if (r < n) {
-          v[k] = b.S[r * n + c];
+          v[k] = ld_sys(&b.S[r * n + c]);
           // LM diagonal (Ceres: clamp(diag(U)) / radius), loaded in the same round
-          if (r == c) v[k] += fmin(fmax(b.diagU[r], o.min_diag), o.max_diag) / radius;
+          if (r == c) v[k] += fmin(fmax(ld_sys(&b.diagU[r]), o.min_diag), o.max_diag) / radius;
         } else if (r == n) {
-          v[k] = -b.bvec[c];
+          v[k] = -ld_sys(&b.bvec[c]);
         }
       } else if (q < NQ && c == n && r < n && (r >> 4) == (n >> 4)) {
-        v[k] = -b.bvec[r];  // the diagonal block must stay symmetric
+        v[k] = -ld_sys(&b.bvec[r]);  // the diagonal block must stay symmetric
       }
     }
     if (done) return;
@@ -2236,6 +2286,7 @@ struct Plan {
   int diag_skip = 0;  // ME_SOLVE_SKIP: timing diagnostics only (results invalid)
   int n_enq = 0;      // linearisations queued so far (the first runs the camera assembly on its own)
   bool sequential = false;  // ME_BA_SEQUENTIAL=1: never fuse (A/B timing)
+  bool no_fused_asm = false;  // ME_BA_NOFUSEASM=1: S assembly in its own launch (A/B timing)
   bool full_S = false;      // assemble both block triangles of S (reduced-system / covariance read-back)
   int solve_workers = -1;   // global-memory camera solve: trailing-update workgroups (-1: by size; ME_SOLVE_WORKERS)
 };
@@ -2270,6 +2321,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
   if (const char* sw = getenv("ME_SOLVE_WORKERS")) P.solve_workers = atoi(sw);  // A/B timing (0: one workgroup)
   if (const char* sq = getenv("ME_BA_SEQUENTIAL")) P.sequential = atoi(sq) != 0;
+  if (const char* fa = getenv("ME_BA_NOFUSEASM")) P.no_fused_asm = atoi(fa) != 0;
   Geo& g = P.g;
   g.nc = p->n_cams;
   g.np = p->n_pts;
@@ -2384,7 +2436,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * (size_t)g.n6, &P.gc_glob);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
-  add(4 * (size_t)(g.m + 1 + 2), &b.cnt);  // last-arrival counters: per camera (cam_assemble) | pt_step | solve sync
+  add(4 * (size_t)(g.m + 1 + 3), &b.cnt);  // counters: per camera (cam_assemble) | pt_step | solve sync (2) | fused assembly
   const size_t work_bytes = 4 * (2 * (size_t)g.np + (size_t)g.nblk_obs * g.nc + 4);
   add(work_bytes, &b.work);
   const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
@@ -2575,15 +2627,34 @@ int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
   return me_check_launch(c, "BA assemble");
 }
 
-int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
+// `last`: the enqueue after max_num_iterations steps.  Its linearisation feeds
+// only the closing gradient test and final cost, and its lin_finalize always
+// ends the solve (iterations == max_num_iterations), so the camera solve and
+// the point step that would follow are never run: they are not queued (two
+// no-op launches fewer per solve; every rank of a sharded solve skips alike).
+int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user, bool last = false) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
   ME_TRY(enqueue_linearize(P, ar, user));
-  // S = U - sum of the Schur partials is assembled by a wide kernel (coalesced,
-  // all CUs) rather than inside the one-workgroup solve, whose dependent
-  // cross-XCD loads would otherwise dominate the iteration.
-  ME_TRY(enqueue_assemble(P, ar));
+  // camera-solve form: 0 = [S; -b^T] in LDS, 1 = global memory, 2 = global
+  // memory with trailing-update workers.  Trailing-update workers pay once the
+  // block steps are many and wide: config 5 (19 steps) 372 -> 274 us per
+  // solve; config 4 (11 steps) is faster on one workgroup (118 vs 131 us: the
+  // per-step hand-offs).
+  const int np0 = (g.Ts - 1) * g.Ts / 2;
+  const int nwk = P.use_lds ? 0
+                  : P.solve_workers >= 0 ? P.solve_workers
+                  : g.Ts >= kSolveMwMinTs ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
+                                          : 0;
+  // S = U - sum of the Schur partials is assembled by wide workgroups
+  // (coalesced, all CUs) rather than by the one-workgroup solve, whose
+  // dependent cross-XCD loads would otherwise dominate the iteration.  Single
+  // GPU (modes 0 and 1) they ride in the camera-solve launch (fused assembly).
+  const bool fuse = !ar && g.m > 0 && !P.full_S && !last && !P.sequential && nwk == 0 && !P.no_fused_asm;
+  const int nasm = fuse ? blocks((long)g.npairs * 256, kSolveBlock / kSaGroups) : 0;
+  if (!fuse) ME_TRY(enqueue_assemble(P, ar));
+  if (last) return me_check_launch(c, "BA iteration");
   if (g.m > 0) {
     if (ar) {
       ME_AR(P.b.S, g.n6 * g.n6 + 2 * g.n6);  // S | b | diag(U) are contiguous
@@ -2594,23 +2665,16 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     me_ktimer t(c, ME_KT_BA_SOLVE);
-    if (P.use_lds) {
-      hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip, 0);
-    } else {
-      // Trailing-update workers pay once the block steps are many and wide:
-      // config 5 (19 steps) 372 -> 274 us per solve; config 4 (11 steps) is
-      // faster on one workgroup (118 vs 131 us: the per-step hand-offs).
-      const int np0 = (g.Ts - 1) * g.Ts / 2;
-      const int nwk = P.solve_workers >= 0 ? P.solve_workers
-                      : g.Ts >= kSolveMwMinTs
-                          ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
-                          : 0;
-      if (nwk > 0)
-        hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o,
-                           P.diag_skip, nwk);
-      else
-        hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip, 0);
-    }
+    const double* gc = P.gc_raw;
+    if (P.use_lds)
+      hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
+                         0, nasm, gc);
+    else if (nwk > 0)
+      hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o,
+                         P.diag_skip, nwk, 0, gc);
+    else
+      hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
+                         0, nasm, gc);
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
@@ -2689,7 +2753,8 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
   const int chunk = 4;
   int it = 0;
   auto enqueue_chunk = [&](int slot) -> int {
-    for (int k = 0; k < chunk && it <= opt->max_num_iterations; ++k, ++it) ME_TRY(enqueue_iteration(P, ar, user));
+    for (int k = 0; k < chunk && it <= opt->max_num_iterations; ++k, ++it)
+      ME_TRY(enqueue_iteration(P, ar, user, it == opt->max_num_iterations));
     ME_HIP(c, hipMemcpyAsync(P.hstate[slot], P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ME_HIP(c, hipEventRecord(c->poll_ev[slot], c->stream));
     return ME_OK;
@@ -2789,7 +2854,8 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   A->set = Q->n == 0 ? 0 : 1 - Q->q[0]->set;
   int rc = plan_build(c, p, opt, A->P, A->set, A->set);
   if (rc == ME_OK) {
-    for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it) rc = enqueue_iteration(A->P, nullptr, nullptr);
+    for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it)
+      rc = enqueue_iteration(A->P, nullptr, nullptr, it == opt->max_num_iterations);
   }
   if (rc == ME_OK) rc = enqueue_output(A->P, &A->prob);
   if (rc == ME_OK && hipEventCreateWithFlags(&A->ev, hipEventDisableTiming) != hipSuccess)
