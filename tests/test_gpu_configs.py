@@ -139,6 +139,26 @@ def test_ba_config3_bench_window(ctx, oracle):
     _ba_fixed(ctx, oracle, S.ba_problem(seed * 7 + 0, c["n_feats"], c["window"], c["width"], c["height"]), 10)
 
 
+@pytest.mark.parametrize("cfg,iters", [(3, 10), (4, 4)])
+def test_ba_fused_assembly_identical(ctx, monkeypatch, cfg, iters):
+    """S assembly inside the camera-solve launch (default; LDS form at config 3,
+    global-memory form at config 4) vs its own s_assemble launch
+    (ME_BA_NOFUSEASM=1): the same sums in the same order, so bit-identical
+    cameras, points and summary."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    c = S.CONFIGS[cfg]
+    bp = S.ba_problem(S.SEED0 + cfg, c["n_feats"], c["window"], c["width"], c["height"])
+    out = {}
+    for sep in ("0", "1"):
+        monkeypatch.setenv("ME_BA_NOFUSEASM", sep)
+        out[sep] = ba_solve(bp.copy(), SolverOptions.fixed_iterations(iters), ctx=ctx)
+    (c0, p0, s0), (c1, p1, s1) = out["0"], out["1"]
+    assert np.array_equal(c0, c1) and np.array_equal(p0, p1)
+    assert (s0["iterations"], s0["successful_steps"], s0["final_cost"]) == \
+        (s1["iterations"], s1["successful_steps"], s1["final_cost"])
+
+
 def test_ba_config4_8000x30(ctx, oracle):
     c = S.CONFIGS[4]
     bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
