@@ -1256,6 +1256,25 @@ __device__ __forceinline__ void trailing_tile(double* A, int ld, int J, int I, i
   for (int s = 0; s < 4; ++s) a_st<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)], acc[s]);
 }
 
+// The same update of one tile, the result left in the MFMA accumulator (lane
+// l holds A_IK[(l >> 4) + 4 s][l & 15] in element s: the layout the one-wave
+// diagonal factorisation takes its block in) instead of stored.
+__device__ __forceinline__ double4_t trailing_tile_acc(const double* A, int ld, int J, int I, int K, int lane) {
+  const int j0 = 16 * J, i0 = 16 * I, k0 = 16 * K;
+  double av[4], bv[4];
+  double4_t acc;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int cc = j0 + 4 * s + (lane >> 4);
+    av[s] = -A[(long)(i0 + (lane & 15)) * ld + cc];
+    bv[s] = A[(long)(k0 + (lane & 15)) * ld + cc];
+    acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)];
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
+  return acc;
+}
+
 // Workers of the multi-workgroup solve.  Tile (I, K), 1 <= K <= I < Ts, is
 // owned by one wave of one worker for the whole solve (linear index
 // (I-1) I / 2 + K - 1, dealt round-robin over the workers' waves), so its
@@ -1441,23 +1460,28 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     const bool worker = wave != 0 && !(nw > 4 && wave == 4);
     const int nwk = nw - 1 - (nw > 4 ? 1 : 0);
     const int widx = wave - 1 - (nw > 4 && wave > 4 ? 1 : 0);
-    auto diag_block = [&](int Jd) {
+    // diagonal block Jd from its (updated) values in the accumulator layout
+    auto diag_factor = [&](int Jd, double4_t A4) {
       const int jd0 = 16 * Jd;
       double* Ablk = A + (long)jd0 * ld + jd0;
       double* XJw = X + 256 * Jd;
       const int q = lane >> 4, c = lane & 15;
       bool ok = true;
-      double4_t A4, Y4;
+      double4_t Y4;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        A4[r] = Ablk[(q + 4 * r) * ld + c];
-        Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
-      }
+      for (int r = 0; r < 4; ++r) Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
       diag_round_mfma<0>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
       diag_round_mfma<1>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
       diag_round_mfma<2>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
       diag_round_mfma<3>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
       if (!ok) sfail = 1;  // benign race: every writer stores 1
+    };
+    auto diag_block = [&](int Jd) {
+      const double* Ablk = A + (long)(16 * Jd) * ld + 16 * Jd;
+      double4_t A4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) A4[r] = Ablk[((lane >> 4) + 4 * r) * ld + (lane & 15)];
+      diag_factor(Jd, A4);
     };
     auto panel_tile = [&](int J, int I) {  // L_IJ = A_IJ X_J^T on the matrix cores
       const int j0 = 16 * J, i0 = 16 * I;
@@ -1488,9 +1512,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         panel_tile(J, J + 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) pflag = (unsigned)(J + 1);
-        trailing_tile<false>(A, ld, J, J + 1, J + 1, lane);  // step J on the diagonal tile
-        solve_wave_sync();
-        diag_block(J + 1);
+        // step J on the diagonal tile, handed to the factorisation in registers
+        // (its updated values are read by no one else: the factorisation
+        // overwrites the lower triangle with L, the upper one is never read)
+        solve_wave_sync();  // the panel tile just stored is an operand
+        diag_factor(J + 1, trailing_tile_acc(A, ld, J, J + 1, J + 1, lane));
       } else if (worker) {
         for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
