@@ -1259,16 +1259,17 @@ __device__ __forceinline__ void trailing_tile(double* A, int ld, int J, int I, i
 // The same update of one tile, the result left in the MFMA accumulator (lane
 // l holds A_IK[(l >> 4) + 4 s][l & 15] in element s: the layout the one-wave
 // diagonal factorisation takes its block in) instead of stored.
-__device__ __forceinline__ double4_t trailing_tile_acc(const double* A, int ld, int J, int I, int K, int lane) {
-  const int j0 = 16 * J, i0 = 16 * I, k0 = 16 * K;
+// (Diagonal tile, K = I: both MFMA operands come from the same panel tile.)
+__device__ __forceinline__ double4_t trailing_diag_acc(const double* A, int ld, int J, int I, int lane) {
+  const int j0 = 16 * J, i0 = 16 * I;
   double av[4], bv[4];
   double4_t acc;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int cc = j0 + 4 * s + (lane >> 4);
-    av[s] = -A[(long)(i0 + (lane & 15)) * ld + cc];
-    bv[s] = A[(long)(k0 + (lane & 15)) * ld + cc];
-    acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + k0 + (lane & 15)];
+    bv[s] = A[(long)(i0 + (lane & 15)) * ld + cc];
+    av[s] = -bv[s];
+    acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + i0 + (lane & 15)];
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
@@ -1516,7 +1517,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         // (its updated values are read by no one else: the factorisation
         // overwrites the lower triangle with L, the upper one is never read)
         solve_wave_sync();  // the panel tile just stored is an operand
-        diag_factor(J + 1, trailing_tile_acc(A, ld, J, J + 1, J + 1, lane));
+        diag_factor(J + 1, trailing_diag_acc(A, ld, J, J + 1, lane));
       } else if (worker) {
         for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
