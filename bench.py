@@ -455,6 +455,30 @@ def pmc_traffic(family: str):
     return None
 
 
+def rocprof_avg_ms(family: str):
+    """Average duration (ms) of the family's kernel in the newest committed
+    headline-frame rocprofv3 summary (profiles/*_kernel_stats.txt written by
+    tools/prof_cycle.sh: the bench's config-3 frame without event timing), and
+    that file's name; (None, None) if absent.  The live HIP-event average
+    brackets each sampled launch with two event packets on the BA stream, so
+    it also carries the dependent-launch gap and the events' own cost."""
+    import glob
+    import re
+
+    ks = FAMILY_KERNELS.get(family, [])
+    files = [f for f in glob.glob(os.path.join(ROOT, "profiles", "*_kernel_stats.txt")) if "_bench_" not in f]
+    files.sort(key=lambda f: ([int(x) for x in re.findall(r"\d+", os.path.basename(f))], os.path.basename(f)))
+    for f in reversed(files):
+        best = None
+        for line in open(f):
+            m = re.match(r"\s*(?:void )?(\S+?)(?:<[^>]*>)?\s+(\d+)\s+([\d.]+) us\s+([\d.]+) us/call", line)
+            if m and ks and m.group(1) in ks and (best is None or int(m.group(2)) > best[0]):
+                best = (int(m.group(2)), float(m.group(4)))
+        if best:
+            return best[1] * 1e-3, os.path.basename(f)
+    return None, None
+
+
 def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
     """Batched MI patch scores (A1, 11x11) on n_pairs pairs of the resident
     frame images: the north-star MI kernel measured on its own (HIP events
@@ -875,6 +899,11 @@ def main():
                 "frac": round(achieved / peak, 5), "traffic": pmc_traffic(dom), "kernel": dom,
                 "kernels": FAMILY_KERNELS.get(dom), "avg_launch_ms": round(avg_ms, 5), "work_per_launch": amount,
                 "timed_live": fams[dom][0] > 0, "timed_launches": n_l, "sampled_every": args.timing_every}
+    rp_ms, rp_file = rocprof_avg_ms(dom)
+    if rp_ms:  # the same kernel in the committed rocprofv3 summary of the headline frame
+        a_rp = amount / (rp_ms * 1e-3) / scale_u
+        roofline.update({"rocprof_avg_launch_ms": round(rp_ms, 5), "rocprof_summary": f"profiles/{rp_file}",
+                         "achieved_rocprof": round(a_rp, 3), "frac_rocprof": round(a_rp / peak, 5)})
     if "BA_SOLVE" in budget:  # the frame's largest kernel has no HBM/MFMA roofline: a latency budget
         b = budget["BA_SOLVE"]
         roofline["solve"] = {"kernel": "cam_solve_kernel", "bound": "latency (dependent blocked-Cholesky chain)",
