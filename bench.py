@@ -72,9 +72,12 @@ def parse():
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
-                         "each timed launch adds two event records to the stream), every family, or none")
-    ap.add_argument("--timing-every", type=int, default=8,
-                    help="time every k-th launch of the timed family inside the timed region (HIP events)")
+                         "the Schur family's sampled launches carry the events themselves, hipExtLaunchKernelGGL: "
+                         "the kernel's own begin/end timestamps; other families record two events around the "
+                         "launch), every family, or none")
+    ap.add_argument("--timing-every", type=int, default=16,
+                    help="time every k-th launch of the timed family inside the timed region (HIP events; "
+                         "config 3: ~20 of the 330 Schur launches, the frame rate within 1 %% of --timing none)")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every family timed, to pick the dominant family")
     return ap.parse_args()

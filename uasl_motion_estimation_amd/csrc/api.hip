@@ -72,16 +72,17 @@ static hipEvent_t pool_get(me_ctx* c) {
   return e;
 }
 
-me_ktimer::me_ktimer(me_ctx* ctx, int kernel) : c(ctx), k(kernel) {
+me_ktimer::me_ktimer(me_ctx* ctx, int kernel, bool ext_launch) : c(ctx), k(kernel), ext(ext_launch) {
   if (c && (c->timing >> kernel & 1) && c->kt_seen[kernel]++ % c->timing_every == 0) {
     a = pool_get(c);
     b = pool_get(c);
-    if (a) hipEventRecord(a, c->stream);
+    if (!a || !b) a = b = nullptr;
+    if (a && !ext) hipEventRecord(a, c->stream);
   }
 }
 me_ktimer::~me_ktimer() {
   if (c && a && b) {
-    hipEventRecord(b, c->stream);
+    if (!ext) hipEventRecord(b, c->stream);
     c->pending.push_back({a, b, k});
   }
 }

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <numeric>
 #include <vector>
+#include <hip/hip_ext.h>
 #include "me_internal.hpp"
 #include "ba_kernels.hpp"
 #include "solve_diag.hpp"
@@ -2602,7 +2603,7 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   }
   {
     // point blocks + Schur partial tiles (BA_SCHUR family)
-    me_ktimer t(c, ME_KT_BA_SCHUR);
+    me_ktimer t(c, ME_KT_BA_SCHUR, true);  // (sampled launches take the timer's events)
     // NT = this wave's tile count, instantiated tight: an unused tile's
     // accumulator costs 8 VGPRs, and at 512 threads (2 waves per SIMD) the
     // budget is 256 registers -- up to 5 tiles nothing spills, 9 tiles (config
@@ -2614,11 +2615,14 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
 #define ME_SCHUR(N)                                                                                          \
   do {                                                                                                       \
     if (g.spts == kSchurPtsWide)                                                                             \
-      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsWide>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca); \
+      hipExtLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsWide>), grd, dim3(512), P.schur_lds, s, t.a, t.b, 0, g, \
+                            P.b, P.o, ca);                                                                   \
     else if (g.spts == kSchurPtsSmall)                                                                       \
-      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsSmall>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca); \
+      hipExtLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPtsSmall>), grd, dim3(512), P.schur_lds, s, t.a, t.b, 0, g, \
+                            P.b, P.o, ca);                                                                   \
     else                                                                                                     \
-      hipLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPts>), grd, dim3(512), P.schur_lds, s, g, P.b, P.o, ca);     \
+      hipExtLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPts>), grd, dim3(512), P.schur_lds, s, t.a, t.b, 0, g, P.b, \
+                            P.o, ca);                                                                        \
   } while (0)
     if (pw8 <= 3) ME_SCHUR(3);
     else if (pw8 <= 4) ME_SCHUR(4);

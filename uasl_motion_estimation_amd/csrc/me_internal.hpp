@@ -85,11 +85,15 @@ int me_pinned(me_ctx* ctx, size_t bytes, void** out);
 int me_check_launch(me_ctx* ctx, const char* what);
 
 // RAII event pair around one launch when timing is enabled.
+// Family timer around a launch.  ext: the launch itself takes the two events
+// (hipExtLaunchKernelGGL: the kernel's own begin / end timestamps, no marker
+// packets of their own on the stream); else they are recorded around it.
 struct me_ktimer {
   me_ctx* c;
   int k;
+  bool ext;
   hipEvent_t a = nullptr, b = nullptr;
-  me_ktimer(me_ctx* ctx, int kernel);
+  me_ktimer(me_ctx* ctx, int kernel, bool ext_launch = false);
   ~me_ktimer();
 };
 
