@@ -296,6 +296,23 @@ __device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected) {
   return slast != 0;
 }
 
+// The same with a written-through hand-off (the form of the camera solve's
+// workers): thread 0 stored the workgroup's partials with sc1 stores, drains
+// them before a relaxed arrival, and the last reads them with sc1 loads --
+// no L2 write-back (release) per arrival and no invalidate (acquire).
+__device__ __forceinline__ bool last_arrival_wt(unsigned* cnt, unsigned expected) {
+  __shared__ int slast;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    slast = k == expected - 1;
+    if (slast) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return slast != 0;
+}
+
 // Camera ci: lane u < 27 sums component u of the ck partials (fixed order)
 // -> raw U, column norms, raw gradient; unless sharded, the Jacobi scaling
 // (iteration 0) and the scaled blocks.  Called by every thread of a block.
@@ -1777,11 +1794,11 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
   __shared__ double lds[32];
   State* st = b.st;
   double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_step; i += blockDim.x) {
-    v[0] += b.part[R_MODEL * g.pstride + i];
-    v[1] += b.part[R_CAND * g.pstride + i];
-    v[2] += b.part[R_STEP2 * g.pstride + i];
-    v[3] += b.part[R_XN2 * g.pstride + i];
+  for (int i = threadIdx.x; i < g.nblk_step; i += blockDim.x) {  // (written through by pt_step's workgroups)
+    v[0] += a_ld<true>(&b.part[R_MODEL * g.pstride + i]);
+    v[1] += a_ld<true>(&b.part[R_CAND * g.pstride + i]);
+    v[2] += a_ld<true>(&b.part[R_STEP2 * g.pstride + i]);
+    v[3] += a_ld<true>(&b.part[R_XN2 * g.pstride + i]);
   }
   double out[4];
   block_sum<4>(v, out, lds);
@@ -1934,14 +1951,14 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   double v4[4] = {mc, cc, s2, xn2}, out[4];
   block_sum<4>(v4, out, lds);
   if (threadIdx.x == 0) {
-    b.part[R_MODEL * g.pstride + blockIdx.x] = out[0];
-    b.part[R_CAND * g.pstride + blockIdx.x] = out[1];
-    b.part[R_STEP2 * g.pstride + blockIdx.x] = out[2];
-    b.part[R_XN2 * g.pstride + blockIdx.x] = out[3];
+    a_st<true>(&b.part[R_MODEL * g.pstride + blockIdx.x], out[0]);
+    a_st<true>(&b.part[R_CAND * g.pstride + blockIdx.x], out[1]);
+    a_st<true>(&b.part[R_STEP2 * g.pstride + blockIdx.x], out[2]);
+    a_st<true>(&b.part[R_XN2 * g.pstride + blockIdx.x], out[3]);
   }
   // the last workgroup to finish reduces the partials (step_finalize) and,
   // single-GPU, runs the Ceres step handling
-  if (!last_arrival(b.cnt + g.m, gridDim.x)) return;
+  if (!last_arrival_wt(b.cnt + g.m, gridDim.x)) return;
   step_finalize_body(g, b, o, do_decide);
 }
 
