@@ -75,9 +75,9 @@ def parse():
                          "the Schur family's sampled launches carry the events themselves, hipExtLaunchKernelGGL: "
                          "the kernel's own begin/end timestamps; other families record two events around the "
                          "launch), every family, or none")
-    ap.add_argument("--timing-every", type=int, default=16,
+    ap.add_argument("--timing-every", type=int, default=8,
                     help="time every k-th launch of the timed family inside the timed region (HIP events; "
-                         "config 3: ~20 of the 330 Schur launches, the frame rate within 1 %% of --timing none)")
+                         "config 3: ~40 of the 330 Schur launches, the frame rate ~1.3 %% below --timing none)")
     ap.add_argument("--profile-steps", type=int, default=3,
                     help="untimed steps with every family timed, to pick the dominant family")
     return ap.parse_args()
