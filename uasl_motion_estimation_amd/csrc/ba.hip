@@ -209,6 +209,28 @@ __device__ __forceinline__ void huber(double s, double* rho0, double* sqrt_rho1)
   }
 }
 
+// Written-through hand-off helpers (see "Hand-off form" at the camera solve).
+template <bool SC1>
+__device__ __forceinline__ double a_ld(const double* p) {
+  if (!SC1) return *p;
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+template <bool SC1>
+__device__ __forceinline__ void a_st(double* p, double v) {
+  if (!SC1) {
+    *p = v;
+    return;
+  }
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_and_barrier() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
+  __syncthreads();
+}
+
+
 // ---------------------------------------------------------------- kernels
 constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups over the CUs
 
@@ -281,25 +303,11 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
 // contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
 // k + ck, ... of 256 slots of camera c into a partial; cam_reduce adds the ck
 // partials in order.
-// the last workgroup to arrive on a counter (release by every arrival,
-// acquire by the last); the last one re-arms the counter for the next launch
-__device__ __forceinline__ bool last_arrival(unsigned* cnt, unsigned expected) {
-  __shared__ int slast;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    slast = k == expected - 1;
-    if (slast) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (slast) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  return slast != 0;
-}
-
-// The same with a written-through hand-off (the form of the camera solve's
-// workers): thread 0 stored the workgroup's partials with sc1 stores, drains
-// them before a relaxed arrival, and the last reads them with sc1 loads --
-// no L2 write-back (release) per arrival and no invalidate (acquire).
+// The last workgroup to arrive on a counter, with a written-through hand-off
+// (the form of the camera solve's workers): thread 0 stored the workgroup's
+// partials with sc1 stores, drains them before a relaxed arrival, and the last
+// reads them with sc1 loads -- no L2 write-back (release) per arrival and no
+// invalidate (acquire).  The last one re-arms the counter for the next launch.
 __device__ __forceinline__ bool last_arrival_wt(unsigned* cnt, unsigned expected) {
   __shared__ int slast;
   __syncthreads();
@@ -324,7 +332,7 @@ __device__ void cam_reduce_body(const Geo& g, const Bufs& b, int sharded, const 
   const int u = threadIdx.x;
   if (u < 27) {
     double sum = 0.0;
-    for (int k = 0; k < g.ck; ++k) sum += cpart[27 * ((long)ci * g.ck + k) + u];
+    for (int k = 0; k < g.ck; ++k) sum += a_ld<true>(&cpart[27 * ((long)ci * g.ck + k) + u]);  // (written through)
     tot[u] = sum;
     if (u < 21) Uraw[21 * (long)ci + u] = sum;
     else gc_raw[6 * ci + u - 21] = sum;
@@ -376,11 +384,11 @@ __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, d
     for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
   double out[27];
   block_sum<27>(v, out, lds, kBlock / 64);
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // written through for the last of the camera's workgroups (no release per arrival)
     double* P = cpart + 27 * ((long)ci * g.ck + k);
-    for (int u = 0; u < 27; ++u) P[u] = out[u];
+    for (int u = 0; u < 27; ++u) a_st<true>(&P[u], out[u]);
   }
-  if (!last_arrival(b.cnt + ci, g.ck)) return;
+  if (!last_arrival_wt(b.cnt + ci, g.ck)) return;
   cam_reduce_body(g, b, sharded, cpart, colnorm, gc_raw, Uraw, ci);
 }
 
@@ -873,26 +881,6 @@ constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // lin_finalize_kernel instead (one launch less per iteration): the assembly
 // blocks do not read what it writes, and the camera solve that follows
 // reads both.
-template <bool SC1>
-__device__ __forceinline__ double a_ld(const double* p) {
-  if (!SC1) return *p;
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
-template <bool SC1>
-__device__ __forceinline__ void a_st(double* p, double v) {
-  if (!SC1) {
-    *p = v;
-    return;
-  }
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void drain_and_barrier() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
-  __syncthreads();
-}
-
 // Assembly of elements blk * EL .. blk * EL + EL - 1 by NTH = 8 EL threads
 // (8 partial groups of EL elements).  No early return: the fused form's
 // workgroup signals after every thread's stores have drained.  SC1: stores
