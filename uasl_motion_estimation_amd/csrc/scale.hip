@@ -273,6 +273,15 @@ __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int 
   return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN);
 }
 
+// Stores a later workgroup of the same launch reduces (residual rows, JJ / Je
+// terms, candidate sums) are written through (agent-scope relaxed atomic
+// store: the line goes to memory), so an arrival needs no release -- no L2
+// write-back per workgroup and phase beside the BA on the other CUs.
+__device__ __forceinline__ void wt_store(double* q, double v) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), __builtin_bit_cast(unsigned long long, v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // A4: compute_residuals, one track per 16-lane group
 __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHist<16>& h,
                                double* __restrict__ res, int* __restrict__ err) {
@@ -280,7 +289,7 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
   const uint8_t fl = td.flags[t];
   if (row < 0 || row >= a.nrows) return;
   if (!(fl & 2)) {  // an owned row stays 0 (the reference leaves it untouched)
-    if (h.gl == 0) res[row] = 0.0;
+    if (h.gl == 0) wt_store(&res[row], 0.0);
     return;
   }
   const bool left = t < a.nL;
@@ -290,12 +299,12 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
   if (left) project_left(a, track_X(td, a, t), p);
   else project_right<false, false>(a, track_X(td, a, t), p, nullptr);
   if (!(rect_contains(bx, by, bw, bh, p.lx, p.ly) && rect_contains(bx, by, bw, bh, p.rx, p.ry))) {
-    if (h.gl == 0) res[row] = 0.0;
+    if (h.gl == 0) wt_store(&res[row], 0.0);
     return;
   }
   int lx = roi_corner(p.lx, w), ly = roi_corner(p.ly, w), rx = roi_corner(p.rx, w), ry = roi_corner(p.ry, w);
   if (!roi_in(a, lx, ly, P) || !roi_in(a, rx, ry, P)) {
-    if (h.gl == 0) res[row] = 0.0;
+    if (h.gl == 0) wt_store(&res[row], 0.0);
     atomicOr(err, 1);
     return;
   }
@@ -316,7 +325,7 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
     mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN);
 #endif
   }
-  if (h.gl == 0) res[row] = (double)mi * wv;
+  if (h.gl == 0) wt_store(&res[row], (double)mi * wv);
 }
 
 __global__ __launch_bounds__(kScBlock) void scale_residual_kernel(ScaleArgs a, TrackDev td, double* __restrict__ res,
@@ -333,8 +342,8 @@ __device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHi
                           const double* __restrict__ res, double* __restrict__ jj, double* __restrict__ je,
                           int* __restrict__ err) {
   if (h.gl == 0) {
-    jj[t] = 0.0;
-    je[t] = 0.0;
+    wt_store(&jj[t], 0.0);
+    wt_store(&je[t], 0.0);
   }
   const int row = td.row[t];
   const uint8_t fl = td.flags[t];
@@ -370,11 +379,11 @@ __device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHi
   double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN);
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) {
-    jj[t] = J * J * wv;
+    wt_store(&jj[t], J * J * wv);
     // coherent load: in the persistent LM the row may have been written by
     // another workgroup in the previous phase (no kernel boundary between)
-    je[t] = J * __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(res + row),
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    wt_store(&je[t], J * __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(res + row),
+                                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
   }
 }
 
@@ -764,11 +773,15 @@ __device__ void scale_ctrl_run(ScaleLM* lm_g, ScaleSpec* __restrict__ sp, const 
 // launch per LM phase instead of two; a launch whose phase is not the current
 // one returns at once (every workgroup reads the phase before the last one can
 // change it).
+// (Arrival: the workgroup's written-through stores are drained by every wave
+// before the barrier, then a relaxed add -- no release, i.e. no L2 write-back
+// per workgroup; the last one's acquire still precedes its reads.)
 __device__ __forceinline__ bool last_block_arrives(unsigned* cnt, unsigned target) {
   __shared__ int slast;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     slast = k == target - 1;
   }
   __syncthreads();
@@ -808,7 +821,7 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
   block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
   if (threadIdx.x == 0) __hip_atomic_store(cnt + 1 + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (phase == PH_C) {
-    if (threadIdx.x == 0) sp->e2[j] = sx;
+    if (threadIdx.x == 0) wt_store(&sp->e2[j], sx);
     if (!last_block_arrives(cnt, ncand)) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (threadIdx.x == 0) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -969,7 +982,7 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
           block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
           if (threadIdx.x == 0) {
             __hip_atomic_store(cnt + 1 + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sp->e2[j] = sx;
+            wt_store(&sp->e2[j], sx);
           }
           if (last_block_arrives(cnt, (unsigned)n)) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
