@@ -547,21 +547,41 @@ def stereo_vo_line(ctx, n: int, reps: int = 5, cpu: bool = True):
     return out
 
 
+def _shard_parity(cams, pts, lo, hi, s_sh, ref_cams, ref_pts, s_ref):
+    """Sharded vs single-device solve of the same window: max relative
+    difference of cameras and of this rank's landmarks, equal iteration and
+    successful-step counts (tolerance 1e-6, the north-star pose bar)."""
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        return float(np.max(np.abs(a - b) / (np.abs(b) + 1e-9))) if a.size else 0.0
+
+    return {"cams_max_rel": rel(cams, ref_cams), "pts_max_rel": rel(pts, ref_pts[lo:hi]),
+            "same_iterations": s_sh["iterations"] == s_ref["iterations"]
+            and s_sh["successful_steps"] == s_ref["successful_steps"]}
+
+
+def _parity_ok(p):
+    return bool(p["same_iterations"] and p["cams_max_rel"] <= 1e-6 and p["pts_max_rel"] <= 1e-6)
+
+
 def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     """Config-4 window (8000 landmarks x 30 keyframes, args.ba_iters LM
-    iterations) solved (a) unsharded on this GPU and (b) landmark-sharded: over
-    RCCL across the world's ranks (one GPU each, torch.distributed all-reduce of
-    S, b and the LM scalars on device buffers) or, at N = 1, over two contexts
-    of this GPU with a host exchange.  Every shard is resident in HBM (reset by
-    a device copy); timing: barrier + MAX over ranks."""
+    iterations) solved (a) unsharded on this GPU and (b) landmark-sharded with
+    the library's communicator (me_ba_solve_comm: one packed all-reduce after
+    the Schur pass and one of the step scalars per LM iteration): native RCCL
+    across the world's ranks (one GPU each), or, at N = 1, RCCL at one rank
+    (the exchange's own overhead) and two contexts of this GPU with a
+    host-staged thread exchange.  Every mode is checked against the
+    single-device solve of the same window (parity).  Shards are resident in
+    HBM (reset by a device copy); timing: barrier + MAX over ranks."""
     import threading
 
     import torch
 
     from uasl_motion_estimation_amd import synthetic as S
     from uasl_motion_estimation_amd._lib import Context
-    from uasl_motion_estimation_amd.optimisation import (DeviceBAProblem, SolverOptions, ThreadAllReduce,
-                                                         shard_landmarks, torch_allreduce)
+    from uasl_motion_estimation_amd.optimisation import (Comm, DeviceBAProblem, SolverOptions, ThreadAllReduce,
+                                                         rccl_comm, shard_landmarks)
 
     c = S.CONFIGS[4]
     bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
@@ -575,49 +595,77 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
         full.reset()
         s1 = full.solve(opts)
     t_single = (time.perf_counter() - t0) / reps
+    ref_cams, ref_pts = full.download()
     full.close()
     out = {"workload": f"config 4 BA: {len(bp.pts)} landmarks x {len(bp.cams)} keyframes, {len(bp.obs)} observations, "
                        f"{args.ba_iters} LM iterations", "single_gpu_ms": round(1e3 * t_single, 3),
-           "single_gpu_ba_iter_per_s": round(s1["iterations"] / t_single, 1)}
+           "single_gpu_ba_iter_per_s": round(s1["iterations"] / t_single, 1),
+           "exchanges_per_lm_iteration": 2}
+
+    def timed_comm(d, comm):
+        d.reset()
+        d.solve_comm(comm, opts)
+        barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            d.reset()
+            ss = d.solve_comm(comm, opts)
+        ctx.synchronize()
+        return (time.perf_counter() - t0) / reps, ss
+
     if dist is not None:
         local, (lo, hi) = shard_landmarks(bp, rank, world)
         d = DeviceBAProblem(local, ctx)
-        ar = torch_allreduce()
-        stream = torch.cuda.Stream()  # kernels and RCCL ordered on one (non-default) stream
-        with torch.cuda.stream(stream):
-            ctx.set_stream(stream.cuda_stream)
-            try:
-                d.solve_sharded(ar, opts)
-                barrier()
-                torch.cuda.synchronize()
-                t0 = time.perf_counter()
-                for _ in range(reps):
-                    d.reset()
-                    ss = d.solve_sharded(ar, opts)
-                torch.cuda.synchronize()
-                el = (time.perf_counter() - t0) / reps
-            finally:
-                ctx.set_stream(None)
+        comm = rccl_comm(ctx)
+        el, ss = timed_comm(d, comm)
+        cams, pts = d.download()
+        comm.close()
         d.close()
-        tt = torch.tensor([el], device=f"cuda:{local_rank}", dtype=torch.float64)
+        par = _shard_parity(cams, pts, lo, hi, ss, ref_cams, ref_pts, s1)
+        tt = torch.tensor([el, par["cams_max_rel"], par["pts_max_rel"], 0.0 if par["same_iterations"] else 1.0],
+                          device=f"cuda:{local_rank}", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-        out.update({"mode": f"landmark-sharded over {dist.get_backend()} (RCCL), {dist.get_world_size()} ranks, "
-                            f"one GPU each", "ranks": dist.get_world_size(), "sharded_ms": round(1e3 * el, 3),
+        el = float(tt[0].item())
+        par = {"cams_max_rel": float("%.3g" % tt[1].item()), "pts_max_rel": float("%.3g" % tt[2].item()),
+               "same_iterations": tt[3].item() == 0.0}
+        par["ok"] = _parity_ok(par)
+        out.update({"mode": f"landmark-sharded over native RCCL (me_comm), {world} ranks, one GPU each",
+                    "ranks": world, "sharded_ms": round(1e3 * el, 3),
                     "sharded_ba_iter_per_s": round(ss["iterations"] / el, 1),
-                    "speedup_vs_single_gpu": round(t_single / el, 3), "landmarks_rank0": hi - lo if rank == 0 else None})
+                    "speedup_vs_single_gpu": round(t_single / el, 3), "landmarks_rank0": hi - lo if rank == 0 else None,
+                    "parity_vs_single_gpu": par})
         return out
-    # N = 1: two contexts on this GPU, threads + host exchange (the crossover point)
+    # N = 1 (a) native RCCL at one rank: the exchange's overhead on the same window
+    try:
+        comm = Comm.rccl(ctx, 1, 0, Comm.unique_id())
+        d = DeviceBAProblem(bp, ctx)
+        el1, ss1 = timed_comm(d, comm)
+        cams, pts = d.download()
+        d.close()
+        comm.close()
+        par = _shard_parity(cams, pts, 0, len(bp.pts), ss1, ref_cams, ref_pts, s1)
+        par = {k: (float("%.3g" % v) if isinstance(v, float) else v) for k, v in par.items()}
+        par["ok"] = _parity_ok(par)
+        out["rccl_1rank"] = {"ms": round(1e3 * el1, 3), "overhead_vs_single_gpu": round(el1 / t_single - 1.0, 4),
+                             "parity_vs_single_gpu": par}
+    except Exception as e:  # reported, never fatal
+        out["rccl_1rank"] = {"error": f"{type(e).__name__}: {e}"}
+    # (b) two contexts on this GPU, threads + host exchange (the crossover point)
     ranks = 2
     ctxs = [Context(local_rank) for _ in range(ranks)]
-    shards = [DeviceBAProblem(shard_landmarks(bp, r, ranks)[0], ctxs[r]) for r in range(ranks)]
+    parts = [shard_landmarks(bp, r, ranks) for r in range(ranks)]
+    shards = [DeviceBAProblem(parts[r][0], ctxs[r]) for r in range(ranks)]
     res, errs = [None] * ranks, []
 
     def run(r, ar):
         try:
+            comm = Comm.callback(ctxs[r], ranks, r, ar.callback(r, ctxs[r]))
             for _ in range(reps):
                 shards[r].reset()
-                res[r] = shards[r].solve_sharded(ar.callback(r, ctxs[r]), opts)
+                res[r] = shards[r].solve_comm(comm, opts)
+            ctxs[r].synchronize()
+            comm.close()
         except Exception as e:  # pragma: no cover
             errs.append(e)
 
@@ -633,15 +681,25 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
 
     timed()
     el = timed()
+    pars = []
+    for r in range(ranks):
+        cams, pts = shards[r].download()
+        lo, hi = parts[r][1]
+        pars.append(_shard_parity(cams, pts, lo, hi, res[r], ref_cams, ref_pts, s1))
     for sh in shards:
         sh.close()
     for cc in ctxs:
         cc.close()
     if errs:
         raise errs[0]
-    out.update({"mode": "landmark-sharded over 2 contexts of one GPU (threads, host-staged exchange)", "ranks": ranks,
+    par = {"cams_max_rel": float("%.3g" % max(p["cams_max_rel"] for p in pars)),
+           "pts_max_rel": float("%.3g" % max(p["pts_max_rel"] for p in pars)),
+           "same_iterations": all(p["same_iterations"] for p in pars)}
+    par["ok"] = _parity_ok(par)
+    out.update({"mode": "landmark-sharded over 2 contexts of one GPU (threads, host-staged exchange through "
+                        "me_comm_create_callback)", "ranks": ranks,
                 "sharded_ms": round(1e3 * el, 3), "sharded_ba_iter_per_s": round(res[0]["iterations"] / el, 1),
-                "speedup_vs_single_gpu": round(t_single / el, 3)})
+                "speedup_vs_single_gpu": round(t_single / el, 3), "parity_vs_single_gpu": par})
     return out
 
 

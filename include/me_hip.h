@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define ME_ABI_VERSION 2
+#define ME_ABI_VERSION 3
 
 enum {
   ME_OK = 0,
@@ -269,12 +269,43 @@ int me_ba_reduced_system(me_ctx* ctx, const me_ba_problem* p, double radius, dou
    positive definite (Ceres reports a rank-deficient Jacobian). */
 int me_ba_covariance(me_ctx* ctx, const me_ba_problem* p, double* cov /* n_cams*36 */, int* ok);
 
-/* Landmark-sharded solve: this rank holds all cameras and a
-   subset of the points with their observations.  At each exchange point the
-   solver calls allreduce(dev_ptr, n_doubles, user) which must sum the device
-   buffer over ranks in place (e.g. RCCL all_reduce through torch.distributed)
-   on the ctx stream. */
+/* ---- §8e: landmark-sharded BA over several GPUs ----------------------
+ * No reference counterpart (the reference solves on one CPU thread); the
+ * sharded solve replaces BundleAdjuster<4>::optimise (BundleAdjuster.h:431-476)
+ * when the window's landmarks are split over ranks: every rank holds all
+ * cameras and a contiguous landmark range with its observations.
+ *
+ * A communicator joins the ranks, one process (one me_ctx) per GPU:
+ *  - me_comm_create_rccl: native RCCL over xGMI.  Rank 0 draws an id with
+ *    me_comm_unique_id and hands the ME_COMM_ID_BYTES bytes to the other
+ *    ranks (any side channel: a torch.distributed store, a file, MPI); every
+ *    rank then creates its communicator on its ctx device (collective call).
+ *    All-reduces are enqueued on the ctx stream: no host round trip.
+ *  - me_comm_create_callback: a caller all-reduce (allreduce(dev_ptr, n, user)
+ *    sums n doubles in place over the ranks, n < 0: max over |n|; it must be
+ *    ordered on the ctx stream, e.g. host-staged gloo, or threads driving
+ *    several contexts of one GPU).
+ * Per LM iteration the sharded solve exchanges twice: one sum of the packed
+ * reduced camera system [S upper block triangle | b | diag(U) | camera
+ * gradient | cost | failure count | per-rank gradient max-norm slots] after
+ * the Schur pass, and one sum of the five step scalars after the point step;
+ * the first linearisation also sums the Jacobi column norms.  Every rank
+ * solves the camera system redundantly and steps its own landmarks. */
 typedef int (*me_allreduce_fn)(double* dev_buf, int n, void* user);
+typedef struct me_comm me_comm;
+#define ME_COMM_ID_BYTES 128
+enum { ME_COMM_SUM = 0, ME_COMM_MAX = 1 };
+int me_comm_unique_id(void* id_out, int id_bytes);
+int me_comm_create_rccl(me_ctx* ctx, int world, int rank, const void* id, me_comm** out);
+int me_comm_create_callback(me_ctx* ctx, int world, int rank, me_allreduce_fn allreduce, void* user,
+                            me_comm** out);
+void me_comm_destroy(me_comm* comm);
+int me_comm_info(const me_comm* comm, int* world, int* rank, int* native);
+/* In-place all-reduce of n doubles of device memory on the ctx stream. */
+int me_comm_allreduce(me_comm* comm, double* dev_buf, long n, int op);
+int me_ba_solve_comm(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_comm* comm, me_ba_summary* s);
+/* The same with a bare callback and no rank information (ABI v2 form): the
+   gradient max-norm then travels in a separate max all-reduce. */
 int me_ba_solve_sharded(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn allreduce,
                         void* user, me_ba_summary* s);
 

@@ -162,3 +162,150 @@ def test_ba_solve_distributed_world2_on_device0(tmp_path, oracle):
         np.testing.assert_allclose(d["cams"], rc, rtol=1e-6, atol=1e-9)
         pts[int(d["lo"]):int(d["hi"])] = d["pts"]
     np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
+
+
+# ------------------------------------------------------------------ me_comm (ABI v3)
+def _two_ctx_comm_solve(bp, opts, world=2, device=0):
+    """Landmark-sharded solve over `world` contexts of one device through
+    me_comm_create_callback (threads + host exchange): returns the gathered
+    cameras per rank, the assembled points and the summaries."""
+    from uasl_motion_estimation_amd._lib import Context
+    from uasl_motion_estimation_amd.optimisation import Comm, ThreadAllReduce, ba_solve_comm
+
+    ar = ThreadAllReduce(world)
+    ctxs = [Context(device) for _ in range(world)]
+    res, errs = [None] * world, []
+
+    def run(r):
+        try:
+            local, rng = shard_landmarks(bp, r, world)
+            comm = Comm.callback(ctxs[r], world, r, ar.callback(r, ctxs[r]))
+            res[r] = (ba_solve_comm(local, comm, opts, ctx=ctxs[r]), rng)
+            comm.close()
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+            ar.barrier.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    for c in ctxs:
+        c.close()
+    assert not errs, errs
+    pts = np.full_like(np.asarray(bp.pts, np.float64), np.nan)
+    cams, summ = [], []
+    for r in range(world):
+        (c, p, s), (lo, hi) = res[r]
+        cams.append(c)
+        summ.append(s)
+        pts[lo:hi] = p
+    return cams, pts, summ
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jacobi", [True, False])
+def test_gpu_comm_sharded_solve_matches_single_device(ctx, jacobi):
+    """me_ba_solve_comm over a 2-rank callback communicator (packed exchange:
+    one all-reduce after the Schur pass, one after the step) = the unsharded
+    device solve."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    bp = _problem()
+    opts = SolverOptions.fixed_iterations(8)
+    opts.jacobi_scaling = jacobi
+    ref_c, ref_p, ref_s = ba_solve(bp.copy(), opts, ctx=ctx)
+    cams, pts, summ = _two_ctx_comm_solve(bp, opts)
+    for c, s in zip(cams, summ):
+        np.testing.assert_allclose(c, ref_c, rtol=1e-6, atol=1e-9)
+        assert (s["iterations"], s["successful_steps"]) == (ref_s["iterations"], ref_s["successful_steps"])
+        assert s["final_cost"] == pytest.approx(ref_s["final_cost"], rel=1e-9)
+    np.testing.assert_allclose(pts, ref_p, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_comm_sharded_config4_8000x30_matches_single_and_oracle(ctx, oracle):
+    """Config 4 (8000 landmarks x 30 keyframes, 10 fixed LM iterations),
+    landmark-sharded over 2 contexts of one GPU: same iterations and
+    successful steps as the unsharded device solve and the oracle, cameras
+    and points within 1e-6 of both."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    c = S.CONFIGS[4]
+    bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
+    assert len(bp.pts) == 8000 and len(bp.cams) == 30
+    opts = SolverOptions.fixed_iterations(10)
+    ref_c, ref_p, ref_s = ba_solve(bp.copy(), opts, ctx=ctx)
+    oc, op, os_ = oracle.ba_solve(bp, max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                                  parameter_tolerance=0.0)
+    cams, pts, summ = _two_ctx_comm_solve(bp, opts)
+    for cm, s in zip(cams, summ):
+        for rc, rs in ((ref_c, ref_s), (oc, os_)):
+            np.testing.assert_allclose(cm, rc, rtol=1e-6, atol=1e-9)
+            assert (s["iterations"], s["successful_steps"]) == (rs["iterations"], rs["successful_steps"])
+    np.testing.assert_allclose(pts, ref_p, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, op, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,iters", [(3, 10), (4, 4)])
+def test_gpu_rccl_one_rank_bit_identical_to_single_device(ctx, cfg, iters):
+    """Native RCCL communicator at one rank (me_comm_create_rccl): the packed
+    exchange reduces in the single-device order, so the sharded solve equals
+    me_ba_solve bit for bit."""
+    from uasl_motion_estimation_amd.optimisation import Comm, SolverOptions, ba_solve, ba_solve_comm
+
+    c = S.CONFIGS[cfg]
+    bp = S.ba_problem(S.SEED0 + cfg, c["n_feats"], c["window"], c["width"], c["height"])
+    opts = SolverOptions.fixed_iterations(iters)
+    ref_c, ref_p, ref_s = ba_solve(bp.copy(), opts, ctx=ctx)
+    comm = Comm.rccl(ctx, 1, 0, Comm.unique_id())
+    try:
+        assert comm.info() == {"world": 1, "rank": 0, "native": True}
+        cams, pts, s = ba_solve_comm(bp.copy(), comm, opts, ctx=ctx)
+    finally:
+        comm.close()
+    assert np.array_equal(cams, ref_c) and np.array_equal(pts, ref_p)
+    assert (s["iterations"], s["successful_steps"], s["final_cost"]) == \
+        (ref_s["iterations"], ref_s["successful_steps"], ref_s["final_cost"])
+
+
+@pytest.mark.gpu
+def test_gpu_comm_allreduce_native_and_callback(ctx):
+    from uasl_motion_estimation_amd.optimisation import Comm
+
+    x = np.arange(1, 1001, dtype=np.float64) * 0.5
+    d = ctx.malloc(x.nbytes)
+    try:
+        ctx.h2d(d, x)
+        comm = Comm.rccl(ctx, 1, 0, Comm.unique_id())
+        comm.allreduce(d, len(x))
+        comm.allreduce(d, len(x), "max")
+        comm.close()
+        y = np.zeros_like(x)
+        ctx.d2h(y, d)
+        assert np.array_equal(x, y)  # one rank: identity
+        seen = []
+        cb = Comm.callback(ctx, 3, 1, lambda ptr, n: seen.append((ptr, n)))
+        cb.allreduce(d, 7)
+        cb.allreduce(d, 5, "max")
+        assert seen == [(d, 7), (d, -5)] and cb.info() == {"world": 3, "rank": 1, "native": False}
+        cb.close()
+    finally:
+        ctx.free(d)
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_infeasible_shard_fails_every_rank(ctx):
+    """A starting point outside the box bounds in ONE shard: every rank ends
+    the solve as FAILURE (the input flags ride in the first exchange), none
+    waits for an exchange the other skipped."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions
+
+    bp = _problem()
+    bp.pts = np.array(bp.pts, np.float64, copy=True)
+    bp.pts[-1, 2] = -5.0  # behind the camera: Z < Zmin, in the last rank's range
+    cams, pts, summ = _two_ctx_comm_solve(bp, SolverOptions.fixed_iterations(4))
+    for s in summ:
+        assert s["status"] == 3 and s["iterations"] == 0

@@ -404,10 +404,32 @@ struct CamArgs {
   int on;
 };
 
+// Sharded mode, first linearisation: the rank's input flags (bad index,
+// infeasible start) ride behind the column norms in the first exchange, so
+// every rank ends the solve alike (each rank only checks its own landmarks).
+__global__ void xch_flags_kernel(Geo g, Bufs b, double* colnorm) {
+  colnorm[g.n6] = b.st->bad_input ? 1.0 : 0.0;
+  colnorm[g.n6 + 1] = b.st->infeasible ? 1.0 : 0.0;
+}
+
 // Sharded mode: scaling from the all-reduced column norms, then scale the
 // (local) U / g blocks.
-__global__ void cam_finish_kernel(Geo g, Bufs b, const double* colnorm, const double* gc_raw, const double* Uraw) {
-  const State* st = b.st;
+__global__ void cam_finish_kernel(Geo g, Bufs b, const double* colnorm, const double* gc_raw, const double* Uraw,
+                                  int first) {
+  State* st = b.st;
+  if (first) {  // (colnorm[n6 ..] = the all-reduced input flags; read before any thread returns)
+    const bool bad = colnorm[g.n6] != 0.0, infeasible = colnorm[g.n6 + 1] != 0.0;
+    __syncthreads();
+    if (bad || infeasible) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->bad_input = bad;
+        st->infeasible = infeasible;
+        st->done = 1;
+        st->termination = 2;
+      }
+      return;
+    }
+  }
   if (st->done || !st->need_lin) return;
   const int ci = blockIdx.x * blockDim.x + threadIdx.x;
   if (ci >= g.m) return;
@@ -797,24 +819,36 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
 // Linearisation bookkeeping + iteration start: reduce the cost / gradient
 // partials (fixed order), Ceres gradient-tolerance test (IterationZero /
 // HandleSuccessfulStep), max-iteration and min-radius tests.
+// The cost partials are summed by the first kFinBlock threads in the same
+// order whatever the block size (256 in s_assemble_kernel, 512 inside the
+// camera-solve launch): the same x_cost bits either way.  Sharded (b.xch):
+// cost, camera gradient and the per-rank gradient max-norms come from the
+// all-reduced exchange.
 constexpr int kFinBlock = 256;
-__device__ void lin_finalize_body(const Geo& g, const Bufs& b, const Opts& o, const double* gc_raw, int use_scal,
+__device__ void lin_finalize_body(const Geo& g, const Bufs& b, const Opts& o, const double* gc_raw,
                                   double* lds /* 16 */) {
   State* st = b.st;
   if (st->done) return;
   if (st->need_lin) {
+    const bool x = b.xch != nullptr;
+    const int t = threadIdx.x;
+    const bool in = t < kFinBlock;
     double c = 0, m = 0;
-    if (!use_scal) {
-      for (int i = threadIdx.x; i < g.nblk_lin; i += blockDim.x) c += b.part[R_COST * g.pstride + i];
-      for (int i = threadIdx.x; i < g.ksplit; i += blockDim.x) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
+    if (!x && in) {
+      for (int i = t; i < g.nblk_lin; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
+      for (int i = t; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
     }
-    for (int i = threadIdx.x; i < g.n6; i += blockDim.x) m = fmax(m, fabs(gc_raw[i]));
+    const double* gcv = x ? b.xch + xo_gc(g) : gc_raw;
+    if (in)
+      for (int i = t; i < g.n6; i += kFinBlock) m = fmax(m, fabs(gcv[i]));
+    if (x && in)
+      for (int i = t; i < g.xslots; i += kFinBlock) m = fmax(m, b.xch[xo_gmax(g) + i]);
     double v[1] = {c}, out[1];
-    block_sum<1>(v, out, lds);
+    block_sum<1>(v, out, lds, kFinBlock / 64);
     const double mm = block_max(m, lds + 8);
     if (threadIdx.x == 0) {
-      st->x_cost = use_scal ? b.scal[R_COST] : out[0];
-      const double gm = use_scal ? fmax(mm, b.scal[R_GMAX_PT]) : mm;
+      st->x_cost = x ? b.xch[xo_cost(g)] : out[0];
+      const double gm = mm;
       if (!st->scaled) {
         st->initial_cost = st->x_cost;
         st->scaled = 1;
@@ -841,28 +875,32 @@ __device__ void lin_finalize_body(const Geo& g, const Bufs& b, const Opts& o, co
   st->iterations += 1;
 }
 
-__global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, Opts o, const double* gc_raw,
-                                                                 int use_scal) {
+__global__ __launch_bounds__(kFinBlock) void lin_finalize_kernel(Geo g, Bufs b, Opts o, const double* gc_raw) {
   __shared__ double lds[16];
-  lin_finalize_body(g, b, o, gc_raw, use_scal, lds);
+  lin_finalize_body(g, b, o, gc_raw, lds);
 }
 
-// Sharded mode: local partial sums into scal (all-reduced by the host callback)
-__global__ __launch_bounds__(kFinBlock) void lin_partials_kernel(Geo g, Bufs b) {
-  __shared__ double lds[16];
+// Sharded mode: this rank's linearisation scalars into the exchange tail --
+// cost (fixed-order sum of the linearize partials), failure flag, gradient
+// max-norm in this rank's slot (0 in the others), raw camera gradient.
+__device__ void xch_tail_body(const Geo& g, const Bufs& b, const double* gc_raw, double* lds /* 16 */) {
   const State* st = b.st;
-  if (st->done) return;
   double c = 0, m = 0;
   if (st->need_lin) {
     for (int i = threadIdx.x; i < g.nblk_lin; i += kFinBlock) c += b.part[R_COST * g.pstride + i];
     for (int i = threadIdx.x; i < g.ksplit; i += kFinBlock) m = fmax(m, b.part[R_GMAX_PT * g.pstride + i]);
   }
+  double* x = b.xch;
+  for (int i = threadIdx.x; i < g.n6; i += kFinBlock) x[xo_gc(g) + i] = gc_raw[i];
+  for (int i = threadIdx.x; i < g.xslots; i += kFinBlock)
+    if (i != g.xrank) x[xo_gmax(g) + i] = 0.0;
   double v[1] = {c}, out[1];
   block_sum<1>(v, out, lds);
   const double mm = block_max(m, lds + 8);
   if (threadIdx.x == 0) {
-    b.scal[R_COST] = out[0];
-    b.scal[R_GMAX_PT] = mm;
+    x[xo_cost(g)] = out[0];
+    x[xo_fail(g)] = st->fail ? 1.0 : 0.0;
+    x[xo_gmax(g) + g.xrank] = mm;
   }
 }
 
@@ -885,8 +923,13 @@ constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // (8 partial groups of EL elements).  No early return: the fused form's
 // workgroup signals after every thread's stores have drained.  SC1: stores
 // written through for a consumer workgroup of the same launch.
+// mode (sharded runs): SA_PACK sums this rank's partials and U
+// into the exchange buffer in the tile layout (element idx of [S | b] at
+// xch[idx], diag(U) in the tail) instead of S; SA_UNPACK reads the all-reduced
+// exchange (no partials, no U) and stores S / b / diag(U) exactly as SA_SUM.
+enum { SA_SUM = 0, SA_PACK = 1, SA_UNPACK = 2 };
 template <int NTH, bool SC1>
-__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full) {
+__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, int mode = SA_SUM) {
   constexpr int EL = NTH / kSaGroups;
   __shared__ double part[kSaGroups][EL];
   const State* st = b.st;
@@ -909,9 +952,9 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full) 
   }
   // S entries (gr, gc < n) and the right-hand side (gc == n); the padding is skipped
   const bool use = live && gr >= 0 && gr < n && gc <= n;
-  const bool fail = st->fail;
+  const bool fail = st->fail || (mode == SA_UNPACK && b.xch[xo_fail(g)] != 0.0);  // (unpack: any rank's failure)
   double acc = 0.0;
-  if (use && !fail) {
+  if (use && !fail && mode != SA_UNPACK) {
     // partials grp, grp + 8, ... added in order; their loads issued 8 at a
     // time (independent addresses: one memory latency per batch, not per add)
     const double* src = b.Spart + idx;
@@ -935,37 +978,63 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full) 
   __syncthreads();
   if (grp == 0 && use) {
     double sum = 0.0;
+    if (mode == SA_UNPACK) {
+      sum = b.xch[idx];
+    } else {
 #pragma unroll
-    for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
+      for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
+    }
     if (gc < n) {
       double v = 0;
-      if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];  // U blocks are symmetric
-      v = fail ? 0.0 : v - sum;
-      if (diag) {
+      if (mode == SA_UNPACK) {
+        v = fail ? 0.0 : sum;
+      } else {
+        if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];  // U blocks are symmetric
+        v = fail ? 0.0 : v - sum;
+      }
+      if (mode == SA_PACK) {
+        b.xch[idx] = v;
+      } else if (diag) {
         a_st<SC1>(&b.S[(long)gr * n + gc], v);
       } else {
         a_st<SC1>(&b.S[(long)gc * n + gr], v);
         if (full) b.S[(long)gr * n + gc] = v;
       }
     } else {
-      a_st<SC1>(&b.bvec[gr], fail ? 0.0 : b.gcs[gr] - sum);
-      a_st<SC1>(&b.diagU[gr], b.U[36 * (gr / 6) + (gr % 6) * 7]);
+      const double bv = fail ? 0.0 : mode == SA_UNPACK ? sum : b.gcs[gr] - sum;
+      const double du = mode == SA_UNPACK ? b.xch[xo_diag(g) + gr] : b.U[36 * (gr / 6) + (gr % 6) * 7];
+      if (mode == SA_PACK) {
+        b.xch[idx] = bv;
+        b.xch[xo_diag(g) + gr] = du;
+      } else {
+        a_st<SC1>(&b.bvec[gr], bv);
+        a_st<SC1>(&b.diagU[gr], du);
+      }
     }
+  } else if (mode == SA_PACK && grp == 0 && idx < g.npairs * 256) {
+    b.xch[idx] = 0.0;  // padding (and a finished solve): defined values in the exchange
   }
 }
 
-__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int use_scal,
-                                                            int full) {
+// mode SA_PACK (sharded, before the exchange): the last workgroup writes the
+// exchange tail instead of finalizing; SA_UNPACK (sharded, after it, when
+// the camera solve does not unpack itself): as SA_SUM from the exchange.
+__global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int full,
+                                                            int mode) {
   static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
   if (blockIdx.x == gridDim.x - 1) {
     __shared__ double lds[16];
+    if (mode == SA_PACK) {
+      xch_tail_body(g, b, gc_raw, lds);
+      return;
+    }
     if (threadIdx.x < 2) b.ssync[threadIdx.x] = 0u;  // the camera solve that follows starts its steps at 0
-    lin_finalize_body(g, b, o, gc_raw, use_scal, lds);
+    lin_finalize_body(g, b, o, gc_raw, lds);
     return;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && !(b.st->done || b.st->final_pass))
-    b.scal[R_COUNT] = b.st->fail ? 1.0 : 0.0;  // failure flag travels with the all-reduce
-  s_assemble_body<kBlock, false>(g, b, blockIdx.x, full);
+  if (mode != SA_PACK && blockIdx.x == 0 && threadIdx.x == 0 && !(b.st->done || b.st->final_pass))
+    b.scal[R_COUNT] = (b.st->fail || (mode == SA_UNPACK && b.xch[xo_fail(g)] != 0.0)) ? 1.0 : 0.0;
+  s_assemble_body<kBlock, false>(g, b, blockIdx.x, full, mode);
 }
 
 // One workgroup: S (assembled by s_assemble_kernel, all-reduced in sharded
@@ -1307,6 +1376,7 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
         __builtin_amdgcn_s_sleep(2);
       }
       sep = k == kSolveSpin ? kSolveTerm : e;
+      if (k == kSolveSpin) b.st->spin_err = 1;  // block 0 never published the step: the solve ends in error
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
     __syncthreads();
@@ -1362,7 +1432,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   }
   unsigned* asm_cnt = b.cnt + g.m + 3;
   if (kMode != 2 && nasm > 0 && blockIdx.x > 0) {
-    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0);
+    // (sharded: the assemblers unpack the all-reduced exchange instead of summing partials)
+    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM);
     drain_and_barrier();  // every wave's written-through stores have left
     if (threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1370,18 +1441,26 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   State* st = b.st;
   const bool fused = kMode != 2 && nasm > 0;
   if (fused) {
-    lin_finalize_body(g, b, o, gc_raw, 0, red);
+    lin_finalize_body(g, b, o, gc_raw, red);
     if (threadIdx.x == 0) {
       const int live = !st->done;
-      b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;  // (what s_assemble's first block wrote; read by decide)
+      // (what s_assemble's first block writes in the unfused form; read by decide)
+      b.scal[R_COUNT] = (st->fail || (b.xch && b.xch[xo_fail(g)] != 0.0)) ? 1.0 : 0.0;
       long k = 0;
       if (live) {
         for (; k < kSolveSpin; ++k) {
           if (__hip_atomic_load(asm_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nasm) break;
           __builtin_amdgcn_s_sleep(1);
         }
-        if (k == kSolveSpin) st->fail = 1;  // a missing assembler: a failed step, never a hang
-        __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
+        if (k == kSolveSpin) {
+          // a missing assembler: the solve ends in error (a late one may still
+          // arrive, so the counter is not re-armed: the next plan clears it)
+          st->spin_err = 1;
+          st->done = 1;
+          st->termination = 2;
+        } else {
+          __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
@@ -1398,7 +1477,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
-  const int fail_in = st->fail || (!fused && b.scal[R_COUNT] != 0.0);
+  const int fail_in = st->fail || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0);
   const double radius = st->radius;
   // the candidate-camera inputs (current cameras, Jacobi scales) are requested
   // now; they are consumed after the factorisation, which hides their latency
@@ -1508,7 +1587,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     auto lds_wait = [&](volatile unsigned* f, unsigned want) {
       long k = 0;
       for (; k < kSolveSpin && *f < want; ++k) __builtin_amdgcn_s_sleep(1);
-      if (k == kSolveSpin) sfail = 1;
+      if (k == kSolveSpin) {
+        sfail = 1;
+        st->spin_err = 1;
+      }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
     if (wave == 0) diag_block(0);
@@ -1629,7 +1711,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
             if (__hip_atomic_load(b.ssync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
             __builtin_amdgcn_s_sleep(1);
           }
-          if (k == kSolveSpin) sfail = 1;
+          if (k == kSolveSpin) {  // a worker not co-resident (narrow CU mask, busy CUs): the solve ends in error
+            sfail = 1;
+            st->spin_err = 1;
+          }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
         __syncthreads();
@@ -1648,6 +1733,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   if (sfail) {
     if (tid == 0) {
       st->fail = 1;
+      if (st->spin_err) {  // a hand-off timed out: not a numerical failure, the solve ends (me_ba_* returns an error)
+        st->done = 1;
+        st->termination = 2;
+      }
       if (kMode == 2 && nworkers > 0) __hip_atomic_store(b.ssync, kSolveTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
@@ -2200,7 +2289,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_scan_kernel(Geo g, Bufs b, Op
     st->done = 0;
     st->termination = 1;
     st->iterations = st->successful = st->invalid_count = 0;
-    st->fail = st->scaled = st->accepted = st->final_pass = 0;
+    st->fail = st->scaled = st->accepted = st->final_pass = st->spin_err = 0;
     st->bad_input = w.flags[F_BAD];
     st->infeasible = w.flags[F_INFEASIBLE];
     st->radius = o.initial_radius;
@@ -2307,7 +2396,6 @@ struct Plan {
   Opts o;
   double* colnorm = nullptr;
   double* gc_raw = nullptr;
-  double* gc_glob = nullptr;
   double* Uraw = nullptr;
   double* cpart = nullptr;  // camera assembly partials (m x ck x 27)
   double* host = nullptr;  // pinned staging (inputs in, State / results out)
@@ -2322,6 +2410,9 @@ struct Plan {
   bool no_fused_asm = false;  // ME_BA_NOFUSEASM=1: S assembly in its own launch (A/B timing)
   bool full_S = false;      // assemble both block triangles of S (reduced-system / covariance read-back)
   int solve_workers = -1;   // global-memory camera solve: trailing-update workgroups (-1: by size; ME_SOLVE_WORKERS)
+  int solve_cap = 0;        // co-resident cam_solve_kernel<2> workgroups on the ctx's CUs (0: not queried)
+  me_comm* comm = nullptr;  // sharded solve: the exchange (null: one GPU)
+  bool xmax_separate = false;  // ABI-v2 callback (no rank): the gradient max-norm travels in its own max all-reduce
 };
 
 inline long rup(long x, long m) { return (x + m - 1) / m * m; }
@@ -2333,7 +2424,7 @@ int ba_drain(me_ctx* c);
 // staging set `async` (0 or 1) while the other set may still be in flight;
 // every other plan first completes the queued solves (they own the scratch)
 int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan& P, int slot_base,
-               int async = -1) {
+               int async = -1, me_comm* comm = nullptr) {
   if (async < 0) ME_TRY(ba_drain(c));
   ME_CHECK(c, p->n_cams > 0 && p->n_pts >= 0 && p->n_obs >= 0, "BA: bad sizes");
   ME_CHECK(c, p->n_cams <= kMaxScanCams, "BA: at most %d cameras per window", kMaxScanCams);
@@ -2361,6 +2452,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.no = p->n_obs;
   g.nf = std::min(std::max(p->fixed_frames, 0), p->n_cams);
   g.od = mono ? 2 : 4;
+  // sharded: one gradient max-norm slot per rank (ABI-v2 callback without rank: one slot, max-reduced apart)
+  P.comm = comm;
+  P.xmax_separate = comm && comm->world == 0;
+  g.xslots = comm && comm->world > 0 ? comm->world : 1;
+  g.xrank = comm && comm->world > 0 ? comm->rank : 0;
   g.m = g.nc - g.nf;
   g.n6 = 6 * g.m;
   g.Rpad = (int)rup(g.n6 + 1, 16);  // camera columns | z_p column n6 | zero padding
@@ -2464,9 +2560,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * R_COUNT * (size_t)nb, &b.part);
   add(8 * (R_COUNT + 2), &b.scal);
   add(sizeof(State), &b.st);
-  add(8 * (size_t)g.n6, &P.colnorm);
+  add(8 * (size_t)(g.n6 + 2), &P.colnorm);  // (+ the sharded first exchange's input flags)
   add(8 * (size_t)g.n6, &P.gc_raw);
-  add(8 * (size_t)g.n6, &P.gc_glob);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
   add(4 * (size_t)(g.m + 1 + 3), &b.cnt);  // counters: per camera (cam_assemble) | pt_step | solve sync (2) | fused assembly
@@ -2474,6 +2569,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(work_bytes, &b.work);
   const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
   add(8 * out_doubles, &b.out);
+  b.xch = nullptr;
+  if (comm) add(8 * (size_t)xo_total(g), &b.xch);
   size_t total = 0, input_span = 0;
   for (size_t k = 0; k < items.size(); ++k) {
     total += items[k].first;
@@ -2561,21 +2658,28 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSchurLdsCap));
     c->ba_lds_attr = 1;
   }
+  // the multi-workgroup camera solve needs block 0 and every worker resident
+  // at once: the workers it may use are capped by the co-resident count on
+  // the ctx's CUs; a hand-off that still times out is an error
+  if (!P.use_lds && g.Ts >= kSolveMwMinTs) {
+    int per_cu = 0;
+    ME_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cam_solve_kernel<2>, kSolveBlock, P.solve_lds));
+    P.solve_cap = std::max(0, per_cu) * (c->cu_active > 0 ? c->cu_active : c->num_cu);
+  }
   return ME_OK;
 }
 
 
 
-#define ME_AR(ptr, n)                                                                         \
-  do {                                                                                        \
-    if (ar((ptr), (n), user) != 0) return me_set_error(c, ME_ERR_HIP, "allreduce callback failed"); \
-  } while (0)
+// all-reduce of n doubles on the ctx stream through the plan's communicator
+#define ME_XCH(ptr, n, op) ME_TRY(me_comm_allreduce_impl(P.comm, (ptr), (long)(n), (op)))
 
 // Linearisation stage (device-skipped when need_lin == 0)
-int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
+int enqueue_linearize(Plan& P) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
+  const bool sh = P.comm != nullptr;
   {
     me_ktimer t(c, ME_KT_BA_LINEARIZE);
     const bool small = lin_block(g.no) == kLinSmall;
@@ -2591,20 +2695,25 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
   // After the first linearisation the Jacobi scaling is fixed and the Schur
   // pass no longer needs the camera assembly: its m x ck workgroups then ride
   // in the Schur launch (one launch fewer per iteration; a second stream with
-  // event fork/join measured slower).
-  const bool fused = P.n_enq > 0 && !ar && g.m > 0 && !P.sequential;
+  // event fork/join measured slower).  Sharded runs too: a rank's U and g
+  // blocks are then scaled by the fixed global scaling, and the exchange sums
+  // them.
+  const bool first = P.n_enq == 0;
+  const bool fused = !first && g.m > 0 && !P.sequential;
   ++P.n_enq;
   CamArgs ca{P.cpart, P.colnorm, P.gc_raw, P.Uraw, fused ? 1 : 0};
-  if (g.m > 0 && !fused) {
-    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart, ar ? 1 : 0,
+  if (g.m > 0 && !fused)
+    hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart, sh ? 1 : 0,
                        P.colnorm, P.gc_raw, P.Uraw);
-    if (ar) {
-      ME_AR(P.colnorm, g.n6);
-      hipLaunchKernelGGL(cam_finish_kernel, dim3(blocks(g.m, 64)), dim3(64), 0, s, g, P.b, (const double*)P.colnorm,
-                         (const double*)P.gc_raw, (const double*)P.Uraw);
-      ME_HIP(c, hipMemcpyAsync(P.gc_glob, P.gc_raw, 8 * (size_t)g.n6, hipMemcpyDeviceToDevice, s));
-      ME_AR(P.gc_glob, g.n6);
+  if (sh && !fused) {
+    // the Jacobi scaling needs the global column norms: the first exchange
+    // (with every rank's input flags behind them), then the local blocks scaled
+    if (first) {
+      hipLaunchKernelGGL(xch_flags_kernel, dim3(1), dim3(1), 0, s, g, P.b, P.colnorm);
+      ME_XCH(P.colnorm, g.n6 + 2, ME_COMM_SUM);
     }
+    hipLaunchKernelGGL(cam_finish_kernel, dim3(blocks(std::max(g.m, 1), 64)), dim3(64), 0, s, g, P.b,
+                       (const double*)P.colnorm, (const double*)P.gc_raw, (const double*)P.Uraw, first ? 1 : 0);
   }
   {
     // point blocks + Schur partial tiles (BA_SCHUR family)
@@ -2642,24 +2751,33 @@ int enqueue_linearize(Plan& P, me_allreduce_fn ar, void* user) {
     else ME_SCHUR(24);
 #undef ME_SCHUR
   }
-  if (ar) {
-    hipLaunchKernelGGL(lin_partials_kernel, dim3(1), dim3(kFinBlock), 0, s, g, P.b);
-    ME_AR(P.b.scal + R_COST, 1);
-    ME_AR(P.b.scal + R_GMAX_PT, -1);
+  if (sh) {
+    // this rank's reduced camera system, gradient and linearisation scalars
+    // packed, then ONE sum over the ranks
+    hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.npairs * 256, kSaElems) + 1), dim3(kBlock), 0, s, g,
+                       P.b, P.o, (const double*)P.gc_raw, 0, (int)SA_PACK);
+    if (P.xmax_separate) {
+      ME_XCH(P.b.xch, xo_gmax(g), ME_COMM_SUM);
+      ME_XCH(P.b.xch + xo_gmax(g), 1, ME_COMM_MAX);
+    } else {
+      ME_XCH(P.b.xch, xo_total(g), ME_COMM_SUM);
+    }
   }
   return me_check_launch(c, "BA linearize");
 }
 
 // S / b assembly; its last workgroup closes the linearisation (lin_finalize).
-int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
+// Sharded: S / b unpacked from the all-reduced exchange.
+int enqueue_assemble(Plan& P) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
-  const double* gc = ar ? P.gc_glob : P.gc_raw;
+  const int mode = P.comm ? SA_UNPACK : SA_SUM;
   if (g.m > 0)
     hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.npairs * 256, kSaElems) + 1), dim3(kBlock), 0,
-                       c->stream, g, P.b, P.o, gc, ar ? 1 : 0, P.full_S ? 1 : 0);
+                       c->stream, g, P.b, P.o, (const double*)P.gc_raw, P.full_S ? 1 : 0, mode);
   else
-    hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o, gc, ar ? 1 : 0);
+    hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o,
+                       (const double*)P.gc_raw);
   return me_check_launch(c, "BA assemble");
 }
 
@@ -2668,37 +2786,33 @@ int enqueue_assemble(Plan& P, me_allreduce_fn ar) {
 // ends the solve (iterations == max_num_iterations), so the camera solve and
 // the point step that would follow are never run: they are not queued (two
 // no-op launches fewer per solve; every rank of a sharded solve skips alike).
-int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user, bool last = false) {
+int enqueue_iteration(Plan& P, bool last = false) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   hipStream_t s = c->stream;
-  ME_TRY(enqueue_linearize(P, ar, user));
+  const bool sh = P.comm != nullptr;
+  ME_TRY(enqueue_linearize(P));
   // camera-solve form: 0 = [S; -b^T] in LDS, 1 = global memory, 2 = global
   // memory with trailing-update workers.  Trailing-update workers pay once the
   // block steps are many and wide: config 5 (19 steps) 372 -> 274 us per
   // solve; config 4 (11 steps) is faster on one workgroup (118 vs 131 us: the
-  // per-step hand-offs).
+  // per-step hand-offs).  The workers are capped by what can be co-resident.
   const int np0 = (g.Ts - 1) * g.Ts / 2;
-  const int nwk = P.use_lds ? 0
-                  : P.solve_workers >= 0 ? P.solve_workers
-                  : g.Ts >= kSolveMwMinTs ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
-                                          : 0;
+  int nwk = P.use_lds ? 0
+            : P.solve_workers >= 0 ? P.solve_workers
+            : g.Ts >= kSolveMwMinTs ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
+                                    : 0;
+  if (nwk > 0) nwk = std::max(0, std::min(nwk, P.solve_cap - 1));
   // S = U - sum of the Schur partials is assembled by wide workgroups
   // (coalesced, all CUs) rather than by the one-workgroup solve, whose
-  // dependent cross-XCD loads would otherwise dominate the iteration.  Single
-  // GPU (modes 0 and 1) they ride in the camera-solve launch (fused assembly).
-  const bool fuse = !ar && g.m > 0 && !P.full_S && !last && !P.sequential && nwk == 0 && !P.no_fused_asm;
+  // dependent cross-XCD loads would otherwise dominate the iteration.  Modes
+  // 0 and 1 they ride in the camera-solve launch (fused assembly; sharded:
+  // they unpack the exchanged system).
+  const bool fuse = g.m > 0 && !P.full_S && !last && !P.sequential && nwk == 0 && !P.no_fused_asm;
   const int nasm = fuse ? blocks((long)g.npairs * 256, kSolveBlock / kSaGroups) : 0;
-  if (!fuse) ME_TRY(enqueue_assemble(P, ar));
+  if (!fuse) ME_TRY(enqueue_assemble(P));
   if (last) return me_check_launch(c, "BA iteration");
-  if (g.m > 0) {
-    if (ar) {
-      ME_AR(P.b.S, g.n6 * g.n6 + 2 * g.n6);  // S | b | diag(U) are contiguous
-      ME_AR(P.b.scal + R_COUNT, 1);          // linear-solver failure flag
-    }
-  } else {
-    ME_HIP(c, hipMemsetAsync(P.b.scal + R_COUNT, 0, 8, s));
-  }
+  if (g.m == 0) ME_HIP(c, hipMemsetAsync(P.b.scal + R_COUNT, 0, 8, s));
   {
     me_ktimer t(c, ME_KT_BA_SOLVE);
     const double* gc = P.gc_raw;
@@ -2716,12 +2830,12 @@ int enqueue_iteration(Plan& P, me_allreduce_fn ar, void* user, bool last = false
     me_ktimer t(c, ME_KT_BA_STEP);
     // (step partials reduced and, single-GPU, the step decided in its last workgroup)
     if (g.od == 4)
-      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
+      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
     else
-      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, ar ? 0 : 1);
+      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
   }
-  if (ar) {
-    ME_AR(P.b.scal + R_MODEL, 5);  // model change, candidate cost, step^2, |x|^2, failure flag
+  if (sh) {
+    ME_XCH(P.b.scal + R_MODEL, 5, ME_COMM_SUM);  // model change, candidate cost, step^2, |x|^2, failure count
     hipLaunchKernelGGL(decide_kernel, dim3(1), dim3(64), 0, s, g, P.b, P.o);
   }
   return me_check_launch(c, "BA iteration");
@@ -2759,6 +2873,9 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = f
     if (g.np) std::memcpy(p->pts, P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
   }
   if (st.bad_input) return me_set_error(c, ME_ERR_INVALID, "BA: an observation indexes outside the window");
+  if (st.spin_err)
+    return me_set_error(c, ME_ERR_STATE, "BA: a cross-workgroup hand-off of the camera solve timed out "
+                                         "(workgroups not co-resident: CU mask or concurrent persistent kernels)");
   if (sum) {
     sum->termination = st.termination;
     sum->iterations = st.iterations;
@@ -2775,12 +2892,11 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = f
   return ME_OK;
 }
 
-int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allreduce_fn ar, void* user,
-               me_ba_summary* sum) {
+int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_comm* comm, me_ba_summary* sum) {
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   Plan P;
-  ME_TRY(plan_build(c, p, opt, P, 0));
+  ME_TRY(plan_build(c, p, opt, P, 0, -1, comm));
   // Enqueue the solve in chunks of iterations.  The device State after each
   // chunk is copied to a pinned slot behind an event, and the host inspects
   // chunk k only after chunk k + 1 is queued, so the GPU never drains while
@@ -2790,7 +2906,7 @@ int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_allredu
   int it = 0;
   auto enqueue_chunk = [&](int slot) -> int {
     for (int k = 0; k < chunk && it <= opt->max_num_iterations; ++k, ++it)
-      ME_TRY(enqueue_iteration(P, ar, user, it == opt->max_num_iterations));
+      ME_TRY(enqueue_iteration(P, it == opt->max_num_iterations));
     ME_HIP(c, hipMemcpyAsync(P.hstate[slot], P.b.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
     ME_HIP(c, hipEventRecord(c->poll_ev[slot], c->stream));
     return ME_OK;
@@ -2891,7 +3007,7 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   int rc = plan_build(c, p, opt, A->P, A->set, A->set);
   if (rc == ME_OK) {
     for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it)
-      rc = enqueue_iteration(A->P, nullptr, nullptr, it == opt->max_num_iterations);
+      rc = enqueue_iteration(A->P, it == opt->max_num_iterations);
   }
   if (rc == ME_OK) rc = enqueue_output(A->P, &A->prob);
   if (rc == ME_OK && hipEventCreateWithFlags(&A->ev, hipEventDisableTiming) != hipSuccess)
@@ -2941,7 +3057,7 @@ extern "C" void me_ba_default_options(me_ba_options* o) {
 }
 
 extern "C" int me_ba_solve(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_ba_summary* s) {
-  return solve_impl(c, p, o, nullptr, nullptr, s);
+  return solve_impl(c, p, o, nullptr, s);
 }
 
 #ifdef ME_ROUND_STAMPS
@@ -2955,10 +3071,27 @@ extern "C" int me_round_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+extern "C" int me_ba_solve_comm(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_comm* comm,
+                                me_ba_summary* s) {
+  if (!c) return ME_ERR_INVALID;
+  if (!comm) return me_set_error(c, ME_ERR_INVALID, "me_ba_solve_comm: null communicator");
+  if (comm->ctx != c) return me_set_error(c, ME_ERR_INVALID, "me_ba_solve_comm: the communicator belongs to another ctx");
+  return solve_impl(c, p, o, comm, s);
+}
+
+// ABI-v2 form: a callback without rank information (world 0: one gradient
+// max-norm slot, reduced by its own max all-reduce)
 extern "C" int me_ba_solve_sharded(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn ar,
                                    void* user, me_ba_summary* s) {
+  if (!c) return ME_ERR_INVALID;
   if (!ar) return me_set_error(c, ME_ERR_INVALID, "me_ba_solve_sharded: null allreduce");
-  return solve_impl(c, p, o, ar, user, s);
+  me_comm m;
+  m.ctx = c;
+  m.world = 0;
+  m.rank = 0;
+  m.ar = ar;
+  m.user = user;
+  return solve_impl(c, p, o, &m, s);
 }
 
 extern "C" int me_ba_cost(me_ctx* c, const me_ba_problem* p, double* cost) {
@@ -3024,8 +3157,8 @@ extern "C" int me_ba_reduced_system(me_ctx* c, const me_ba_problem* p, double ra
   if (rc < 0) return rc;
   P.full_S = true;
   const Geo& g = P.g;
-  ME_TRY(enqueue_linearize(P, nullptr, nullptr));
-  ME_TRY(enqueue_assemble(P, nullptr));
+  ME_TRY(enqueue_linearize(P));
+  ME_TRY(enqueue_assemble(P));
   std::vector<double> Sh((size_t)g.n6 * g.n6 + 2 * g.n6);
   if (g.m > 0)
     ME_HIP(c, hipMemcpyAsync(Sh.data(), P.b.S, 8 * Sh.size(), hipMemcpyDeviceToHost, c->stream));
@@ -3055,8 +3188,8 @@ extern "C" int me_ba_covariance(me_ctx* c, const me_ba_problem* p, double* cov, 
   P.full_S = true;
   const Geo& g = P.g;
   hipLaunchKernelGGL(cov_prep_kernel, dim3(1), dim3(1), 0, c->stream, P.b);
-  ME_TRY(enqueue_linearize(P, nullptr, nullptr));
-  ME_TRY(enqueue_assemble(P, nullptr));
+  ME_TRY(enqueue_linearize(P));
+  ME_TRY(enqueue_assemble(P));
   void* d;
   const size_t nx = (size_t)g.n6 * g.n6;
   ME_TRY(me_scratch(c, SLOT_GENERIC, 8 * (nx + 36 * (size_t)g.nc) + 64, &d));

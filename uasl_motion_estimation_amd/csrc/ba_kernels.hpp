@@ -55,7 +55,8 @@ struct State {
   int bad_input;      // device-resident input: an observation indexes outside the window
   int infeasible;     // a starting point violates the box bounds (Ceres IsFeasible -> FAILURE)
   int final_pass;     // set by pt_schur: this linearisation only feeds the closing gradient test
-  int pad[3];
+  int spin_err;       // a bounded cross-workgroup wait timed out (partner not co-resident): the solve ends in error
+  int pad[2];
   double radius, decrease;
   double x_cost, cand_cost, model_change, initial_cost;
   double cam_step2, cam_xn2, cam_gmax;
@@ -70,6 +71,7 @@ struct Geo {
   int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_lin, nblk_pts, nblk_step, pstride, jacobi,
       ck;
   int od;                  // residual rows per observation: 4 StereoReprojectionError, 2 Standard/StereoRight
+  int xslots, xrank;       // sharded: gradient max-norm slots in the exchange (one per rank) and this rank's
   double K0[9], K1[9];
   double baseline, sinv;
   double lo[3], hi[3];     // point bounds (BundleAdjuster.h:442-460)
@@ -118,6 +120,20 @@ struct Bufs {
   unsigned* cnt;      // last-arrival counters: m (cam_assemble, per camera) + 1 (pt_step); re-armed by the last
   unsigned* ssync;    // camera solve, global-memory form: {step epoch, worker step count} (zeroed by s_assemble)
   double* out;        // State | cams[cur] | pts[cur] for the single read-back
+  double* xch;        // sharded only (else null): the packed per-iteration exchange, see xo_* below
 };
+
+// Layout of the sharded exchange buffer (one all-reduce per LM iteration after
+// the Schur pass): the reduced camera system in the Schur tile layout
+// [npairs x 16 x 16: the upper block triangle of [S | b], tile pair p = (I <= J)]
+// | diag(U) (n6) | raw camera gradient (n6, the gradient-tolerance test) |
+// cost | failure count | one gradient max-norm slot per rank (a max carried by
+// a sum: every rank writes its own slot, the others hold 0).
+__host__ __device__ inline long xo_diag(const Geo& g) { return (long)g.npairs * 256; }
+__host__ __device__ inline long xo_gc(const Geo& g) { return xo_diag(g) + g.n6; }
+__host__ __device__ inline long xo_cost(const Geo& g) { return xo_gc(g) + g.n6; }
+__host__ __device__ inline long xo_fail(const Geo& g) { return xo_cost(g) + 1; }
+__host__ __device__ inline long xo_gmax(const Geo& g) { return xo_fail(g) + 1; }
+__host__ __device__ inline long xo_total(const Geo& g) { return xo_gmax(g) + g.xslots; }
 
 }  // namespace ba

@@ -55,6 +55,17 @@ struct me_ctx {
   float* mi_table[256] = {nullptr};
 };
 
+// Multi-GPU communicator (comm.hip): RCCL, or a caller callback.
+struct me_comm {
+  me_ctx* ctx = nullptr;
+  int world = 1, rank = 0;
+  void* nccl = nullptr;            // ncclComm_t (native RCCL over xGMI)
+  me_allreduce_fn ar = nullptr;    // else: caller all-reduce (host-staged)
+  void* user = nullptr;
+};
+// All-reduce of n doubles in place on the ctx stream (op ME_COMM_SUM / ME_COMM_MAX).
+int me_comm_allreduce_impl(me_comm* m, double* buf, long n, int op);
+
 // Device table of every MI term value for patches of N pixels (mi.hip).
 int me_mi_table(me_ctx* ctx, int npx, const float** out);
 

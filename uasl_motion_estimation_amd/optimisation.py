@@ -395,6 +395,82 @@ def ba_solve(bp, options: SolverOptions | None = None, ctx: Context | None = Non
     return cams, pts, _summary(s)
 
 
+class Comm:
+    """me_comm: the communicator of the landmark-sharded BA, one
+    per rank.  ``Comm.rccl`` joins the ranks with native RCCL (all-reduces
+    enqueued on the ctx stream, no host round trip); ``Comm.callback`` wraps
+    an ``allreduce(dev_ptr, n)`` callable (n > 0 sum, n < 0 max), e.g. a
+    host-staged gloo exchange or threads driving several contexts."""
+
+    def __init__(self, ctx: Context, handle, keep=None):
+        self.ctx, self.h, self._keep = ctx, handle, keep
+
+    @staticmethod
+    def unique_id() -> bytes:
+        from ._lib import load_library
+        buf = ctypes.create_string_buffer(128)
+        rc = load_library().me_comm_unique_id(buf, 128)
+        if rc != 0:
+            from ._lib import MEError
+            raise MEError(rc, "me_comm_unique_id (ncclGetUniqueId) failed")
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, ctx: Context, world: int, rank: int, uid: bytes) -> "Comm":
+        h = ctypes.c_void_p()
+        idb = ctypes.create_string_buffer(bytes(uid), 128)
+        ctx.check(ctx.lib.me_comm_create_rccl(ctx.h, int(world), int(rank), idb, byref(h)), "me_comm_create_rccl")
+        return cls(ctx, h)
+
+    @classmethod
+    def callback(cls, ctx: Context, world: int, rank: int, allreduce) -> "Comm":
+        def _cb(ptr, n, user):
+            try:
+                allreduce(ctypes.cast(ptr, ctypes.c_void_p).value, int(n))
+                return 0
+            except Exception:  # pragma: no cover
+                import traceback
+                traceback.print_exc()
+                return -1
+
+        cb = ALLREDUCE_FN(_cb)
+        h = ctypes.c_void_p()
+        ctx.check(ctx.lib.me_comm_create_callback(ctx.h, int(world), int(rank), cb, None, byref(h)),
+                  "me_comm_create_callback")
+        return cls(ctx, h, keep=cb)
+
+    def info(self) -> dict:
+        w, r, nat = c_int(), c_int(), c_int()
+        self.ctx.check(self.ctx.lib.me_comm_info(self.h, byref(w), byref(r), byref(nat)), "me_comm_info")
+        return dict(world=w.value, rank=r.value, native=bool(nat.value))
+
+    def allreduce(self, dev_ptr: int, n: int, op: str = "sum"):
+        self.ctx.check(self.ctx.lib.me_comm_allreduce(self.h, ctypes.c_void_p(dev_ptr), int(n),
+                                                      0 if op == "sum" else 1), "me_comm_allreduce")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.me_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def ba_solve_comm(bp_local, comm: "Comm", options: SolverOptions | None = None, ctx: Context | None = None):
+    """Landmark-sharded solve of this rank's shard over a communicator (me_ba_solve_comm)."""
+    ctx = ctx or comm.ctx
+    keep = []
+    p, cams, pts = ba_struct(bp_local, keep)
+    o = (options or SolverOptions()).to_c()
+    s = BASummaryC()
+    ctx.check(ctx.lib.me_ba_solve_comm(ctx.h, byref(p), byref(o), comm.h, byref(s)), "me_ba_solve_comm")
+    return cams, pts, _summary(s)
+
+
 def ba_solve_sharded(bp_local, allreduce, options: SolverOptions | None = None, ctx: Context | None = None):
     """Landmark-sharded solve; ``allreduce(dev_ptr, n)`` sums n doubles in place (n < 0: max over |n|)."""
     ctx = ctx or default_context()
@@ -501,6 +577,15 @@ class DeviceBAProblem:
         cb = ALLREDUCE_FN(_cb)
         self.ctx.check(self.ctx.lib.me_ba_solve_sharded(self.ctx.h, byref(p), byref(o), cb, None, byref(s)),
                        "me_ba_solve_sharded")
+        return _summary(s)
+
+    def solve_comm(self, comm: "Comm", options: SolverOptions | None = None) -> dict:
+        """me_ba_solve_comm on this device-resident shard."""
+        p = self.struct()
+        o = (options or SolverOptions()).to_c()
+        s = BASummaryC()
+        self.ctx.check(self.ctx.lib.me_ba_solve_comm(self.ctx.h, byref(p), byref(o), comm.h, byref(s)),
+                       "me_ba_solve_comm")
         return _summary(s)
 
     def solve_async(self, options: SolverOptions | None = None) -> None:
@@ -621,33 +706,65 @@ def host_staged_allreduce(group=None):
     return _ar
 
 
+def rccl_comm(ctx: Context, group=None, key: str = "me_rccl_uid") -> "Comm":
+    """A native RCCL me_comm over the ranks of a torch.distributed group: rank
+    0 draws the id (ncclGetUniqueId), the others read it from the group's
+    store; every rank then joins on its ctx device (one process per GPU)."""
+    import torch.distributed as dist
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    store = dist.distributed_c10d._get_default_store()
+    k = f"{key}/{getattr(rccl_comm, '_n', 0)}"
+    rccl_comm._n = getattr(rccl_comm, "_n", 0) + 1
+    if rank == 0:
+        uid = Comm.unique_id()
+        store.set(k, uid)
+    else:
+        uid = store.get(k)
+    return Comm.rccl(ctx, world, rank, uid)
+
+
 def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context | None = None, group=None,
-                         allreduce=None):
+                         allreduce=None, comm: "Comm | None" = None):
     """Landmark-sharded BA over torch.distributed: each rank holds
     the cameras and a contiguous, observation-balanced landmark range; the
-    reduced camera system S, b (and the scalar LM quantities) are summed
-    across ranks once per LM iteration, every rank solves the same camera
-    step and updates its own landmarks.  The exchange runs on device buffers
-    through RCCL for the nccl backend, host-staged for gloo (or the given
-    ``allreduce(dev_ptr, n)`` callback).  Returns (cams, local pts, (lo, hi), summary)."""
+    packed reduced camera system (S, b, gradient, LM scalars) is summed across
+    ranks once per LM iteration after the Schur pass and the step scalars once
+    after the point step; every rank solves the same camera step and updates
+    its own landmarks.  The exchange is the library's native RCCL communicator
+    for the nccl backend (``comm``, or one created here), host-staged through
+    the group for gloo, or the given ``allreduce(dev_ptr, n)`` callback.
+    Returns (cams, local pts, (lo, hi), summary)."""
     import torch
     import torch.distributed as dist
 
     ctx = ctx or default_context()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     local, rng = shard_landmarks(bp, rank, world)
-    if allreduce is None:
-        allreduce = host_staged_allreduce(group) if dist.get_backend(group) == "gloo" else torch_allreduce(group)
-    # kernels and the exchange ordered on one stream: a dedicated torch stream
-    # (the default stream's handle is 0, which me_set_stream reads as "the
-    # ctx-owned stream", and that one is not ordered with torch's)
-    stream = torch.cuda.Stream()
-    with torch.cuda.stream(stream):
-        ctx.set_stream(stream.cuda_stream)
-        try:
-            cams, pts, summ = ba_solve_sharded(local, allreduce, options, ctx)
-        finally:
-            ctx.set_stream(None)
+    own = False
+    if comm is None:
+        if allreduce is None and dist.get_backend(group) != "gloo":
+            comm, own = rccl_comm(ctx, group), True
+        else:
+            comm = Comm.callback(ctx, world, rank, allreduce or host_staged_allreduce(group))
+            own = True
+    try:
+        if comm.info()["native"]:
+            cams, pts, summ = ba_solve_comm(local, comm, options, ctx)
+        else:
+            # host-staged: kernels and the exchange ordered on one torch stream
+            # (the default stream's handle is 0, which me_set_stream reads as
+            # "the ctx-owned stream", and that one is not ordered with torch's)
+            stream = torch.cuda.Stream()
+            with torch.cuda.stream(stream):
+                ctx.set_stream(stream.cuda_stream)
+                try:
+                    cams, pts, summ = ba_solve_comm(local, comm, options, ctx)
+                finally:
+                    ctx.set_stream(None)
+    finally:
+        if own:
+            comm.close()
     return cams, pts, rng, summ
 
 
