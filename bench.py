@@ -65,10 +65,11 @@ def parse():
     ap.add_argument("--sharded-reps", type=int, default=3)
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at one rank (exercises the RCCL exchange path)")
-    ap.add_argument("--pipeline-frames", type=int, default=24,
-                    help="keyframes of the end-to-end windowed VO line (config 5 shape: KLT -> MI stereo matching -> "
-                         "WBA_Point tracks -> scale LM -> sliding-window BA); 0: off")
-    ap.add_argument("--pipeline-config", type=int, default=5)
+    ap.add_argument("--pipeline-frames", type=int, default=40,
+                    help="keyframes of the end-to-end windowed VO line at the headline config (KLT -> epipolar MI "
+                         "matching -> WBA_Point tracks -> scale LM -> sliding-window BA, pipelined); 0: off")
+    ap.add_argument("--pipeline-c5-frames", type=int, default=64,
+                    help="keyframes of the same loop at config 5 (W = 50: the window fills and slides); 0: off")
     ap.add_argument("--mi-pairs", type=int, default=1 << 20, help="pairs of the batched MI-kernel roofline line (0: off)")
     ap.add_argument("--timing", choices=("dominant", "all", "none"), default="dominant",
                     help="HIP-event timing inside the timed region: only the dominant kernel family (default; "
@@ -703,42 +704,69 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     return out
 
 
-def pipeline_line(args, ctx, cpu: bool):
-    """End-to-end windowed stereo VO (uasl_motion_estimation_amd/pipeline.py)
-    on one synthetic stream of the pipeline config: every keyframe runs KLT,
-    MI stereo matching, the WBA_Point bookkeeping, the scale LM and the
-    sliding-window BA (10 LM iterations).  Images are uploaded before the
-    timed loop; the host bookkeeping (numpy) is inside it.  With cpu=True the
-    same loop runs on the oracle backend (1 thread) and its track IDs, feature
+def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
+    """The windowed stereo VO loop itself (uasl_motion_estimation_amd/
+    pipeline.py) on one synthetic stream of config c: per keyframe KLT, the
+    epipolar MI matcher (tracked and new features), the WBA_Point
+    bookkeeping, the scale LM and the sliding-window BA (10 LM iterations),
+    every decision taken on the host from the hot path's results.  The loop
+    runs pipelined (KLT and scale LM on a front-end context beside the BA,
+    WindowedStereoVO(overlap=True)).  Images are uploaded before the timed
+    loop; the host bookkeeping (numpy) is inside it.  Frames/s over the
+    keyframes after `warm`; host time = bookkeeping outside the backend
+    calls, wait = time blocked on device results; a second, event-timed pass
+    gives the device time per kernel family.  With cpu=True the same loop runs
+    sequentially on the oracle backend (1 thread) and its track IDs, feature
     positions and poses are compared with the GPU's."""
     from uasl_motion_estimation_amd import pipeline as PL
 
-    c = args.pipeline_config
-    n = args.pipeline_frames
     t0 = time.perf_counter()
     fr, K, p0, v, truth = PL.synthetic_sequence(c, n)
     gen = time.perf_counter() - t0
-    be = PL.GPUBackend(ctx)
     cfg = PL.PipelineConfig.from_config(c)
-    for t in range(n):
-        be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
-    ctx.synchronize()
-    vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=cpu)
-    ts = []
-    for t in range(n):
+
+    def run(timed_families=False):
+        be = PL.GPUBackend(ctx)
+        for t in range(n):
+            be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
+        ctx.synchronize()
+        vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=cpu, overlap=True)
+        for t in range(warm):
+            vo.process(t, fr[t].left, fr[t].right)
+        vo.finish()  # (the warm-up keyframes complete outside the timed span)
+        for cc in (ctx, be.tctx):
+            cc.timing_reset()
+            cc.timing(timed_families)
+        h0, w0 = vo.stage_s["host"], vo.stage_s["wait"]
         t1 = time.perf_counter()
-        vo.process(t, fr[t].left, fr[t].right)
-        ts.append(time.perf_counter() - t1)
-    be.close()
-    warm = min(4, n // 2)
-    steady = ts[warm:]
+        for t in range(warm, n):
+            vo.process(t, fr[t].left, fr[t].right)
+        vo.finish()
+        el = time.perf_counter() - t1
+        fam = {}
+        if timed_families:
+            for name in ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_SCHUR", "BA_SOLVE", "BA_STEP", "KLT",
+                         "PYR"):
+                ms = sum(cc.timing_read(name)[1] for cc in (ctx, be.tctx))
+                if ms > 0:
+                    fam[name] = round(1e3 * ms / (n - warm), 1)
+            for cc in (ctx, be.tctx):
+                cc.timing(False)
+        be.close()
+        return vo, el, (vo.stage_s["host"] - h0), (vo.stage_s["wait"] - w0), fam
+
+    vo, el, host_s, wait_s, _ = run()
+    _, _, _, _, fam = run(timed_families=True)
+    m = n - warm
     last = vo.results[-1]
     out = {"workload": f"config {c}: {cfg.width}x{cfg.height} stereo, {cfg.n_feats} features, {cfg.window}-keyframe "
-                       f"sliding window, {n} keyframes (KLT + MI stereo match + tracks + scale LM + "
-                       f"{cfg.ba_iters}-iteration BA per keyframe)",
-           "frames_per_s": round(len(steady) / sum(steady), 2), "ms_per_frame": round(1e3 * np.mean(steady), 3),
-           "frames_timed": len(steady), "window_landmarks_last": last.n_window_pts,
-           "window_observations_last": last.n_window_obs, "tracks_created": int(vo.latest_id),
+                       f"sliding window, {n} keyframes (KLT + epipolar MI matching + tracks + scale LM + "
+                       f"{cfg.ba_iters}-iteration BA per keyframe), pipelined on two contexts",
+           "frames_per_s": round(m / el, 2), "ms_per_frame": round(1e3 * el / m, 3), "frames_timed": m,
+           "host_ms_per_frame": round(1e3 * host_s / m, 3), "wait_ms_per_frame": round(1e3 * wait_s / m, 3),
+           "device_us_per_frame": fam,
+           "window_landmarks_last": last.n_window_pts, "window_observations_last": last.n_window_obs,
+           "tracked_last": last.n_tracked, "tracks_created": int(vo.latest_id),
            "pose_drift_m_last": round(float(np.abs(vo.poses[n - 1][:3] - truth[n - 1][:3]).max()), 4),
            "render_s": round(gen, 1)}
     if cpu:
@@ -749,11 +777,13 @@ def pipeline_line(args, ctx, cpu: bool):
         t1 = time.perf_counter()
         for t in range(n):
             ov.process(t, fr[t].left, fr[t].right)
+        ov.finish()
         ct = time.perf_counter() - t1
         pose_rel = max(float(np.max(np.abs(vo.poses[t] - ov.poses[t]) / (np.abs(ov.poses[t]) + 1e-3)))
                        for t in range(n))
         out["cpu_baseline"] = {"frames_per_s": round(n / ct, 3), "cores": 1, "kind": "port",
-                               "sample": f"the same {n} keyframes on the oracle backend, 1 thread; {ct:.1f} s"}
+                               "sample": f"the same {n} keyframes on the oracle backend, sequential, 1 thread; "
+                                         f"{ct:.1f} s"}
         out["parity"] = {"events_bit_exact": vo.events == ov.events, "track_ids_equal": bool(np.array_equal(vo.ids, ov.ids)),
                          "pose_max_rel_diff": float("%.3g" % pose_rel)}
     return out
@@ -974,9 +1004,12 @@ def main():
                                                                                   * max(world, 1)), 4)}
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
-    pipe_line = None
+    pipe_line = pipe_c5 = None
     if args.pipeline_frames > 0 and rank == 0:
-        pipe_line = pipeline_line(args, ctx, cpu=world == 1 and not args.no_cpu_baseline)
+        cpu_leg = world == 1 and not args.no_cpu_baseline
+        pipe_line = pipeline_line(args, ctx, cpu_leg, args.config, args.pipeline_frames)
+        if args.pipeline_c5_frames > 0:
+            pipe_c5 = pipeline_line(args, ctx, False, 5, args.pipeline_c5_frames)
     sharded = None
     if args.sharded_ba:
         try:
@@ -1045,6 +1078,8 @@ def main():
                                    f"{cfg['n_feats']} feats, {cfg['window']}-keyframe window, 11x11 MI patches",
                        "frame": f"KLT + MI scale LM (LM, MAX_NB_ITER {args.scale_iters}, tolerances off) + "
                                 f"{args.ba_iters} BA LM iterations",
+                       "frame_kind": "composite: the three stages on independent synthetic inputs of the config's "
+                                     "shape (the connected VO loop is the `pipeline` line)",
                        "parallelism": f"{world} independent streams (one per GPU)",
                        "pipeline": None if pipe is None else (
                            ("front end (KLT + scale LM) of frame t+1 overlaps the BA of frame t" + (
@@ -1061,6 +1096,7 @@ def main():
             "multi_stream": multi,
             "sharded_ba": sharded,
             "pipeline": pipe_line,
+            "pipeline_config5": pipe_c5,
             "stereo_vo": vo_line,
             "cpu_baseline": cpu,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},

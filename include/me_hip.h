@@ -66,6 +66,11 @@ int me_free(me_ctx* ctx, void* dptr);
 int me_memcpy_h2d(me_ctx* ctx, void* dst, const void* src, size_t bytes);
 int me_memcpy_d2h(me_ctx* ctx, void* dst, const void* src, size_t bytes);
 int me_memcpy_d2d(me_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Asynchronous copy in any direction on the ctx stream (page-locked host
+   memory from me_host_alloc for a truly asynchronous host side). */
+int me_memcpy_async(me_ctx* ctx, void* dst, const void* src, size_t bytes);
+int me_host_alloc(me_ctx* ctx, void** hptr, size_t bytes);
+int me_host_free(me_ctx* ctx, void* hptr);
 
 /* Per-kernel timing with HIP events on the ctx stream (for bench.py's
    roofline): enable a bitmask of families (bit k = ME_KT k; ME_KT_ALL = every
@@ -97,6 +102,23 @@ int me_mi_scores(me_ctx* ctx, me_mem mem, const uint8_t* imgL, int strideL, cons
 /* Whole-patch form (any size, the literal computeMutualInformation(L, R)). */
 int me_mutual_information(me_ctx* ctx, me_mem mem, const uint8_t* L, int strideL, const uint8_t* R, int strideR,
                           int w, int h, float* mi_out);
+/* Epipolar stereo matcher of the VO loop (the application's MI stereo
+   matching around me::computeMutualInformation; build-defined like KLT, no
+   reference symbol): feature k at (u_k, v_k) of imgL (rectified pair, one
+   stride), candidate disparities d = lo_k .. lo_k + nd - 1, left patch at
+   (floor(u - patch/2), floor(v - patch/2)), right patch d pixels to its
+   left; a candidate is scored (MI, the bits of me_mi_scores) iff its right
+   patch starts at x >= 0, d <= d_max and the feature is valid (valid_k != 0
+   when valid is given; status_k == 1 and margin <= u < width - margin,
+   margin <= v < height - margin when status is given -- the KLT gate).
+   Pick: first maximum, interior, FP64 parabola vertex, optional uniqueness
+   (best >= ratio * best outside +-2 candidates); xr_k = u_k - disparity
+   (float), ok_k = 1 iff the pick holds and xr_k >= margin.  Every array is
+   device memory; asynchronous on the ctx stream. */
+int me_mi_epipolar_match(me_ctx* ctx, const uint8_t* imgL, const uint8_t* imgR, int width, int height, int stride,
+                         const float* uv, const int32_t* lo, const uint8_t* valid, const uint8_t* status, int n,
+                         int nd, int patch, int d_max, int unique, double ratio, float margin, float* xr_out,
+                         uint8_t* ok_out);
 /* me::computeEntropy (src/core/mutual_information.cpp:28-45). */
 int me_entropy(me_ctx* ctx, me_mem mem, const uint8_t* img, int stride, int w, int h, float* out);
 

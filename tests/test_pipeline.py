@@ -4,8 +4,10 @@ CPU: the loop on the oracle backend, its WBA_Point bookkeeping replayed
 through feature_types.WBA_Point (include/MotionEstimation/core/
 feature_types.h:121-197: IDs from the value constructor, contiguous
 addMatch, pop of the oldest feature).
-GPU: the same loop on libme_hip.so vs the oracle backend over >= 20
-keyframes: track IDs and feature positions bit-exact, poses 1e-6.
+GPU: the same loop on libme_hip.so (pipelined: KLT, the device epipolar
+matcher and the scale LM on a front-end context beside the BA) vs the
+oracle backend, sequential: track IDs and feature positions bit-exact,
+poses 1e-6, over 56 keyframes of a sliding W = 50 window.
 """
 import numpy as np
 import pytest
@@ -14,7 +16,7 @@ from uasl_motion_estimation_amd import pipeline as PL
 from uasl_motion_estimation_amd.feature_types import WBA_Point
 
 
-def _run(cfg_id, n_frames, backend, window=None, ba_iters=5, log=True, frames=None):
+def _run(cfg_id, n_frames, backend, window=None, ba_iters=5, log=True, frames=None, overlap=False):
     if frames is None:
         frames = PL.synthetic_sequence(cfg_id, n_frames)
     fr, K, p0, v, truth = frames
@@ -22,10 +24,24 @@ def _run(cfg_id, n_frames, backend, window=None, ba_iters=5, log=True, frames=No
     cfg = PL.PipelineConfig.from_config(cfg_id, **kw)
     if window is not None:
         cfg.window = window
-    vo = PL.WindowedStereoVO(cfg, backend, K, p0, v, log_events=log)
+    vo = PL.WindowedStereoVO(cfg, backend, K, p0, v, log_events=log, overlap=overlap)
     for t in range(n_frames):
         vo.process(t, fr[t].left, fr[t].right)
+    vo.finish()
     return vo
+
+
+def test_pipelined_loop_equals_sequential_loop(oracle):
+    """overlap=True (KLT of t queued before frame t-1 completes, BA and scale
+    LM queued) takes exactly the decisions of the sequential loop."""
+    from pipeline_oracle import OracleBackend
+
+    frames = PL.synthetic_sequence(1, 10)
+    a = _run(1, 10, OracleBackend(), window=4, ba_iters=2, frames=frames)
+    b = _run(1, 10, OracleBackend(), window=4, ba_iters=2, frames=frames, overlap=True)
+    assert a.events == b.events and np.array_equal(a.ids, b.ids) and np.array_equal(a.X, b.X)
+    assert all(np.array_equal(a.poses[t], b.poses[t]) for t in a.poses)
+    assert [r.n_window_obs for r in a.results] == [r.n_window_obs for r in b.results]
 
 
 def _replay(vo):
@@ -82,24 +98,31 @@ def test_pipeline_tracks_the_synthetic_trajectory(oracle):
     assert err < 0.1  # metres over 8 keyframes of 0.5 m: VO drift, not a convention error
 
 
+N_SLIDE = 56  # config 5: the W = 50 window fills at keyframe 49 and slides 6 times
+
+
 @pytest.fixture(scope="module")
 def seq5():
-    return PL.synthetic_sequence(5, 24)
+    return PL.synthetic_sequence(5, N_SLIDE)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("window", [50, 8])
-def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window):
-    """Config 5 (1280 x 720, 2000 features, W = 50 sliding window) over 24
-    keyframes, and a W = 8 window so that pops and track deletion run."""
+@pytest.mark.parametrize("window,n", [(50, N_SLIDE), (8, 24)])
+def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window, n):
+    """Config 5 (1280 x 720, 2000 features, W = 50 sliding window) over 56
+    keyframes -- the window fills and slides (pops of the oldest keyframe,
+    feature_types.h:142) -- and a W = 8 window over 24 keyframes (many pops
+    and track deletions)."""
     from pipeline_oracle import OracleBackend
 
-    be = PL.GPUBackend(ctx)
+    be = PL.GPUBackend(ctx)  # front end on its own context, the loop pipelined
     try:
-        g = _run(5, 24, be, window=window, frames=seq5)
+        g = _run(5, n, be, window=window, frames=seq5, overlap=True)
     finally:
         be.close()
-    o = _run(5, 24, OracleBackend(), window=window, frames=seq5)
+    o = _run(5, n, OracleBackend(), window=window, frames=seq5)
+    if window == 50:  # the window slid: its oldest keyframe is n - 50, and pops happened
+        assert min(g.obs) == n - window and any(ev[0] == "pop" for ev in g.events)
     assert g.events == o.events  # track IDs, frames and feature positions, bit for bit
     assert np.array_equal(g.ids, o.ids)
     for rg, ro in zip(g.results, o.results):
@@ -110,3 +133,49 @@ def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window):
     for t in g.poses:
         np.testing.assert_allclose(g.poses[t], o.poses[t], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(g.X, o.X, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unique", [False, True])
+def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
+    """me_mi_epipolar_match (device MI scores + FP64 pick) = match_host (MI
+    scores + the numpy pick) bit for bit, on features across a config-3
+    stereo pair: per-feature windows (tracked form, with invalid features)
+    and the full [d_min, d_max] range with the uniqueness test (new form)."""
+    from pipeline_oracle import OracleBackend
+
+    fr = PL.synthetic_sequence(3, 1)[0]
+    be = PL.GPUBackend(ctx)
+    try:
+        imgs = be.frame_images(0, fr[0].left, fr[0].right)
+        rng = np.random.default_rng(7)
+        n = 600
+        uv = np.stack([rng.uniform(PL.MARGIN, 1280 - PL.MARGIN, n), rng.uniform(PL.MARGIN, 720 - PL.MARGIN, n)],
+                      -1).astype(np.float32)
+        if unique:
+            lo, nd, dvalid = np.full(n, 2, np.int64), 127, None
+            got = be.match(imgs, uv, lo, nd, True)
+        else:
+            lo = rng.integers(2, 120, n).astype(np.int64)
+            nd = 13
+            dvalid = rng.random(n) > 0.1
+            # tracked form with per-feature validity (device layout uv | lo | xr | valid | ok)
+            c = be.tctx
+            d = be._dbuf("t_uv", 18 * n)
+            hp = be._hbuf("t_uv", 18 * n)
+            be._view(hp, np.float32, 2 * n)[:] = uv.ravel()
+            be._view(hp, np.int32, n, 8 * n)[:] = lo
+            be._view(hp, np.uint8, n, 16 * n)[:] = dvalid
+            c.copy_async(d, hp, 18 * n)
+            be._epipolar(imgs, d, d + 8 * n, d + 16 * n, 0, n, nd, False, d + 12 * n, d + 17 * n)
+            c.copy_async(hp, d, 18 * n)
+            c.synchronize()
+            got = (be._view(hp, np.float32, n, 12 * n).copy(), be._view(hp, np.uint8, n, 17 * n).astype(bool))
+        ob = OracleBackend()
+        oimgs = ob.frame_images(0, fr[0].left, fr[0].right)
+        ref = PL.match_host(ob, oimgs, uv, lo, nd, dvalid, unique, 128)
+    finally:
+        be.close()
+    assert np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0][ref[1]].view(np.uint32), ref[0][ref[1]].view(np.uint32))
+    assert ref[1].sum() > n // 4  # the comparison covers many accepted matches

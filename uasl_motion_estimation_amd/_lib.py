@@ -117,8 +117,9 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 EXPORTS = [
     "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
     "me_get_stream", "me_set_cu_mask", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
+    "me_memcpy_async", "me_host_alloc", "me_host_free",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
-    "me_mi_scores", "me_mutual_information", "me_entropy", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
+    "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
@@ -169,6 +170,9 @@ def load_library(path: str = LIB_PATH):
         "me_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
         "me_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
         "me_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+        "me_memcpy_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+        "me_host_alloc": (c_int, [c_void_p, P(c_void_p), c_size_t]),
+        "me_host_free": (c_int, [c_void_p, c_void_p]),
         "me_timing_enable": (c_int, [c_void_p, c_int]),
         "me_timing_sample": (c_int, [c_void_p, c_int]),
         "me_timing_read": (c_int, [c_void_p, c_int, P(c_long), P(c_double)]),
@@ -177,6 +181,9 @@ def load_library(path: str = LIB_PATH):
                                  c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_mutual_information": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
                                           c_void_p]),
+        "me_mi_epipolar_match": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_float,
+                                         c_void_p, c_void_p]),
         "me_compare_pc": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_ccoeff_normed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_quantise": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int]),
@@ -319,6 +326,18 @@ class Context:
 
     def d2d(self, dst: int, src: int, nbytes: int):
         self.check(self.lib.me_memcpy_d2d(self.h, c_void_p(dst), c_void_p(src), int(nbytes)), "me_memcpy_d2d")
+
+    def copy_async(self, dst: int, src: int, nbytes: int):
+        """hipMemcpyAsync (any direction) on the ctx stream."""
+        self.check(self.lib.me_memcpy_async(self.h, c_void_p(dst), c_void_p(src), int(nbytes)), "me_memcpy_async")
+
+    def host_alloc(self, nbytes: int) -> int:
+        p = c_void_p()
+        self.check(self.lib.me_host_alloc(self.h, ctypes.byref(p), int(nbytes)), "me_host_alloc")
+        return p.value
+
+    def host_free(self, ptr: int):
+        self.check(self.lib.me_host_free(self.h, c_void_p(ptr)), "me_host_free")
 
     # --- kernel timing (HIP events on the ctx stream) ---
     def timing(self, on: bool = True, families=None):

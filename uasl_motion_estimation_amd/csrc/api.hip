@@ -220,6 +220,22 @@ int me_memcpy_d2d(me_ctx* c, void* d, const void* s, size_t n) {
   ME_HIP(c, hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, c->stream));
   return ME_OK;
 }
+int me_memcpy_async(me_ctx* c, void* d, const void* s, size_t n) {
+  if (!c) return ME_ERR_INVALID;
+  if (n) ME_HIP(c, hipMemcpyAsync(d, s, n, hipMemcpyDefault, c->stream));
+  return ME_OK;
+}
+int me_host_alloc(me_ctx* c, void** p, size_t bytes) {
+  if (!c || !p) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  ME_HIP(c, hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault));
+  return ME_OK;
+}
+int me_host_free(me_ctx* c, void* p) {
+  if (!c) return ME_ERR_INVALID;
+  if (p) ME_HIP(c, hipHostFree(p));
+  return ME_OK;
+}
 
 int me_timing_enable(me_ctx* c, int family_mask) {
   c->timing = family_mask & ME_KT_ALL;

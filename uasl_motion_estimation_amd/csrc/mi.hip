@@ -382,7 +382,87 @@ __global__ __launch_bounds__(kLargeBlock) void entropy_kernel(const uint8_t* __r
 
 inline float inv_count(long n) { return (float)(1.0 / (double)n); }
 
+// Epipolar MI stereo matcher of the VO loop (pipeline.WindowedStereoVO.
+// stereo_match / _pick, restated on the device): one workgroup per feature,
+// 16 lane groups score its candidate disparities (group_mi: the bits of
+// me_mi_scores), then one lane picks the best in FP64 exactly as the numpy
+// restatement does (first maximum, interior, parabola vertex, uniqueness
+// against the best outside +-2 candidates, x_r = u - disparity, margin test).
+constexpr int kEpiBlock = 256, kEpiGroups = kEpiBlock / 16, kEpiMaxNd = 512;
+__global__ __launch_bounds__(kEpiBlock) void mi_epipolar_kernel(
+    const uint8_t* __restrict__ L, const uint8_t* __restrict__ R, int stride, int width, int height,
+    const float* __restrict__ uv, const int32_t* __restrict__ lo, const uint8_t* __restrict__ valid,
+    const uint8_t* __restrict__ status, int n, int nd, int patch, int d_max, int unique, double ratio, float margin,
+    float invN, float* __restrict__ xr_out, uint8_t* __restrict__ ok_out) {
+  __shared__ uint32_t lds[kEpiGroups * kGroupWords];
+  __shared__ double sc[kEpiMaxNd];
+  const int f = blockIdx.x;
+  if (f >= n) return;
+  const int grp = threadIdx.x >> 4;
+  GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
+  const float u = uv[2 * f], v = uv[2 * f + 1];
+  const int half = patch / 2;
+  // Rect(x - w, y - w, ..) corner (floor of the FP64 value, as the restatement)
+  const int x0 = (int)floor((double)u - half), y0 = (int)floor((double)v - half);
+  bool fv = valid ? valid[f] != 0 : true;
+  if (status)  // the KLT gate: status 1 and inside the feature margin
+    fv = fv && status[f] == 1 && u >= margin && u < (float)width - margin && v >= margin && v < (float)height - margin;
+  const int l0 = lo[f];
+  for (int c = grp; c < nd; c += kEpiGroups) {
+    const int d = l0 + c, xr = x0 - d;
+    const bool ok = fv && xr >= 0 && d <= d_max;  // (group-uniform)
+    float s = 0.0f;
+    if (ok) s = group_mi<false>(h, L + (long)y0 * stride + x0, stride, R + (long)y0 * stride + xr, stride, patch, patch,
+                                invN);
+    if (h.gl == 0) sc[c] = ok ? (double)s : -INFINITY;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int k = 0;
+  double best = -INFINITY;
+  for (int c = 0; c < nd; ++c)
+    if (sc[c] > best) {  // np.argmax: the first maximum
+      best = sc[c];
+      k = c;
+    }
+  bool ok = k > 0 && k < nd - 1 && isfinite(best);
+  const int kk = min(max(k, 1), nd - 2);
+  const double sm = sc[kk - 1], s0 = sc[kk], sp = sc[kk + 1];
+  const double den = sm - 2.0 * s0 + sp;
+  ok = ok && isfinite(sm) && isfinite(sp) && den < 0.0;
+  if (unique) {
+    double second = -INFINITY;
+    for (int c = 0; c < nd; ++c)
+      if ((c < k - 2 || c > k + 2) && sc[c] > second) second = sc[c];
+    ok = ok && best >= ratio * second;
+  }
+  const double den_s = ok ? den : -1.0;
+  const double delta = ok ? 0.5 * (sm - sp) / den_s : 0.0;
+  const double disp = (double)(l0 + kk) + delta;
+  const float xr_f = (float)((double)u - disp);
+  ok = ok && xr_f >= margin;
+  xr_out[f] = xr_f;
+  ok_out[f] = ok ? 1 : 0;
+}
+
 }  // namespace
+
+extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
+                                    int stride, const float* uv, const int32_t* lo, const uint8_t* valid,
+                                    const uint8_t* status, int n, int nd, int patch, int d_max, int unique,
+                                    double ratio, float margin, float* xr_out, uint8_t* ok_out) {
+  if (!c) return ME_ERR_INVALID;
+  ME_CHECK(c, n >= 0 && nd >= 3 && nd <= kEpiMaxNd && patch > 0 && patch * patch <= 255 && width > 0 && height > 0 &&
+                  stride >= width,
+           "me_mi_epipolar_match: bad sizes (3 <= nd <= %d, patch <= 15)", kEpiMaxNd);
+  if (n == 0) return ME_OK;
+  ME_HIP(c, hipSetDevice(c->device));
+  me_ktimer t(c, ME_KT_MI);
+  hipLaunchKernelGGL(mi_epipolar_kernel, dim3(n), dim3(kEpiBlock), 0, c->stream, imgL, imgR, stride, width, height, uv,
+                     lo, valid, status, n, nd, patch, d_max, unique, ratio, margin, inv_count((long)patch * patch), xr_out,
+                     ok_out);
+  return me_check_launch(c, "mi_epipolar_kernel");
+}
 
 // Shared launcher (also used by scale.hip for raw device buffers).
 int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, int width, int height,

@@ -96,9 +96,69 @@ class FrameResult:
     pose: np.ndarray = field(repr=False)
 
 
+def match_host(be, imgs, uv, lo, nd, dvalid, unique: bool, d_max: int, ratio: float = 1.2):
+    """MI disparity search, the numpy restatement (the oracle backend's
+    matcher; the GPU backend runs the same on the device,
+    me_mi_epipolar_match): feature k searches d = lo_k .. lo_k + nd - 1;
+    returns (xr float32, ok).  Best integer candidate, parabola sub-pixel
+    refinement, the best must be an interior maximum; with `unique` it must
+    also be >= ratio x the best outside +-2 px of it."""
+    n = len(uv)
+    if n == 0:
+        return np.zeros(0, np.float32), np.zeros(0, bool)
+    x0 = np.floor(uv[:, 0].astype(np.float64) - W_SCALE).astype(np.int64)  # Rect(x - w, ..) truncation
+    y0 = np.floor(uv[:, 1].astype(np.float64) - W_SCALE).astype(np.int64)
+    d = lo[:, None] + np.arange(nd, dtype=np.int64)[None, :]
+    xr = x0[:, None] - d
+    valid = (xr >= 0) & (d <= d_max)
+    if dvalid is not None:
+        valid &= dvalid[:, None]
+    xr_c = np.where(valid, xr, 0)
+    xyL = np.stack([np.repeat(x0, nd), np.repeat(y0, nd)], -1)
+    xyR = np.stack([xr_c.ravel(), np.repeat(y0, nd)], -1)
+    sc = be.mi_scores(imgs, xyL, xyR).reshape(n, nd).astype(np.float64)
+    sc = np.where(valid, sc, -np.inf)
+    with np.errstate(invalid="ignore", divide="ignore"):  # -inf candidates (outside the image)
+        return _pick(uv, d, sc, nd, unique, ratio)
+
+
+def _pick(uv, d, sc, nd, unique, ratio):
+    n = len(uv)
+    rows = np.arange(n)
+    k = np.argmax(sc, axis=1)
+    best = sc[rows, k]
+    ok = (k > 0) & (k < nd - 1) & np.isfinite(best)
+    kk = np.clip(k, 1, nd - 2)
+    s_m, s_0, s_p = sc[rows, kk - 1], sc[rows, kk], sc[rows, kk + 1]
+    den = s_m - 2 * s_0 + s_p
+    ok &= np.isfinite(s_m) & np.isfinite(s_p) & (den < 0)
+    if unique:  # uniqueness against the best candidate outside +-2 px
+        m = sc.copy()
+        for j in range(-2, 3):
+            m[rows, np.clip(k + j, 0, nd - 1)] = -np.inf
+        second = m.max(axis=1)
+        ok &= best >= ratio * second
+    den_s = np.where(ok, den, -1.0)
+    delta = np.where(ok, 0.5 * (s_m - s_p) / den_s, 0.0)
+    disp = d[rows, kk].astype(np.float64) + delta
+    xr_f = (uv[:, 0].astype(np.float64) - disp).astype(np.float32)
+    ok &= xr_f >= MARGIN
+    return xr_f, ok
+
+
+def in_margin(uv, width, height):
+    return ((uv[:, 0] >= MARGIN) & (uv[:, 0] < width - MARGIN) & (uv[:, 1] >= MARGIN)
+            & (uv[:, 1] < height - MARGIN))
+
+
 class Backend:
     """The hot-path calls of the loop.  Images are handles returned by
-    frame_images(); corner / point arrays are host numpy."""
+    frame_images(); corner / point arrays are host numpy.  The staged calls
+    (klt_submit / klt_match, ba_submit / ba_result, scale_submit /
+    scale_result) default to the plain ones run synchronously; the GPU
+    backend queues them (front end and BA on separate streams)."""
+
+    d_max = 128
 
     def frame_images(self, t: int, left: np.ndarray, right: np.ndarray):
         raise NotImplementedError
@@ -118,15 +178,92 @@ class Backend:
         """(cams, pts, summary dict) after `iters` fixed LM iterations."""
         raise NotImplementedError
 
+    # ---- staged forms
+    def klt_submit(self, prev, cur, pts):
+        return (prev, cur, np.ascontiguousarray(pts, np.float32))
+
+    def klt_match(self, h, imgs, lo, nd, dvalid):
+        """KLT of the submitted points, then the MI search (lo, nd, dvalid per
+        point) of those that pass the KLT gate: (uv, status, xr, ok)."""
+        prev, cur, pts = h
+        uv, st = self.klt(prev, cur, pts)
+        H, W = imgs[2]
+        keep = (st == 1) & in_margin(uv, W, H)
+        xr = np.zeros(len(uv), np.float32)
+        ok = np.zeros(len(uv), bool)
+        xk, okk = match_host(self, imgs, uv[keep], lo[keep], nd, dvalid[keep], False, self.d_max)
+        xr[keep], ok[keep] = xk, okk
+        return uv, st, xr, ok
+
+    def match(self, imgs, uv, lo, nd, unique):
+        return match_host(self, imgs, uv, lo, nd, None, unique, self.d_max)
+
+    def scale_submit(self, sp, params):
+        self._scale_res = self.scale_optimise(sp, params)
+
+    def scale_result(self) -> dict:
+        r, self._scale_res = self._scale_res, None
+        return r
+
+    def ba_submit(self, bp, iters: int):
+        self._ba_res = self.ba_solve(bp, iters)
+
+    def ba_result(self):
+        r, self._ba_res = self._ba_res, None
+        return r
+
 
 class GPUBackend(Backend):
-    """libme_hip.so through the C ABI; images resident in HBM (one upload per frame)."""
+    """libme_hip.so through the C ABI; images resident in HBM (one upload per
+    frame).  Two contexts of the device: `ctx` runs the BA, `tctx` the front
+    end (KLT, the epipolar MI matcher, the scale LM), so the scale LM of frame
+    t and the KLT of frame t + 1 run beside the BA of frame t.  Device buffers
+    and page-locked staging are persistent (grow-only); per stage one H2D and
+    one D2H."""
 
-    def __init__(self, ctx=None):
-        from ._lib import default_context
+    def __init__(self, ctx=None, tctx=None, overlap: bool = True):
+        from ._lib import Context, default_context
 
         self.ctx = ctx or default_context()
+        self._own_t = tctx is None and overlap
+        self.tctx = tctx or (Context(self.ctx.device) if overlap else self.ctx)
         self._imgs = {}
+        self._dev = {}   # name -> [ptr, bytes] on the device
+        self._pin = {}   # name -> [ptr, bytes] page-locked host
+        self._ba = None
+        self._scale_res = None
+
+    # ---- persistent buffers
+    def _dbuf(self, name, nbytes):
+        b = self._dev.get(name)
+        if b is None or b[1] < nbytes:
+            if b is not None:
+                self.tctx.synchronize()
+                self.ctx.synchronize()
+                self.tctx.free(b[0])
+            nb = max(4096, int(nbytes * 1.5))
+            self._dev[name] = b = [self.tctx.malloc(nb), nb]
+        return b[0]
+
+    def _hbuf(self, name, nbytes):
+        b = self._pin.get(name)
+        if b is None or b[1] < nbytes:
+            if b is not None:
+                self.tctx.synchronize()
+                self.tctx.host_free(b[0])
+            nb = max(4096, int(nbytes * 1.5))
+            self._pin[name] = b = [self.tctx.host_alloc(nb), nb]
+        return b[0]
+
+    @staticmethod
+    def _view(ptr, dtype, count, offset=0):
+        import ctypes
+
+        nbytes = np.dtype(dtype).itemsize * count
+        if count == 0:
+            return np.zeros(0, dtype)
+        buf = (ctypes.c_char * nbytes).from_address(ptr + offset)
+        return np.frombuffer(buf, dtype, count)
 
     def frame_images(self, t, left, right):
         if t in self._imgs:
@@ -147,70 +284,165 @@ class GPUBackend(Backend):
             self.ctx.free(h[1])
 
     def close(self):
+        if self._ba is not None:
+            self.ba_result()
         for t in list(self._imgs):
             self.release(t)
+        self.tctx.synchronize()
+        for p, _ in self._dev.values():
+            self.tctx.free(p)
+        for p, _ in self._pin.values():
+            self.tctx.host_free(p)
+        self._dev, self._pin = {}, {}
+        if self._own_t:
+            self.tctx.close()
+            self._own_t = False
 
+    # ---- plain calls (tests, tools)
     def klt(self, prev, cur, pts):
-        import ctypes
-
-        from ._lib import ME_DEVICE
-        from .klt import klt_params
-
+        h = self.klt_submit(prev, cur, pts)
         n = len(pts)
-        out = np.zeros((n, 2), np.float32)
-        st = np.zeros(n, np.uint8)
         if n == 0:
-            return out, st
-        H, W = prev[2]
-        c = self.ctx
-        pts = np.ascontiguousarray(pts, np.float32)
-        d_in, d_out, d_st = c.malloc(8 * n), c.malloc(8 * n), c.malloc(max(n, 16))
-        try:
-            c.h2d(d_in, pts)
-            kp = klt_params()
-            c.check(c.lib.me_klt_track(c.h, ME_DEVICE, ctypes.c_void_p(prev[0]), ctypes.c_void_p(cur[0]), W, H, W,
-                                       ctypes.c_void_p(d_in), ctypes.c_void_p(d_out), ctypes.c_void_p(d_st), n,
-                                       ctypes.byref(kp)), "me_klt_track")
-            c.d2h(out, d_out)
-            c.d2h(st, d_st)
-        finally:
-            for p in (d_in, d_out, d_st):
-                c.free(p)
-        return out, st
+            return np.zeros((0, 2), np.float32), np.zeros(0, np.uint8)
+        c = self.tctx
+        hp = self._hbuf("out", 14 * n)
+        dres = self._dbuf("res", 14 * n)
+        c.copy_async(hp, dres, 13 * n)
+        c.synchronize()
+        return self._view(hp, np.float32, 2 * n).reshape(n, 2).copy(), self._view(hp, np.uint8, n, 12 * n).copy()
 
     def mi_scores(self, imgs, xyL, xyR):
         from .mutual_information import mi_scores_device
 
         n = len(xyL)
-        out = np.zeros(n, np.float32)
         if n == 0:
-            return out
+            return np.zeros(0, np.float32)
         H, W = imgs[2]
-        c = self.ctx
-        xyL = np.ascontiguousarray(xyL, np.int32)
-        xyR = np.ascontiguousarray(xyR, np.int32)
-        dl, dr, do = c.malloc(xyL.nbytes), c.malloc(xyR.nbytes), c.malloc(4 * n)
-        try:
-            c.h2d(dl, xyL)
-            c.h2d(dr, xyR)
-            mi_scores_device(c, imgs[0], W, imgs[1], W, W, H, dl, dr, n, (PATCH, PATCH), do)
-            c.d2h(out, do)
-        finally:
-            for p in (dl, dr, do):
-                c.free(p)
-        return out
+        c = self.tctx
+        hp = self._hbuf("mi_in", 16 * n)
+        self._view(hp, np.int32, 2 * n)[:] = np.asarray(xyL, np.int32).ravel()
+        self._view(hp, np.int32, 2 * n, 8 * n)[:] = np.asarray(xyR, np.int32).ravel()
+        d = self._dbuf("mi", 20 * n)
+        c.copy_async(d, hp, 16 * n)
+        mi_scores_device(c, imgs[0], W, imgs[1], W, W, H, d, d + 8 * n, n, (PATCH, PATCH), d + 16 * n)
+        ho = self._hbuf("mi_out", 4 * n)
+        c.copy_async(ho, d + 16 * n, 4 * n)
+        c.synchronize()
+        return self._view(ho, np.float32, n).copy()
 
     def scale_optimise(self, sp, params):
         from ._lib import ME_DEVICE
         from .optimisation import scale_optimise
 
         imgs = sp.imgs_handle
-        return scale_optimise(sp, params, ctx=self.ctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
+        return scale_optimise(sp, params, ctx=self.tctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
 
     def ba_solve(self, bp, iters):
-        from .optimisation import SolverOptions, ba_solve
+        self.ba_submit(bp, iters)
+        return self.ba_result()
 
-        return ba_solve(bp, SolverOptions.fixed_iterations(iters), ctx=self.ctx)
+    # ---- staged calls
+    # device result block of a KLT + match: uv (8n) | xr (4n) | status (n) | ok (n)
+    def klt_submit(self, prev, cur, pts):
+        import ctypes
+
+        from ._lib import ME_DEVICE
+        from .klt import klt_params
+
+        n = len(pts)
+        if n == 0:
+            return (0, prev, cur)
+        H, W = prev[2]
+        c = self.tctx
+        hp = self._hbuf("klt_in", 8 * n)
+        self._view(hp, np.float32, 2 * n)[:] = np.asarray(pts, np.float32).ravel()
+        d_in = self._dbuf("klt_in", 8 * n)
+        dres = self._dbuf("res", 14 * n)
+        c.copy_async(d_in, hp, 8 * n)
+        kp = klt_params()
+        c.check(c.lib.me_klt_track(c.h, ME_DEVICE, ctypes.c_void_p(prev[0]), ctypes.c_void_p(cur[0]), W, H, W,
+                                   ctypes.c_void_p(d_in), ctypes.c_void_p(dres), ctypes.c_void_p(dres + 12 * n), n,
+                                   ctypes.byref(kp)), "me_klt_track")
+        return (n, prev, cur)
+
+    def _epipolar(self, imgs, d_uv, d_lo, d_valid, d_status, n, nd, unique, d_xr, d_ok):
+        import ctypes
+
+        H, W = imgs[2]
+        c = self.tctx
+        V = ctypes.c_void_p
+        c.check(c.lib.me_mi_epipolar_match(c.h, V(imgs[0]), V(imgs[1]), W, H, W, V(d_uv), V(d_lo),
+                                           V(d_valid) if d_valid else None, V(d_status) if d_status else None, n, nd,
+                                           PATCH, self.d_max, 1 if unique else 0, 1.2, float(MARGIN), V(d_xr),
+                                           V(d_ok)), "me_mi_epipolar_match")
+
+    def klt_match(self, h, imgs, lo, nd, dvalid):
+        n = h[0]
+        if n == 0:
+            z = np.zeros(0, np.float32)
+            return np.zeros((0, 2), np.float32), np.zeros(0, np.uint8), z, np.zeros(0, bool)
+        c = self.tctx
+        hp = self._hbuf("lo", 5 * n)
+        self._view(hp, np.int32, n)[:] = lo
+        self._view(hp, np.uint8, n, 4 * n)[:] = dvalid
+        dl = self._dbuf("lo", 5 * n)
+        c.copy_async(dl, hp, 5 * n)
+        dres = self._dbuf("res", 14 * n)
+        self._epipolar(imgs, dres, dl, dl + 4 * n, dres + 12 * n, n, nd, False, dres + 8 * n, dres + 13 * n)
+        ho = self._hbuf("out", 14 * n)
+        c.copy_async(ho, dres, 14 * n)
+        c.synchronize()
+        uv = self._view(ho, np.float32, 2 * n).reshape(n, 2).copy()
+        xr = self._view(ho, np.float32, n, 8 * n).copy()
+        st = self._view(ho, np.uint8, n, 12 * n).copy()
+        ok = self._view(ho, np.uint8, n, 13 * n).astype(bool)
+        return uv, st, xr, ok
+
+    def match(self, imgs, uv, lo, nd, unique):
+        n = len(uv)
+        if n == 0:
+            return np.zeros(0, np.float32), np.zeros(0, bool)
+        c = self.tctx
+        hp = self._hbuf("m_in", 12 * n)
+        self._view(hp, np.float32, 2 * n)[:] = np.asarray(uv, np.float32).ravel()
+        self._view(hp, np.int32, n, 8 * n)[:] = lo
+        d = self._dbuf("m", 17 * n)
+        c.copy_async(d, hp, 12 * n)
+        self._epipolar(imgs, d, d + 8 * n, 0, 0, n, nd, unique, d + 12 * n, d + 16 * n)
+        ho = self._hbuf("m_out", 5 * n)
+        c.copy_async(ho, d + 12 * n, 5 * n)
+        c.synchronize()
+        return self._view(ho, np.float32, n).copy(), self._view(ho, np.uint8, n, 4 * n).astype(bool)
+
+    def scale_submit(self, sp, params):
+        self._scale_res = self.scale_optimise(sp, params)
+
+    def ba_submit(self, bp, iters):
+        """Queue the window's solve on the BA context (me_ba_solve_async: the
+        host arrays are staged into page-locked memory at once)."""
+        from ._lib import BAOptionsC  # noqa: F401
+        from .optimisation import SolverOptions, ba_struct
+
+        keep = []
+        p, cams, pts = ba_struct(bp, keep)
+        o = SolverOptions.fixed_iterations(iters).to_c()
+        c = self.ctx
+        import ctypes
+        c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(o)), "me_ba_solve_async")
+        self._ba = (p, o, cams, pts, keep)
+
+    def ba_result(self):
+        import ctypes
+
+        from ._lib import BASummaryC
+        from .optimisation import _summary
+
+        p, o, cams, pts, keep = self._ba
+        self._ba = None
+        s = BASummaryC()
+        c = self.ctx
+        c.check(c.lib.me_ba_wait(c.h, ctypes.byref(s)), "me_ba_wait")
+        return cams, pts, _summary(s)
 
 
 def _cell_jitter(t: int, cells: np.ndarray) -> np.ndarray:
@@ -226,12 +458,19 @@ def _cell_jitter(t: int, cells: np.ndarray) -> np.ndarray:
 class WindowedStereoVO:
     """The loop of the module docstring.  `events` logs the WBA_Point calls
     (("new", id, t, (l, r)), ("add", id, t, (l, r)), ("pop", id), ("del", id))
-    when log_events is set."""
+    when log_events is set.
+
+    overlap=True pipelines the loop without changing any decision: process(t)
+    queues the KLT of frame t first, then completes frame t - 1 (its BA
+    result, the pops, its FrameResult), then matches, books and queues the BA
+    and the scale LM of frame t; call finish() after the last frame.  With
+    overlap=False every process(t) completes frame t before returning."""
 
     def __init__(self, cfg: PipelineConfig, backend: Backend, K=None, first_pose=None, velocity=None,
-                 log_events: bool = False):
+                 log_events: bool = False, overlap: bool = False):
         self.cfg = cfg
         self.be = backend
+        self.be.d_max = cfg.d_max
         self.K = np.asarray(S.intrinsics(cfg.width, cfg.height) if K is None else K, np.float64)
         self.f, self.cx, self.cy = self.K[0, 0], self.K[0, 2], self.K[1, 2]
         # grid of feature cells over the margin-free interior
@@ -253,66 +492,46 @@ class WindowedStereoVO:
         self.prev_imgs = None
         self.prev_t = None
         self.log_events = log_events
-        self.events = []
+        self.overlap = overlap
+        self._ev = []                        # compact event records, expanded by .events
         self.results = []
+        self._pending = None                 # frame whose BA / scale LM are queued
+        self.stage_s = {"host": 0.0, "wait": 0.0}  # host bookkeeping vs time blocked in the backend
+
+    @property
+    def events(self):
+        out = []
+        for rec in self._ev:
+            if rec[0] == "frame":
+                _, ids, t, feats, is_new = rec
+                out.extend(("new" if nw else "add", int(i), t, tuple(float(v) for v in fe))
+                           for i, fe, nw in zip(ids, feats, is_new))
+            else:
+                out.extend((rec[0], int(i)) for i in rec[1])
+        return out
 
     # ---------------------------------------------------------------- matching
-    def stereo_match(self, imgs, uv: np.ndarray, d_pred=None, ratio: float = 1.2, half: int = 6):
-        """MI disparity search for features uv (n, 2) float32 -> (xr float32, ok).
-
-        Tracked features (d_pred given) search +-half px around the disparity
-        their 3-D point predicts at the predicted pose; new features search
-        [d_min, d_max] and must pass a uniqueness test (best MI >= ratio x
-        the best outside +-2 px of it).  Best integer candidate, parabola
-        sub-pixel refinement; the best must be an interior maximum."""
+    def search_window(self, d_pred=None, half: int = 6):
+        """Disparity candidates per feature: tracked features (d_pred given)
+        search +-half px around the disparity their 3-D point predicts at the
+        predicted pose; new features search [d_min, d_max] (uniqueness test).
+        Returns (lo, nd, dvalid)."""
         cfg = self.cfg
-        n = len(uv)
-        if n == 0:
-            return np.zeros(0, np.float32), np.zeros(0, bool)
-        x0 = np.floor(uv[:, 0].astype(np.float64) - W_SCALE).astype(np.int64)  # Rect(x - w, ..) truncation
-        y0 = np.floor(uv[:, 1].astype(np.float64) - W_SCALE).astype(np.int64)
         if d_pred is None:
-            lo = np.full(n, cfg.d_min, np.int64)
-            nd = cfg.d_max - cfg.d_min + 1
-        else:
-            dp = np.where(np.isfinite(d_pred), d_pred, -1e9)
-            lo = np.clip(np.rint(dp).astype(np.int64) - half, cfg.d_min, cfg.d_max)
-            nd = 2 * half + 1
-        d = lo[:, None] + np.arange(nd, dtype=np.int64)[None, :]
-        xr = x0[:, None] - d
-        valid = (xr >= 0) & (d <= cfg.d_max)
-        if d_pred is not None:
-            valid &= np.isfinite(d_pred)[:, None] & (d_pred > 0)[:, None]
-        xr_c = np.where(valid, xr, 0)
-        xyL = np.stack([np.repeat(x0, nd), np.repeat(y0, nd)], -1)
-        xyR = np.stack([xr_c.ravel(), np.repeat(y0, nd)], -1)
-        sc = self.be.mi_scores(imgs, xyL, xyR).reshape(n, nd).astype(np.float64)
-        sc = np.where(valid, sc, -np.inf)
-        with np.errstate(invalid="ignore", divide="ignore"):  # -inf candidates (outside the image)
-            return self._pick(uv, d, sc, nd, d_pred, ratio)
+            return None, cfg.d_max - cfg.d_min + 1, None
+        dp = np.where(np.isfinite(d_pred), d_pred, -1e9)
+        lo = np.clip(np.rint(dp).astype(np.int64) - half, cfg.d_min, cfg.d_max)
+        with np.errstate(invalid="ignore"):
+            dvalid = np.isfinite(d_pred) & (d_pred > 0)
+        return lo, 2 * half + 1, dvalid
 
-    def _pick(self, uv, d, sc, nd, d_pred, ratio):
+    def stereo_match(self, imgs, uv: np.ndarray, d_pred=None, ratio: float = 1.2, half: int = 6):
+        """MI disparity search for features uv (n, 2) float32 -> (xr float32, ok)."""
         n = len(uv)
-        rows = np.arange(n)
-        k = np.argmax(sc, axis=1)
-        best = sc[rows, k]
-        ok = (k > 0) & (k < nd - 1) & np.isfinite(best)
-        kk = np.clip(k, 1, nd - 2)
-        s_m, s_0, s_p = sc[rows, kk - 1], sc[rows, kk], sc[rows, kk + 1]
-        den = s_m - 2 * s_0 + s_p
-        ok &= np.isfinite(s_m) & np.isfinite(s_p) & (den < 0)
-        if d_pred is None:  # uniqueness against the best candidate outside +-2 px
-            m = sc.copy()
-            for j in range(-2, 3):
-                m[rows, np.clip(k + j, 0, nd - 1)] = -np.inf
-            second = m.max(axis=1)
-            ok &= best >= ratio * second
-        den_s = np.where(ok, den, -1.0)
-        delta = np.where(ok, 0.5 * (s_m - s_p) / den_s, 0.0)
-        disp = d[rows, kk].astype(np.float64) + delta
-        xr_f = (uv[:, 0].astype(np.float64) - disp).astype(np.float32)
-        ok &= xr_f >= MARGIN
-        return xr_f, ok
+        lo, nd, dvalid = self.search_window(d_pred, half)
+        if lo is None:
+            lo = np.full(n, self.cfg.d_min, np.int64)
+        return match_host(self.be, imgs, uv, lo, nd, dvalid, d_pred is None, self.cfg.d_max, ratio)
 
     def _predicted_disparity(self, idx, pose):
         R = aa_to_R(pose[3:])
@@ -322,9 +541,7 @@ class WindowedStereoVO:
 
     # ---------------------------------------------------------------- helpers
     def _in_margin(self, uv):
-        cfg = self.cfg
-        return ((uv[:, 0] >= MARGIN) & (uv[:, 0] < cfg.width - MARGIN) & (uv[:, 1] >= MARGIN)
-                & (uv[:, 1] < cfg.height - MARGIN))
+        return in_margin(uv, self.cfg.width, self.cfg.height)
 
     def _predict_pose(self, t):
         if t == 0:
@@ -355,28 +572,42 @@ class WindowedStereoVO:
         self.last = np.concatenate([self.last, np.full(n, t, np.int64)])
         return np.arange(len(self.ids) - n, len(self.ids), dtype=np.int64)
 
+    def _wait(self, fn, *a):
+        import time
+        t0 = time.perf_counter()
+        r = fn(*a)
+        self.stage_s["wait"] += time.perf_counter() - t0
+        return r
+
     # ---------------------------------------------------------------- one keyframe
-    def process(self, t: int, left: np.ndarray, right: np.ndarray) -> FrameResult:
+    def process(self, t: int, left: np.ndarray, right: np.ndarray):
+        import time
+        t_in = time.perf_counter()
+        w0 = self.stage_s["wait"]
         cfg = self.cfg
         imgs = self.be.frame_images(t, left, right)
-        pose = self._predict_pose(t)
-        self.poses[t] = pose
-        trk_idx = np.zeros(0, np.int64)
-        trk_uv = np.zeros((0, 2), np.float32)
-        # 1. KLT of the active tracks
+        # 1. KLT of the active tracks, queued first (it needs only frame t-1's features)
+        kh = None
         if self.prev_imgs is not None and self.active.any():
             act = np.flatnonzero(self.active)
             pi, puv = self.obs[self.prev_t]
             pos = np.searchsorted(pi, act)
-            prev_uv = np.ascontiguousarray(puv[pos, :2])
-            uv, st = self.be.klt(self.prev_imgs, imgs, prev_uv)
+            kh = self.be.klt_submit(self.prev_imgs, imgs, np.ascontiguousarray(puv[pos, :2]))
+        self._complete()  # frame t-1: BA result, pops (active tracks keep their order)
+        pose = self._predict_pose(t)
+        self.poses[t] = pose
+        trk_idx = np.zeros(0, np.int64)
+        trk_uv = np.zeros((0, 2), np.float32)
+        xr = np.zeros(0, np.float32)
+        if kh is not None:
+            # 2. KLT gate + stereo matching of the tracked features (around their predicted disparity)
+            act = np.flatnonzero(self.active)
+            lo, nd, dvalid = self.search_window(self._predicted_disparity(act, pose))
+            uv, st, xr_all, ok = self._wait(self.be.klt_match, kh, imgs, lo, nd, dvalid)
             keep = (st == 1) & self._in_margin(uv)
-            self.active[act[~keep]] = False
-            trk_idx, trk_uv = act[keep], uv[keep]
-        # 2. stereo matching of the tracked features (around their predicted disparity)
-        xr, ok = self.stereo_match(imgs, trk_uv, self._predicted_disparity(trk_idx, pose))
-        self.active[trk_idx[~ok]] = False
-        trk_idx, trk_uv, xr = trk_idx[ok], trk_uv[ok], xr[ok]
+            good = keep & ok
+            self.active[act[~good]] = False
+            trk_idx, trk_uv, xr = act[good], uv[good], xr_all[good]
         n_tracked = len(trk_idx)
         # 3a. new tracks in empty cells
         occ = np.zeros(self.nx * self.ny, bool)
@@ -387,7 +618,8 @@ class WindowedStereoVO:
         empty = np.flatnonzero(~occ)[: max(0, cfg.n_feats - n_tracked)]
         cyx = np.stack([empty % self.nx, empty // self.nx], -1).astype(np.float64)
         nuv = (MARGIN + (cyx + 0.5 + _cell_jitter(t, empty)) * np.array([self.cw, self.ch])).astype(np.float32)
-        nxr, nok = self.stereo_match(imgs, nuv)
+        _, nd_new, _ = self.search_window()
+        nxr, nok = self._wait(self.be.match, imgs, nuv, np.full(len(nuv), cfg.d_min, np.int64), nd_new, True)
         nuv, nxr = nuv[nok], nxr[nok]
         new_idx = self._add_tracks(t, nuv, nxr, pose)
         # 3b. this frame's features (tracked first, then new; sorted by track = ID order)
@@ -401,21 +633,38 @@ class WindowedStereoVO:
         if self.log_events:
             is_new = np.zeros(len(self.ids), bool)
             is_new[new_idx] = True
-            for i, fe in zip(idx, feats):
-                self.events.append(("new" if is_new[i] else "add", int(self.ids[i]), t, tuple(float(v) for v in fe)))
-        # 5. scale LM over the tracks seen in t
-        sc = self._scale(t, imgs, idx)
-        # 6. windowed BA
-        nwp, nwo, bs = self._ba(t)
-        # 3c. pop the features that leave the window with the next keyframe
-        self._pop(t + 1 - cfg.window)
+            self._ev.append(("frame", self.ids[idx].copy(), t, feats.copy(), is_new[idx]))
+        # 5./6. windowed BA queued, then the scale LM over the tracks seen in t (beside the BA)
+        ba = self._ba_submit(t)
+        self._scale_submit(t, imgs, idx)
+        self._pending = (t, n_tracked, len(new_idx), int(self.active.sum()), ba)
         self.prev_imgs, self.prev_t = imgs, t
-        r = FrameResult(t, n_tracked, len(new_idx), int(self.active.sum()), nwp, nwo, sc["scale"], int(sc["stop"]),
-                        int(sc["iterations"]), int(bs["iterations"]), float(bs["final_cost"]), self.poses[t].copy())
-        self.results.append(r)
-        return r
+        if not self.overlap:
+            self._complete()
+        self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
 
-    def _scale(self, t, imgs, idx):
+    def finish(self):
+        """Complete the last queued frame (overlap mode)."""
+        import time
+        t_in = time.perf_counter()
+        w0 = self.stage_s["wait"]
+        self._complete()
+        self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
+
+    def _complete(self):
+        if self._pending is None:
+            return
+        t, n_tracked, n_new, n_active, ba = self._pending
+        self._pending = None
+        sc = self._wait(self.be.scale_result)
+        nwp, nwo, bs = self._ba_finish(ba)
+        # 3c. pop the features that leave the window with the next keyframe
+        self._pop(t + 1 - self.cfg.window)
+        self.results.append(FrameResult(t, n_tracked, n_new, n_active, nwp, nwo, sc["scale"], int(sc["stop"]),
+                                        int(sc["iterations"]), int(bs["iterations"]), float(bs["final_cost"]),
+                                        self.poses[t].copy()))
+
+    def _scale_submit(self, t, imgs, idx):
         from .optimisation import OptimisationParams
 
         pose = self.poses[t]
@@ -428,45 +677,70 @@ class WindowedStereoVO:
                             pose[:3].copy(), q.copy(), pose[:3].copy(), 1.0, self.cfg.baseline, W_SCALE, imgs[3],
                             imgs[4])
         sp.imgs_handle = imgs
-        return self.be.scale_optimise(sp, OptimisationParams.fixed_iterations(self.cfg.scale_iters))
+        self._wait(self.be.scale_submit, sp, OptimisationParams.fixed_iterations(self.cfg.scale_iters))
 
-    def _ba(self, t):
+    def _ba_submit(self, t):
+        """The window's BA problem in initialiseObservations order
+        (BundleAdjuster.h:354-376: points in track order, each track's
+        features in frame order), built in O(observations): the window's
+        points are the tracks seen in [f0, t] (last >= f0), their features
+        are contiguous in frames (addMatch, feature_types.h:140), so track
+        j's features land at offset_j + (f - max(first_j, f0))."""
         cfg = self.cfg
         f0 = max(0, t - cfg.window + 1)
-        frames = [f for f in range(f0, t + 1) if f in self.obs]
         if t - f0 + 1 <= cfg.fixed_frames:
-            return 0, 0, {"iterations": 0, "final_cost": float("nan")}
-        ti = np.concatenate([self.obs[f][0] for f in frames])
-        fe = np.concatenate([self.obs[f][1] for f in frames])
-        fr = np.concatenate([np.full(len(self.obs[f][0]), f, np.int64) for f in frames])
-        # initialiseObservations order (BundleAdjuster.h:354-376): points in track order, features in frame order
-        o = np.lexsort((fr, ti))
-        ti, fe, fr = ti[o], fe[o], fr[o]
-        upts, pt_idx = np.unique(ti, return_inverse=True)
+            return None
+        win = self.last >= f0
+        upts = np.flatnonzero(win)
+        local = np.cumsum(win) - 1                  # table index -> window point index
+        first = np.maximum(self.first[upts], f0)
+        cnt = self.last[upts] - first + 1
+        off = np.zeros(len(cnt) + 1, np.int64)
+        np.cumsum(cnt, out=off[1:])
+        n_obs = int(off[-1])
+        fe = np.empty((n_obs, 4), np.float64)
+        cam = np.empty(n_obs, np.int32)
+        pti = np.empty(n_obs, np.int32)
+        seen = 0
+        for f in range(f0, t + 1):
+            if f not in self.obs:
+                continue
+            i, feats = self.obs[f]
+            j = local[i]
+            q = off[j] + (f - first[j])
+            fe[q] = feats
+            cam[q] = f - f0
+            pti[q] = j
+            seen += len(i)
+        assert seen == n_obs, "window tracks must have contiguous features in the window"
         cams = np.stack([self.poses[f] for f in range(f0, t + 1)])
-        bp = S.BAProblem(cams, self.X[upts].copy(), fe.astype(np.float64), (fr - f0).astype(np.int32),
-                         pt_idx.astype(np.int32), self.K.copy(), self.K.copy(), cfg.baseline, cfg.feat_var,
+        bp = S.BAProblem(cams, self.X[upts], fe, cam, pti, self.K.copy(), self.K.copy(), cfg.baseline, cfg.feat_var,
                          cfg.fixed_frames)
-        c, p, s = self.be.ba_solve(bp, cfg.ba_iters)
+        self._wait(self.be.ba_submit, bp, cfg.ba_iters)
+        return (t, f0, upts, n_obs)
+
+    def _ba_finish(self, ba):
+        if ba is None:
+            return 0, 0, {"iterations": 0, "final_cost": float("nan")}
+        t, f0, upts, nobs = ba
+        c, p, s = self._wait(self.be.ba_result)
         if s.get("status", 2) == 2:
             for k, f in enumerate(range(f0, t + 1)):
                 self.poses[f] = np.asarray(c[k], np.float64).copy()
             self.X[upts] = p
-        return len(upts), len(ti), s
+        return len(upts), nobs, s
 
     def _pop(self, new_first):
         """WBA_Point::pop() of every feature older than `new_first`; empty tracks deleted."""
         for f in [f for f in self.obs if f < new_first]:
             idx, _ = self.obs.pop(f)
             if self.log_events:
-                for i in idx:
-                    self.events.append(("pop", int(self.ids[i])))
+                self._ev.append(("pop", self.ids[idx].copy()))
             self.first[idx] = f + 1
         dead = (self.last < new_first)
         if dead.any():
             if self.log_events:
-                for i in np.flatnonzero(dead):
-                    self.events.append(("del", int(self.ids[i])))
+                self._ev.append(("del", self.ids[np.flatnonzero(dead)].copy()))
             keep = ~dead
             remap = np.cumsum(keep) - 1
             self.ids, self.X, self.active = self.ids[keep], self.X[keep], self.active[keep]
@@ -474,13 +748,16 @@ class WindowedStereoVO:
             self.obs = {f: (remap[i], fe) for f, (i, fe) in self.obs.items()}
 
 
-def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_div: int = 1):
-    """Stereo keyframes of config c's synthetic trajectory (0.5 m forward and
-    0.3 deg yaw per keyframe), the true first pose and the per-frame motion
-    prior used for the second keyframe."""
+def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_div: int = 1, first_id: int = 0):
+    """Stereo keyframes of config c's synthetic sequence (0.5 m forward along
+    the heading and 0.3 deg yaw per keyframe: the arc through the ring
+    corridor, synthetic.trajectory_arc, any length), the true first pose and
+    the per-frame motion prior used for the second keyframe.  first_id starts
+    the sequence at keyframe first_id of the arc (chunked long runs)."""
     cfg = S.CONFIGS[c]
     seed = S.SEED0 + c if seed is None else seed
-    scene, K, frames = S.stereo_stream(seed, cfg["width"], cfg["height"], n_frames, render_div=render_div)
+    scene, K, frames = S.stereo_stream(seed, cfg["width"], cfg["height"], n_frames, first_id=first_id,
+                                       render_div=render_div, scene_kind="corridor")
     poses = []
     for fr in frames:
         poses.append(np.concatenate([fr.t, S.R_to_aa(fr.R)]))

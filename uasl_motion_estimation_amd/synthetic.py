@@ -17,6 +17,7 @@ and of bench.py is generated here from a seed (seed = 20261015 + config):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -270,17 +271,27 @@ def render(scene: Scene, K, R, t, width, height, shift=0.0):
     Rw = R.T
     C = -Rw @ t + Rw @ np.array([shift, 0.0, 0.0])
     dw = d @ Rw.T
+    # nearest plane per pixel first (the first plane reaching the minimum
+    # depth, as a sequential s < best scan), then the texture once per pixel
+    # at that plane's hit point: the same values as texturing every plane
     best = np.full(u.shape, np.inf)
-    tex = np.zeros(u.shape)
-    for (x0, x1, Z) in scene.planes:
+    which = np.full(u.shape, -1, np.int32)
+    for k, (x0, x1, Z) in enumerate(scene.planes):
         s = (Z - C[2]) / dw[..., 2]
         X = C[0] + s * dw[..., 0]
-        Y = C[1] + s * dw[..., 1]
         hit = (s > 0) & (X >= x0) & (X < x1) & (s < best)
-        if hit.any():
-            best = np.where(hit, s, best)
-            val = _value_noise(X, Y, scene.seed)
-            tex = np.where(hit, val, tex)
+        best = np.where(hit, s, best)
+        which = np.where(hit, k, which)
+    tex = np.zeros(u.shape)
+    for k, (x0, x1, Z) in enumerate(scene.planes):
+        m = which == k
+        if not m.any():
+            continue
+        dwm = dw[m]
+        s = (Z - C[2]) / dwm[:, 2]
+        X = C[0] + s * dwm[:, 0]
+        Y = C[1] + s * dwm[:, 1]
+        tex[m] = _value_noise(X, Y, scene.seed)
     img = np.clip(np.rint(tex * 255.0), 0, 255).astype(np.uint8)
     return img
 
@@ -301,6 +312,88 @@ def depth_at(scene: Scene, K, R, t, u, v):
     return best, Xw
 
 
+# ------------------------------------------------------------------ long sequences
+# The strip scene above is a short-window fixture: the straight forward path
+# flies through its planes within ~40 keyframes.  Long sequences (the
+# config-5 10k-frame stream) use a heading-consistent arc -- 0.5 m chord and
+# 0.3 deg yaw per keyframe, a circle of radius 0.5 / (2 sin 0.15 deg) = 95.5 m
+# (1200 keyframes per lap) -- inside a ring corridor that follows it: floor,
+# ceiling and two cylindrical walls 6 m to either side, value-noise
+# textured, so every keyframe sees the same kind of structure at 5-35 m.
+YAW_STEP_DEG = 0.3
+
+
+def arc_radius(step: float = 0.5, yaw_deg: float = YAW_STEP_DEG) -> float:
+    return step / (2.0 * math.sin(math.radians(yaw_deg) / 2.0))
+
+
+def trajectory_arc(n: int, first_id: int = 0):
+    """World->camera poses (R, t) on the arc: camera centre C(psi) =
+    (R0 (1 - cos psi), 0, R0 sin psi), heading = camera z, psi = 0.3 deg k."""
+    R0 = arc_radius()
+    poses = []
+    for i in range(n):
+        psi = math.radians(YAW_STEP_DEG) * (first_id + i)
+        Rw = rot_y(psi)
+        C = np.array([R0 * (1.0 - math.cos(psi)), 0.0, R0 * math.sin(psi)])
+        R = Rw.T
+        poses.append((R, -R @ C))
+    return poses
+
+
+@dataclass
+class CorridorScene:
+    seed: int
+    radius: float                 # trajectory radius (corridor centre line)
+    half_width: float = 6.0       # walls at radius -+ half_width
+    floor_y: float = 1.6          # (y points down: the floor is below the camera)
+    ceil_y: float = -3.0
+
+
+def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
+    u, v = np.meshgrid(np.arange(width, dtype=np.float64), np.arange(height, dtype=np.float64))
+    d = np.stack([(u - K[0, 2]) / K[0, 0], (v - K[1, 2]) / K[1, 1], np.ones_like(u)], -1)
+    Rw = R.T
+    C = -Rw @ t + Rw @ np.array([shift, 0.0, 0.0])
+    dw = (d @ Rw.T).reshape(-1, 3)
+    n = dw.shape[0]
+    best = np.full(n, np.inf)
+    surf = np.full(n, -1, np.int32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for k, y in enumerate((scene.floor_y, scene.ceil_y)):
+            s = (y - C[1]) / dw[:, 1]
+            hit = (s > 0) & (s < best)
+            best = np.where(hit, s, best)
+            surf = np.where(hit, k, surf)
+        O = np.array([scene.radius, 0.0, 0.0])
+        ox, oz = C[0] - O[0], C[2] - O[2]
+        a = dw[:, 0] ** 2 + dw[:, 2] ** 2
+        bq = 2.0 * (ox * dw[:, 0] + oz * dw[:, 2])
+        for k, r in ((2, scene.radius - scene.half_width), (3, scene.radius + scene.half_width)):
+            c = ox * ox + oz * oz - r * r
+            disc = bq * bq - 4.0 * a * c
+            sq = np.sqrt(np.maximum(disc, 0.0))
+            s1 = (-bq - sq) / (2.0 * a)
+            s2 = (-bq + sq) / (2.0 * a)
+            s = np.where(s1 > 0, s1, s2)
+            hit = (disc >= 0) & (s > 0) & (s < best)
+            best = np.where(hit, s, best)
+            surf = np.where(hit, k, surf)
+    tex = np.zeros(n)
+    for k in range(4):
+        m = surf == k
+        if not m.any():
+            continue
+        P = C[None, :] + best[m, None] * dw[m]
+        if k < 2:  # floor / ceiling: world (x, z)
+            cu, cv = P[:, 0], P[:, 2]
+        else:      # walls: arc length, height
+            r = scene.radius + (-1 if k == 2 else 1) * scene.half_width
+            cu, cv = r * np.arctan2(P[:, 2] - O[2], P[:, 0] - O[0]), P[:, 1]
+        tex[m] = _value_noise(cu, cv, scene.seed * 4 + k)
+    return np.clip(np.rint(tex.reshape(height, width) * 255.0), 0, 255).astype(np.uint8)
+
+
 @dataclass
 class StereoFrame:
     left: np.ndarray
@@ -309,12 +402,15 @@ class StereoFrame:
     t: np.ndarray
 
 
-def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: int = 0, render_div: int = 1):
+def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: int = 0, render_div: int = 1,
+                  scene_kind: str = "strips"):
     """Stereo keyframes of the synthetic trajectory.  render_div > 1 renders
     each image at 1/render_div resolution and replicates pixels (4K test
     inputs in seconds instead of minutes; the geometry -- intrinsics, poses,
-    depth_at -- stays at full resolution)."""
-    scene = make_scene(seed)
+    depth_at -- stays at full resolution).  scene_kind "corridor": the arc
+    trajectory in the ring corridor (long sequences, see trajectory_arc)."""
+    corridor = scene_kind == "corridor"
+    scene = CorridorScene(seed, arc_radius()) if corridor else make_scene(seed)
     K = intrinsics(width, height)
     lut = tone_map()
     frames = []
@@ -322,16 +418,27 @@ def stereo_stream(seed: int, width: int, height: int, n_frames: int, first_id: i
     w_r, h_r = -(-width // d), -(-height // d)
     K_r = intrinsics(w_r, h_r)
 
+    rf = render_corridor if corridor else render
+
     def rend(R, t, shift=0.0):
         if d == 1:
-            return render(scene, K, R, t, width, height, shift=shift)
-        img = render(scene, K_r, R, t, w_r, h_r, shift=shift)
+            return rf(scene, K, R, t, width, height, shift=shift)
+        img = rf(scene, K_r, R, t, w_r, h_r, shift=shift)
         return np.ascontiguousarray(np.kron(img, np.ones((d, d), np.uint8))[:height, :width])
 
-    for (R, t) in trajectory(n_frames, first_id):
-        L = rend(R, t)
-        Rraw = rend(R, t, shift=BASELINE)
-        frames.append(StereoFrame(L, lut[Rraw], R, t))
+    poses = list(trajectory_arc(n_frames, first_id) if corridor else trajectory(n_frames, first_id))
+    jobs = [(R, t, sh) for (R, t) in poses for sh in (0.0, BASELINE)]
+    # images are independent: rendered by a thread pool (numpy releases the GIL in the array work)
+    workers = min(len(jobs), 16, os.cpu_count() or 1)
+    if workers > 1:
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(workers) as ex:
+            imgs = list(ex.map(lambda j: rend(*j), jobs))
+    else:
+        imgs = [rend(*j) for j in jobs]
+    for k, (R, t) in enumerate(poses):
+        frames.append(StereoFrame(imgs[2 * k], lut[imgs[2 * k + 1]], R, t))
     return scene, K, frames
 
 
