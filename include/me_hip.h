@@ -274,6 +274,15 @@ int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_sum
    readable by me_ba_wait). */
 int me_ba_solve_async(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o);
 int me_ba_wait(me_ctx* ctx, me_ba_summary* s);
+/* BundleAdjuster<M>::initialiseObservations (BundleAdjuster.h:354-376) for a
+   device-resident window: observation i was seen in frame[i] by the track
+   ids[i]; cam_idx[i] = frame[i] - first_frame and pt_idx[i] = the position of
+   ids[i] in win_ids (the window's track IDs, ascending), -1 if absent.  All
+   arrays device memory; asynchronous on the ctx stream.  With the
+   observations stored frame by frame, a sliding window appends one keyframe's
+   observations per step and re-indexes on the device. */
+int me_ba_window_indices(me_ctx* ctx, const int32_t* frame, const int32_t* ids, int n_obs, int first_frame,
+                         const int32_t* win_ids, int n_pts, int32_t* cam_idx, int32_t* pt_idx);
 /* Cost (Ceres ½Σρ) at the problem's current parameters. */
 int me_ba_cost(me_ctx* ctx, const me_ba_problem* p, double* cost);
 /* Residuals (sigma-scaled, uncorrected) and Jacobian blocks per observation:

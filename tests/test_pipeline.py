@@ -144,7 +144,7 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
     and the full [d_min, d_max] range with the uniqueness test (new form)."""
     from pipeline_oracle import OracleBackend
 
-    fr = PL.synthetic_sequence(3, 1)[0]
+    fr = PL.synthetic_sequence(3, 2)[0]
     be = PL.GPUBackend(ctx)
     try:
         imgs = be.frame_images(0, fr[0].left, fr[0].right)
@@ -160,7 +160,7 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
             nd = 13
             dvalid = rng.random(n) > 0.1
             # tracked form with per-feature validity (device layout uv | lo | xr | valid | ok)
-            c = be.tctx
+            c = be.mctx  # (the stream the backend's matcher runs on)
             d = be._dbuf("t_uv", 18 * n)
             hp = be._hbuf("t_uv", 18 * n)
             be._view(hp, np.float32, 2 * n)[:] = uv.ravel()

@@ -123,7 +123,7 @@ EXPORTS = [
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
-    "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait",
+    "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_window_indices",
     "me_comm_unique_id", "me_comm_create_rccl", "me_comm_create_callback", "me_comm_destroy", "me_comm_info",
     "me_comm_allreduce", "me_ba_solve_comm",
     "me_klt_default_params", "me_klt_track",
@@ -203,6 +203,8 @@ def load_library(path: str = LIB_PATH):
         "me_ba_solve_async": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC)]),
         "me_ba_wait": (c_int, [c_void_p, P(BASummaryC)]),
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
+        "me_ba_window_indices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
+                                         c_void_p]),
         "me_ba_evaluate": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_double), P(c_double)]),
         "me_ba_reduced_system": (c_int, [c_void_p, P(BAProblemC), c_double, P(c_double), P(c_double)]),
         "me_ba_covariance": (c_int, [c_void_p, P(BAProblemC), P(c_double), P(c_int)]),

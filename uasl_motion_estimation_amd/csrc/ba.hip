@@ -3208,6 +3208,40 @@ extern "C" int me_ba_covariance(me_ctx* c, const me_ba_problem* p, double* cov, 
   return ME_OK;
 }
 
+// BundleAdjuster<M>::initialiseObservations on the device
+// (BundleAdjuster.h:354-376): for a window whose observations are stored by
+// frame and track ID, camIdx = frame - first_frame and ptIdx = the track's
+// index among the window's tracks (win_ids ascending: the order of the
+// reference's observations vector).  One thread per observation, binary
+// search over win_ids; an ID absent from the window gets -1 (the BA plan then
+// reports bad input).
+__global__ void window_indices_kernel(const int32_t* __restrict__ frame, const int32_t* __restrict__ ids, int n_obs,
+                                      int f0, const int32_t* __restrict__ win_ids, int n_pts,
+                                      int32_t* __restrict__ cam_idx, int32_t* __restrict__ pt_idx) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_obs) return;
+  const int32_t id = ids[i];
+  int lo = 0, hi = n_pts;  // first win_ids[k] >= id
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (win_ids[mid] < id) lo = mid + 1;
+    else hi = mid;
+  }
+  cam_idx[i] = frame[i] - f0;
+  pt_idx[i] = (lo < n_pts && win_ids[lo] == id) ? lo : -1;
+}
+
+extern "C" int me_ba_window_indices(me_ctx* c, const int32_t* frame, const int32_t* ids, int n_obs, int first_frame,
+                                    const int32_t* win_ids, int n_pts, int32_t* cam_idx, int32_t* pt_idx) {
+  if (!c) return ME_ERR_INVALID;
+  ME_CHECK(c, n_obs >= 0 && n_pts >= 0, "me_ba_window_indices: bad sizes");
+  if (n_obs == 0) return ME_OK;
+  ME_HIP(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(window_indices_kernel, dim3(blocks(n_obs, kBlock)), dim3(kBlock), 0, c->stream, frame, ids, n_obs,
+                     first_frame, win_ids, n_pts, cam_idx, pt_idx);
+  return me_check_launch(c, "window_indices_kernel");
+}
+
 extern "C" int me_debug_read(me_ctx* c, long long* out, int n) {
   if (!c || n < 0 || n > 16) return ME_ERR_INVALID;
   std::memcpy(out, c->dbg, 8 * (size_t)n);

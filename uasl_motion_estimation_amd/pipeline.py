@@ -212,6 +212,15 @@ class Backend:
         r, self._ba_res = self._ba_res, None
         return r
 
+    # ---- device-resident BA window (GPU): observations appended per keyframe
+    device_window = False
+
+    def window_add(self, t, ids, feats):
+        pass
+
+    def window_pop(self, t):
+        pass
+
 
 class GPUBackend(Backend):
     """libme_hip.so through the C ABI; images resident in HBM (one upload per
@@ -221,13 +230,35 @@ class GPUBackend(Backend):
     and page-locked staging are persistent (grow-only); per stage one H2D and
     one D2H."""
 
-    def __init__(self, ctx=None, tctx=None, overlap: bool = True):
+    def __init__(self, ctx=None, tctx=None, overlap: bool = True, front_cus: int = 4, match_on_ba: bool = True):
         from ._lib import Context, default_context
 
         self.ctx = ctx or default_context()
         self._own_t = tctx is None and overlap
         self.tctx = tctx or (Context(self.ctx.device) if overlap else self.ctx)
+        # the two contexts run side by side on disjoint CU sets (CU i with
+        # i % 16 < front_cus: front end; every XCD keeps CUs of both): the
+        # persistent scale-LM kernel needs its workgroups co-resident, which
+        # the BA's kernels on shared CUs would not leave room for
+        self._masked = False
+        if self.tctx is not self.ctx and 0 < front_cus < 16:
+            import torch
+
+            ncu = torch.cuda.get_device_properties(self.ctx.device).multi_processor_count
+            self.tctx.set_cu_mask([i for i in range(ncu) if i % 16 < front_cus])
+            self.ctx.set_cu_mask([i for i in range(ncu) if i % 16 >= front_cus])
+            self._masked = True
+        # the matchers sit on the loop's critical path between two BAs, when
+        # the BA context is idle: they run there (its larger CU share)
+        self.mctx = self.ctx if match_on_ba else self.tctx
         self._imgs = {}
+        # device-resident BA window: obs (4 doubles) | frame | track ID per
+        # observation, frame by frame; [_wstart, _wend) live in store _wcur
+        self._wcap = 0
+        self._wstore = [None, None]
+        self._wcur = 0
+        self._wend = 0
+        self._wfrm = {}  # frame -> (offset, count)
         self._dev = {}   # name -> [ptr, bytes] on the device
         self._pin = {}   # name -> [ptr, bytes] page-locked host
         self._ba = None
@@ -286,6 +317,10 @@ class GPUBackend(Backend):
     def close(self):
         if self._ba is not None:
             self.ba_result()
+        for st in self._wstore:
+            if st is not None:
+                self.ctx.free(st)
+        self._wstore = [None, None]
         for t in list(self._imgs):
             self.release(t)
         self.tctx.synchronize()
@@ -294,6 +329,10 @@ class GPUBackend(Backend):
         for p, _ in self._pin.values():
             self.tctx.host_free(p)
         self._dev, self._pin = {}, {}
+        if self._masked:
+            self.ctx.set_cu_mask(None)
+            self.tctx.set_cu_mask(None)
+            self._masked = False
         if self._own_t:
             self.tctx.close()
             self._own_t = False
@@ -369,7 +408,7 @@ class GPUBackend(Backend):
         import ctypes
 
         H, W = imgs[2]
-        c = self.tctx
+        c = self.mctx
         V = ctypes.c_void_p
         c.check(c.lib.me_mi_epipolar_match(c.h, V(imgs[0]), V(imgs[1]), W, H, W, V(d_uv), V(d_lo),
                                            V(d_valid) if d_valid else None, V(d_status) if d_status else None, n, nd,
@@ -381,7 +420,9 @@ class GPUBackend(Backend):
         if n == 0:
             z = np.zeros(0, np.float32)
             return np.zeros((0, 2), np.float32), np.zeros(0, np.uint8), z, np.zeros(0, bool)
-        c = self.tctx
+        c = self.mctx
+        if c is not self.tctx:
+            self.tctx.synchronize()  # the KLT results
         hp = self._hbuf("lo", 5 * n)
         self._view(hp, np.int32, n)[:] = lo
         self._view(hp, np.uint8, n, 4 * n)[:] = dvalid
@@ -402,7 +443,7 @@ class GPUBackend(Backend):
         n = len(uv)
         if n == 0:
             return np.zeros(0, np.float32), np.zeros(0, bool)
-        c = self.tctx
+        c = self.mctx
         hp = self._hbuf("m_in", 12 * n)
         self._view(hp, np.float32, 2 * n)[:] = np.asarray(uv, np.float32).ravel()
         self._view(hp, np.int32, n, 8 * n)[:] = lo
@@ -417,6 +458,102 @@ class GPUBackend(Backend):
     def scale_submit(self, sp, params):
         self._scale_res = self.scale_optimise(sp, params)
 
+    # ---- device-resident BA window
+    device_window = True
+
+    def _wview(self, k):
+        """(obs, frame, id) device pointers of store k (capacity _wcap)."""
+        base = self._wstore[k]
+        return base, base + 32 * self._wcap, base + 36 * self._wcap
+
+    def window_add(self, t, ids, feats):
+        """Append keyframe t's observations (one H2D); the live window is
+        compacted into the other store when the tail is full (no BA is in
+        flight here: the loop completes frame t - 1 first)."""
+        n = len(ids)
+        live0 = min((o for o, _ in self._wfrm.values()), default=self._wend)
+        live = self._wend - live0
+        c = self.ctx
+        if self._wend + n > self._wcap:
+            cap = max(1 << 16, 2 * (live + n), self._wcap)
+            k = 1 - self._wcur
+            if self._wstore[k] is not None:
+                c.free(self._wstore[k])
+            old = self._wcap
+            self._wstore[k] = c.malloc(40 * cap)
+            if live:
+                ob, fb, ib = self._wstore[self._wcur], self._wstore[self._wcur] + 32 * old, \
+                    self._wstore[self._wcur] + 36 * old
+                self._wcap = cap
+                no, nf, ni = self._wview(k)
+                c.d2d(no, ob + 32 * live0, 32 * live)
+                c.d2d(nf, fb + 4 * live0, 4 * live)
+                c.d2d(ni, ib + 4 * live0, 4 * live)
+            self._wcap = cap
+            self._wcur = k
+            self._wfrm = {f: (o - live0, m) for f, (o, m) in self._wfrm.items()}
+            self._wend = live
+        if n:
+            hp = self._hbuf("w_add", 40 * n)
+            self._view(hp, np.float64, 4 * n)[:] = np.asarray(feats, np.float64).ravel()
+            self._view(hp, np.int32, n, 32 * n)[:] = t
+            self._view(hp, np.int32, n, 36 * n)[:] = ids
+            o, f, i = self._wview(self._wcur)
+            e = self._wend
+            c.copy_async(o + 32 * e, hp, 32 * n)
+            c.copy_async(f + 4 * e, hp + 32 * n, 4 * n)
+            c.copy_async(i + 4 * e, hp + 36 * n, 4 * n)
+        self._wfrm[t] = (self._wend, n)
+        self._wend += n
+
+    def window_pop(self, t):
+        self._wfrm.pop(t, None)
+
+    def ba_submit_window(self, t, f0, win_ids, X, cams, iters):
+        """Queue the BA of the device-resident window [f0, t]: the window's
+        track IDs, points and cameras go up (one H2D), the observation indices
+        are built on the device (me_ba_window_indices), the solve runs on the
+        device-resident problem (me_ba_solve_async, ME_DEVICE)."""
+        import ctypes
+
+        from ._lib import ME_DEVICE, BAProblemC
+        from .optimisation import SolverOptions
+
+        off0 = self._wfrm[f0][0]
+        n_obs = self._wend - off0
+        npts, nc = len(win_ids), len(cams)
+        c = self.ctx
+        V = ctypes.c_void_p
+        # cams | pts (solved in place) | win_ids, one page-locked block and one H2D
+        nb = 48 * nc + 24 * npts + 4 * npts
+        hp = self._hbuf("bw", nb)
+        self._view(hp, np.float64, 6 * nc)[:] = np.asarray(cams, np.float64).ravel()
+        self._view(hp, np.float64, 3 * npts, 48 * nc)[:] = np.asarray(X, np.float64).ravel()
+        self._view(hp, np.int32, npts, 48 * nc + 24 * npts)[:] = win_ids
+        d = self._dbuf("bw", nb)
+        c.copy_async(d, hp, nb)
+        di = self._dbuf("bw_idx", 8 * max(n_obs, 1))
+        o, f, i = self._wview(self._wcur)
+        c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
+                                           V(d + 48 * nc + 24 * npts), npts, V(di), V(di + 4 * n_obs)),
+                "me_ba_window_indices")
+        p = BAProblemC()
+        p.n_cams, p.n_pts, p.n_obs = nc, npts, n_obs
+        p.cams = ctypes.cast(d, ctypes.POINTER(ctypes.c_double))
+        p.pts = ctypes.cast(d + 48 * nc, ctypes.POINTER(ctypes.c_double))
+        p.obs = ctypes.cast(o + 32 * off0, ctypes.POINTER(ctypes.c_double))
+        p.cam_idx = ctypes.cast(di, ctypes.POINTER(ctypes.c_int32))
+        p.pt_idx = ctypes.cast(di + 4 * n_obs, ctypes.POINTER(ctypes.c_int32))
+        K = np.asarray(self._K, np.float64).ravel()
+        p.K0[:] = [float(x) for x in K]
+        p.K1[:] = [float(x) for x in K]
+        p.baseline, p.feat_var, p.fixed_frames = self._calib
+        p.mem, p.obs_dim = ME_DEVICE, 4
+        opt = SolverOptions.fixed_iterations(iters).to_c()
+        c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(opt)), "me_ba_solve_async")
+        self._ba = ("dev", p, opt, d, nc, npts)
+        return n_obs
+
     def ba_submit(self, bp, iters):
         """Queue the window's solve on the BA context (me_ba_solve_async: the
         host arrays are staged into page-locked memory at once)."""
@@ -429,7 +566,7 @@ class GPUBackend(Backend):
         c = self.ctx
         import ctypes
         c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(o)), "me_ba_solve_async")
-        self._ba = (p, o, cams, pts, keep)
+        self._ba = ("host", p, o, cams, pts, keep)
 
     def ba_result(self):
         import ctypes
@@ -437,11 +574,21 @@ class GPUBackend(Backend):
         from ._lib import BASummaryC
         from .optimisation import _summary
 
-        p, o, cams, pts, keep = self._ba
+        rec = self._ba
         self._ba = None
         s = BASummaryC()
         c = self.ctx
         c.check(c.lib.me_ba_wait(c.h, ctypes.byref(s)), "me_ba_wait")
+        if rec[0] == "dev":  # device-resident window: cams | pts back in one D2H
+            _, p, o, d, nc, npts = rec
+            nb = 48 * nc + 24 * npts
+            hp = self._hbuf("bw_out", nb)
+            c.copy_async(hp, d, nb)
+            c.synchronize()
+            cams = self._view(hp, np.float64, 6 * nc).reshape(nc, 6).copy()
+            pts = self._view(hp, np.float64, 3 * npts, 48 * nc).reshape(npts, 3).copy()
+            return cams, pts, _summary(s)
+        _, p, o, cams, pts, keep = rec
         return cams, pts, _summary(s)
 
 
@@ -630,6 +777,7 @@ class WindowedStereoVO:
         idx, feats = idx[o], feats[o]
         self.obs[t] = (idx, feats)
         self.last[idx] = t
+        self.be.window_add(t, self.ids[idx].astype(np.int32), feats)
         if self.log_events:
             is_new = np.zeros(len(self.ids), bool)
             is_new[new_idx] = True
@@ -692,6 +840,13 @@ class WindowedStereoVO:
             return None
         win = self.last >= f0
         upts = np.flatnonzero(win)
+        if self.be.device_window:  # observations already on the device, frame by frame
+            cams = np.stack([self.poses[f] for f in range(f0, t + 1)])
+            assert self.latest_id < 2 ** 31
+            self.be._K, self.be._calib = self.K, (cfg.baseline, cfg.feat_var, cfg.fixed_frames)
+            n_obs = self._wait(self.be.ba_submit_window, t, f0, self.ids[upts].astype(np.int32), self.X[upts], cams,
+                               cfg.ba_iters)
+            return (t, f0, upts, n_obs)
         local = np.cumsum(win) - 1                  # table index -> window point index
         first = np.maximum(self.first[upts], f0)
         cnt = self.last[upts] - first + 1
@@ -734,6 +889,7 @@ class WindowedStereoVO:
         """WBA_Point::pop() of every feature older than `new_first`; empty tracks deleted."""
         for f in [f for f in self.obs if f < new_first]:
             idx, _ = self.obs.pop(f)
+            self.be.window_pop(f)
             if self.log_events:
                 self._ev.append(("pop", self.ids[idx].copy()))
             self.first[idx] = f + 1
