@@ -253,7 +253,6 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
   if (o < g.no) {
     const int cur = st->cur;
     const int ci = b.cam_idx[o], pi = b.pt_idx[o];
-    double* L = b.lin + (long)o * kLinStride;
     double r[4], Jc[24], Jp[12];
     obs_residual<OD>(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
     const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
@@ -263,9 +262,6 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
     for (int k = 0; k < 4; ++k) r[k] *= sc;
     for (int k = 0; k < 24; ++k) Jc[k] *= sc;
     for (int k = 0; k < 12; ++k) Jp[k] *= sc;
-    for (int k = 0; k < 4; ++k) L[k] = r[k];
-    for (int k = 0; k < 24; ++k) L[4 + k] = Jc[k];
-    for (int k = 0; k < 12; ++k) L[28 + k] = Jp[k];
     const long slot = b.pos[o];  // CSR-by-point slot: per-point stages read contiguously
     double* X = b.obsx + slot * kObsxStride;
     X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
@@ -1797,11 +1793,21 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     s2 += dd * dd;
     xn2 += xi * xi;
   }
-  double v2[2] = {s2, xn2}, out[2];
-  block_sum<2>(v2, out, red);
+  // camera part of the model cost change (scaled space; see pt_step_kernel)
+  double cm = 0;
+  for (int r = tid; r < n; r += nt) {
+    const double* U = b.U + 36 * (long)(r / 6) + 6 * (r % 6);
+    const int c0 = r - r % 6;
+    double uy = 0.0;
+    for (int k = 0; k < 6; ++k) uy += U[k] * u[c0 + k];
+    cm += b.gcs[r] * u[r] + 0.5 * u[r] * uy;
+  }
+  double v2[3] = {s2, xn2, -cm}, out[3];
+  block_sum<3>(v2, out, red);
   if (tid == 0) {
     st->cam_step2 = out[0];
     st->cam_xn2 = out[1];
+    st->cam_model = out[2];
   }
 }
 
@@ -1880,7 +1886,7 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
   double out[4];
   block_sum<4>(v, out, lds);
   if (threadIdx.x == 0) {
-    b.scal[R_MODEL] = out[0];
+    b.scal[R_MODEL] = out[0] + st->cam_model;  // (+ this rank's camera part, cam_solve)
     b.scal[R_CAND] = out[1];
     b.scal[R_STEP2] = out[2];
     b.scal[R_XN2] = out[3];
@@ -1893,6 +1899,14 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
 // last arrival then reduces 4x the partials)
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 
+// Model cost change in the normal-equation form (Ceres computes
+// -(J dx).(r + J dx / 2) per residual block; summed over the blocks that is
+// -(g.dx + dx^T J^T J dx / 2) with g = J^T r): per point, in the scaled space,
+// -(g_p.y_p + y_p^T V_p y_p / 2 + (D_p y_p).sum_q W_q^T (D_c y_c)) -- the last
+// sum is the one the point's back-substitution forms anyway -- and per camera
+// -(g_c.y_c + y_c^T U_c y_c / 2) (cam_solve).  The same quantity as the
+// per-observation form (rounding aside), without the per-observation Jacobian
+// traffic (320 B / observation written by linearize and read here before).
 template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
@@ -1903,18 +1917,21 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   double mc = 0, cc = 0, s2 = 0, xn2 = 0;
   if (j < g.np && !st->fail) {  // uniform within a 16-lane group
     // Every load of the point and of this lane's first CSR slot is requested
-    // in three dependent rounds (point data + offsets | slot: camera, obs
-    // index, W | camera step / scales, linearisation, observation, candidate
-    // camera) before any arithmetic; further slots (points with more than 16
-    // observations) load in the loops.  Same operations in the same order.
+    // in two dependent rounds (point data + offsets | slot: camera, obs
+    // index, W | camera step / scales, observation, candidate camera) before
+    // any arithmetic; further slots (points with more than 16 observations)
+    // load in the loops.
     const int cur = st->cur;
-    double psv[3], gpv[3], Lv[9], xv[3];
+    double psv[3], gpv[3], Lv[9], xv[3], Vv[9];
     for (int a = 0; a < 3; ++a) {
       psv[a] = b.psc[3 * (long)j + a];
       gpv[a] = b.gps[3 * (long)j + a];
       xv[a] = b.pts[cur][3 * (long)j + a];
     }
-    for (int i = 0; i < 9; ++i) Lv[i] = b.Lp[9 * (long)j + i];
+    for (int i = 0; i < 9; ++i) {
+      Lv[i] = b.Lp[9 * (long)j + i];
+      Vv[i] = b.V[9 * (long)j + i];
+    }
     const int beg = b.p_off[j], end = b.p_off[j + 1];
     const int q0 = beg + gl;
     const bool has0 = q0 < end;
@@ -1926,15 +1943,11 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       for (int i = 0; i < 18; ++i) W0[i] = b.Wo[18 * (long)q0 + i];  // (unused for a fixed camera)
     }
     const double* cams_c = b.cams[1 - cur];
-    double ys0[6], dc0[6], Lo0[kLinStride], f0[4];
+    double ys0[6], f0[4];
     int cam0 = 0, right0 = 0;
     if (has0) {
       if (ci0 >= 0)
-        for (int a = 0; a < 6; ++a) {
-          ys0[a] = b.csc[6 * ci0 + a] * b.yc[6 * ci0 + a];
-          dc0[a] = b.dc[6 * ci0 + a];
-        }
-      for (int k = 0; k < kLinStride; ++k) Lo0[k] = b.lin[(long)o0 * kLinStride + k];
+        for (int a = 0; a < 6; ++a) ys0[a] = b.csc[6 * ci0 + a] * b.yc[6 * ci0 + a];
       cam0 = b.cam_idx[o0];
       for (int k = 0; k < OD; ++k) f0[k] = b.obs[(long)OD * o0 + k];
       if (OD == 2) right0 = b.cam_id[o0] != 0;
@@ -1975,44 +1988,36 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       xc[a] = fmin(fmax(xv[a] + d[a], g.lo[a]), g.hi[a]);
     }
     if (gl == 0) {
+      double gy = 0.0, yvy = 0.0, cross = 0.0;
       for (int a = 0; a < 3; ++a) {
         b.dp[3 * (long)j + a] = d[a];
         b.pts[1 - cur][3 * (long)j + a] = xc[a];
         const double dd = xc[a] - xv[a];
         s2 += dd * dd;
         xn2 += xv[a] * xv[a];
+        gy += gpv[a] * yp[a];
+        cross += d[a] * t[a];
+        double vy = 0.0;
+        for (int c = 0; c < 3; ++c) vy += Vv[3 * a + c] * yp[c];
+        yvy += yp[a] * vy;
       }
+      mc = -(gy + 0.5 * yvy + cross);
     }
-    // (3) model cost change and candidate cost of the point's observations
+    // (3) candidate cost of the point's observations
     for (int q = q0; q < end; q += kStepG) {
       const bool first = q == q0;
-      double Lo[kLinStride], dcv[6], cv[6], f[4];
-      int ci, right = 0;
+      double cv[6], f[4];
+      int right = 0;
       if (first) {
-        for (int k = 0; k < kLinStride; ++k) Lo[k] = Lo0[k];
-        ci = cam0 - g.nf;
-        if (ci >= 0)
-          for (int i = 0; i < 6; ++i) dcv[i] = dc0[i];
         for (int a = 0; a < 6; ++a) cv[a] = cv0[a];
         for (int k = 0; k < OD; ++k) f[k] = f0[k];
         right = right0;
       } else {
         const int o = b.p_obs[q];
-        for (int k = 0; k < kLinStride; ++k) Lo[k] = b.lin[(long)o * kLinStride + k];
         const int cam = b.cam_idx[o];
-        ci = cam - g.nf;
-        if (ci >= 0)
-          for (int i = 0; i < 6; ++i) dcv[i] = b.dc[6 * ci + i];
         for (int a = 0; a < 6; ++a) cv[a] = cams_c[6 * cam + a];
         for (int k = 0; k < OD; ++k) f[k] = b.obs[(long)OD * o + k];
         if (OD == 2) right = b.cam_id[o] != 0;
-      }
-      for (int k = 0; k < 4; ++k) {
-        double jd = 0;
-        if (ci >= 0)
-          for (int i = 0; i < 6; ++i) jd += Lo[4 + k * 6 + i] * dcv[i];
-        jd += Lo[28 + k * 3 + 0] * d[0] + Lo[28 + k * 3 + 1] * d[1] + Lo[28 + k * 3 + 2] * d[2];
-        mc -= jd * (Lo[k] + jd / 2.0);
       }
       double r[4];
       if (OD == 4)
@@ -2295,7 +2300,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_scan_kernel(Geo g, Bufs b, Op
     st->radius = o.initial_radius;
     st->decrease = 2.0;
     st->x_cost = st->cand_cost = st->model_change = st->initial_cost = 0.0;
-    st->cam_step2 = st->cam_xn2 = st->cam_gmax = st->last_q = 0.0;
+    st->cam_step2 = st->cam_xn2 = st->cam_model = st->last_q = 0.0;
     for (int k = 0; k < 16; ++k) st->stamps[k] = 0;
     if (st->bad_input || st->infeasible) {
       st->done = 1;
@@ -2539,7 +2544,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(4 * (size_t)g.no, &b.tmp_obs);
   add(4 * (size_t)g.no, &b.cpos);
   add(8 * 27 * (size_t)g.no, &b.cvec);
-  add(8 * kLinStride * (size_t)g.no, &b.lin);
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);
   add((size_t)g.no, &b.dup);
   add(8 * solve_a_doubles(g.Ts), &b.Abuf);

@@ -8,7 +8,9 @@
 //                  StandardReprojectionError (:71-103) / StereoRightError
 //                  (:106-139) chosen by camID for <2>, value + analytic
 //                  Jacobian (2-row residuals padded with zero rows, so every
-//                  later stage is shared), HuberLoss(1.0) corrector, cost.
+//                  later stage is shared), HuberLoss(1.0) corrector, cost;
+//                  stores only the normal-equation pieces (J^T J, J^T r
+//                  blocks), never the Jacobian itself.
 //   cam_assemble   ck workgroups per variable camera, the last to finish
 //                  reduces: Jacobi column norms (iteration 0), scaled
 //                  U = Jc'Jc, g_c = Jc'r.
@@ -20,8 +22,9 @@
 //   cam_solve      one workgroup: S = U + D/radius - sum(partials), dense
 //                  Cholesky, y_c = -S^-1 b, candidate cameras.
 //   pt_step        16 lanes per point: y_p, candidate point (bounds
-//                  projection), step norms, and the model cost change and
-//                  candidate cost of the point's observations; its last
+//                  projection), step norms, the point's part of the model
+//                  cost change (normal-equation form) and the candidate
+//                  cost of the point's observations; its last
 //                  workgroup reduces them and runs decide (Ceres LM
 //                  acceptance / radius / termination).
 #pragma once
@@ -33,7 +36,6 @@ namespace ba {
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;
-constexpr int kLinStride = 40;   // r[4], Jc[24], Jp[12] per observation (corrected, unscaled)
 constexpr int kObsxStride = 9;   // V_o (6 unique) + g_o (3), unscaled
 
 struct Opts {
@@ -59,7 +61,7 @@ struct State {
   int pad[2];
   double radius, decrease;
   double x_cost, cand_cost, model_change, initial_cost;
-  double cam_step2, cam_xn2, cam_gmax;
+  double cam_step2, cam_xn2, cam_model;  // cam_model: -(g_c.y_c + y_c^T U y_c / 2), this rank's camera part
   double last_q;
   long long stamps[16];  // s_memtime at cam_solve phase ends (ME_SOLVE_SKIP & 256)
 };
@@ -93,7 +95,6 @@ struct Bufs {
   int* tmp_obs;       // plan: unsorted CSR-by-point slots
   int* cpos;          // obs -> slot in c_obs (-1: fixed camera)
   double* cvec;       // 27 x no (component-major by c_obs slot): Jc'Jc (21) + Jc'r (6) per observation
-  double* lin;        // no * 40
   double* obsx;       // no * 9  (V_o, g_o unscaled)
   uint8_t* dup;       // obs shares (point, camera) with another obs
   double* Abuf;       // n6 * (n6|1) factorisation workspace (when S does not fit LDS)
