@@ -443,7 +443,7 @@ FAMILY_KERNELS = {
 
 def pmc_traffic(family: str):
     """HBM bytes per family launch from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools_pmc_summary.py from separate
+    (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench); None if absent."""
     import glob
     import re

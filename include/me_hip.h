@@ -45,6 +45,11 @@ typedef struct me_ctx me_ctx;
 
 /* ---- context ---------------------------------------------------------- */
 int me_abi_version(void);
+/* roctx ranges (rocprofv3 --marker-trace): every compute entry point opens
+   one named after itself; callers can bracket their own stages (the VO
+   loop's KLT / matching / BA / scale stages). */
+int me_range_push(const char* name);
+int me_range_pop(void);
 int me_device_count(int* n);
 int me_create(me_ctx** out, int hip_device);
 void me_destroy(me_ctx* ctx);
@@ -58,8 +63,13 @@ void* me_get_stream(me_ctx* ctx);
    hipExtStreamCreateWithCUMask after the old one drains.  Lets two contexts
    of one GPU (e.g. a tracking front end and a BA back end) run side by side
    on disjoint CUs instead of sharing every CU's issue slots.  No reference
-   counterpart (the reference runs one CPU thread). */
+   counterpart (the reference runs one CPU thread).  hipExtStreamCreateWithCUMask
+   takes no flags: the masked stream is a blocking stream (it orders with
+   work on the legacy null stream, e.g. torch's default stream), unlike the
+   hipStreamNonBlocking stream a ctx owns otherwise; me_stream_flags reports
+   the flags of the ctx's current stream. */
 int me_set_cu_mask(me_ctx* ctx, const uint32_t* mask, int nwords);
+int me_stream_flags(me_ctx* ctx, unsigned* flags);
 int me_synchronize(me_ctx* ctx);
 int me_malloc(me_ctx* ctx, void** dptr, size_t bytes);
 int me_free(me_ctx* ctx, void* dptr);

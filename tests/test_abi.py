@@ -53,3 +53,30 @@ def test_no_device_fails_loudly():
         pytest.skip("a device is present")
     with pytest.raises(_lib.MEError):
         _lib.Context(0)
+
+
+@pytest.mark.gpu
+def test_masked_stream_flags_reported(ctx):
+    """the ctx-owned stream is non-blocking; the CU-masked stream
+    from hipExtStreamCreateWithCUMask is whatever HIP makes it -- reported by
+    me_stream_flags (documented in me_hip.h), and unmasking restores a
+    non-blocking stream."""
+    import ctypes
+
+    from uasl_motion_estimation_amd._lib import Context
+
+    c = Context(0)
+    try:
+        f = ctypes.c_uint()
+        c.check(c.lib.me_stream_flags(c.h, ctypes.byref(f)))
+        assert f.value == 1  # hipStreamNonBlocking
+        c.set_cu_mask(range(0, 256, 2))
+        c.check(c.lib.me_stream_flags(c.h, ctypes.byref(f)))
+        masked = f.value
+        c.set_cu_mask(None)
+        c.check(c.lib.me_stream_flags(c.h, ctypes.byref(f)))
+        assert f.value == 1
+        print("masked stream flags", masked)
+        assert masked in (0, 1)
+    finally:
+        c.close()

@@ -9,5 +9,5 @@ for v in default "$@"; do
   d="$GRAFT_REPO_ROOT/gpurun_out/abk_$v"
   rm -rf "$d"
   (cd /tmp && TMPDIR=/tmp LIB=$lib CONFIGS=$cfg timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$d" -o run -- python3 "$GRAFT_REPO_ROOT/tools/ab_ba_fams.py" > "$d.log" 2>&1) || exit 1
-  echo "== $v"; python tools_kstats.py "$d/run_results.db" 8
+  echo "== $v"; python tools/kstats.py "$d/run_results.db" 8
 done

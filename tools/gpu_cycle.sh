@@ -11,4 +11,4 @@ grep '^{' gpurun_out/bench.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/bench_prof.log" 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline --timing none --mi-pairs 0 > "$GRAFT_REPO_ROOT/gpurun_out/bench_trace.log" 2>&1 || exit 1
-cd "$GRAFT_REPO_ROOT" && bash tools_pmc.sh
+cd "$GRAFT_REPO_ROOT" && bash tools/pmc.sh

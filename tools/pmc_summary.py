@@ -1,4 +1,4 @@
-"""Per-kernel HBM traffic per launch from the two rocprofv3 --pmc passes of tools_pmc.sh.
+"""Per-kernel HBM traffic per launch from the two rocprofv3 --pmc passes of tools/pmc.sh.
 
 traffic = 2 x FETCH_SIZE + WRITE_SIZE (bytes per launch, averaged over launches): on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, WRITE_SIZE is exact

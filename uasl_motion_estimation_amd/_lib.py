@@ -115,8 +115,8 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 
 # every symbol include/me_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
-    "me_abi_version", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
-    "me_get_stream", "me_set_cu_mask", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
+    "me_abi_version", "me_range_push", "me_range_pop", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
+    "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_memcpy_async", "me_host_alloc", "me_host_free",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
@@ -157,6 +157,8 @@ def load_library(path: str = LIB_PATH):
     P = POINTER
     sig = {
         "me_abi_version": (c_int, []),
+        "me_range_push": (c_int, [ctypes.c_char_p]),
+        "me_range_pop": (c_int, []),
         "me_device_count": (c_int, [P(c_int)]),
         "me_create": (c_int, [P(c_void_p), c_int]),
         "me_destroy": (None, [c_void_p]),
@@ -165,6 +167,7 @@ def load_library(path: str = LIB_PATH):
         "me_get_stream": (c_void_p, [c_void_p]),
         "me_set_cu_mask": (c_int, [c_void_p, P(ctypes.c_uint32), c_int]),
         "me_synchronize": (c_int, [c_void_p]),
+        "me_stream_flags": (c_int, [c_void_p, P(ctypes.c_uint)]),
         "me_malloc": (c_int, [c_void_p, P(c_void_p), c_size_t]),
         "me_free": (c_int, [c_void_p, c_void_p]),
         "me_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
@@ -361,6 +364,23 @@ class Context:
         ms = c_double()
         self.check(self.lib.me_timing_read(self.h, KT[family], ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
+
+
+class roctx_range:
+    """roctx range around a block (rocprofv3 --marker-trace), through
+    me_range_push / me_range_pop; a no-op unless `on`."""
+
+    def __init__(self, name: str, on: bool = True):
+        self.name, self.on = name.encode(), on
+
+    def __enter__(self):
+        if self.on:
+            load_library().me_range_push(self.name)
+        return self
+
+    def __exit__(self, *a):
+        if self.on:
+            load_library().me_range_pop()
 
 
 _default_ctx = None

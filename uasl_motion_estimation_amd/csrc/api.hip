@@ -2,6 +2,10 @@
 // api.hip — context, memory and timing entry points of the C ABI (me_hip.h).
 #include "me_internal.hpp"
 #include <cstring>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+me_range::me_range(const char* name) { roctxRangePushA(name); }
+me_range::~me_range() { roctxRangePop(); }
 
 int me_set_error(me_ctx* ctx, int code, const char* fmt, ...) {
   if (ctx) {
@@ -105,6 +109,9 @@ extern "C" {
 
 int me_abi_version(void) { return ME_ABI_VERSION; }
 
+int me_range_push(const char* name) { return roctxRangePushA(name ? name : "me"); }
+int me_range_pop(void) { return roctxRangePop(); }
+
 int me_device_count(int* n) {
   int c = 0;
   if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
@@ -188,6 +195,12 @@ int me_set_cu_mask(me_ctx* c, const uint32_t* mask, int nwords) {
   if (own) c->stream = s;
   c->cu_active = nwords > 0 ? on : 0;
   c->scale_lm_cap = -1;  // co-residency of the persistent scale LM re-queried for the new CU set
+  return ME_OK;
+}
+
+int me_stream_flags(me_ctx* c, unsigned* flags) {
+  if (!c || !flags) return ME_ERR_INVALID;
+  ME_HIP(c, hipStreamGetFlags(c->stream, flags));
   return ME_OK;
 }
 

@@ -213,7 +213,7 @@ __device__ __forceinline__ void huber(double s, double* rho0, double* sqrt_rho1)
 template <bool SC1>
 __device__ __forceinline__ double a_ld(const double* p) {
   if (!SC1) return *p;
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), ME_HO_LD,
                                                       __HIP_MEMORY_SCOPE_AGENT));
 }
 template <bool SC1>
@@ -223,7 +223,7 @@ __device__ __forceinline__ void a_st(double* p, double v) {
     return;
   }
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                     ME_HO_ST, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain_and_barrier() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave, before the barrier
@@ -309,7 +309,7 @@ __device__ __forceinline__ bool last_arrival_wt(unsigned* cnt, unsigned expected
   __syncthreads();
   if (threadIdx.x == 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, ME_HO_RMW, __HIP_MEMORY_SCOPE_AGENT);
     slast = k == expected - 1;
     if (slast) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -2897,6 +2897,7 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = f
 }
 
 int solve_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, me_comm* comm, me_ba_summary* sum) {
+  me_range range_("me_ba_solve");
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   Plan P;
@@ -2999,6 +3000,7 @@ int ba_drain(me_ctx* c) {
 }  // namespace
 
 extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
+  me_range range_("me_ba_solve_async");
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   AsyncQueue* Q = ba_queue(c);
@@ -3030,6 +3032,7 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
 }
 
 extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) {
+  me_range range_("me_ba_wait");
   if (!c) return ME_ERR_INVALID;
   auto* Q = (AsyncQueue*)c->ba_async;
   if (!Q || Q->n == 0) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");

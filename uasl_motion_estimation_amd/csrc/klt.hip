@@ -366,6 +366,7 @@ static int build_pyramids(me_ctx* c, const uint8_t* dprev, const uint8_t* dnext,
 extern "C" int me_klt_track(me_ctx* c, me_mem mem, const uint8_t* prev, const uint8_t* next, int w, int h,
                             int stride, const float* pin, float* pout, uint8_t* status, int n,
                             const me_klt_params* kp) {
+  me_range range_("me_klt_track");
   if (!c || !kp) return ME_ERR_INVALID;
   ME_CHECK(c, w > 0 && h > 0 && stride >= w && n >= 0, "me_klt_track: bad image");
   ME_CHECK(c, kp->win >= 3 && (kp->win & 1) && kp->win * kp->win <= 64 * kMaxWinPx,

@@ -12,6 +12,32 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Cross-workgroup hand-offs inside one launch (ba.hip: last_arrival_wt, the
+// fused assembly, the multi-workgroup camera solve; scale.hip:
+// last_block_arrives, wt_store): the producer stores with agent-scope
+// atomics (written through, sc1), every storing wave drains (s_waitcnt
+// vmcnt(0)) before the workgroup barrier, one lane arrives with a RELAXED
+// agent-scope atomic, and the consumer reads the data only through
+// agent-scope atomic loads (a_ld<true> / the coherent loads).  This is
+// correct because on gfx950 sc1 stores write through to memory and vmcnt
+// counts stores -- under the HIP / C++ memory model alone the relaxed
+// arrival would be a data race.  Every cross-workgroup read of same-launch
+// data in a reducer must go through such a coherent load; a plain load may
+// hit a stale line of another XCD's L2.  -DME_HANDOFF_ACQREL restores
+// release / acquire ordering on these operations (A/B checks).
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "the written-through hand-offs rely on gfx950 cache behaviour (build with --offload-arch=gfx950)"
+#endif
+#ifdef ME_HANDOFF_ACQREL
+#define ME_HO_LD __ATOMIC_ACQUIRE
+#define ME_HO_ST __ATOMIC_RELEASE
+#define ME_HO_RMW __ATOMIC_ACQ_REL
+#else
+#define ME_HO_LD __ATOMIC_RELAXED
+#define ME_HO_ST __ATOMIC_RELAXED
+#define ME_HO_RMW __ATOMIC_RELAXED
+#endif
+
 namespace me_dev {
 
 __constant__ const double kLog2fInvc[16] = {

@@ -95,6 +95,12 @@ int me_scratch(me_ctx* ctx, int slot, size_t bytes, void** out);
 int me_pinned(me_ctx* ctx, size_t bytes, void** out);
 int me_check_launch(me_ctx* ctx, const char* what);
 
+// roctx range (rocprofv3 --marker-trace) around an entry point's host work.
+struct me_range {
+  explicit me_range(const char* name);
+  ~me_range();
+};
+
 // RAII event pair around one launch when timing is enabled.
 // Family timer around a launch.  ext: the launch itself takes the two events
 // (hipExtLaunchKernelGGL: the kernel's own begin / end timestamps, no marker

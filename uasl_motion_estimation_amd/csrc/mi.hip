@@ -451,6 +451,7 @@ extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_
                                     int stride, const float* uv, const int32_t* lo, const uint8_t* valid,
                                     const uint8_t* status, int n, int nd, int patch, int d_max, int unique,
                                     double ratio, float margin, float* xr_out, uint8_t* ok_out) {
+  me_range range_("me_mi_epipolar_match");
   if (!c) return ME_ERR_INVALID;
   ME_CHECK(c, n >= 0 && nd >= 3 && nd <= kEpiMaxNd && patch > 0 && patch * patch <= 255 && width > 0 && height > 0 &&
                   stride >= width,
@@ -518,6 +519,7 @@ int me_mi_table(me_ctx* c, int npx, const float** out) {
 extern "C" int me_mi_scores(me_ctx* c, me_mem mem, const uint8_t* imgL, int strideL, const uint8_t* imgR,
                             int strideR, int width, int height, const int32_t* xyL, const int32_t* xyR, int n,
                             int pw, int ph, float* out) {
+  me_range range_("me_mi_scores");
   if (!c) return ME_ERR_INVALID;
   ME_CHECK(c, n >= 0 && pw > 0 && ph > 0 && width > 0 && height > 0, "me_mi_scores: bad sizes");
   ME_CHECK(c, pw * ph <= 255, "me_mi_scores: patch of %d px exceeds the 255-px lane-histogram limit; use "

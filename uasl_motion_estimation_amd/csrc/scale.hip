@@ -279,7 +279,7 @@ __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int 
 // write-back per workgroup and phase beside the BA on the other CUs.
 __device__ __forceinline__ void wt_store(double* q, double v) {
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(q), __builtin_bit_cast(unsigned long long, v),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                     ME_HO_ST, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // A4: compute_residuals, one track per 16-lane group
@@ -781,7 +781,7 @@ __device__ __forceinline__ bool last_block_arrives(unsigned* cnt, unsigned targe
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned k = __hip_atomic_fetch_add(cnt, 1u, ME_HO_RMW, __HIP_MEMORY_SCOPE_AGENT);
     slast = k == target - 1;
   }
   __syncthreads();
@@ -1401,6 +1401,7 @@ extern "C" int me_scale_jacobian(me_ctx* c, const me_scale_state* s, int weighti
 // enqueues blocks of phase-predicated launches and polls the state.
 extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_params* pin, int test, int* stop_out,
                                  int* iterations, double* trace, int trace_cap, long* mi_evals) {
+  me_range range_("me_scale_optimise");
   if (!c || !s || !pin) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   me_optim_params p = *pin;

@@ -611,6 +611,7 @@ extern "C" int me_vo_rand(me_ctx* c, int* out) {
 extern "C" int me_vo_process(me_ctx* c, const float* matches, int n, const double* init6, const me_vo_params* p,
                              int max_outer, double* motion, double* state, double* pts3d, int* inliers,
                              int* n_inliers, int* ok) {
+  me_range range_("me_vo_process");
   if (!c || !p || !motion || !n_inliers || !ok) return ME_ERR_INVALID;
   ME_CHECK(c, n >= 0 && (n == 0 || matches), "me_vo_process: bad matches");
   ME_CHECK(c, p->method == 0 || p->method == 1, "me_vo_process: method must be GN (0) or LM (1)");

@@ -40,11 +40,14 @@ the event log through feature_types.WBA_Point.
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
 
 from . import synthetic as S
+
+ROCTX = os.environ.get("ME_ROCTX", "0") == "1"  # roctx ranges around the loop's stages (rocprofv3 --marker-trace)
 
 PATCH = 11          # MI patch (11 x 11, window_size 5)
 W_SCALE = 5         # ScaleState::window_size
@@ -721,8 +724,11 @@ class WindowedStereoVO:
 
     def _wait(self, fn, *a):
         import time
+
+        from ._lib import roctx_range
         t0 = time.perf_counter()
-        r = fn(*a)
+        with roctx_range(getattr(fn, "__name__", "stage"), ROCTX):
+            r = fn(*a)
         self.stage_s["wait"] += time.perf_counter() - t0
         return r
 
