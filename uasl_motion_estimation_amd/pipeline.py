@@ -311,9 +311,21 @@ class GPUBackend(Backend):
         self._imgs[t] = h
         return h
 
+    def frame_images_device(self, t, left, right):
+        """Images already resident on the device (e.g. rendered there): `left`
+        / `right` expose data_ptr() and shape (torch uint8 tensors, kept
+        referenced until release(t))."""
+        if t in self._imgs:
+            return self._imgs[t]
+        shape = tuple(left.shape)
+        ph = np.lib.stride_tricks.as_strided(np.zeros(1, np.uint8), shape=shape, strides=(0, 0))  # shape only
+        h = (int(left.data_ptr()), int(right.data_ptr()), shape, ph, ph, (left, right))
+        self._imgs[t] = h
+        return h
+
     def release(self, t):
         h = self._imgs.pop(t, None)
-        if h is not None:
+        if h is not None and len(h) == 5:  # (device-resident inputs of frame_images_device are the caller's)
             self.ctx.free(h[0])
             self.ctx.free(h[1])
 
@@ -853,7 +865,15 @@ class WindowedStereoVO:
             n_obs = self._wait(self.be.ba_submit_window, t, f0, self.ids[upts].astype(np.int32), self.X[upts], cams,
                                cfg.ba_iters)
             return (t, f0, upts, n_obs)
-        local = np.cumsum(win) - 1                  # table index -> window point index
+        bp = self.ba_problem(t, f0, upts)
+        self._wait(self.be.ba_submit, bp, cfg.ba_iters)
+        return (t, f0, upts, len(bp.obs))
+
+    def ba_problem(self, t, f0, upts):
+        """The window [f0, t]'s BA problem on the host (host-path backends;
+        diagnostics)."""
+        cfg = self.cfg
+        local = np.cumsum(self.last >= f0) - 1      # table index -> window point index
         first = np.maximum(self.first[upts], f0)
         cnt = self.last[upts] - first + 1
         off = np.zeros(len(cnt) + 1, np.int64)
@@ -875,16 +895,20 @@ class WindowedStereoVO:
             seen += len(i)
         assert seen == n_obs, "window tracks must have contiguous features in the window"
         cams = np.stack([self.poses[f] for f in range(f0, t + 1)])
-        bp = S.BAProblem(cams, self.X[upts], fe, cam, pti, self.K.copy(), self.K.copy(), cfg.baseline, cfg.feat_var,
-                         cfg.fixed_frames)
-        self._wait(self.be.ba_submit, bp, cfg.ba_iters)
-        return (t, f0, upts, n_obs)
+        return S.BAProblem(cams, self.X[upts], fe, cam, pti, self.K.copy(), self.K.copy(), cfg.baseline, cfg.feat_var,
+                           cfg.fixed_frames)
 
     def _ba_finish(self, ba):
         if ba is None:
             return 0, 0, {"iterations": 0, "final_cost": float("nan")}
         t, f0, upts, nobs = ba
         c, p, s = self._wait(self.be.ba_result)
+        if s.get("status", 2) != 2 and os.environ.get("ME_VO_DUMP_FAILED"):  # diagnostics: the failed window
+            bp = self.ba_problem(t, f0, upts)
+            np.savez(os.environ["ME_VO_DUMP_FAILED"], cams=bp.cams, pts=bp.pts, obs=bp.obs, cam_idx=bp.cam_idx,
+                     pt_idx=bp.pt_idx, K=bp.K0, t=t, f0=f0, ids=self.ids[upts], first=self.first[upts],
+                     last=self.last[upts], status=s.get("status"), termination=s.get("termination"))
+            os.environ.pop("ME_VO_DUMP_FAILED")
         if s.get("status", 2) == 2:
             for k, f in enumerate(range(f0, t + 1)):
                 self.poses[f] = np.asarray(c[k], np.float64).copy()

@@ -321,6 +321,12 @@ def depth_at(scene: Scene, K, R, t, u, v):
 # ceiling and two cylindrical walls 6 m to either side, value-noise
 # textured, so every keyframe sees the same kind of structure at 5-35 m.
 YAW_STEP_DEG = 0.3
+# The arc is placed at world z >= 400 m: the reference's BA bounds points in
+# WORLD coordinates (Z in [fx b / (2 cx), fx b / 0.1], BundleAdjuster.h:442-460),
+# which assumes the scene stays in front of the world origin; a point at world
+# z < Zmin -- e.g. a far mismatch, up to fx b / d_min = 288 m (720p) from the
+# camera -- makes the whole window infeasible (Ceres: FAILURE, no step).
+ARC_Z0 = 400.0 + 0.5 / (2.0 * math.sin(math.radians(0.3) / 2.0))
 
 
 def arc_radius(step: float = 0.5, yaw_deg: float = YAW_STEP_DEG) -> float:
@@ -329,13 +335,13 @@ def arc_radius(step: float = 0.5, yaw_deg: float = YAW_STEP_DEG) -> float:
 
 def trajectory_arc(n: int, first_id: int = 0):
     """World->camera poses (R, t) on the arc: camera centre C(psi) =
-    (R0 (1 - cos psi), 0, R0 sin psi), heading = camera z, psi = 0.3 deg k."""
+    (R0 (1 - cos psi), 0, Z0 + R0 sin psi), heading = camera z, psi = 0.3 deg k."""
     R0 = arc_radius()
     poses = []
     for i in range(n):
         psi = math.radians(YAW_STEP_DEG) * (first_id + i)
         Rw = rot_y(psi)
-        C = np.array([R0 * (1.0 - math.cos(psi)), 0.0, R0 * math.sin(psi)])
+        C = np.array([R0 * (1.0 - math.cos(psi)), 0.0, ARC_Z0 + R0 * math.sin(psi)])
         R = Rw.T
         poses.append((R, -R @ C))
     return poses
@@ -348,6 +354,7 @@ class CorridorScene:
     half_width: float = 6.0       # walls at radius -+ half_width
     floor_y: float = 1.6          # (y points down: the floor is below the camera)
     ceil_y: float = -3.0
+    z0: float = ARC_Z0            # world z of the circle's centre
 
 
 def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
@@ -365,7 +372,7 @@ def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
             hit = (s > 0) & (s < best)
             best = np.where(hit, s, best)
             surf = np.where(hit, k, surf)
-        O = np.array([scene.radius, 0.0, 0.0])
+        O = np.array([scene.radius, 0.0, scene.z0])
         ox, oz = C[0] - O[0], C[2] - O[2]
         a = dw[:, 0] ** 2 + dw[:, 2] ** 2
         bq = 2.0 * (ox * dw[:, 0] + oz * dw[:, 2])
@@ -392,6 +399,99 @@ def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
             cu, cv = r * np.arctan2(P[:, 2] - O[2], P[:, 0] - O[0]), P[:, 1]
         tex[m] = _value_noise(cu, cv, scene.seed * 4 + k)
     return np.clip(np.rint(tex.reshape(height, width) * 255.0), 0, 255).astype(np.uint8)
+
+
+def _value_noise_torch(X, Y, rng_seed: int, octaves: int = 4, base: float = 0.35):
+    """_value_noise on torch tensors (same integer hash, same interpolation)."""
+    import torch
+
+    out = torch.zeros_like(X)
+    amp, tot = 1.0, 0.0
+    for o in range(octaves):
+        cell = base / (2 ** o)
+        gx, gy = X / cell, Y / cell
+        ix, iy = torch.floor(gx).to(torch.int64), torch.floor(gy).to(torch.int64)
+        fx, fy = gx - ix.to(X.dtype), gy - iy.to(X.dtype)
+        sx, sy = fx * fx * (3 - 2 * fx), fy * fy * (3 - 2 * fy)
+        salt = (rng_seed * 83492791 + o * 2654435761) & 0xFFFFFFFFFFFFFFFF
+        salt = salt - (1 << 64) if salt >= (1 << 63) else salt
+
+        def h(a, c):
+            v = (a * 73856093) ^ (c * 19349663) ^ salt
+            v = (v ^ (v >> 13)) * 1274126177
+            v = v ^ (v >> 16)
+            return (v & 0xFFFF).to(X.dtype) / 65535.0
+
+        v00, v10, v01, v11 = h(ix, iy), h(ix + 1, iy), h(ix, iy + 1), h(ix + 1, iy + 1)
+        val = (v00 * (1 - sx) + v10 * sx) * (1 - sy) + (v01 * (1 - sx) + v11 * sx) * sy
+        out += amp * val
+        tot += amp
+        amp *= 0.55
+    return out / tot
+
+
+def render_corridor_torch(scene: CorridorScene, K, R, t, width, height, shift=0.0, device="cuda"):
+    """render_corridor on the GPU through torch (long synthetic sequences: a
+    720p frame in about a millisecond instead of ~0.6 s of numpy); returns a
+    uint8 (height, width) tensor on `device`."""
+    import torch
+
+    f64 = torch.float64
+    v, u = torch.meshgrid(torch.arange(height, dtype=f64, device=device), torch.arange(width, dtype=f64, device=device),
+                          indexing="ij")
+    d = torch.stack([(u - K[0, 2]) / K[0, 0], (v - K[1, 2]) / K[1, 1], torch.ones_like(u)], -1).reshape(-1, 3)
+    Rw = R.T
+    C = -Rw @ t + Rw @ np.array([shift, 0.0, 0.0])
+    dw = d @ torch.as_tensor(Rw.T.copy(), device=device)
+    n = dw.shape[0]
+    best = torch.full((n,), float("inf"), dtype=f64, device=device)
+    surf = torch.full((n,), -1, dtype=torch.int32, device=device)
+    for k, y in enumerate((scene.floor_y, scene.ceil_y)):
+        s = (y - C[1]) / dw[:, 1]
+        hit = (s > 0) & (s < best)
+        best = torch.where(hit, s, best)
+        surf = torch.where(hit, torch.full_like(surf, k), surf)
+    ox, oz = C[0] - scene.radius, C[2] - scene.z0
+    a = dw[:, 0] ** 2 + dw[:, 2] ** 2
+    bq = 2.0 * (ox * dw[:, 0] + oz * dw[:, 2])
+    for k, r in ((2, scene.radius - scene.half_width), (3, scene.radius + scene.half_width)):
+        c = ox * ox + oz * oz - r * r
+        disc = bq * bq - 4.0 * a * c
+        sq = torch.sqrt(torch.clamp(disc, min=0.0))
+        s1 = (-bq - sq) / (2.0 * a)
+        s2 = (-bq + sq) / (2.0 * a)
+        s = torch.where(s1 > 0, s1, s2)
+        hit = (disc >= 0) & (s > 0) & (s < best)
+        best = torch.where(hit, s, best)
+        surf = torch.where(hit, torch.full_like(surf, k), surf)
+    tex = torch.zeros(n, dtype=f64, device=device)
+    Cw = torch.as_tensor(C, device=device)
+    for k in range(4):
+        m = surf == k
+        P = Cw[None, :] + best[m, None] * dw[m]
+        if k < 2:
+            cu, cv = P[:, 0], P[:, 2]
+        else:
+            r = scene.radius + (-1 if k == 2 else 1) * scene.half_width
+            cu, cv = r * torch.atan2(P[:, 2] - scene.z0, P[:, 0] - scene.radius), P[:, 1]
+        tex[m] = _value_noise_torch(cu, cv, scene.seed * 4 + k)
+    return torch.clamp(torch.round(tex.reshape(height, width) * 255.0), 0, 255).to(torch.uint8)
+
+
+def corridor_frames_torch(seed: int, width: int, height: int, first_id: int, n: int, device="cuda"):
+    """Stereo keyframes first_id .. first_id + n - 1 of the corridor sequence
+    rendered on the GPU: [(left, right) uint8 device tensors, R, t]."""
+    import torch
+
+    scene = CorridorScene(seed, arc_radius())
+    K = intrinsics(width, height)
+    lut = torch.as_tensor(tone_map(), device=device)
+    out = []
+    for (R, t) in trajectory_arc(n, first_id):
+        L = render_corridor_torch(scene, K, R, t, width, height, 0.0, device)
+        Rr = lut[render_corridor_torch(scene, K, R, t, width, height, BASELINE, device).long()]
+        out.append((L, Rr, R, t))
+    return K, out
 
 
 @dataclass
