@@ -767,7 +767,8 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
            "device_us_per_frame": fam,
            "window_landmarks_last": last.n_window_pts, "window_observations_last": last.n_window_obs,
            "tracked_last": last.n_tracked, "tracks_created": int(vo.latest_id),
-           "pose_drift_m_last": round(float(np.abs(vo.poses[n - 1][:3] - truth[n - 1][:3]).max()), 4),
+           "drift_m_last": round(float(np.abs(PL.camera_centre(vo.poses[n - 1]) -
+                                              PL.camera_centre(truth[n - 1])).max()), 4),
            "render_s": round(gen, 1)}
     if cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))

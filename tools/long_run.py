@@ -69,7 +69,7 @@ def main():
                 del pending[old]
             if args.trace and t % args.trace == 0 and vo.results:
                 r = vo.results[-1]
-                e = np.abs(vo.poses[r.t][:3] - truth[r.t][:3]).max()
+                e = np.abs(PL.camera_centre(vo.poses[r.t]) - PL.camera_centre(truth[r.t])).max()
                 print(f"t={r.t} tracked={r.n_tracked} new={r.n_new} win_pts={r.n_window_pts} "
                       f"ba_cost={r.ba_cost:.4g} err={e:.4f}", flush=True)
             if (t + 1) % args.segment == 0:
@@ -81,7 +81,7 @@ def main():
     vo.finish()
     wall = time.perf_counter() - t_all
     be.close()
-    err = np.array([np.abs(vo.poses[t][:3] - truth[t][:3]).max() for t in range(n)])
+    err = np.array([np.abs(PL.camera_centre(vo.poses[t]) - PL.camera_centre(truth[t])).max() for t in range(n)])
     res = vo.results
     out = {"workload": f"config {c}: {cfg.width}x{cfg.height} stereo, {cfg.n_feats} features, {cfg.window}-keyframe "
                        f"sliding window, {n} keyframes on the ring-corridor arc, 10-iteration BA per keyframe, "

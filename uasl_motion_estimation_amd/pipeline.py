@@ -149,6 +149,14 @@ def _pick(uv, d, sc, nd, unique, ratio):
     return xr_f, ok
 
 
+def camera_centre(pose) -> np.ndarray:
+    """World position of a {t, angle-axis} world->camera pose: -R^T t (drift
+    is measured on centres: the world->camera translation also carries the
+    rotation error times the distance from the world origin)."""
+    pose = np.asarray(pose, np.float64)
+    return -aa_to_R(pose[3:]).T @ pose[:3]
+
+
 def in_margin(uv, width, height):
     return ((uv[:, 0] >= MARGIN) & (uv[:, 0] < width - MARGIN) & (uv[:, 1] >= MARGIN)
             & (uv[:, 1] < height - MARGIN))
