@@ -954,5 +954,5 @@ def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_di
                                        render_div=render_div, scene_kind="corridor")
     poses = []
     for fr in frames:
-        poses.append(np.concatenate([fr.t, S.R_to_aa(fr.R)]))
+        poses.append(np.concatenate([fr.t, S.R_to_aa_robust(fr.R)]))
     return frames, K, poses[0], poses[1] - poses[0], poses

@@ -62,6 +62,31 @@ def R_to_aa(R: np.ndarray) -> np.ndarray:
     return v * th / (2 * math.sin(th))
 
 
+def R_to_aa_robust(R: np.ndarray) -> np.ndarray:
+    """Angle-axis of R through its quaternion (Shepperd): well defined up to
+    and at a half turn, where R_to_aa's trace formula loses the axis."""
+    m = np.asarray(R, np.float64)
+    tr = np.trace(m)
+    if tr > max(m[0, 0], m[1, 1], m[2, 2]):
+        w = 0.5 * math.sqrt(1.0 + tr)
+        v = np.array([m[2, 1] - m[1, 2], m[0, 2] - m[2, 0], m[1, 0] - m[0, 1]]) / (4.0 * w)
+    else:
+        i = int(np.argmax([m[0, 0], m[1, 1], m[2, 2]]))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        r = math.sqrt(max(0.0, 1.0 + m[i, i] - m[j, j] - m[k, k]))
+        v = np.zeros(3)
+        v[i] = 0.5 * r
+        v[j] = (m[j, i] + m[i, j]) / (2.0 * r)
+        v[k] = (m[k, i] + m[i, k]) / (2.0 * r)
+        w = (m[k, j] - m[j, k]) / (2.0 * r)
+    if w < 0:
+        w, v = -w, -v
+    s = float(np.linalg.norm(v))
+    if s < 1e-15:
+        return np.zeros(3)
+    return v / s * (2.0 * math.atan2(s, w))
+
+
 def R_to_quat(R: np.ndarray) -> np.ndarray:
     """(w, x, y, z) with w >= 0, matching Quat::getR3 (rotation_utils.h:232-237)."""
     aa = R_to_aa(R)
@@ -316,17 +341,21 @@ def depth_at(scene: Scene, K, R, t, u, v):
 # The strip scene above is a short-window fixture: the straight forward path
 # flies through its planes within ~40 keyframes.  Long sequences (the
 # config-5 10k-frame stream) use a heading-consistent arc -- 0.5 m chord and
-# 0.3 deg yaw per keyframe, a circle of radius 0.5 / (2 sin 0.15 deg) = 95.5 m
-# (1200 keyframes per lap) -- inside a ring corridor that follows it: floor,
-# ceiling and two cylindrical walls 6 m to either side, value-noise
-# textured, so every keyframe sees the same kind of structure at 5-35 m.
+# 0.3 deg yaw (to the right) per keyframe, a circle of radius
+# 0.5 / (2 sin 0.15 deg) = 95.5 m (1200 keyframes per lap) -- inside a ring
+# corridor that follows it: floor, ceiling and two cylindrical walls 6 m to
+# either side, value-noise textured, so every keyframe sees the same kind of
+# structure at 5-35 m.
+#
+# World frame: z up, the circle centred on the z axis, the camera plane at
+# height ARC_H.  The reference's BA bounds the points in WORLD coordinates
+# (Z in [fx b / (2 cx), fx b / 0.1], BundleAdjuster.h:442-460): with z the
+# height, every point -- a far mismatch included, up to fx b / d_min = 288 m
+# away, i.e. at most ~90 m above or below the camera -- stays feasible, and
+# the world origin stays within ~130 m of every camera (the world->camera
+# translation carries no large offset to cancel against).
 YAW_STEP_DEG = 0.3
-# The arc is placed at world z >= 400 m: the reference's BA bounds points in
-# WORLD coordinates (Z in [fx b / (2 cx), fx b / 0.1], BundleAdjuster.h:442-460),
-# which assumes the scene stays in front of the world origin; a point at world
-# z < Zmin -- e.g. a far mismatch, up to fx b / d_min = 288 m (720p) from the
-# camera -- makes the whole window infeasible (Ceres: FAILURE, no step).
-ARC_Z0 = 400.0 + 0.5 / (2.0 * math.sin(math.radians(0.3) / 2.0))
+ARC_H = 100.0
 
 
 def arc_radius(step: float = 0.5, yaw_deg: float = YAW_STEP_DEG) -> float:
@@ -334,14 +363,17 @@ def arc_radius(step: float = 0.5, yaw_deg: float = YAW_STEP_DEG) -> float:
 
 
 def trajectory_arc(n: int, first_id: int = 0):
-    """World->camera poses (R, t) on the arc: camera centre C(psi) =
-    (R0 (1 - cos psi), 0, Z0 + R0 sin psi), heading = camera z, psi = 0.3 deg k."""
+    """World->camera poses (R, t) on the arc: heading psi = 0.3 deg k, camera
+    forward (cos psi, -sin psi, 0), down (0, 0, -1), right (-sin psi, -cos psi,
+    0) -- towards the circle's centre -- and centre C = R0 (sin psi, cos psi, 0)
+    + (0, 0, ARC_H)."""
     R0 = arc_radius()
     poses = []
     for i in range(n):
         psi = math.radians(YAW_STEP_DEG) * (first_id + i)
-        Rw = rot_y(psi)
-        C = np.array([R0 * (1.0 - math.cos(psi)), 0.0, ARC_Z0 + R0 * math.sin(psi)])
+        c, s = math.cos(psi), math.sin(psi)
+        Rw = np.array([[-s, 0.0, c], [-c, 0.0, -s], [0.0, -1.0, 0.0]])  # columns: right, down, forward
+        C = np.array([R0 * s, R0 * c, ARC_H])
         R = Rw.T
         poses.append((R, -R @ C))
     return poses
@@ -350,11 +382,10 @@ def trajectory_arc(n: int, first_id: int = 0):
 @dataclass
 class CorridorScene:
     seed: int
-    radius: float                 # trajectory radius (corridor centre line)
+    radius: float                 # trajectory radius (corridor centre line), circle centred on the z axis
     half_width: float = 6.0       # walls at radius -+ half_width
-    floor_y: float = 1.6          # (y points down: the floor is below the camera)
-    ceil_y: float = -3.0
-    z0: float = ARC_Z0            # world z of the circle's centre
+    floor_z: float = ARC_H - 1.6
+    ceil_z: float = ARC_H + 3.0
 
 
 def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
@@ -367,17 +398,15 @@ def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
     best = np.full(n, np.inf)
     surf = np.full(n, -1, np.int32)
     with np.errstate(divide="ignore", invalid="ignore"):
-        for k, y in enumerate((scene.floor_y, scene.ceil_y)):
-            s = (y - C[1]) / dw[:, 1]
+        for k, z in enumerate((scene.floor_z, scene.ceil_z)):
+            s = (z - C[2]) / dw[:, 2]
             hit = (s > 0) & (s < best)
             best = np.where(hit, s, best)
             surf = np.where(hit, k, surf)
-        O = np.array([scene.radius, 0.0, scene.z0])
-        ox, oz = C[0] - O[0], C[2] - O[2]
-        a = dw[:, 0] ** 2 + dw[:, 2] ** 2
-        bq = 2.0 * (ox * dw[:, 0] + oz * dw[:, 2])
+        a = dw[:, 0] ** 2 + dw[:, 1] ** 2
+        bq = 2.0 * (C[0] * dw[:, 0] + C[1] * dw[:, 1])
         for k, r in ((2, scene.radius - scene.half_width), (3, scene.radius + scene.half_width)):
-            c = ox * ox + oz * oz - r * r
+            c = C[0] * C[0] + C[1] * C[1] - r * r
             disc = bq * bq - 4.0 * a * c
             sq = np.sqrt(np.maximum(disc, 0.0))
             s1 = (-bq - sq) / (2.0 * a)
@@ -392,11 +421,11 @@ def render_corridor(scene: CorridorScene, K, R, t, width, height, shift=0.0):
         if not m.any():
             continue
         P = C[None, :] + best[m, None] * dw[m]
-        if k < 2:  # floor / ceiling: world (x, z)
-            cu, cv = P[:, 0], P[:, 2]
+        if k < 2:  # floor / ceiling: world (x, y)
+            cu, cv = P[:, 0], P[:, 1]
         else:      # walls: arc length, height
             r = scene.radius + (-1 if k == 2 else 1) * scene.half_width
-            cu, cv = r * np.arctan2(P[:, 2] - O[2], P[:, 0] - O[0]), P[:, 1]
+            cu, cv = r * np.arctan2(P[:, 1], P[:, 0]), P[:, 2]
         tex[m] = _value_noise(cu, cv, scene.seed * 4 + k)
     return np.clip(np.rint(tex.reshape(height, width) * 255.0), 0, 255).astype(np.uint8)
 
@@ -432,8 +461,8 @@ def _value_noise_torch(X, Y, rng_seed: int, octaves: int = 4, base: float = 0.35
 
 def render_corridor_torch(scene: CorridorScene, K, R, t, width, height, shift=0.0, device="cuda"):
     """render_corridor on the GPU through torch (long synthetic sequences: a
-    720p frame in about a millisecond instead of ~0.6 s of numpy); returns a
-    uint8 (height, width) tensor on `device`."""
+    720p frame in milliseconds instead of ~0.6 s of numpy); returns a uint8
+    (height, width) tensor on `device`."""
     import torch
 
     f64 = torch.float64
@@ -446,16 +475,15 @@ def render_corridor_torch(scene: CorridorScene, K, R, t, width, height, shift=0.
     n = dw.shape[0]
     best = torch.full((n,), float("inf"), dtype=f64, device=device)
     surf = torch.full((n,), -1, dtype=torch.int32, device=device)
-    for k, y in enumerate((scene.floor_y, scene.ceil_y)):
-        s = (y - C[1]) / dw[:, 1]
+    for k, z in enumerate((scene.floor_z, scene.ceil_z)):
+        s = (z - C[2]) / dw[:, 2]
         hit = (s > 0) & (s < best)
         best = torch.where(hit, s, best)
         surf = torch.where(hit, torch.full_like(surf, k), surf)
-    ox, oz = C[0] - scene.radius, C[2] - scene.z0
-    a = dw[:, 0] ** 2 + dw[:, 2] ** 2
-    bq = 2.0 * (ox * dw[:, 0] + oz * dw[:, 2])
+    a = dw[:, 0] ** 2 + dw[:, 1] ** 2
+    bq = 2.0 * (C[0] * dw[:, 0] + C[1] * dw[:, 1])
     for k, r in ((2, scene.radius - scene.half_width), (3, scene.radius + scene.half_width)):
-        c = ox * ox + oz * oz - r * r
+        c = C[0] * C[0] + C[1] * C[1] - r * r
         disc = bq * bq - 4.0 * a * c
         sq = torch.sqrt(torch.clamp(disc, min=0.0))
         s1 = (-bq - sq) / (2.0 * a)
@@ -470,10 +498,10 @@ def render_corridor_torch(scene: CorridorScene, K, R, t, width, height, shift=0.
         m = surf == k
         P = Cw[None, :] + best[m, None] * dw[m]
         if k < 2:
-            cu, cv = P[:, 0], P[:, 2]
+            cu, cv = P[:, 0], P[:, 1]
         else:
             r = scene.radius + (-1 if k == 2 else 1) * scene.half_width
-            cu, cv = r * torch.atan2(P[:, 2] - scene.z0, P[:, 0] - scene.radius), P[:, 1]
+            cu, cv = r * torch.atan2(P[:, 1], P[:, 0]), P[:, 2]
         tex[m] = _value_noise_torch(cu, cv, scene.seed * 4 + k)
     return torch.clamp(torch.round(tex.reshape(height, width) * 255.0), 0, 255).to(torch.uint8)
 
