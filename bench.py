@@ -565,6 +565,46 @@ def _parity_ok(p):
     return bool(p["same_iterations"] and p["cams_max_rel"] <= 1e-6 and p["pts_max_rel"] <= 1e-6)
 
 
+def crossover_model(ctx, opts, reps, ar_us=(25.0, 30.0, 40.0)):
+    """Where landmark sharding pays, from one GPU: the device time of the
+    largest rank's shard (1/G of the landmarks, all cameras, the same fixed
+    LM iterations) plus two all-reduces per iteration at an ASSUMED RCCL
+    latency over xGMI (ar_us for G = 2, 4, 8: small-message all-reduce of the
+    packed S (<= 370 KB)); the measured 1-rank RCCL overhead is in
+    rccl_1rank.  A prediction for the driver's 8-GPU run, not a measurement."""
+    from uasl_motion_estimation_amd import synthetic as S
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, shard_landmarks
+
+    rows = []
+    for name, (npts, win, w, h, seed) in {"config 3 (2000 x 20)": (2000, 20, 1280, 720, 3),
+                                          "config 4 (8000 x 30)": (8000, 30, 3840, 2160, 4),
+                                          "VO window at W = 50 (8000 x 50)": (8000, 50, 1280, 720, 5)}.items():
+        bp = S.ba_problem(S.SEED0 + seed, npts, win, w, h)
+        row = {"window": name, "observations": len(bp.obs)}
+        t1 = None
+        for G in (1, 2, 4, 8):
+            local = bp if G == 1 else shard_landmarks(bp, 0, G)[0]
+            d = DeviceBAProblem(local, ctx)
+            d.solve(opts)
+            ctx.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                d.reset()
+                s1 = d.solve(opts)
+            el = (time.perf_counter() - t0) / reps
+            d.close()
+            if G == 1:
+                t1 = el
+                row["ms_1gpu"] = round(1e3 * el, 3)
+                continue
+            pred = el + 2 * s1["iterations"] * ar_us[(2, 4, 8).index(G)] * 1e-6
+            row[f"ms_shard_{G}"] = round(1e3 * el, 3)
+            row[f"predicted_ms_{G}gpu"] = round(1e3 * pred, 3)
+            row[f"predicted_speedup_{G}gpu"] = round(t1 / pred, 2)
+        rows.append(row)
+    return {"assumed_allreduce_us": dict(zip(("2", "4", "8"), ar_us)), "rows": rows}
+
+
 def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     """Config-4 window (8000 landmarks x 30 keyframes, args.ba_iters LM
     iterations) solved (a) unsharded on this GPU and (b) landmark-sharded with
@@ -697,6 +737,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
            "pts_max_rel": float("%.3g" % max(p["pts_max_rel"] for p in pars)),
            "same_iterations": all(p["same_iterations"] for p in pars)}
     par["ok"] = _parity_ok(par)
+    out["crossover_model"] = crossover_model(ctx, opts, reps)
     out.update({"mode": "landmark-sharded over 2 contexts of one GPU (threads, host-staged exchange through "
                         "me_comm_create_callback)", "ranks": ranks,
                 "sharded_ms": round(1e3 * el, 3), "sharded_ba_iter_per_s": round(res[0]["iterations"] / el, 1),

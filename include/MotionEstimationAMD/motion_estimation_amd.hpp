@@ -62,6 +62,31 @@ class Context {
   std::unique_ptr<me_ctx, Del> c_;
 };
 
+// The landmark-sharded BA's communicator (me_comm): native RCCL
+// over xGMI, one process per GPU.  Rank 0 draws unique_id() and hands the
+// bytes to the other ranks; every rank constructs its Comm (collective).
+class Comm {
+ public:
+  using Id = std::array<uint8_t, ME_COMM_ID_BYTES>;
+  static Id unique_id() {
+    Id id{};
+    if (me_comm_unique_id(id.data(), (int)id.size()) != ME_OK) throw std::runtime_error("me_comm_unique_id failed");
+    return id;
+  }
+  Comm(Context& ctx, int world, int rank, const Id& id) {
+    me_comm* m = nullptr;
+    ctx.check(me_comm_create_rccl(ctx.get(), world, rank, id.data(), &m), "me_comm_create_rccl");
+    m_.reset(m);
+  }
+  me_comm* get() const { return m_.get(); }
+
+ private:
+  struct Del {
+    void operator()(me_comm* m) const { me_comm_destroy(m); }
+  };
+  std::unique_ptr<me_comm, Del> m_;
+};
+
 // Row-major 8-bit grayscale view (cv::Mat CV_8U: data, rows, cols, step).
 struct ImageView {
   const uint8_t* data = nullptr;
@@ -175,7 +200,9 @@ class BundleAdjuster {
 
   me_ba_options& options() { return opts_; }
 
-  Status optimise(int fixedFrames) {
+  // comm: this rank holds all cameras and its landmark shard (ptIdx local to
+  // the shard); the cameras come out identical on every rank.
+  Status optimise(int fixedFrames, amd::Comm* comm = nullptr) {
     if (status_ == Status::UNINITIALISED) {
       std::cerr << "[Bundle Adjuster] parameters and observations must be initialised first" << std::endl;
       return status_;
@@ -207,7 +234,8 @@ class BundleAdjuster {
     p.baseline = calib_.baseline;
     p.feat_var = calib_.feat_var;
     p.fixed_frames = fixedFrames;
-    int rc = me_ba_solve(ctx_->get(), &p, &opts_, &summary_);
+    int rc = comm ? me_ba_solve_comm(ctx_->get(), &p, &opts_, comm->get(), &summary_)
+                  : me_ba_solve(ctx_->get(), &p, &opts_, &summary_);
     if (rc != ME_OK) {
       std::cerr << "[Bundle Adjuster] " << me_last_error(ctx_->get()) << std::endl;
       return status_ = Status::FAILED;

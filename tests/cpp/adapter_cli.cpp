@@ -4,6 +4,7 @@
 // host built like the reference's src/ gets the same results as the Python
 // mirror and the oracle.
 //   adapter_cli ba  <in.bin> <out.bin>   BundleAdjuster<M>-style solve (M = 4 or 2, optional covariance)
+//   adapter_cli ba_rccl <in.bin> <out.bin>  the same through a one-rank RCCL amd::Comm (me_ba_solve_comm)
 //   adapter_cli mi  <in.bin> <out.bin>   computeMutualInformation / computeEntropy
 //   adapter_cli nms <in.bin> <out.bin>   nonMaxSupScanline3x3
 //   adapter_cli scale <in.bin> <out.bin> Optimiser<ScaleState,...>: compute_residuals, optimise, compute_inliers,
@@ -43,7 +44,7 @@ Reader read_file(const char* path) {
 }
 
 template <int M>
-int solve_ba(Reader& in, FILE* out, int nc, int np, int no, int fixed, int compute_cov) {
+int solve_ba(Reader& in, FILE* out, int nc, int np, int no, int fixed, int compute_cov, bool rccl) {
   using namespace me::optimisation;
   CalibrationParameters calib;
   calib.K.resize(2);
@@ -70,7 +71,9 @@ int solve_ba(Reader& in, FILE* out, int nc, int np, int no, int fixed, int compu
     obs[k].camID = cid[k];
   }
   BundleAdjuster<M> ba(calib, cams, pts, obs);
-  const auto status = ba.optimise(fixed);
+  std::unique_ptr<me::amd::Comm> comm;
+  if (rccl) comm.reset(new me::amd::Comm(me::amd::Context::thread_default(), 1, 0, me::amd::Comm::unique_id()));
+  const auto status = ba.optimise(fixed, comm.get());
   const int32_t st = (int32_t)status, it = ba.summary().iterations;
   const double cost = ba.summary().final_cost;
   fwrite(&st, 4, 1, out);
@@ -85,10 +88,10 @@ int solve_ba(Reader& in, FILE* out, int nc, int np, int no, int fixed, int compu
 }
 
 // payload: nc np no fixed obs_dim compute_cov | K0 K1 | baseline feat_var | cams pts obs cam_idx pt_idx [cam_id]
-int run_ba(Reader& in, FILE* out) {
+int run_ba(Reader& in, FILE* out, bool rccl = false) {
   const int nc = in.get<int32_t>(), np = in.get<int32_t>(), no = in.get<int32_t>(), fixed = in.get<int32_t>();
   const int od = in.get<int32_t>(), cov = in.get<int32_t>();
-  return od == 2 ? solve_ba<2>(in, out, nc, np, no, fixed, cov) : solve_ba<4>(in, out, nc, np, no, fixed, cov);
+  return od == 2 ? solve_ba<2>(in, out, nc, np, no, fixed, cov, rccl) : solve_ba<4>(in, out, nc, np, no, fixed, cov, rccl);
 }
 
 int run_mi(Reader& in, FILE* out) {
@@ -255,6 +258,7 @@ int main(int argc, char** argv) {
   int rc = 2;
   try {
     if (!std::strcmp(argv[1], "ba")) rc = run_ba(in, out);
+    else if (!std::strcmp(argv[1], "ba_rccl")) rc = run_ba(in, out, true);
     else if (!std::strcmp(argv[1], "mi")) rc = run_mi(in, out);
     else if (!std::strcmp(argv[1], "nms")) rc = run_nms(in, out);
     else if (!std::strcmp(argv[1], "scale")) rc = run_scale(in, out);

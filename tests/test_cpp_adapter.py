@@ -103,6 +103,16 @@ def test_cpp_bundle_adjuster_matches_oracle(tmp_path, oracle):
 
 
 @pytest.mark.gpu
+def test_cpp_bundle_adjuster_over_rccl_comm_bit_identical(tmp_path):
+    """BundleAdjuster<4>::optimise(fixed, &comm) with a one-rank RCCL
+    amd::Comm (me_ba_solve_comm, the packed exchange) = the plain solve."""
+    bp = S.ba_problem(20261020, 150, 6, 640, 480)
+    _, a = _run("ba", _ba_payload(bp), tmp_path)
+    _, b = _run("ba_rccl", _ba_payload(bp), tmp_path)
+    assert a == b
+
+
+@pytest.mark.gpu
 def test_cpp_mono_bundle_adjuster_with_covariance(tmp_path, oracle):
     bp = S.ba_problem_mono(20261021, 150, 6, 640, 480)
     _, out = _run("ba", _ba_payload(bp, compute_cov=1), tmp_path)
