@@ -488,14 +488,24 @@ __device__ __forceinline__ void bwd3(const double* L, const double* y, double* x
 //      accumulated over all the workgroup's sub-chunks in registers.  A K-step
 //      of 4 rows is skipped for a tile when the rows' camera band (a track's
 //      cameras are contiguous in CSR order) misses the tile's columns.
-// Partials (workgroup x tile) are summed in fixed order by s_assemble:
-// deterministic, no atomics.  Operand map of the MFMA: lane l holds
+// Band-sorted runs (plan_order_kernel): a workgroup takes one run of rlen
+// landmarks in (first tile, last tile) order -- landmarks with similar camera
+// bands together -- and one group of stpw tiles of the run's tile set (the
+// pairs of tiles in its band plus the z tile), so a wave holds at most 5
+// accumulator tiles and a run stores only its band's tiles (config 5: ~16 MB
+// of partials per iteration instead of 97, config 4: 12 instead of 33).
+// Partials (run x tile) are summed in fixed run order by s_assemble through
+// the per-tile slot lists: deterministic, no atomics.  Operand map of the MFMA: lane l holds
 // A[l&15][l>>4] and B[l>>4][l&15]; result register i holds D[(l>>4)+4i][l&15].
 // Landmarks per sub-chunk: 32 (96 rows of Y, 16 lanes per landmark) while the
 // Y block fits the LDS budget, else 16 (48 rows, 32 lanes per landmark).  Each
 // Schur workgroup leaves one set of partial tiles that s_assemble sums, so
 // twice the landmarks per workgroup halve that traffic.
 constexpr int kSchurPts = 16, kSchurPtsWide = 32, kSchurPtsSmall = 8;
+#ifndef ME_SCHUR_NT
+#define ME_SCHUR_NT 5
+#endif
+constexpr int kSchurNtMax = ME_SCHUR_NT;  // accumulator tiles per wave (3..5)
 constexpr size_t kSchurLdsCap = 150 * 1024;
 __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (size_t)3 * P * Rz + 4 * 3 * (size_t)P; }
 
@@ -551,30 +561,42 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   const bool final_pass = st->iterations >= o.max_num_iterations;
   if (blockIdx.x == 0 && threadIdx.x == 0) st->final_pass = final_pass;
   const int P = g.spts, Rz = g.Rpad, rows = 3 * P, nks = rows / 4;
+  // this workgroup's run and tile group; the run's tile set is [bA, bB] plus the z tile T - 1
+  const int run = blockIdx.x / g.sgrp, tgrp = blockIdx.x - run * g.sgrp;
+  const int bA = g.sorted ? b.rband[2 * run] : 0, bB = g.sorted ? b.rband[2 * run + 1] : g.T - 1;
+  const int nb = bB - bA + 1, ns = nb + (bB < g.T - 1 ? 1 : 0), ntile = ns * (ns + 1) / 2;
+  if (tgrp * g.stpw >= ntile) {  // (uniform) the run's tiles are all taken by lower groups
+    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = 0.0;
+    return;
+  }
+  const bool lead = tgrp == 0;  // the run's first group writes the per-landmark results (the others recompute them)
   double* Y = smem;
   int* band = reinterpret_cast<int*>(Y + (size_t)rows * Rz);  // per landmark: first / last camera column, live
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int gi = tid / SL, gl = tid & (SL - 1);
-  // this wave's tiles (wave-uniform: scalar registers)
+  // this wave's tiles (wave-uniform: scalar registers): canonical index c of
+  // the run's tile set (row ka of the set's upper triangle holds ns - ka pairs)
   int tI[NT], tJ[NT];
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
-    int p = wave + NW * u, I = 0;
-    if (p >= g.npairs) p = -1;
+    int p = tgrp * g.stpw + wave + NW * u, ka = 0;
+    if (p >= ntile) p = -1;
     int rem = p < 0 ? 0 : p;
-    while (rem >= g.T - I) {
-      rem -= g.T - I;
-      ++I;
+    while (rem >= ns - ka) {
+      rem -= ns - ka;
+      ++ka;
     }
-    tI[u] = p < 0 ? -1 : I;
-    tJ[u] = p < 0 ? -1 : I + rem;
+    const int kb = ka + rem;
+    tI[u] = p < 0 ? -1 : (ka < nb ? bA + ka : g.T - 1);
+    tJ[u] = p < 0 ? -1 : (kb < nb ? bA + kb : g.T - 1);
   }
   double4_t acc[NT];
 #pragma unroll
   for (int u = 0; u < NT; ++u) acc[u] = double4_t{0.0, 0.0, 0.0, 0.0};
   double gm = 0;
-  for (int sc = blockIdx.x; sc < g.nsub; sc += g.ksplit) {
-    const int j = sc * P + gi;
+  for (int sc = 0; sc < g.rsub; ++sc) {
+    const int pos = run * g.rlen + sc * P + gi;
+    const int j = pos < g.np ? (g.sorted ? b.order[pos] : pos) : g.np;
     double* Yp = Y + (size_t)(3 * gi) * Rz;  // this landmark's 3 rows, written by its own lane group only
     for (int i = gl; i < 3 * Rz / 2; i += SL) reinterpret_cast<double2*>(Yp)[i] = double2{0.0, 0.0};
     if (j < g.np) {
@@ -618,7 +640,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         gs[0] = V[6] * p0;
         gs[1] = V[7] * p1;
         gs[2] = V[8] * p2;
-        if (gl == 0) {
+        if (gl == 0 && lead) {
           if (!scaled)
             for (int a = 0; a < 3; ++a) b.psc[3 * (long)j + a] = pv[a];
           for (int i = 0; i < 9; ++i) b.V[9 * (long)j + i] = Vs[i];
@@ -645,8 +667,10 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
       const double rL0 = 1.0 / L[0], rL4 = 1.0 / L[4], rL8 = 1.0 / L[8];
       if (gl == 0) {
         if (!ok) st->fail = 1;
-        for (int i = 0; i < 9; ++i) b.Lp[9 * (long)j + i] = L[i];
-        for (int a = 0; a < 3; ++a) b.zp[3 * (long)j + a] = z[a];
+        if (lead) {
+          for (int i = 0; i < 9; ++i) b.Lp[9 * (long)j + i] = L[i];
+          for (int a = 0; a < 3; ++a) b.zp[3 * (long)j + a] = z[a];
+        }
       }
       SCHUR_T(2);  // group sums, point block
       // (B) this lane's slots -> the landmark's rows of Y (first slot of each camera run only;
@@ -800,9 +824,9 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   if (final_pass) return;
 #pragma unroll
   for (int u = 0; u < NT; ++u) {
-    const int p = wave + NW * u;
-    if (p >= g.npairs) continue;
-    double* dst = b.Spart + ((long)blockIdx.x * g.npairs + p) * 256;
+    const int p = tgrp * g.stpw + wave + NW * u;
+    if (p >= ntile) continue;
+    double* dst = b.Spart + ((long)run * g.npairs + p) * 256;
 #pragma unroll
     for (int i = 0; i < 4; ++i) dst[((lane >> 4) + 4 * i) * 16 + (lane & 15)] = acc[u][i];
   }
@@ -900,10 +924,11 @@ __device__ void xch_tail_body(const Geo& g, const Bufs& b, const double* gc_raw,
   }
 }
 
-// S = U - sum over the Schur workgroups' partial tiles, b = g - Y^T z, diag(U)
+// S = U - sum over the Schur runs' partial tiles, b = g - Y^T z, diag(U)
 // (sharded mode: the local pieces, no LM diagonal).  256 threads = 32
-// elements x 8 partial groups: group k sums partials k, k + 8, ... in order,
-// then the 8 group sums are added in order (deterministic).  The threads walk
+// elements x 8 partial groups: group k sums entries k, k + 8, ... of the
+// tile's slot list (the runs covering the tile, in run order), then the 8
+// group sums are added in order (deterministic).  The threads walk
 // the partial tiles in their own layout (the upper block triangle, tile pair
 // p = (I <= J), row-major 16 x 16), so consecutive threads read consecutive
 // doubles of every partial; the sums land in the lower block triangle of S
@@ -951,23 +976,44 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
   const bool fail = st->fail || (mode == SA_UNPACK && b.xch[xo_fail(g)] != 0.0);  // (unpack: any rank's failure)
   double acc = 0.0;
   if (use && !fail && mode != SA_UNPACK) {
-    // partials grp, grp + 8, ... added in order; their loads issued 8 at a
-    // time (independent addresses: one memory latency per batch, not per add)
-    const double* src = b.Spart + idx;
-    const long stride = (long)g.npairs * 256;
+    // the partials of the runs covering this tile (run order): entries grp,
+    // grp + 8, ... added in order; their loads issued 8 at a time
+    // (independent addresses: one memory latency per batch, not per add)
 #ifndef ME_SA_BATCH
 #define ME_SA_BATCH 8
 #endif
-    for (int q0 = grp; q0 < g.ksplit; q0 += ME_SA_BATCH * kSaGroups) {
-      double v[ME_SA_BATCH];
+    if (g.sorted) {
+      const int cnt = b.tcnt[idx >> 8];
+      const int* tl = b.tl + (long)(idx >> 8) * g.nruns;
+      const double* src = b.Spart + (idx & 255);
+      for (int q0 = grp; q0 < cnt; q0 += ME_SA_BATCH * kSaGroups) {
+        int sl[ME_SA_BATCH];
 #pragma unroll
-      for (int k = 0; k < ME_SA_BATCH; ++k) {
-        const int q = q0 + k * kSaGroups;
-        v[k] = q < g.ksplit ? src[q * stride] : 0.0;
+        for (int k = 0; k < ME_SA_BATCH; ++k) {
+          const int q = q0 + k * kSaGroups;
+          sl[k] = q < cnt ? tl[q] : -1;
+        }
+        double v[ME_SA_BATCH];
+#pragma unroll
+        for (int k = 0; k < ME_SA_BATCH; ++k) v[k] = sl[k] >= 0 ? src[(long)sl[k] * 256] : 0.0;
+#pragma unroll
+        for (int k = 0; k < ME_SA_BATCH; ++k)
+          if (sl[k] >= 0) acc += v[k];
       }
+    } else {  // every run holds every tile, at slot run * npairs + tile
+      const double* src = b.Spart + idx;
+      const long stride = (long)g.npairs * 256;
+      for (int q0 = grp; q0 < g.nruns; q0 += ME_SA_BATCH * kSaGroups) {
+        double v[ME_SA_BATCH];
 #pragma unroll
-      for (int k = 0; k < ME_SA_BATCH; ++k)
-        if (q0 + k * kSaGroups < g.ksplit) acc += v[k];
+        for (int k = 0; k < ME_SA_BATCH; ++k) {
+          const int q = q0 + k * kSaGroups;
+          v[k] = q < g.nruns ? src[q * stride] : 0.0;
+        }
+#pragma unroll
+        for (int k = 0; k < ME_SA_BATCH; ++k)
+          if (q0 + k * kSaGroups < g.nruns) acc += v[k];
+      }
     }
   }
   part[grp][e] = acc;
@@ -2382,6 +2428,137 @@ __global__ __launch_bounds__(kSortBlock) void plan_segsort_kernel(Geo g, Bufs b)
   }
 }
 
+// Band order of the landmarks for the Schur runs (pt_schur_kernel): key =
+// first tile * T + last tile of the landmark's variable-camera columns
+// (slots are sorted by camera: the first variable slot and the last slot), a
+// landmark without variable cameras in the last bucket.  Stable counting
+// sort: per 256-landmark block, the rank of each key among the block's
+// earlier landmarks (within a wave by ballots over its distinct keys, plus the
+// counts of the earlier waves) and the block's key counts (bucket-major),
+// then plan_order_kernel scans the counts and scatters.  Only for windows
+// with many tile pairs (g.sorted); otherwise the runs keep the landmark order
+// and every run takes the whole tile set.
+constexpr int kMaxBandKeys = 19 * 19;  // T <= 19 (npairs <= 192)
+__global__ __launch_bounds__(kBlock) void plan_band_kernel(Geo g, Bufs b) {
+  __shared__ int wcnt[kBlock / 64][kMaxBandKeys];
+  const PlanWork w = plan_work(g, b.work);
+  const int t = threadIdx.x, blk = blockIdx.x, j = blk * kBlock + t, lane = t & 63, wv = t >> 6;
+  const int K = g.T * g.T;
+  for (int k = t; k < (kBlock / 64) * K; k += kBlock) wcnt[k / K][k % K] = 0;
+  int key = -1;
+  if (j < g.np) {
+    key = K - 1;
+    const int beg = b.p_off[j], end = b.p_off[j + 1];
+    const int hi = (!w.flags[F_BAD] && end > beg) ? b.p_cam[end - 1] : -1;
+    if (hi >= 0) {
+      int q = beg;
+      while (b.p_cam[q] < 0) ++q;  // fixed cameras (negative) sort first
+      key = (6 * b.p_cam[q] / 16) * g.T + (6 * hi + 5) / 16;
+    }
+  }
+  __syncthreads();
+  // rank among the wave's lower lanes with the same key: one ballot per distinct key
+  int rank = 0;
+  unsigned long long todo = __ballot(key >= 0);
+  while (todo) {
+    const int lead = __builtin_ctzll(todo);
+    const int kl = __shfl(key, lead, 64);
+    const unsigned long long m = __ballot(key == kl);
+    if (key == kl) rank = __builtin_popcountll(m & ((1ull << lane) - 1ull));
+    if (lane == lead) wcnt[wv][kl] = __builtin_popcountll(m);
+    todo &= ~m;
+  }
+  __syncthreads();
+  if (j < g.np) {
+    for (int v = 0; v < wv; ++v) rank += wcnt[v][key];
+    b.pkey[j] = key;
+    b.prank[j] = rank;
+  }
+  for (int k = t; k < K; k += kBlock) {
+    int c = 0;
+#pragma unroll
+    for (int v = 0; v < kBlock / 64; ++v) c += wcnt[v][k];
+    b.phist[(long)k * g.nblkp + blk] = c;
+  }
+}
+
+// One workgroup: exclusive scan of the block key counts -> band order, and
+// with the scatter each run's band (first tile of its first landmark, largest
+// last tile: LDS max); then per tile pair the partial slots of the runs whose
+// tile set holds it, in run order.
+constexpr int kMaxRuns = 1024;
+__global__ __launch_bounds__(kScanBlock) void plan_order_kernel(Geo g, Bufs b) {
+  __shared__ int wsum[kScanBlock / 64];
+  __shared__ int rA[kMaxRuns], rB[kMaxRuns];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int r = t; r < g.nruns; r += kScanBlock) {
+    rA[r] = g.T - 1;  // (a run past the last landmark: the z tile alone)
+    rB[r] = 0;
+  }
+  const long nh = (long)g.T * g.T * g.nblkp;
+  const long chunk = (nh + kScanBlock - 1) / kScanBlock;
+  const long beg = min(nh, t * chunk), end = min(nh, beg + chunk);
+  int s = 0;
+  for (long i = beg; i < end; ++i) s += b.phist[i];
+  int x = s;  // inclusive wave scan
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < kScanBlock / 64; ++k) {
+      const int v = wsum[k];
+      wsum[k] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+  int run = wsum[wv] + x - s;
+  for (long i = beg; i < end; ++i) {
+    const int v = b.phist[i];
+    b.phist[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int j = t; j < g.np; j += kScanBlock) {
+    const int key = b.pkey[j];
+    const int pos = b.phist[(long)key * g.nblkp + j / kBlock] + b.prank[j];
+    b.order[pos] = j;
+    const int r = pos / g.rlen;
+    if (pos == r * g.rlen) rA[r] = key / g.T;  // keys ascend: the run's first landmark has its smallest first tile
+    atomicMax(&rB[r], key % g.T);
+  }
+  __syncthreads();
+  for (int r = t; r < g.nruns; r += kScanBlock) {
+    const int B = max(rA[r], rB[r]);
+    rB[r] = B;
+    b.rband[2 * r] = rA[r];
+    b.rband[2 * r + 1] = B;
+  }
+  __syncthreads();
+  for (int p = t; p < g.npairs; p += kScanBlock) {
+    int I = 0, rem = p;
+    while (rem >= g.T - I) {
+      rem -= g.T - I;
+      ++I;
+    }
+    const int J = I + rem;
+    int cnt = 0;
+    for (int r = 0; r < g.nruns; ++r) {
+      const int A = rA[r], B = rB[r];
+      const int nb = B - A + 1, ns = nb + (B < g.T - 1 ? 1 : 0);
+      const int ka = (I >= A && I <= B) ? I - A : (I == g.T - 1 ? nb : -1);
+      const int kb = (J >= A && J <= B) ? J - A : (J == g.T - 1 ? nb : -1);
+      if (ka < 0 || kb < 0) continue;
+      b.tl[(long)p * g.nruns + cnt++] = r * g.npairs + ka * ns - ka * (ka - 1) / 2 + (kb - ka);
+    }
+    b.tcnt[p] = cnt;
+  }
+}
+
 // State | cams[cur] | pts[cur] -> one contiguous read-back (or straight into
 // the caller's device arrays for a device-resident problem)
 __global__ __launch_bounds__(kBlock) void output_kernel(Geo g, Bufs b, double* cams_dst, double* pts_dst) {
@@ -2486,7 +2663,22 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       g.spts = v;
   }
   g.nsub = (int)std::max(1L, ((long)g.np + g.spts - 1) / g.spts);
-  g.ksplit = std::min(g.nsub, 256);  // Schur workgroups = partial slices summed by s_assemble
+  // Schur runs: rsub sub-chunks of spts landmarks each (at most ~256 runs), in
+  // band order; each run split into tile groups of 8 waves x NT <= 5 tiles
+  g.rsub = (int)std::max(1L, ((long)g.nsub + 255) / 256);
+  g.rlen = g.spts * g.rsub;
+  g.nruns = (int)std::max(1L, ((long)g.np + g.rlen - 1) / g.rlen);
+  // (measured, tools/ab_schur.py: 4 tiles per wave at config 4 -- 5 spill -- but 5 for
+  // the 50-keyframe window, where fewer tile groups per run recompute fewer Y blocks)
+  g.stpw = 8 * std::min((g.npairs + 7) / 8, g.npairs > 100 ? kSchurNtMax : std::min(kSchurNtMax, 4));
+  g.sgrp = (g.npairs + g.stpw - 1) / g.stpw;
+  g.ksplit = g.nruns * g.sgrp;  // Schur workgroups (a run's surplus tile groups exit at once)
+  // band order pays once the tile set is large (config 4: 66 pairs, config 5: 190); for
+  // config 3 (28 pairs) the two plan launches cost more than the partial traffic saves
+  g.sorted = g.npairs > 40 ? 1 : 0;
+  if (const char* e = getenv("ME_SCHUR_SORT")) g.sorted = atoi(e) != 0;  // A/B timing only
+  ME_CHECK(c, g.nruns <= kMaxRuns, "BA: %d Schur runs exceed %d", g.nruns, kMaxRuns);
+  g.nblkp = blocks(std::max(g.np, 1), kBlock);
   ME_CHECK(c, g.npairs <= 8 * 24, "BA: %d variable cameras exceed the Schur tile budget", g.m);
   g.nblk_obs = (int)std::max(1L, rup(std::max(g.no, 1), kBlock) / kBlock);
   g.nblk_lin = (int)std::max(1L, rup(std::max(g.no, 1), lin_block(g.no)) / lin_block(g.no));
@@ -2556,7 +2748,14 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * 3 * (size_t)g.np, &b.gps);
   add(8 * 9 * (size_t)g.np, &b.Lp);
   add(8 * 3 * (size_t)g.np, &b.zp);
-  add(8 * 256 * (size_t)g.ksplit * g.npairs, &b.Spart);
+  add(8 * 256 * (size_t)g.nruns * g.npairs, &b.Spart);
+  add(4 * (size_t)std::max(g.np, 1), &b.order);
+  add(4 * (size_t)std::max(g.np, 1), &b.pkey);
+  add(4 * (size_t)std::max(g.np, 1), &b.prank);
+  add(4 * (size_t)g.T * g.T * g.nblkp, &b.phist);
+  add(8 * (size_t)g.nruns, &b.rband);
+  add(4 * (size_t)g.npairs * g.nruns, &b.tl);
+  add(4 * (size_t)g.npairs, &b.tcnt);
   add(8 * (size_t)g.n6 * g.n6 + 8 * (size_t)(2 * g.n6 + 2), &b.S);  // S | b | diagU | fail (contiguous for all-reduce)
   add(8 * (size_t)g.n6, &b.yc);
   add(8 * (size_t)g.n6, &b.dc);
@@ -2639,6 +2838,10 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   hipLaunchKernelGGL(plan_scatter_kernel, dim3(g.nblk_obs), dim3(kBlock), 0, s, g, b);
   hipLaunchKernelGGL(plan_segsort_kernel, dim3(blocks(std::max(g.np, 1), kSortBlock / 64)), dim3(kSortBlock), 0, s, g,
                      b);
+  if (g.sorted) {
+    hipLaunchKernelGGL(plan_band_kernel, dim3(g.nblkp), dim3(kBlock), 0, s, g, b);
+    hipLaunchKernelGGL(plan_order_kernel, dim3(1), dim3(kScanBlock), 0, s, g, b);
+  }
   ME_TRY(me_check_launch(c, "BA plan"));
   // LDS for the camera solve
   P.solve_lds = 8 * (solve_small_doubles(g.Ts) + solve_a_doubles(g.Ts));
@@ -2656,8 +2859,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
 #define ME_SCHUR_K(N)                                                                                   \
   (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>, \
       (const void*)pt_schur_kernel<N, 512, kSchurPtsSmall>
-    for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5), ME_SCHUR_K(6), ME_SCHUR_K(7), ME_SCHUR_K(8),
-                          ME_SCHUR_K(9), ME_SCHUR_K(10), ME_SCHUR_K(12), ME_SCHUR_K(16), ME_SCHUR_K(24)})
+    for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5)})
 #undef ME_SCHUR_K
       ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSchurLdsCap));
     c->ba_lds_attr = 1;
@@ -2724,11 +2926,9 @@ int enqueue_linearize(Plan& P) {
     me_ktimer t(c, ME_KT_BA_SCHUR, true);  // (sampled launches take the timer's events)
     // NT = this wave's tile count, instantiated tight: an unused tile's
     // accumulator costs 8 VGPRs, and at 512 threads (2 waves per SIMD) the
-    // budget is 256 registers -- up to 5 tiles nothing spills, 9 tiles (config
-    // 4) spill 120 B.  (A 256-thread, AGPR-accumulator variant measured slower
-    // at 9-17 tiles than the small spill, and beyond 12 tiles per wave it spills
-    // more than the 512-thread instances.)
-    const int pw8 = (g.npairs + 7) / 8;
+    // budget is 256 registers -- up to 5 tiles nothing spills (9 tiles spilled
+    // 120 B); wider windows take more tile groups per run instead.
+    const int pw8 = g.stpw / 8;
     const dim3 grd(g.ksplit + (fused ? g.m * g.ck : 0));
 #define ME_SCHUR(N)                                                                                          \
   do {                                                                                                       \
@@ -2742,17 +2942,10 @@ int enqueue_linearize(Plan& P) {
       hipExtLaunchKernelGGL((pt_schur_kernel<N, 512, kSchurPts>), grd, dim3(512), P.schur_lds, s, t.a, t.b, 0, g, P.b, \
                             P.o, ca);                                                                        \
   } while (0)
+    static_assert(kSchurNtMax >= 3 && kSchurNtMax <= 5, "instantiated tile counts");
     if (pw8 <= 3) ME_SCHUR(3);
     else if (pw8 <= 4) ME_SCHUR(4);
-    else if (pw8 <= 5) ME_SCHUR(5);
-    else if (pw8 <= 6) ME_SCHUR(6);
-    else if (pw8 <= 7) ME_SCHUR(7);
-    else if (pw8 <= 8) ME_SCHUR(8);
-    else if (pw8 <= 9) ME_SCHUR(9);
-    else if (pw8 <= 10) ME_SCHUR(10);
-    else if (pw8 <= 12) ME_SCHUR(12);
-    else if (pw8 <= 16) ME_SCHUR(16);
-    else ME_SCHUR(24);
+    else ME_SCHUR(5);
 #undef ME_SCHUR
   }
   if (sh) {

@@ -72,6 +72,10 @@ enum { R_COST = 0, R_GMAX_PT, R_MODEL, R_CAND, R_STEP2, R_XN2, R_COUNT };
 struct Geo {
   int nc, np, no, nf, m, n6, Rpad, T, Ts, spts, nsub, ksplit, npairs, nblk_obs, nblk_lin, nblk_pts, nblk_step, pstride, jacobi,
       ck;
+  // band-sorted Schur pass (plan_band / plan_order): landmark runs of rlen = spts x rsub landmarks in
+  // (first tile, last tile) order, each split into sgrp tile groups of stpw tiles (ksplit = nruns x sgrp)
+  int nruns, rlen, rsub, sgrp, stpw, nblkp;
+  int sorted;              // 0: runs in landmark order, every run takes the whole tile set (small windows)
   int od;                  // residual rows per observation: 4 StereoReprojectionError, 2 Standard/StereoRight
   int xslots, xrank;       // sharded: gradient max-norm slots in the exchange (one per rank) and this rank's
   double K0[9], K1[9];
@@ -107,7 +111,14 @@ struct Bufs {
   double* gps;        // 3np scaled gradient
   double* Lp;         // np * 9 Cholesky of V + D/radius
   double* zp;         // 3np
-  double* Spart;      // ksplit (Schur workgroups) * npairs * 256 partial tiles of Y^T [Y | z]
+  double* Spart;      // nruns * npairs * 256 partial tiles of Y^T [Y | z]: run r's tile c at slot r * npairs + c
+  int* order;         // np landmarks in band order (the Schur runs)
+  int* rband;         // 2 * nruns: first / last tile of each run's camera band (its tile set adds the z tile T-1)
+  int* tl;            // npairs * nruns: per tile pair, the partial slots of the runs covering it, in run order
+  int* tcnt;          // npairs: entries of tl per tile pair
+  int* pkey;          // plan: per landmark band key (first tile * T + last tile)
+  int* prank;         // plan: stable rank of the key inside its 256-landmark block
+  int* phist;         // plan: T^2 x nblkp key counts per block, scanned in place into offsets
   double* S;          // n6 * n6 (assembled / reduced)
   double* bvec;       // n6
   double* diagU;      // n6 (for the sharded all-reduce)
