@@ -129,6 +129,25 @@ int me_mi_epipolar_match(me_ctx* ctx, const uint8_t* imgL, const uint8_t* imgR, 
                          const float* uv, const int32_t* lo, const uint8_t* valid, const uint8_t* status, int n,
                          int nd, int patch, int d_max, int unique, double ratio, float margin, float* xr_out,
                          uint8_t* ok_out);
+/* me_mi_epipolar_match over the first *n_dev features (a device count left
+   by a preceding kernel, at most n_max), no valid / status gate. */
+int me_mi_epipolar_match_count(me_ctx* ctx, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
+                               int stride, const float* uv, const int32_t* lo, const int32_t* n_dev, int n_max,
+                               int nd, int patch, int d_max, int unique, double ratio, float margin, float* xr_out,
+                               uint8_t* ok_out);
+/* New-feature cells of the VO loop (pipeline.new_cells on the device; no
+   reference symbol -- the application's grid detector around WBA_Point
+   creation): tracked feature k is good iff status_k == 1, ok_k != 0 and it
+   lies inside the margin; good features occupy their grid cell
+   (trunc((u - margin) / cw), trunc((v - margin) / ch)) clamped, FP64; the
+   first max(0, n_feats - #good) empty cells in ascending order get a feature
+   at margin + (cell + 0.5 + jitter(t, cell)) * (cw, ch) (float), lo = d_min;
+   *out_count = their number.  Device memory, asynchronous on the ctx stream:
+   with me_mi_epipolar_match_count the new features are matched in the same
+   submission as the tracked ones. */
+int me_vo_new_cells(me_ctx* ctx, const float* uv, const uint8_t* status, const uint8_t* ok, int n, int width,
+                    int height, float margin, int nx, int ny, double cw, double ch, int n_feats, int t, int d_min,
+                    float* out_uv, int32_t* out_lo, int32_t* out_count);
 /* me::computeEntropy (src/core/mutual_information.cpp:28-45). */
 int me_entropy(me_ctx* ctx, me_mem mem, const uint8_t* img, int stride, int w, int h, float* out);
 

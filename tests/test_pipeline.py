@@ -75,9 +75,9 @@ def test_pipeline_bookkeeping_matches_wba_point(oracle):
     assert sorted(live) == sorted(int(i) for i in vo.ids)
     per_track = {int(i): [] for i in vo.ids}
     for t in sorted(vo.obs):
-        idx, fe = vo.obs[t]
-        for i, f in zip(idx, fe):
-            per_track[int(vo.ids[i])].append((t, tuple(float(x) for x in f)))
+        fid, fe = vo.obs[t]
+        for i, f in zip(fid, fe):
+            per_track[int(i)].append((t, tuple(float(x) for x in f)))
     for tid, p in live.items():
         got = per_track[tid]
         assert [g[0] for g in got] == p.indices

@@ -36,7 +36,7 @@ def wrap(obj, name):
     setattr(obj, name, w)
 
 
-for nm in ("klt_submit", "klt_match", "match", "ba_submit_window", "scale_submit", "ba_result", "scale_result",
+for nm in ("klt_submit", "klt_match", "klt_match_new", "match", "ba_submit_window", "scale_submit", "ba_result", "scale_result",
            "window_add", "frame_images", "frame_images_device"):
     wrap(be, nm)
 for nm in ("process", "_complete", "_pop"):

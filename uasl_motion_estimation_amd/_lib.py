@@ -119,7 +119,7 @@ EXPORTS = [
     "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_memcpy_async", "me_host_alloc", "me_host_free",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
-    "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
+    "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
@@ -187,6 +187,11 @@ def load_library(path: str = LIB_PATH):
         "me_mi_epipolar_match": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double, c_float,
                                          c_void_p, c_void_p]),
+        "me_mi_epipolar_match_count": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                               c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_double,
+                                               c_float, c_void_p, c_void_p]),
+        "me_vo_new_cells": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_int, c_int,
+                                    c_double, c_double, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
         "me_compare_pc": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_ccoeff_normed": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_quantise": (c_int, [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_int]),

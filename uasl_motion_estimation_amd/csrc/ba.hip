@@ -2653,7 +2653,9 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   // contraction is MFMA-bound per workgroup: twice the workgroups spread it
   // over more CUs; config 5: BA 5.2 -> 4.96 ms per 10 iterations, config 3
   // slower with 8)
-  if (g.npairs > 40 && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap)
+  // (and once 16-landmark sub-chunks outnumber 256 workgroups: the config-3
+  // VO window, ~4 400 landmarks, BA_SCHUR 430 -> 340 us per keyframe)
+  if ((g.npairs > 40 || g.np > 256 * kSchurPts) && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap)
     g.spts = kSchurPtsWide;
   else
     g.spts = g.npairs > 100 ? kSchurPtsSmall : kSchurPts;

@@ -388,16 +388,21 @@ inline float inv_count(long n) { return (float)(1.0 / (double)n); }
 // me_mi_scores), then one lane picks the best in FP64 exactly as the numpy
 // restatement does (first maximum, interior, parabola vertex, uniqueness
 // against the best outside +-2 candidates, x_r = u - disparity, margin test).
-constexpr int kEpiBlock = 256, kEpiGroups = kEpiBlock / 16, kEpiMaxNd = 512;
+// Block size by candidate count: 16 groups for the tracked features' short
+// windows (~13 candidates), 64 for the new features' full range (127: two
+// candidates per group instead of eight on the per-feature chain).
+constexpr int kEpiMaxNd = 512, kEpiWideNd = 32;
+template <int kEpiBlock>
 __global__ __launch_bounds__(kEpiBlock) void mi_epipolar_kernel(
     const uint8_t* __restrict__ L, const uint8_t* __restrict__ R, int stride, int width, int height,
     const float* __restrict__ uv, const int32_t* __restrict__ lo, const uint8_t* __restrict__ valid,
-    const uint8_t* __restrict__ status, int n, int nd, int patch, int d_max, int unique, double ratio, float margin,
-    float invN, float* __restrict__ xr_out, uint8_t* __restrict__ ok_out) {
+    const uint8_t* __restrict__ status, int n, const int32_t* __restrict__ n_dev, int nd, int patch, int d_max,
+    int unique, double ratio, float margin, float invN, float* __restrict__ xr_out, uint8_t* __restrict__ ok_out) {
+  constexpr int kEpiGroups = kEpiBlock / 16;
   __shared__ uint32_t lds[kEpiGroups * kGroupWords];
   __shared__ double sc[kEpiMaxNd];
   const int f = blockIdx.x;
-  if (f >= n) return;
+  if (f >= n || (n_dev && f >= *n_dev)) return;  // (n_dev: the count a preceding kernel left on the device)
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
   const float u = uv[2 * f], v = uv[2 * f + 1];
@@ -447,11 +452,10 @@ __global__ __launch_bounds__(kEpiBlock) void mi_epipolar_kernel(
 
 }  // namespace
 
-extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
-                                    int stride, const float* uv, const int32_t* lo, const uint8_t* valid,
-                                    const uint8_t* status, int n, int nd, int patch, int d_max, int unique,
-                                    double ratio, float margin, float* xr_out, uint8_t* ok_out) {
-  me_range range_("me_mi_epipolar_match");
+static int epipolar_launch(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height, int stride,
+                           const float* uv, const int32_t* lo, const uint8_t* valid, const uint8_t* status, int n,
+                           const int32_t* n_dev, int nd, int patch, int d_max, int unique, double ratio, float margin,
+                           float* xr_out, uint8_t* ok_out) {
   if (!c) return ME_ERR_INVALID;
   ME_CHECK(c, n >= 0 && nd >= 3 && nd <= kEpiMaxNd && patch > 0 && patch * patch <= 255 && width > 0 && height > 0 &&
                   stride >= width,
@@ -459,10 +463,35 @@ extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_
   if (n == 0) return ME_OK;
   ME_HIP(c, hipSetDevice(c->device));
   me_ktimer t(c, ME_KT_MI);
-  hipLaunchKernelGGL(mi_epipolar_kernel, dim3(n), dim3(kEpiBlock), 0, c->stream, imgL, imgR, stride, width, height, uv,
-                     lo, valid, status, n, nd, patch, d_max, unique, ratio, margin, inv_count((long)patch * patch), xr_out,
-                     ok_out);
+  if (nd > kEpiWideNd)
+    hipLaunchKernelGGL(mi_epipolar_kernel<1024>, dim3(n), dim3(1024), 0, c->stream, imgL, imgR, stride, width, height,
+                       uv, lo, valid, status, n, n_dev, nd, patch, d_max, unique, ratio, margin,
+                       inv_count((long)patch * patch), xr_out, ok_out);
+  else
+    hipLaunchKernelGGL(mi_epipolar_kernel<256>, dim3(n), dim3(256), 0, c->stream, imgL, imgR, stride, width, height,
+                       uv, lo, valid, status, n, n_dev, nd, patch, d_max, unique, ratio, margin,
+                       inv_count((long)patch * patch), xr_out, ok_out);
   return me_check_launch(c, "mi_epipolar_kernel");
+}
+
+extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
+                                    int stride, const float* uv, const int32_t* lo, const uint8_t* valid,
+                                    const uint8_t* status, int n, int nd, int patch, int d_max, int unique,
+                                    double ratio, float margin, float* xr_out, uint8_t* ok_out) {
+  me_range range_("me_mi_epipolar_match");
+  return epipolar_launch(c, imgL, imgR, width, height, stride, uv, lo, valid, status, n, nullptr, nd, patch, d_max,
+                         unique, ratio, margin, xr_out, ok_out);
+}
+
+extern "C" int me_mi_epipolar_match_count(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
+                                          int stride, const float* uv, const int32_t* lo, const int32_t* n_dev,
+                                          int n_max, int nd, int patch, int d_max, int unique, double ratio,
+                                          float margin, float* xr_out, uint8_t* ok_out) {
+  me_range range_("me_mi_epipolar_match_count");
+  if (!c) return ME_ERR_INVALID;
+  ME_CHECK(c, n_dev != nullptr, "me_mi_epipolar_match_count: null count");
+  return epipolar_launch(c, imgL, imgR, width, height, stride, uv, lo, nullptr, nullptr, n_max, n_dev, nd, patch, d_max,
+                         unique, ratio, margin, xr_out, ok_out);
 }
 
 // Shared launcher (also used by scale.hip for raw device buffers).

@@ -567,6 +567,86 @@ int GlibcRand_next(int32_t st[31], int& f, int& r) {
   return res;
 }
 
+
+// New-feature cells of the windowed VO loop (pipeline.new_cells, restated on
+// the device so the tracked and the new-feature matching share one round
+// trip): a tracked feature k is good iff status_k == 1, it lies inside the
+// feature margin and its stereo match held (ok_k); a good feature occupies
+// grid cell (trunc((u - margin) / cw), trunc((v - margin) / ch)), clamped,
+// in FP64; the first max(0, n_feats - #good) empty cells in ascending order
+// get a new feature at margin + (cell + 0.5 + jitter(t, cell)) * (cw, ch),
+// rounded to float; lo = d_min.  One workgroup.
+constexpr int kCellBlock = 1024, kMaxCells = 65536;
+__global__ __launch_bounds__(kCellBlock) void vo_cells_kernel(const float* __restrict__ uv,
+                                                              const uint8_t* __restrict__ status,
+                                                              const uint8_t* __restrict__ ok, int n, int width,
+                                                              int height, float margin, int nx, int ny, double cw,
+                                                              double ch, int n_feats, unsigned t, int d_min,
+                                                              float* __restrict__ out_uv, int32_t* __restrict__ out_lo,
+                                                              int32_t* __restrict__ out_count) {
+  __shared__ uint32_t occ[kMaxCells / 32];
+  __shared__ int wsum[kCellBlock / 64];
+  __shared__ int ngood;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ncell = nx * ny;
+  for (int i = tid; i < (ncell + 31) / 32; i += kCellBlock) occ[i] = 0u;
+  if (tid == 0) ngood = 0;
+  __syncthreads();
+  int cnt = 0;
+  for (int k = tid; k < n; k += kCellBlock) {
+    const float u = uv[2 * k], v = uv[2 * k + 1];
+    const bool good = status[k] == 1 && ok[k] != 0 && u >= margin && u < (float)width - margin && v >= margin &&
+                      v < (float)height - margin;
+    if (!good) continue;
+    ++cnt;
+    const int cx = min(max((int)(((double)u - (double)margin) / cw), 0), nx - 1);
+    const int cy = min(max((int)(((double)v - (double)margin) / ch), 0), ny - 1);
+    const int cell = cy * nx + cx;
+    atomicOr(&occ[cell >> 5], 1u << (cell & 31));
+  }
+  atomicAdd(&ngood, cnt);
+  __syncthreads();
+  const int want = max(0, n_feats - ngood);
+  // empty cells in ascending order: contiguous chunk per thread, block scan of the counts
+  const int chunk = (ncell + kCellBlock - 1) / kCellBlock;
+  const int c0 = min(ncell, tid * chunk), c1 = min(ncell, c0 + chunk);
+  int e = 0;
+  for (int c = c0; c < c1; ++c) e += ((occ[c >> 5] >> (c & 31)) & 1u) ? 0 : 1;
+  int x = e;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wv] = x;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int k = 0; k < kCellBlock / 64; ++k) {
+      const int v = wsum[k];
+      wsum[k] = acc;
+      acc += v;
+    }
+    *out_count = min(want, acc);
+  }
+  __syncthreads();
+  int r = wsum[wv] + x - e;
+  for (int c = c0; c < c1 && r < want; ++c) {
+    if ((occ[c >> 5] >> (c & 31)) & 1u) continue;
+    // pipeline._cell_jitter: 32-bit hash of (cell, t), two 16-bit fractions * 0.6 - 0.3
+    uint32_t h = (uint32_t)c * 2654435761u + t * 40503u;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    const double ja = (double)(h & 0xFFFFu) / 65536.0 * 0.6 - 0.3;
+    const double jb = (double)((h >> 16) & 0xFFFFu) / 65536.0 * 0.6 - 0.3;
+    const double px = (double)margin + (((double)(c % nx) + 0.5) + ja) * cw;
+    const double py = (double)margin + (((double)(c / nx) + 0.5) + jb) * ch;
+    out_uv[2 * r] = (float)px;
+    out_uv[2 * r + 1] = (float)py;
+    out_lo[r] = d_min;
+    ++r;
+  }
+}
+
 }  // namespace
 
 void me_rand_seed(me_ctx* c, unsigned seed) {
@@ -729,4 +809,18 @@ extern "C" int me_vo_process(me_ctx* c, const float* matches, int n, const doubl
   *ok = hout[6] == 1.0 ? 1 : 0;
   motion_of(hout);
   return ME_OK;
+}
+
+extern "C" int me_vo_new_cells(me_ctx* c, const float* uv, const uint8_t* status, const uint8_t* ok, int n, int width,
+                               int height, float margin, int nx, int ny, double cw, double ch, int n_feats, int t,
+                               int d_min, float* out_uv, int32_t* out_lo, int32_t* out_count) {
+  me_range range_("me_vo_new_cells");
+  if (!c) return ME_ERR_INVALID;
+  ME_CHECK(c, n >= 0 && nx > 0 && ny > 0 && (long)nx * ny <= kMaxCells && n_feats >= 0 && cw > 0 && ch > 0 &&
+                  width > 0 && height > 0,
+           "me_vo_new_cells: bad sizes (at most %d cells)", kMaxCells);
+  ME_HIP(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(vo_cells_kernel, dim3(1), dim3(kCellBlock), 0, c->stream, uv, status, ok, n, width, height, margin,
+                     nx, ny, cw, ch, n_feats, (unsigned)t, d_min, out_uv, out_lo, out_count);
+  return me_check_launch(c, "vo_cells_kernel");
 }

@@ -149,6 +149,23 @@ def _pick(uv, d, sc, nd, unique, ratio):
     return xr_f, ok
 
 
+def new_cells(t: int, uv_good: np.ndarray, grid) -> np.ndarray:
+    """New features of keyframe t: the good tracked features (uv_good) occupy
+    their grid cell (trunc((u - MARGIN) / cw), trunc((v - MARGIN) / ch)),
+    clamped, in FP64; the first max(0, n_feats - #good) empty cells in
+    ascending order get a feature at MARGIN + (cell + 0.5 + jitter) * (cw, ch),
+    rounded to float32 (me_vo_new_cells computes the same on the device)."""
+    nx, ny, cw, ch, n_feats = grid
+    occ = np.zeros(nx * ny, bool)
+    if len(uv_good):
+        cx = np.clip(((uv_good[:, 0].astype(np.float64) - MARGIN) / cw).astype(np.int64), 0, nx - 1)
+        cy = np.clip(((uv_good[:, 1].astype(np.float64) - MARGIN) / ch).astype(np.int64), 0, ny - 1)
+        occ[cy * nx + cx] = True
+    empty = np.flatnonzero(~occ)[: max(0, n_feats - len(uv_good))]
+    cyx = np.stack([empty % nx, empty // nx], -1).astype(np.float64)
+    return (MARGIN + (cyx + 0.5 + _cell_jitter(t, empty)) * np.array([cw, ch])).astype(np.float32)
+
+
 def camera_centre(pose) -> np.ndarray:
     """World position of a {t, angle-axis} world->camera pose: -R^T t (drift
     is measured on centres: the world->camera translation also carries the
@@ -208,6 +225,17 @@ class Backend:
 
     def match(self, imgs, uv, lo, nd, unique):
         return match_host(self, imgs, uv, lo, nd, None, unique, self.d_max)
+
+    def klt_match_new(self, h, imgs, lo, nd, dvalid, t, grid, d_min, nd_new):
+        """klt_match, then the new features of the cells the good tracked
+        features leave empty (new_cells) matched with the uniqueness test:
+        (uv, status, xr, ok, new_uv, new_xr, new_ok)."""
+        uv, st, xr, ok = self.klt_match(h, imgs, lo, nd, dvalid)
+        H, W = imgs[2]
+        good = (st == 1) & in_margin(uv, W, H) & ok
+        nuv = new_cells(t, uv[good], grid)
+        nxr, nok = self.match(imgs, nuv, np.full(len(nuv), d_min, np.int64), nd_new, True)
+        return uv, st, xr, ok, nuv, nxr, nok
 
     def scale_submit(self, sp, params):
         self._scale_res = self.scale_optimise(sp, params)
@@ -462,6 +490,53 @@ class GPUBackend(Backend):
         ok = self._view(ho, np.uint8, n, 13 * n).astype(bool)
         return uv, st, xr, ok
 
+    def klt_match_new(self, h, imgs, lo, nd, dvalid, t, grid, d_min, nd_new):
+        """One submission and one round trip: the tracked features' matcher,
+        me_vo_new_cells (the cells they leave empty) and the new features'
+        matcher (me_mi_epipolar_match_count over the device count)."""
+        import ctypes
+
+        n = h[0]
+        if n == 0:
+            return Backend.klt_match_new(self, h, imgs, lo, nd, dvalid, t, grid, d_min, nd_new)
+        c = self.mctx
+        if c is not self.tctx:
+            self.tctx.synchronize()  # the KLT results
+        nx, ny, cw, ch, nf = grid
+        H, W = imgs[2]
+        V = ctypes.c_void_p
+        hp = self._hbuf("lo", 5 * n)
+        self._view(hp, np.int32, n)[:] = lo
+        self._view(hp, np.uint8, n, 4 * n)[:] = dvalid
+        dl = self._dbuf("lo", 5 * n)
+        c.copy_async(dl, hp, 5 * n)
+        dres = self._dbuf("res", 14 * n)
+        self._epipolar(imgs, dres, dl, dl + 4 * n, dres + 12 * n, n, nd, False, dres + 8 * n, dres + 13 * n)
+        # new-feature block: count (16 B) | uv (8 nf) | xr (4 nf) | lo (4 nf) | ok (nf)
+        m = max(nf, 1)
+        dn = self._dbuf("new", 16 + 17 * m)
+        c.check(c.lib.me_vo_new_cells(c.h, V(dres), V(dres + 12 * n), V(dres + 13 * n), n, W, H, float(MARGIN), nx,
+                                      ny, float(cw), float(ch), nf, t, d_min, V(dn + 16), V(dn + 16 + 12 * m), V(dn)),
+                "me_vo_new_cells")
+        c.check(c.lib.me_mi_epipolar_match_count(c.h, V(imgs[0]), V(imgs[1]), W, H, W, V(dn + 16), V(dn + 16 + 12 * m),
+                                                 V(dn), m, nd_new, PATCH, self.d_max, 1, 1.2, float(MARGIN),
+                                                 V(dn + 16 + 8 * m), V(dn + 16 + 16 * m)),
+                "me_mi_epipolar_match_count")
+        o = 16 * ((14 * n + 15) // 16)
+        ho = self._hbuf("out", o + 16 + 17 * m)
+        c.copy_async(ho, dres, 14 * n)
+        c.copy_async(ho + o, dn, 16 + 17 * m)
+        c.synchronize()
+        uv = self._view(ho, np.float32, 2 * n).reshape(n, 2).copy()
+        xr = self._view(ho, np.float32, n, 8 * n).copy()
+        st = self._view(ho, np.uint8, n, 12 * n).copy()
+        ok = self._view(ho, np.uint8, n, 13 * n).astype(bool)
+        k = int(self._view(ho, np.int32, 1, o)[0])
+        nuv = self._view(ho, np.float32, 2 * k, o + 16).reshape(k, 2).copy()
+        nxr = self._view(ho, np.float32, k, o + 16 + 8 * m).copy()
+        nok = self._view(ho, np.uint8, k, o + 16 + 16 * m).astype(bool)
+        return uv, st, xr, ok, nuv, nxr, nok
+
     def match(self, imgs, uv, lo, nd, unique):
         n = len(uv)
         if n == 0:
@@ -631,10 +706,11 @@ class WindowedStereoVO:
     when log_events is set.
 
     overlap=True pipelines the loop without changing any decision: process(t)
-    queues the KLT of frame t first, then completes frame t - 1 (its BA
-    result, the pops, its FrameResult), then matches, books and queues the BA
-    and the scale LM of frame t; call finish() after the last frame.  With
-    overlap=False every process(t) completes frame t before returning."""
+    queues the KLT of frame t first, then completes frame t - 1 (queues its
+    scale LM behind that KLT, both beside frame t - 1's BA, then waits for the
+    BA result; pops; its FrameResult), then matches, books and queues the BA
+    of frame t; call finish() after the last frame.  With overlap=False every
+    process(t) completes frame t before returning."""
 
     def __init__(self, cfg: PipelineConfig, backend: Backend, K=None, first_pose=None, velocity=None,
                  log_events: bool = False, overlap: bool = False):
@@ -655,7 +731,7 @@ class WindowedStereoVO:
         self.first = np.zeros(0, np.int64)   # first frame still held (after pops)
         self.last = np.zeros(0, np.int64)    # last frame observed
         self.latest_id = 0                   # WBA_Point<pair<Point2f,Point2f>>::latestID
-        self.obs = {}                        # t -> (track indices int64, (n, 4) float32 {xl, yl, xr, yr})
+        self.obs = {}                        # t -> (track IDs int64, ascending; (n, 4) float32 {xl, yl, xr, yr})
         self.poses = {}                      # t -> {t, angle-axis} world -> camera
         self.first_pose = np.zeros(6) if first_pose is None else np.asarray(first_pose, np.float64)
         self.velocity = velocity             # prior {t, aa} step for the second frame
@@ -665,7 +741,8 @@ class WindowedStereoVO:
         self.overlap = overlap
         self._ev = []                        # compact event records, expanded by .events
         self.results = []
-        self._pending = None                 # frame whose BA / scale LM are queued
+        self._pending = None                 # frame whose BA (and, once _complete runs, scale LM) are queued
+        self._scale_args = None
         self.stage_s = {"host": 0.0, "wait": 0.0}  # host bookkeeping vs time blocked in the backend
 
     @property
@@ -763,8 +840,8 @@ class WindowedStereoVO:
         kh = None
         if self.prev_imgs is not None and self.active.any():
             act = np.flatnonzero(self.active)
-            pi, puv = self.obs[self.prev_t]
-            pos = np.searchsorted(pi, act)
+            pid, puv = self.obs[self.prev_t]
+            pos = np.searchsorted(pid, self.ids[act])
             kh = self.be.klt_submit(self.prev_imgs, imgs, np.ascontiguousarray(puv[pos, :2]))
         self._complete()  # frame t-1: BA result, pops (active tracks keep their order)
         pose = self._predict_pose(t)
@@ -772,27 +849,22 @@ class WindowedStereoVO:
         trk_idx = np.zeros(0, np.int64)
         trk_uv = np.zeros((0, 2), np.float32)
         xr = np.zeros(0, np.float32)
+        grid = (self.nx, self.ny, self.cw, self.ch, cfg.n_feats)
+        _, nd_new, _ = self.search_window()
         if kh is not None:
-            # 2. KLT gate + stereo matching of the tracked features (around their predicted disparity)
+            # 2. KLT gate + stereo matching of the tracked features (around their predicted disparity),
+            # 3a. then the new features of the cells they leave empty -- one backend round trip
             act = np.flatnonzero(self.active)
             lo, nd, dvalid = self.search_window(self._predicted_disparity(act, pose))
-            uv, st, xr_all, ok = self._wait(self.be.klt_match, kh, imgs, lo, nd, dvalid)
-            keep = (st == 1) & self._in_margin(uv)
-            good = keep & ok
+            uv, st, xr_all, ok, nuv, nxr, nok = self._wait(self.be.klt_match_new, kh, imgs, lo, nd, dvalid, t, grid,
+                                                           cfg.d_min, nd_new)
+            good = (st == 1) & self._in_margin(uv) & ok
             self.active[act[~good]] = False
             trk_idx, trk_uv, xr = act[good], uv[good], xr_all[good]
+        else:
+            nuv = new_cells(t, trk_uv, grid)
+            nxr, nok = self._wait(self.be.match, imgs, nuv, np.full(len(nuv), cfg.d_min, np.int64), nd_new, True)
         n_tracked = len(trk_idx)
-        # 3a. new tracks in empty cells
-        occ = np.zeros(self.nx * self.ny, bool)
-        if n_tracked:
-            cx = np.clip(((trk_uv[:, 0] - MARGIN) / self.cw).astype(np.int64), 0, self.nx - 1)
-            cy = np.clip(((trk_uv[:, 1] - MARGIN) / self.ch).astype(np.int64), 0, self.ny - 1)
-            occ[cy * self.nx + cx] = True
-        empty = np.flatnonzero(~occ)[: max(0, cfg.n_feats - n_tracked)]
-        cyx = np.stack([empty % self.nx, empty // self.nx], -1).astype(np.float64)
-        nuv = (MARGIN + (cyx + 0.5 + _cell_jitter(t, empty)) * np.array([self.cw, self.ch])).astype(np.float32)
-        _, nd_new, _ = self.search_window()
-        nxr, nok = self._wait(self.be.match, imgs, nuv, np.full(len(nuv), cfg.d_min, np.int64), nd_new, True)
         nuv, nxr = nuv[nok], nxr[nok]
         new_idx = self._add_tracks(t, nuv, nxr, pose)
         # 3b. this frame's features (tracked first, then new; sorted by track = ID order)
@@ -801,16 +873,18 @@ class WindowedStereoVO:
                                 np.concatenate([nuv, nxr[:, None], nuv[:, 1:2]], 1)]).astype(np.float32)
         o = np.argsort(idx, kind="stable")
         idx, feats = idx[o], feats[o]
-        self.obs[t] = (idx, feats)
+        fid = self.ids[idx]
+        self.obs[t] = (fid, feats)
         self.last[idx] = t
-        self.be.window_add(t, self.ids[idx].astype(np.int32), feats)
+        self.be.window_add(t, fid.astype(np.int32), feats)
         if self.log_events:
             is_new = np.zeros(len(self.ids), bool)
             is_new[new_idx] = True
             self._ev.append(("frame", self.ids[idx].copy(), t, feats.copy(), is_new[idx]))
-        # 5./6. windowed BA queued, then the scale LM over the tracks seen in t (beside the BA)
+        # 5./6. windowed BA queued; the scale LM over the tracks seen in t is queued by the next
+        # keyframe behind its KLT (both beside this BA; the scale only enters the frame's result)
         ba = self._ba_submit(t)
-        self._scale_submit(t, imgs, idx)
+        self._scale_args = (t, imgs, idx)
         self._pending = (t, n_tracked, len(new_idx), int(self.active.sum()), ba)
         self.prev_imgs, self.prev_t = imgs, t
         if not self.overlap:
@@ -830,6 +904,8 @@ class WindowedStereoVO:
             return
         t, n_tracked, n_new, n_active, ba = self._pending
         self._pending = None
+        self._scale_submit(*self._scale_args)
+        self._scale_args = None
         sc = self._wait(self.be.scale_result)
         nwp, nwo, bs = self._ba_finish(ba)
         # 3c. pop the features that leave the window with the next keyframe
@@ -894,13 +970,13 @@ class WindowedStereoVO:
         for f in range(f0, t + 1):
             if f not in self.obs:
                 continue
-            i, feats = self.obs[f]
-            j = local[i]
+            fid, feats = self.obs[f]
+            j = local[np.searchsorted(self.ids, fid)]
             q = off[j] + (f - first[j])
             fe[q] = feats
             cam[q] = f - f0
             pti[q] = j
-            seen += len(i)
+            seen += len(fid)
         assert seen == n_obs, "window tracks must have contiguous features in the window"
         cams = np.stack([self.poses[f] for f in range(f0, t + 1)])
         return S.BAProblem(cams, self.X[upts], fe, cam, pti, self.K.copy(), self.K.copy(), cfg.baseline, cfg.feat_var,
@@ -926,20 +1002,18 @@ class WindowedStereoVO:
     def _pop(self, new_first):
         """WBA_Point::pop() of every feature older than `new_first`; empty tracks deleted."""
         for f in [f for f in self.obs if f < new_first]:
-            idx, _ = self.obs.pop(f)
+            fid, _ = self.obs.pop(f)
             self.be.window_pop(f)
             if self.log_events:
-                self._ev.append(("pop", self.ids[idx].copy()))
-            self.first[idx] = f + 1
+                self._ev.append(("pop", fid.copy()))
+            self.first[np.searchsorted(self.ids, fid)] = f + 1
         dead = (self.last < new_first)
         if dead.any():
             if self.log_events:
                 self._ev.append(("del", self.ids[np.flatnonzero(dead)].copy()))
-            keep = ~dead
-            remap = np.cumsum(keep) - 1
+            keep = ~dead  # (the observation store holds IDs: nothing to re-index)
             self.ids, self.X, self.active = self.ids[keep], self.X[keep], self.active[keep]
             self.first, self.last = self.first[keep], self.last[keep]
-            self.obs = {f: (remap[i], fe) for f, (i, fe) in self.obs.items()}
 
 
 def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_div: int = 1, first_id: int = 0):
