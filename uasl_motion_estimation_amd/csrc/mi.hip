@@ -163,27 +163,62 @@ __device__ __forceinline__ void lane_hist_pair(uint32_t* h, const uint8_t* __res
   }
 }
 
+// Candidate pairs of the epipolar matcher (EPI instances): pair k is
+// candidate c = k mod nd of feature f = k / nd, left patch at (floor(u - h),
+// floor(v - h)), right patch d = lo_f + c pixels to its left; scored iff the
+// right patch starts at x >= 0, d <= d_max and the feature passes the gates
+// (valid_f; status_f == 1 inside the margin); score -inf otherwise.
+struct EpiMap {
+  const float* uv;
+  const int32_t* lo;
+  const uint8_t* valid;
+  const uint8_t* status;
+  const int32_t* n_dev;  // feature count on the device (or null)
+  int nd, d_max, width, height, half;
+  float margin;
+  double* sc;  // n x nd scores
+};
+
 // PW, PH > 0: patch size known at compile time (11x11 residual, 10x10 finite-difference ROIs).
-template <int PW, int PH>
+template <int PW, int PH, bool EPI = false>
 __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                              const uint8_t* __restrict__ imgR, int strideR,
                                                              long bytesL, long bytesR,
                                                              const int32_t* __restrict__ xyL,
                                                              const int32_t* __restrict__ xyR, int n, int pw, int ph,
                                                              const float* __restrict__ tab, int tab_bytes,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, EpiMap em = EpiMap{}) {
   __shared__ uint32_t lds[kLaneWords * kLaneBlock];
   const int lane = threadIdx.x;
   uint32_t* h = lds + lane;
   for (int w = 0; w < kLaneWords; ++w) h[64 * w] = 0u;
   // table entry of (a, b, cJ) is c3(a) + b(b-1)/2 + cJ - 1; buffer loads past tab_bytes return 0
   const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)tab, (short)0, tab_bytes, 0x00020000);
-  for (int k0 = blockIdx.x * kLaneBlock; k0 < n; k0 += gridDim.x * kLaneBlock) {
+  const int ntot = EPI ? (em.n_dev ? min(n, *em.n_dev) : n) * em.nd : n;
+  for (int k0 = blockIdx.x * kLaneBlock; k0 < ntot; k0 += gridDim.x * kLaneBlock) {
     const int k = k0 + lane;
-    if (k < n) {
+    bool live = k < ntot;
+    long oL = 0, oR = 0;
+    if (EPI && live) {
+      const int f = k / em.nd, c = k - f * em.nd;
+      const float u = em.uv[2 * f], v = em.uv[2 * f + 1];
+      // Rect(x - w, y - w, ..) corner (floor of the FP64 value, as the restatement)
+      const int x0 = (int)floor((double)u - em.half), y0 = (int)floor((double)v - em.half);
+      bool fv = em.valid ? em.valid[f] != 0 : true;
+      if (em.status)  // the KLT gate: status 1 and inside the feature margin
+        fv = fv && em.status[f] == 1 && u >= em.margin && u < (float)em.width - em.margin && v >= em.margin &&
+             v < (float)em.height - em.margin;
+      const int d = em.lo[f] + c, xr = x0 - d;
+      live = fv && xr >= 0 && d <= em.d_max;
+      oL = (long)y0 * strideL + x0;
+      oR = (long)y0 * strideR + xr;
+    } else if (!EPI && live) {
       const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
       const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
-      const long oL = (long)cl.y * strideL + cl.x, oR = (long)cr.y * strideR + cr.x;
+      oL = (long)cl.y * strideL + cl.x;
+      oR = (long)cr.y * strideR + cr.x;
+    }
+    if (live) {
       const int rows = PH > 0 ? PH : ph;
       // 16-byte windows start at most 3 bytes before a row and end at most 16 after its start
       const bool fast = oL >= 3 && oR >= 3 && oL + (long)(rows - 1) * strideL + 16 <= bytesL &&
@@ -303,7 +338,11 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
 #pragma unroll
     for (int u = 0; u < kLaneUnroll; ++u) MI += vp[u];
     // the joint words were cleared by the walk; bitmap and marginals are rewritten per pair
-    if (k < n) out[k] = MI;
+    if (EPI) {
+      if (k < ntot) em.sc[k] = live ? (double)MI : -INFINITY;
+    } else if (k < n) {
+      out[k] = MI;
+    }
   }
 }
 
@@ -383,68 +422,97 @@ __global__ __launch_bounds__(kLargeBlock) void entropy_kernel(const uint8_t* __r
 inline float inv_count(long n) { return (float)(1.0 / (double)n); }
 
 // Epipolar MI stereo matcher of the VO loop (pipeline.WindowedStereoVO.
-// stereo_match / _pick, restated on the device): one workgroup per feature,
-// 16 lane groups score its candidate disparities (group_mi: the bits of
-// me_mi_scores), then one lane picks the best in FP64 exactly as the numpy
-// restatement does (first maximum, interior, parabola vertex, uniqueness
-// against the best outside +-2 candidates, x_r = u - disparity, margin test).
-// Block size by candidate count: 16 groups for the tracked features' short
-// windows (~13 candidates), 64 for the new features' full range (127: two
-// candidates per group instead of eight on the per-feature chain).
-constexpr int kEpiMaxNd = 512, kEpiWideNd = 32;
-template <int kEpiBlock>
-__global__ __launch_bounds__(kEpiBlock) void mi_epipolar_kernel(
+// stereo_match / _pick, restated on the device).  Two passes:
+//  * score: every (feature, candidate disparity) pair is one 16-lane group's
+//    MI (group_mi: the bits of me_mi_scores), dealt flat over a grid-stride
+//    loop -- a feature's candidates run side by side, not on one workgroup's
+//    chain (the full-range search of new features has 127 of them);
+//  * pick: one thread per feature, exactly as the numpy restatement, in FP64
+//    (first maximum, interior, parabola vertex, uniqueness against the best
+//    outside +-2 candidates, x_r = u - disparity, margin test).
+// n_dev (optional): the feature count a preceding kernel left on the device.
+constexpr int kEpiMaxNd = 512, kEpiBlock = 256, kEpiGroups = kEpiBlock / 16, kBlockPick = 256;
+__global__ __launch_bounds__(kEpiBlock) void mi_epi_score_kernel(
     const uint8_t* __restrict__ L, const uint8_t* __restrict__ R, int stride, int width, int height,
     const float* __restrict__ uv, const int32_t* __restrict__ lo, const uint8_t* __restrict__ valid,
     const uint8_t* __restrict__ status, int n, const int32_t* __restrict__ n_dev, int nd, int patch, int d_max,
-    int unique, double ratio, float margin, float invN, float* __restrict__ xr_out, uint8_t* __restrict__ ok_out) {
-  constexpr int kEpiGroups = kEpiBlock / 16;
+    float margin, float invN, double* __restrict__ sc) {
   __shared__ uint32_t lds[kEpiGroups * kGroupWords];
-  __shared__ double sc[kEpiMaxNd];
-  const int f = blockIdx.x;
-  if (f >= n || (n_dev && f >= *n_dev)) return;  // (n_dev: the count a preceding kernel left on the device)
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
-  const float u = uv[2 * f], v = uv[2 * f + 1];
+  const int nf = n_dev ? min(n, *n_dev) : n;
+  const long total = (long)nf * nd;
   const int half = patch / 2;
-  // Rect(x - w, y - w, ..) corner (floor of the FP64 value, as the restatement)
-  const int x0 = (int)floor((double)u - half), y0 = (int)floor((double)v - half);
-  bool fv = valid ? valid[f] != 0 : true;
-  if (status)  // the KLT gate: status 1 and inside the feature margin
-    fv = fv && status[f] == 1 && u >= margin && u < (float)width - margin && v >= margin && v < (float)height - margin;
-  const int l0 = lo[f];
-  for (int c = grp; c < nd; c += kEpiGroups) {
-    const int d = l0 + c, xr = x0 - d;
+  for (long q = (long)blockIdx.x * kEpiGroups + grp; q < total; q += (long)gridDim.x * kEpiGroups) {
+    const int f = (int)(q / nd), c = (int)(q - (long)f * nd);
+    const float u = uv[2 * f], v = uv[2 * f + 1];
+    // Rect(x - w, y - w, ..) corner (floor of the FP64 value, as the restatement)
+    const int x0 = (int)floor((double)u - half), y0 = (int)floor((double)v - half);
+    bool fv = valid ? valid[f] != 0 : true;
+    if (status)  // the KLT gate: status 1 and inside the feature margin
+      fv = fv && status[f] == 1 && u >= margin && u < (float)width - margin && v >= margin &&
+           v < (float)height - margin;
+    const int d = lo[f] + c, xr = x0 - d;
     const bool ok = fv && xr >= 0 && d <= d_max;  // (group-uniform)
     float s = 0.0f;
     if (ok) s = group_mi<false>(h, L + (long)y0 * stride + x0, stride, R + (long)y0 * stride + xr, stride, patch, patch,
                                 invN);
-    if (h.gl == 0) sc[c] = ok ? (double)s : -INFINITY;
+    if (h.gl == 0) sc[q] = ok ? (double)s : -INFINITY;
   }
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  int k = 0;
-  double best = -INFINITY;
-  for (int c = 0; c < nd; ++c)
-    if (sc[c] > best) {  // np.argmax: the first maximum
-      best = sc[c];
-      k = c;
+}
+
+// One wave per feature: lanes take candidates lane, lane + 64, ...; the first
+// maximum (largest score, smallest index on ties: np.argmax) and the best
+// outside +-2 candidates by wave reductions (exact: max / compare only).
+__global__ __launch_bounds__(kBlockPick) void mi_epi_pick_kernel(const float* __restrict__ uv,
+                                                                 const int32_t* __restrict__ lo, int n,
+                                                                 const int32_t* __restrict__ n_dev, int nd, int unique,
+                                                                 double ratio, float margin,
+                                                                 const double* __restrict__ scores,
+                                                                 float* __restrict__ xr_out,
+                                                                 uint8_t* __restrict__ ok_out) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * (kBlockPick / 64) + (threadIdx.x >> 6);
+  if (f >= (n_dev ? min(n, *n_dev) : n)) return;  // (wave-uniform)
+  const double* sc = scores + (long)f * nd;
+  double bv = -INFINITY;
+  int bi = nd;  // (no score above -inf: np.argmax gives 0)
+  for (int c = lane; c < nd; c += 64) {
+    const double x = sc[c];
+    if (x > bv) {
+      bv = x;
+      bi = c;
     }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double ov = __shfl_xor(bv, off, 64);
+    const int oi = __shfl_xor(bi, off, 64);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  const int k = bi == nd ? 0 : bi;
+  const double best = bi == nd ? -INFINITY : bv;
+  double second = -INFINITY;
+  if (unique) {
+    for (int c = lane; c < nd; c += 64)
+      if (c < k - 2 || c > k + 2) second = fmax(second, sc[c]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) second = fmax(second, __shfl_xor(second, off, 64));
+  }
+  if (lane != 0) return;
   bool ok = k > 0 && k < nd - 1 && isfinite(best);
   const int kk = min(max(k, 1), nd - 2);
   const double sm = sc[kk - 1], s0 = sc[kk], sp = sc[kk + 1];
   const double den = sm - 2.0 * s0 + sp;
   ok = ok && isfinite(sm) && isfinite(sp) && den < 0.0;
-  if (unique) {
-    double second = -INFINITY;
-    for (int c = 0; c < nd; ++c)
-      if ((c < k - 2 || c > k + 2) && sc[c] > second) second = sc[c];
-    ok = ok && best >= ratio * second;
-  }
+  if (unique) ok = ok && best >= ratio * second;
   const double den_s = ok ? den : -1.0;
   const double delta = ok ? 0.5 * (sm - sp) / den_s : 0.0;
-  const double disp = (double)(l0 + kk) + delta;
-  const float xr_f = (float)((double)u - disp);
+  const double disp = (double)(lo[f] + kk) + delta;
+  const float xr_f = (float)((double)uv[2 * f] - disp);
   ok = ok && xr_f >= margin;
   xr_out[f] = xr_f;
   ok_out[f] = ok ? 1 : 0;
@@ -462,16 +530,34 @@ static int epipolar_launch(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, 
            "me_mi_epipolar_match: bad sizes (3 <= nd <= %d, patch <= 15)", kEpiMaxNd);
   if (n == 0) return ME_OK;
   ME_HIP(c, hipSetDevice(c->device));
+  ME_CHECK(c, (long)n * nd < (1L << 31), "me_mi_epipolar_match: too many candidates");
+  void* sc;
+  ME_TRY(me_scratch(c, SLOT_EPI, 8 * (size_t)n * nd, &sc));
+  const float* tab = nullptr;
+  if (patch == 11) ME_TRY(me_mi_table(c, 121, &tab));
   me_ktimer t(c, ME_KT_MI);
-  if (nd > kEpiWideNd)
-    hipLaunchKernelGGL(mi_epipolar_kernel<1024>, dim3(n), dim3(1024), 0, c->stream, imgL, imgR, stride, width, height,
-                       uv, lo, valid, status, n, n_dev, nd, patch, d_max, unique, ratio, margin,
-                       inv_count((long)patch * patch), xr_out, ok_out);
-  else
-    hipLaunchKernelGGL(mi_epipolar_kernel<256>, dim3(n), dim3(256), 0, c->stream, imgL, imgR, stride, width, height,
-                       uv, lo, valid, status, n, n_dev, nd, patch, d_max, unique, ratio, margin,
-                       inv_count((long)patch * patch), xr_out, ok_out);
-  return me_check_launch(c, "mi_epipolar_kernel");
+  const long pairs = (long)n * nd;
+  if (patch == 11) {
+    // one lane per candidate pair (table-driven terms, the batch kernel's bits)
+    EpiMap em{uv, lo, valid, status, n_dev, nd, d_max, width, height, patch / 2, margin, (double*)sc};
+    const long img_bytes = (long)stride * (height - 1) + width;
+    const int blocks = (int)std::min<long>((pairs + kLaneBlock - 1) / kLaneBlock, 8192);
+    hipLaunchKernelGGL((mi_lane_kernel<11, 11, true>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, imgL, stride, imgR,
+                       stride, img_bytes, img_bytes, nullptr, nullptr, n, 11, 11, tab, (int)(4 * mi_tab_size(121)),
+                       nullptr, em);
+    ME_TRY(me_check_launch(c, "mi_lane_kernel<epi>"));
+  } else {
+    // grid-stride over n x nd 16-lane groups: at most ~8 workgroups per CU (28 KB of LDS each)
+    const int blocks = (int)std::min<long>((pairs + kEpiGroups - 1) / kEpiGroups, 8L * std::max(c->num_cu, 1));
+    hipLaunchKernelGGL(mi_epi_score_kernel, dim3(blocks), dim3(kEpiBlock), 0, c->stream, imgL, imgR, stride, width,
+                       height, uv, lo, valid, status, n, n_dev, nd, patch, d_max, margin,
+                       inv_count((long)patch * patch), (double*)sc);
+    ME_TRY(me_check_launch(c, "mi_epi_score_kernel"));
+  }
+  hipLaunchKernelGGL(mi_epi_pick_kernel, dim3((n + kBlockPick / 64 - 1) / (kBlockPick / 64)), dim3(kBlockPick), 0,
+                     c->stream, uv,
+                     lo, n, n_dev, nd, unique, ratio, margin, (const double*)sc, xr_out, ok_out);
+  return me_check_launch(c, "mi_epi_pick_kernel");
 }
 
 extern "C" int me_mi_epipolar_match(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, int width, int height,
