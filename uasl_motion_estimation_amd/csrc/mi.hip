@@ -12,6 +12,7 @@
 //  * terms use the glibc log2f restatement (me_device.hpp): bit-exact floats.
 #include "me_internal.hpp"
 #include "me_device.hpp"
+#include <cstring>
 
 using namespace me_dev;
 
@@ -25,6 +26,9 @@ using namespace me_dev;
 #endif
 #ifndef MI_UCLR
 #define MI_UCLR 1  // joint-word clear in the walk: 1 unconditional store, 0 predicated
+#endif
+#ifndef QUAD_EXP
+#define QUAD_EXP 0  // quad kernel timing variants (tools/build_variant.sh): 1 no walk, 2 no histogram updates, 4 no gathers
 #endif
 #ifndef MI_PERM
 #define MI_PERM 37  // histogram update order: pixel p = (k * MI_PERM) mod (PW PH), 1 = row-major
@@ -346,6 +350,327 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
   }
 }
 
+// ---------------------------------------------------------------------
+// Batched MI, four lanes per patch pair (the default batch kernel).  The
+// lane kernel above is LDS-bound at ~1.25 waves per SIMD (124 lane-private
+// words).  Here the four lanes q = 0..3 of a quad share one pair's 100 joint
+// words, so a wave holds 16 pairs in 16 x (105 + N) words (N = patch pixels,
+// the term slots) and ~11 waves fit a CU:
+//  * histogram: lane q bins patch rows q, q + 4, ... into the shared joint
+//    words (LDS atomics; same-word updates of a quad serialise, counts are
+//    order-free);
+//  * lane q derives joint rows i = q + 4k (k = 0..4) from one read of their
+//    25 words: left marginals, occupancy (20 bits per row), bin counts; the
+//    right marginal is the quad sum of the column partials (DPP);
+//  * quad prefix sums over the per-row counts give every row its first slot
+//    in the reference's i-outer / j-inner order and its index in a compacted
+//    table of non-empty rows;
+//  * the walk is balanced by bins, not rows: lane q takes the slots
+//    [floor(qT/4), floor((q+1)T/4)) of the pair's T non-empty bins, starting
+//    from the row the row's owner names, gathers their terms from the per-N
+//    table and stores them in their slots;
+//  * lane 0 of the quad adds the slots left to right (bit-identical to the
+//    reference's float loop, mutual_information.cpp:78-84).
+// Group g's word w lives at lds[16 w + g]: the 16 quads of a wave never
+// share a bank; lanes of one quad do when their words agree mod 4.
+// group words: [0,100) joint, [100,105) right marginal, [105,126) compacted row table (20 + 1 spare),
+// [126,132) its left marginals (bytes), [132,136) lane starts, [136, 136 + N) term slots
+constexpr int kQuadBlock = 64, kQuadGroups = 16, kQuadJoint = 100, kQuadCR = 100, kQuadRows = 105, kQuadRowCL = 126,
+              kQuadStart = 132, kQuadTerms = 136;
+
+template <int PW, int PH>
+struct QuadShape {
+  static constexpr int kSlots = (PW > 0 && PH > 0) ? PW * PH : 255;  // >= non-empty bins
+  static constexpr int kWords = kQuadTerms + kSlots;
+  static constexpr int kRows = PH > 0 ? (PH + 3) / 4 : 4;  // patch rows per lane (PH <= 15)
+};
+
+// Quad reductions over lanes 4g..4g+3 by DPP quad permutes (no LDS round trip).
+template <int CTRL>
+__device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t quad_sum(uint32_t v) {
+  v += quad_perm<0xB1>(v);     // lanes [1,0,3,2]
+  return v + quad_perm<0x4E>(v);  // lanes [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t quad_exscan(uint32_t v, int q) {
+  uint32_t s = v;
+  const uint32_t a = quad_perm<0x90>(s);  // lanes [0,0,1,2]
+  s += q >= 1 ? a : 0u;
+  const uint32_t b = quad_perm<0x44>(s);  // lanes [0,1,0,1]
+  s += q >= 2 ? b : 0u;
+  return s - v;
+}
+
+template <int PW, int PH, bool FAST>
+__device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restrict__ imgL, int strideL, long oL,
+                                          const uint8_t* __restrict__ imgR, int strideR, long oR, int pw, int ph,
+                                          int q) {
+  using QS = QuadShape<PW, PH>;
+  if (PH > 0) {
+    uint32_t pl[QS::kRows][3], pr[QS::kRows][3];
+#pragma unroll
+    for (int rr = 0; rr < QS::kRows; ++rr) {
+      const int r = q + 4 * rr;
+      pl[rr][0] = pl[rr][1] = pl[rr][2] = pr[rr][0] = pr[rr][1] = pr[rr][2] = 0u;
+      if (r < PH) {
+        load_row12<FAST>(imgL, oL + (long)r * strideL, PW, pl[rr]);
+        load_row12<FAST>(imgR, oR + (long)r * strideR, PW, pr[rr]);
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < QS::kRows; ++rr) {
+      if (QUAD_EXP == 6 && q + 4 * rr < PH) {  // run-length merged updates along the row
+        int code[PW > 0 ? PW : 1];
+#pragma unroll
+        for (int x = 0; x < PW; ++x)
+          code[x] = bin20((pl[rr][x >> 2] >> (8 * (x & 3))) & 0xff) * 20 + bin20((pr[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
+        uint32_t run = 1;
+#pragma unroll
+        for (int x = 0; x < PW; ++x) {
+          if (x + 1 < PW && code[x + 1] == code[x]) {
+            ++run;
+          } else {
+            atomicAdd(&hg[16 * (code[x] >> 2)], run << ((code[x] & 3) * 8));
+            run = 1;
+          }
+        }
+      } else if (q + 4 * rr < PH) {
+#pragma unroll
+        for (int k = 0; k < PW; ++k) {
+          // scattered (a multiplier coprime to PW): neighbouring pixels often share a joint word
+          const int x = PW > 0 ? (k * (PW % 5 == 0 ? 3 : 5)) % (PW > 0 ? PW : 1) : k;
+          const int bl = bin20((pl[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
+          const int br = bin20((pr[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
+          const int code = bl * 20 + br;
+          if (QUAD_EXP == 5) hg[16 * (code >> 2)] = 1u << ((code & 3) * 8);  // timing only: plain stores
+          else if (QUAD_EXP != 2) atomicAdd(&hg[16 * (code >> 2)], 1u << ((code & 3) * 8));
+          else if (code == 1023) hg[0] = 1u;
+        }
+      }
+    }
+  } else {
+    for (int r = q; r < ph; r += 4) {
+      uint32_t pl[3], pr[3];
+      load_row12<FAST>(imgL, oL + (long)r * strideL, pw, pl);
+      load_row12<FAST>(imgR, oR + (long)r * strideR, pw, pr);
+#pragma unroll
+      for (int x = 0; x < 12; ++x) {
+        if (x < pw) {
+          const int bl = bin20((pl[x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[x >> 2] >> (8 * (x & 3))) & 0xff);
+          const int code = bl * 20 + br;
+          atomicAdd(&hg[16 * (code >> 2)], 1u << ((code & 3) * 8));
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_u8(const uint32_t* word, int byte) {
+  return (uint32_t)reinterpret_cast<const uint8_t*>(word)[byte];
+}
+
+template <int PW, int PH, bool EPI = false>
+__global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __restrict__ imgL, int strideL,
+                                                             const uint8_t* __restrict__ imgR, int strideR,
+                                                             long bytesL, long bytesR,
+                                                             const int32_t* __restrict__ xyL,
+                                                             const int32_t* __restrict__ xyR, int n, int pw, int ph,
+                                                             const float* __restrict__ tab, int tab_bytes,
+                                                             float* __restrict__ out, EpiMap em = EpiMap{}) {
+  using QS = QuadShape<PW, PH>;
+  __shared__ uint32_t lds[QS::kWords * kQuadGroups];
+  const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
+  uint32_t* hg = lds + g;  // word w of this quad's pair: hg[16 w]
+  // joint words zero (the walk's clears keep them so); row table entries always name a row of this region
+  for (int w = q; w < kQuadRowCL; w += 4) hg[16 * w] = 0u;
+  const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)tab, (short)0, tab_bytes, 0x00020000);
+  const int ntot = EPI ? (em.n_dev ? min(n, *em.n_dev) : n) * em.nd : n;
+  for (int k0 = blockIdx.x * kQuadGroups; k0 < ntot; k0 += gridDim.x * kQuadGroups) {
+    const int k = k0 + g;
+    bool live = k < ntot;
+    long oL = 0, oR = 0;
+    if (EPI && live) {
+      const int f = k / em.nd, c = k - f * em.nd;
+      const float u = em.uv[2 * f], v = em.uv[2 * f + 1];
+      const int x0 = (int)floor((double)u - em.half), y0 = (int)floor((double)v - em.half);
+      bool fv = em.valid ? em.valid[f] != 0 : true;
+      if (em.status)
+        fv = fv && em.status[f] == 1 && u >= em.margin && u < (float)em.width - em.margin && v >= em.margin &&
+             v < (float)em.height - em.margin;
+      const int d = em.lo[f] + c, xr = x0 - d;
+      live = fv && xr >= 0 && d <= em.d_max;
+      oL = (long)y0 * strideL + x0;
+      oR = (long)y0 * strideR + xr;
+    } else if (!EPI && live) {
+      const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
+      const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
+      oL = (long)cl.y * strideL + cl.x;
+      oR = (long)cr.y * strideR + cr.x;
+    }
+    wave_sync();  // the previous pair's clears and slot reads precede this pair's updates
+    if (live) {
+      const int rows = PH > 0 ? PH : ph;
+      const bool fast = oL >= 3 && oR >= 3 && oL + (long)(rows - 1) * strideL + 16 <= bytesL &&
+                        oR + (long)(rows - 1) * strideR + 16 <= bytesR;
+      if (fast)
+        quad_hist<PW, PH, true>(hg, imgL, strideL, oL, imgR, strideR, oR, pw, ph, q);
+      else
+        quad_hist<PW, PH, false>(hg, imgL, strideL, oL, imgR, strideR, oR, pw, ph, q);
+    }
+    wave_sync();
+    // Own rows i = q + 4 kk: left marginals (bytes of cl), column partials,
+    // occupancy (20 bits per row), bin counts (bytes of c03 / c4).
+    uint32_t cr4[5] = {0, 0, 0, 0, 0}, rb[5];
+    uint64_t cl = 0;
+    uint32_t c03 = 0, c4 = 0;
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const uint32_t* row = hg + 16 * 5 * (q + 4 * kk);
+      uint32_t s = 0, bits = 0;
+#pragma unroll
+      for (int m = 0; m < 5; ++m) {
+        const uint32_t w = row[16 * m];
+        s = __builtin_amdgcn_sad_u8(w, 0u, s);
+        cr4[m] += w;
+        const uint32_t f = (w + 0x7f7f7f7fu) & 0x80808080u;
+        bits |= ((f * 0x00204081u) >> 28) << (4 * m);
+      }
+      rb[kk] = bits;
+      cl |= (uint64_t)s << (8 * kk);
+      const uint32_t cnt = __builtin_popcount(bits);
+      if (kk < 4) c03 |= cnt << (8 * kk);
+      else c4 = cnt;
+    }
+#pragma unroll
+    for (int m = 0; m < 5; ++m) cr4[m] = quad_sum(cr4[m]);
+    if (q == 0) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) hg[16 * (kQuadCR + m)] = cr4[m];
+    }
+    // Global order = rows ascending, bins ascending within a row.  Per own row:
+    // P = bins in earlier rows (its first slot), E = non-empty rows before it
+    // (its index in the compacted row table).  Row i = q + 4 kk comes after
+    // all rows of earlier kk and the rows of lanes < q at this kk: quad
+    // reductions / exclusive scans of the packed per-kk bytes (no byte ever
+    // carries: every partial sum is <= N <= 255).
+    const uint32_t a03 = quad_sum(c03), a4 = quad_sum(c4);
+    const uint32_t p03 = a03 * 0x01010100u + quad_exscan(c03, q);
+    const uint32_t p4 = __builtin_amdgcn_sad_u8(a03, 0u, 0u) + quad_exscan(c4, q);
+    const int total = (int)(__builtin_amdgcn_sad_u8(a03, 0u, 0u) + a4);
+    const uint32_t n03 = ((c03 + 0x7f7f7f7fu) & 0x80808080u) >> 7, n4 = c4 ? 1u : 0u;
+    const uint32_t na03 = quad_sum(n03);
+    const uint32_t e03 = na03 * 0x01010100u + quad_exscan(n03, q);
+    const uint32_t e4 = __builtin_amdgcn_sad_u8(na03, 0u, 0u) + quad_exscan(n4, q);
+    // Lane q' takes the bins with slots [b_q', b_q'+1), b_q' = floor(q' T / 4): the
+    // owner of the row holding slot b_q' leaves lane q' its start (table entry, bins to skip).
+    uint32_t* rowtab = hg + 16 * kQuadRows;
+    uint8_t* clc = reinterpret_cast<uint8_t*>(hg + 16 * kQuadRowCL);
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int cnt = kk < 4 ? (int)((c03 >> (8 * kk)) & 0xff) : (int)c4;
+      const int P = kk < 4 ? (int)((p03 >> (8 * kk)) & 0xff) : (int)p4;
+      const int E = kk < 4 ? (int)((e03 >> (8 * kk)) & 0xff) : (int)e4;
+      if (cnt > 0) {
+        rowtab[16 * E] = rb[kk] | ((uint32_t)(q + 4 * kk) << 20);
+        clc[64 * (E >> 2) + (E & 3)] = (uint8_t)(cl >> (8 * kk));
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int bq = (qq * total) >> 2;
+          if (P <= bq && bq < P + cnt) hg[16 * (kQuadStart + qq)] = (uint32_t)E | ((uint32_t)(bq - P) << 8);
+        }
+      }
+    }
+    wave_sync();  // right marginal, row table and starts visible to the quad
+    const int s0 = (q * total) >> 2, nq = (((q + 1) * total) >> 2) - s0;
+    const int tmax = QUAD_EXP == 1 ? 0 : wave_max(nq);
+    float* slots = reinterpret_cast<float*>(hg + 16 * kQuadTerms);
+    const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * kQuadCR);
+    const uint8_t* jnt = reinterpret_cast<const uint8_t*>(hg);
+    int e = 0;
+    uint32_t bits = 0, ent = 0, cL = 0, nxt = 0, ncl = 0;
+    if (nq > 0) {
+      const uint32_t st = hg[16 * (kQuadStart + q)];
+      e = (int)(st & 0xff);
+      ent = rowtab[16 * e];
+      cL = clc[64 * (e >> 2) + (e & 3)];
+      bits = ent & 0xfffffu;
+      for (uint32_t sk = st >> 8; sk > 0; --sk) bits &= bits - 1u;
+    }
+    nxt = rowtab[16 * (e + 1)];
+    ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+    int rowb = 64 * 5 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
+    constexpr int kU = 4;
+    float vp[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
+    for (int t = 0; t < tmax; t += kU) {
+      float v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int j = __builtin_ctz(bits | 0x100000u);  // < 21
+        bits &= bits - 1u;
+        const int jo = 64 * (j >> 2) + (j & 3);
+        const uint32_t cJ = jnt[rowb + jo];
+        const uint32_t cR = crb[jo];
+        const int a = (int)max(cL, cR), b = (int)min(cL, cR);
+        const int idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + (int)cJ;
+        const int off = t + u < nq ? 4 * (idx - 1) : 0x7ffffff0;
+        if (QUAD_EXP == 4)
+          v[u] = (float)off;
+        else
+          v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
+        // next non-empty row of the compacted table (read one ahead)
+        const bool z = bits == 0u;
+        e = z ? min(e + 1, 20) : e;
+        bits = z ? (nxt & 0xfffffu) : bits;
+        cL = z ? ncl : cL;
+        rowb = z ? 64 * 5 * (int)(nxt >> 20) : rowb;
+        nxt = rowtab[16 * min(e + 1, 20)];
+        ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) vp[u] = v[u];
+    }
+    {
+      const int t = (tmax + kU - 1) / kU * kU;
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+    }
+    wave_sync();  // the walk's joint reads precede the clears
+    // clear the lane's joint rows for the next pair
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      uint32_t* row = hg + 16 * 5 * (q + 4 * kk);
+#pragma unroll
+      for (int m = 0; m < 5; ++m) row[16 * m] = 0u;
+    }
+    wave_sync();  // slots written by the quad
+    if (q == 0) {
+      float MI = 0.0f;
+      int s = 0;
+      for (; s + 8 <= total; s += 8) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = slots[16 * (s + u)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) MI += x[u];
+      }
+      for (; s < total; ++s) MI += slots[16 * s];
+      if (EPI) {
+        if (k < ntot) em.sc[k] = live ? (double)MI : -INFINITY;
+      } else if (k < n) {
+        out[k] = MI;
+      }
+    }
+  }
+}
+
 // Latency-bound batches: 16 lanes per pair (me_device.hpp GroupHist).
 constexpr int kGroupBlock = 256;
 __global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8_t* __restrict__ imgL, int strideL,
@@ -420,6 +745,15 @@ __global__ __launch_bounds__(kLargeBlock) void entropy_kernel(const uint8_t* __r
 }
 
 inline float inv_count(long n) { return (float)(1.0 / (double)n); }
+
+// ME_MI_KERNEL=lane selects the one-lane-per-pair kernel (A/B timing; same results)
+inline bool mi_use_lane_kernel() {
+  static const bool lane = [] {
+    const char* e = getenv("ME_MI_KERNEL");
+    return e && strcmp(e, "lane") == 0;
+  }();
+  return lane;
+}
 
 // Epipolar MI stereo matcher of the VO loop (pipeline.WindowedStereoVO.
 // stereo_match / _pick, restated on the device).  Two passes:
@@ -541,11 +875,19 @@ static int epipolar_launch(me_ctx* c, const uint8_t* imgL, const uint8_t* imgR, 
     // one lane per candidate pair (table-driven terms, the batch kernel's bits)
     EpiMap em{uv, lo, valid, status, n_dev, nd, d_max, width, height, patch / 2, margin, (double*)sc};
     const long img_bytes = (long)stride * (height - 1) + width;
-    const int blocks = (int)std::min<long>((pairs + kLaneBlock - 1) / kLaneBlock, 8192);
-    hipLaunchKernelGGL((mi_lane_kernel<11, 11, true>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, imgL, stride, imgR,
-                       stride, img_bytes, img_bytes, nullptr, nullptr, n, 11, 11, tab, (int)(4 * mi_tab_size(121)),
-                       nullptr, em);
-    ME_TRY(me_check_launch(c, "mi_lane_kernel<epi>"));
+    if (!mi_use_lane_kernel()) {
+      const int qb = (int)std::min<long>((pairs + kQuadGroups - 1) / kQuadGroups, 16384);
+      hipLaunchKernelGGL((mi_quad_kernel<11, 11, true>), dim3(qb), dim3(kQuadBlock), 0, c->stream, imgL, stride, imgR,
+                         stride, img_bytes, img_bytes, nullptr, nullptr, n, 11, 11, tab, (int)(4 * mi_tab_size(121)),
+                         nullptr, em);
+      ME_TRY(me_check_launch(c, "mi_quad_kernel<epi>"));
+    } else {
+      const int blocks = (int)std::min<long>((pairs + kLaneBlock - 1) / kLaneBlock, 8192);
+      hipLaunchKernelGGL((mi_lane_kernel<11, 11, true>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, imgL, stride,
+                         imgR, stride, img_bytes, img_bytes, nullptr, nullptr, n, 11, 11, tab,
+                         (int)(4 * mi_tab_size(121)), nullptr, em);
+      ME_TRY(me_check_launch(c, "mi_lane_kernel<epi>"));
+    }
   } else {
     // grid-stride over n x nd 16-lane groups: at most ~8 workgroups per CU (28 KB of LDS each)
     const int blocks = (int)std::min<long>((pairs + kEpiGroups - 1) / kEpiGroups, 8L * std::max(c->num_cu, 1));
@@ -602,10 +944,24 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
   }
   const float* tab;
   ME_TRY(me_mi_table(c, npx, &tab));
-  int blocks = (n + kLaneBlock - 1) / kLaneBlock;
-  if (blocks > 8192) blocks = 8192;
   // bounds of the realigned 16-byte row loads: never read past the images
   const long img_bytes_L = (long)sL * (height - 1) + width, img_bytes_R = (long)sR * (height - 1) + width;
+  if (!mi_use_lane_kernel()) {
+    const int qb = (int)std::min<long>(((long)n + kQuadGroups - 1) / kQuadGroups, 16384);
+    const int tb = (int)(4 * mi_tab_size(npx));
+    if (pw == 11 && ph == 11)
+      hipLaunchKernelGGL((mi_quad_kernel<11, 11>), dim3(qb), dim3(kQuadBlock), 0, c->stream, dL, sL, dR, sR,
+                         img_bytes_L, img_bytes_R, dxyL, dxyR, n, pw, ph, tab, tb, dout);
+    else if (pw == 10 && ph == 10)
+      hipLaunchKernelGGL((mi_quad_kernel<10, 10>), dim3(qb), dim3(kQuadBlock), 0, c->stream, dL, sL, dR, sR,
+                         img_bytes_L, img_bytes_R, dxyL, dxyR, n, pw, ph, tab, tb, dout);
+    else
+      hipLaunchKernelGGL((mi_quad_kernel<0, 0>), dim3(qb), dim3(kQuadBlock), 0, c->stream, dL, sL, dR, sR,
+                         img_bytes_L, img_bytes_R, dxyL, dxyR, n, pw, ph, tab, tb, dout);
+    return me_check_launch(c, "mi_quad_kernel");
+  }
+  int blocks = (n + kLaneBlock - 1) / kLaneBlock;
+  if (blocks > 8192) blocks = 8192;
   if (pw == 11 && ph == 11)
     hipLaunchKernelGGL((mi_lane_kernel<11, 11>), dim3(blocks), dim3(kLaneBlock), 0, c->stream, dL, sL, dR, sR, img_bytes_L,
                        img_bytes_R, dxyL, dxyR, n, pw, ph, tab, (int)(4 * mi_tab_size(npx)), dout);
