@@ -80,6 +80,32 @@ __device__ __forceinline__ float log2f_glibc(float x) {
 // calcHist 8U, 20 uniform bins over [0,256): floor(v*20/256) = (5v)>>6
 __device__ __forceinline__ int bin20(int v) { return (v * 5) >> 6; }
 
+// (a-1) a (a+1) / 6 for 1 <= a <= 255: the product is < 2^24 (exact in float)
+// and the quotient is an integer < 2^22, so the rounded float product is within
+// 0.21 of it (checked exhaustively in tests/test_host.py).
+// fl32(1/6) > 1/6 and the quotient k < 2^22 is representable, so the rounded
+// product lies in [k, k + 0.21] and truncation gives k.
+__device__ __forceinline__ int mi_c3(int a) {
+  const float af = (float)a;
+  const float p = __builtin_fmaf(af, af, -1.0f) * af;  // exact: < 2^24
+  return (int)(uint32_t)(p * (1.0f / 6.0f));
+}
+
+// v_mul_u32_u24 (full rate); the compiler otherwise folds these into the
+// quarter-rate v_mul_lo_u32.
+__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Index of T(cJ, cL, cR) in the per-N term table (mi.hip mi_table_kernel):
+// c3(max) + min (min - 1) / 2 + cJ - 1.
+__device__ __forceinline__ int mi_tab_idx(int cJ, int cL, int cR) {
+  const int a = max(cL, cR), b = min(cL, cR);
+  return mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + cJ - 1;
+}
+
 // One MI term of mutual_information.cpp:82-83.
 __device__ __forceinline__ float mi_term(int cJ, int cL, int cR, float invN) {
   float pJ = (float)cJ * invN;
@@ -171,7 +197,8 @@ struct GroupHist {
     atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
   }
   // Returns the MI in lane gl == 0 of the group (other lanes: unspecified).
-  __device__ __forceinline__ float mi(float invN) {
+  // tab: the per-N term table (bit-identical values, one gather per term) or null.
+  __device__ __forceinline__ float mi(float invN, const float* __restrict__ tab = nullptr) {
     wave_sync();
     float* terms = reinterpret_cast<float*>(h + kHistWords);
     uint32_t bits = gl < 13 ? h[110 + gl] : 0u;
@@ -202,7 +229,10 @@ struct GroupHist {
         const int cJ = (h[code[u] >> 2] >> ((code[u] & 3) * 8)) & 0xff;
         const int cL = (h[100 + (i >> 2)] >> ((i & 3) * 8)) & 0xff;
         const int cR = (h[105 + (j >> 2)] >> ((j & 3) * 8)) & 0xff;
-        tv[u] = mi_term(cJ, cL > 0 ? cL : 1, cR > 0 ? cR : 1, invN);  // padded slots: any finite value
+        if (tab)
+          tv[u] = ok[u] ? tab[mi_tab_idx(cJ, cL, cR)] : 0.0f;
+        else
+          tv[u] = mi_term(cJ, cL > 0 ? cL : 1, cR > 0 ? cR : 1, invN);  // padded slots: any finite value
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
@@ -228,7 +258,8 @@ struct GroupHist {
 // Patch pair MI by a 16-lane group; pixels strided over the group.
 template <bool BIN>
 __device__ __forceinline__ float group_mi(GroupHist<16>& h, const uint8_t* A, long astride, const uint8_t* B,
-                                          long bstride, int pw, int ph, float invN) {
+                                          long bstride, int pw, int ph, float invN,
+                                          const float* __restrict__ tab = nullptr) {
   h.clear();
   const int npx = pw * ph;
   // Pixels in batches of 8 per lane: every load of a batch is issued before
@@ -256,7 +287,7 @@ __device__ __forceinline__ float group_mi(GroupHist<16>& h, const uint8_t* A, lo
       }
     }
   }
-  return h.mi(invN);
+  return h.mi(invN, tab);
 }
 
 // ---------------------------------------------------------------------

@@ -83,25 +83,6 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
-// (a-1) a (a+1) / 6 for 1 <= a <= 255: the product is < 2^24 (exact in float)
-// and the quotient is an integer < 2^22, so the rounded float product is within
-// 0.21 of it (checked exhaustively in tests/test_host.py).
-// fl32(1/6) > 1/6 and the quotient k < 2^22 is representable, so the rounded
-// product lies in [k, k + 0.21] and truncation gives k.
-__device__ __forceinline__ int mi_c3(int a) {
-  const float af = (float)a;
-  const float p = __builtin_fmaf(af, af, -1.0f) * af;  // exact: < 2^24
-  return (int)(uint32_t)(p * (1.0f / 6.0f));
-}
-
-// v_mul_u32_u24 (full rate); the compiler otherwise folds these into the
-// quarter-rate v_mul_lo_u32.
-__device__ __forceinline__ uint32_t mul_u24(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-  return r;
-}
-
 // One patch row (PW <= 12 bytes) as three realigned dwords: FAST = the
 // 16-byte window around the row lies inside the image (checked once per pair).
 template <bool FAST>
@@ -677,7 +658,8 @@ __global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8
                                                                      const uint8_t* __restrict__ imgR, int strideR,
                                                                      const int32_t* __restrict__ xyL,
                                                                      const int32_t* __restrict__ xyR, int n, int pw,
-                                                                     int ph, float invN, float* __restrict__ out) {
+                                                                     int ph, float invN, const float* __restrict__ tab,
+                                                                     float* __restrict__ out) {
   __shared__ uint32_t lds[(kGroupBlock / 16) * kGroupWords];
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
@@ -685,7 +667,7 @@ __global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8
     const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
     const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
     const float mi = group_mi<false>(h, imgL + (long)cl.y * strideL + cl.x, strideL,
-                                     imgR + (long)cr.y * strideR + cr.x, strideR, pw, ph, invN);
+                                     imgR + (long)cr.y * strideR + cr.x, strideR, pw, ph, invN, tab);
     if (h.gl == 0) out[k] = mi;
   }
 }
@@ -927,19 +909,21 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
                        const int32_t* dxyL, const int32_t* dxyR, int n, int pw, int ph, float* dout) {
   if (n <= 0) return ME_OK;
   me_ktimer t(c, ME_KT_MI);
+  const float* gtab;  // the group kernels' terms come from the same per-N table
+  ME_TRY(me_mi_table(c, pw * ph, &gtab));
   if (n < kGroupThreshold) {
     // fewer pairs than lanes to fill the chip: 16 lanes per pair
     const int per = kGroupBlock / 16;
     int blocks = (n + per - 1) / per;
     hipLaunchKernelGGL(mi_pairs_group_kernel, dim3(blocks), dim3(kGroupBlock), 0, c->stream, dL, sL, dR, sR, dxyL,
-                       dxyR, n, pw, ph, inv_count((long)pw * ph), dout);
+                       dxyR, n, pw, ph, inv_count((long)pw * ph), gtab, dout);
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
   const int npx = pw * ph;
   if (pw > 12) {  // wider than one realigned 16-byte row load: the group kernel handles any shape
     const int per = kGroupBlock / 16;
     hipLaunchKernelGGL(mi_pairs_group_kernel, dim3((n + per - 1) / per), dim3(kGroupBlock), 0, c->stream, dL, sL, dR,
-                       sR, dxyL, dxyR, n, pw, ph, inv_count((long)npx), dout);
+                       sR, dxyL, dxyR, n, pw, ph, inv_count((long)npx), gtab, dout);
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
   const float* tab;

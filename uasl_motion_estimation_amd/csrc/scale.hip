@@ -40,6 +40,9 @@ struct ScaleArgs {
   int bb_cols, bb_rows;
   int weighting;
   float invN;          // 1/(P*P)
+  const float* tab;    // term table of the P*P-pixel patches (me_mi_table), or null
+  const float* tab_r;  // tables of the residual ((2w+1)^2) and normal-equation ((2w)^2) patches
+  const float* tab_n;
   int nrows;           // residual rows (rows >= nrows are never written: the prep kernel flags them)
 };
 
@@ -269,8 +272,8 @@ constexpr int kTracksPerBlock = kScBlock / 16;
 
 template <bool BIN>
 __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int ax, int ay, const uint8_t* B, int bx,
-                                        int by, int stride, int P, float invN) {
-  return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN);
+                                        int by, int stride, int P, float invN, const float* tab) {
+  return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN, tab);
 }
 
 // Stores a later workgroup of the same launch reduces (residual rows, JJ / Je
@@ -315,14 +318,14 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
 #if ME_SCALE_EXP == 2  // timing experiment: projection only, no MI
     mi = (float)lx;
 #else
-    mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN);
+    mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN, a.tab);
 #endif
   } else {
     if (a.weighting) wv = sobel_weight(a.imgR, a.stride, a.cols, a.rows, rx, ry, P);
 #if ME_SCALE_EXP == 2
     mi = (float)rx;
 #else
-    mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN);
+    mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN, a.tab);
 #endif
   }
   if (h.gl == 0) wt_store(&res[row], (double)mi * wv);
@@ -375,8 +378,8 @@ __device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHi
   const uint8_t* I0 = left ? a.imgL : a.imgR;
   const uint8_t* I1 = left ? a.imgR : a.imgL;
   double wv = a.weighting ? sobel_weight(I0, a.stride, a.cols, a.rows, x0x, x0y, P) : 1.0;
-  double MIp = grp_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN);
-  double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN);
+  double MIp = grp_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN, a.tab);
+  double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN, a.tab);
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) {
     wt_store(&jj[t], J * J * wv);
@@ -432,12 +435,12 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
   double MIp, MIm, wv = 1.0;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, x0x, x0y, P);
-    MIp = grp_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN);
-    MIm = grp_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN);
+    MIp = grp_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab);
+    MIm = grp_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab);
   } else {
     if (a.weighting) wv = sobel_weight_bin(a.imgR, a.stride, x0x, x0y, P);
-    MIp = grp_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN);
-    MIm = grp_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN);
+    MIp = grp_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab);
+    MIm = grp_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab);
   }
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) jj[t] = J * J * wv;
@@ -1139,6 +1142,7 @@ struct ScaleProblem {
 
 ScaleArgs with_invN(ScaleArgs a, int P) {
   a.invN = (float)(1.0 / (double)(P * P));
+  a.tab = P == 2 * a.w + 1 ? a.tab_r : P == 2 * a.w ? a.tab_n : nullptr;
   return a;
 }
 
@@ -1172,6 +1176,9 @@ int upload(me_ctx* c, const me_scale_state* s, int weighting, ScaleProblem& P, c
   a.bb_rows = s->bb_rows;
   a.weighting = weighting;
   a.invN = 1.0f;
+  a.tab = nullptr;
+  ME_TRY(me_mi_table(c, (2 * a.w + 1) * (2 * a.w + 1), &a.tab_r));
+  ME_TRY(me_mi_table(c, 4 * a.w * a.w, &a.tab_n));
   const bool has_mask = s->mask && s->mask_len > 0;
   int tot = 0;
   if (has_mask) {
