@@ -403,6 +403,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MI_COUNTERS = "r03_b_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
@@ -437,7 +438,7 @@ FAMILY_KERNELS = {
     "SCALE_RES": ["scale_res_ctrl_kernel"], "SCALE_NEQ": ["scale_neq_ctrl_kernel"], "KLT": ["klt_kernel"],
     "BA_LINEARIZE": ["linearize_kernel"],
     "BA_SCHUR": ["pt_schur_kernel"], "BA_SOLVE": ["cam_solve_kernel"],
-    "BA_STEP": ["pt_step_kernel"], "MI": ["mi_lane_kernel"],
+    "BA_STEP": ["pt_step_kernel"], "MI": ["mi_quad_kernel"],
 }
 
 
@@ -513,9 +514,24 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
         ctx.free(p)
     avg = ms / max(n, 1)
     achieved = 262.0 * n_pairs / (avg * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc_traffic("MI"), "kernel": "mi_lane_kernel",
-            "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
+    kernel = "mi_lane_kernel" if os.environ.get("ME_MI_KERNEL") == "lane" else "mi_quad_kernel"
+    out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+           "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc_traffic("MI"), "kernel": kernel,
+           "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
+    # VALU-issue roofline: the kernel's wave instructions per pair (SQ_INSTS_VALU of the committed
+    # tools/mi_pmc.sh pass) against one wave64 VALU instruction per SIMD per 4 cycles (1024 SIMDs, 2.4 GHz)
+    cpath = os.path.join(ROOT, "profiles", MI_COUNTERS + ".json")
+    if os.path.exists(cpath):
+        cnt = json.load(open(cpath))
+        if cnt.get("kernel", "").startswith(kernel):
+            peak = 1024 * 2.4e9 / 4 / 1e9
+            ach = cnt["valu_insts_per_pair"] * n_pairs / (avg * 1e-3) / 1e9
+            out["valu_issue"] = {"bound": "valu-issue", "achieved": round(ach, 1), "peak": round(peak, 1),
+                                 "unit": "G wave-instr/s", "frac": round(ach / peak, 4),
+                                 "valu_insts_per_pair": round(cnt["valu_insts_per_pair"], 2),
+                                 "resident_waves_per_cu": round(cnt["resident_waves_per_cu"], 2),
+                                 "counters": "profiles/" + MI_COUNTERS + ".txt"}
+    return out
 
 
 def stereo_vo_line(ctx, n: int, reps: int = 5, cpu: bool = True):
@@ -1099,6 +1115,11 @@ def main():
                                 "sample": f"{cpu_workers} processes x {2 * len(pls)} frames (independent frames, "
                                           f"one process per core: an upper bound for a multi-threaded CPU path); "
                                           f"{wall:.1f} s"}
+            if avail > cpu_workers:
+                # the GPU box grants one GPU's job 16 cores; the frames are independent, so the
+                # host's other cores would add linearly at best: a stated upper bound, not a run
+                cpu["all_cores"]["linear_extrapolation_to_cores_available"] = {
+                    "value": round(nf_all / wall * avail / cpu_workers, 3), "cores": avail}
     if pool is not None:
         pool.close()
         pool.join()
