@@ -271,16 +271,8 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
     X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
     X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
     for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
-    const int cs = b.cpos[o];
-    if (cs >= 0) {  // camera normal-equation pieces, component-major by camera slot
-      double* C = b.cvec + cs;
-      int u = 0;
-      for (int a = 0; a < 6; ++a)
-        for (int c = a; c < 6; ++c, ++u)
-          C[(long)u * g.no] = Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c] + Jc[12 + a] * Jc[12 + c] + Jc[18 + a] * Jc[18 + c];
-      for (int a = 0; a < 6; ++a)
-        C[(long)(21 + a) * g.no] = Jc[a] * r[0] + Jc[6 + a] * r[1] + Jc[12 + a] * r[2] + Jc[18 + a] * r[3];
-    }
+    // (the camera normal-equation pieces are formed by cam_assemble from the
+    // same residual and Jacobian: no 216 B per observation through HBM)
     if (ci - g.nf >= 0) {
       double* W = b.Wo + 18 * slot;
       for (int a = 0; a < 6; ++a)
@@ -295,10 +287,9 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
 }
 
 // Unscaled U = Jc^T Jc (21 unique) and g = Jc^T r per variable camera, in
-// two deterministic stages over the per-observation pieces linearize wrote
-// contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
-// k + ck, ... of 256 slots of camera c into a partial; cam_reduce adds the ck
-// partials in order.
+// two deterministic stages (cam_assemble_body): workgroup (c, k) sums chunks
+// k, k + ck, ... of 256 slots of camera c into a partial; cam_reduce adds
+// the ck partials in order.
 // The last workgroup to arrive on a counter, with a written-through hand-off
 // (the form of the camera solve's workers): thread 0 stored the workgroup's
 // partials with sc1 stores, drains them before a relaxed arrival, and the last
@@ -362,12 +353,14 @@ __device__ void cam_reduce_body(const Geo& g, const Bufs& b, int sharded, const 
 }
 
 // Unscaled U = Jc^T Jc (21 unique) and g = Jc^T r per variable camera, in
-// two deterministic stages over the per-observation pieces linearize wrote
-// contiguously by camera slot (cvec): workgroup (c, k) sums chunks k,
-// k + ck, ... of 256 slots of camera c into a partial; the last of the ck
+// two deterministic stages over the camera's observations in c_obs slot
+// order (each piece formed here from the observation's residual and
+// Jacobian): workgroup (c, k) sums chunks k, k + ck, ... of 256 slots of
+// camera c into a partial; the last of the ck
 // workgroups of camera c to finish adds the ck partials in order.
 // Threads 0 .. kBlock-1 of the block take part (in a wider block the other
 // waves have exited: barriers count only live waves).
+template <int OD>
 __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, double* cpart, int sharded,
                                                   double* colnorm, double* gc_raw, double* Uraw, int ci, int k) {
   __shared__ double lds[4 * 27];
@@ -376,8 +369,26 @@ __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, d
   const int beg = b.c_off[ci], end = b.c_off[ci + 1];
   double v[27];
   for (int i = 0; i < 27; ++i) v[i] = 0;
-  for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock)
-    for (int u = 0; u < 27; ++u) v[u] += b.cvec[(long)u * g.no + q];
+  const int cur = st->cur;
+  for (int q = beg + k * kBlock + threadIdx.x; q < end; q += g.ck * kBlock) {
+    // the observation's residual and Jacobian at the linearisation point, as
+    // linearize_kernel forms them (same function, same Huber scaling: the same
+    // pieces bit for bit), then Jc^T Jc (21) and Jc^T r (6)
+    const int o = b.c_obs[q];
+    const int cam = b.cam_idx[o], pi = b.pt_idx[o];
+    double r[4], Jc[24], Jp[12];
+    obs_residual<OD>(g, b, o, b.cams[cur] + 6 * cam, b.pts[cur] + 3 * pi, r, Jc, Jp);
+    const double s2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    double rho0, sc;
+    huber(s2, &rho0, &sc);
+    for (int kk = 0; kk < 4; ++kk) r[kk] *= sc;
+    for (int kk = 0; kk < 24; ++kk) Jc[kk] *= sc;
+    int u = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int c = a; c < 6; ++c, ++u)
+        v[u] += Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c] + Jc[12 + a] * Jc[12 + c] + Jc[18 + a] * Jc[18 + c];
+    for (int a = 0; a < 6; ++a) v[21 + a] += Jc[a] * r[0] + Jc[6 + a] * r[1] + Jc[12 + a] * r[2] + Jc[18 + a] * r[3];
+  }
   double out[27];
   block_sum<27>(v, out, lds, kBlock / 64);
   if (threadIdx.x == 0) {  // written through for the last of the camera's workgroups (no release per arrival)
@@ -390,7 +401,12 @@ __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, d
 
 __global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart, int sharded,
                                                               double* colnorm, double* gc_raw, double* Uraw) {
-  cam_assemble_body(g, b, cpart, sharded, colnorm, gc_raw, Uraw, blockIdx.x, blockIdx.y);
+  // (one instance per model: the mono model's row selection would otherwise
+  // keep the stereo path's Jacobian arrays out of registers)
+  if (g.od == 4)
+    cam_assemble_body<4>(g, b, cpart, sharded, colnorm, gc_raw, Uraw, blockIdx.x, blockIdx.y);
+  else
+    cam_assemble_body<2>(g, b, cpart, sharded, colnorm, gc_raw, Uraw, blockIdx.x, blockIdx.y);
 }
 
 // Camera assembly riding in the Schur launch (iterations after the first,
@@ -544,7 +560,10 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   if (ca.on && (int)blockIdx.x >= g.ksplit) {  // camera-assembly blocks of a fused launch
     if (threadIdx.x >= kBlock) return;
     const int q = blockIdx.x - g.ksplit;
-    cam_assemble_body(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
+    if (g.od == 4)
+      cam_assemble_body<4>(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
+    else
+      cam_assemble_body<2>(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
     return;
   }
   State* st = b.st;
@@ -2737,7 +2756,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(4 * (size_t)g.no, &b.c_obs);
   add(4 * (size_t)g.no, &b.tmp_obs);
   add(4 * (size_t)g.no, &b.cpos);
-  add(8 * 27 * (size_t)g.no, &b.cvec);
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);
   add((size_t)g.no, &b.dup);
   add(8 * solve_a_doubles(g.Ts), &b.Abuf);

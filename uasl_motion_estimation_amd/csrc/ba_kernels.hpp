@@ -98,7 +98,6 @@ struct Bufs {
   int* c_obs;
   int* tmp_obs;       // plan: unsorted CSR-by-point slots
   int* cpos;          // obs -> slot in c_obs (-1: fixed camera)
-  double* cvec;       // 27 x no (component-major by c_obs slot): Jc'Jc (21) + Jc'r (6) per observation
   double* obsx;       // no * 9  (V_o, g_o unscaled)
   uint8_t* dup;       // obs shares (point, camera) with another obs
   double* Abuf;       // n6 * (n6|1) factorisation workspace (when S does not fit LDS)
