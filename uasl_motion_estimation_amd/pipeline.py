@@ -300,6 +300,7 @@ class GPUBackend(Backend):
         self._wfrm = {}  # frame -> (offset, count)
         self._dev = {}   # name -> [ptr, bytes] on the device
         self._pin = {}   # name -> [ptr, bytes] page-locked host
+        self._hview = {}  # page-locked ptr -> uint8 view of the whole buffer
         self._ba = None
         self._scale_res = None
 
@@ -320,20 +321,29 @@ class GPUBackend(Backend):
         if b is None or b[1] < nbytes:
             if b is not None:
                 self.tctx.synchronize()
+                self._hview.pop(b[0], None)
                 self.tctx.host_free(b[0])
             nb = max(4096, int(nbytes * 1.5))
             self._pin[name] = b = [self.tctx.host_alloc(nb), nb]
+            self._hview[b[0]] = self._map(b[0], nb)  # one numpy view of the whole buffer
         return b[0]
 
     @staticmethod
-    def _view(ptr, dtype, count, offset=0):
+    def _map(ptr, nbytes):
         import ctypes
 
+        return np.frombuffer((ctypes.c_char * nbytes).from_address(ptr), np.uint8, nbytes)
+
+    def _view(self, ptr, dtype, count, offset=0):
+        """count items of dtype at byte offset of the page-locked buffer ptr (a
+        slice of the buffer's cached view: no ctypes type built per call)."""
         nbytes = np.dtype(dtype).itemsize * count
         if count == 0:
             return np.zeros(0, dtype)
-        buf = (ctypes.c_char * nbytes).from_address(ptr + offset)
-        return np.frombuffer(buf, dtype, count)
+        base = self._hview.get(ptr)
+        if base is None:
+            return self._map(ptr + offset, nbytes).view(dtype)
+        return base[offset:offset + nbytes].view(dtype)
 
     def frame_images(self, t, left, right):
         if t in self._imgs:
@@ -377,6 +387,7 @@ class GPUBackend(Backend):
         self.tctx.synchronize()
         for p, _ in self._dev.values():
             self.tctx.free(p)
+        self._hview = {}
         for p, _ in self._pin.values():
             self.tctx.host_free(p)
         self._dev, self._pin = {}, {}
