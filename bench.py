@@ -55,7 +55,7 @@ def parse():
                          "(frontend), or only KLT of frame t+1 beside the scale LM + BA of frame t (klt)")
     ap.add_argument("--front-cus", type=int, default=8,
                     help="frontend overlap: the tracker context's stream runs on CUs i with i %% 16 < F and the "
-                         "back-end stream on the others (me_set_cu_mask; every XCD keeps CUs of both); 0: shared CUs")
+                         "back-end stream on the others (me_set_cu_mask; whole XCDs per side, _lib.cu_split); 0: shared CUs")
     ap.add_argument("--streams", type=int, default=1,
                     help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
                          "thread each), reported as multi_stream; the headline value stays one stream per GPU")
@@ -959,8 +959,10 @@ def main():
         the persistent scale LM otherwise share every CU's issue slots and slow each other."""
         if pipe is None or args.overlap != "frontend" or not 0 < args.front_cus < 16:
             return
-        tctx.set_cu_mask([i for i in range(ncu) if i % 16 < args.front_cus] if on else None)
-        ctx.set_cu_mask([i for i in range(ncu) if i % 16 >= args.front_cus] if on else None)
+        from uasl_motion_estimation_amd._lib import cu_split
+        front, back = cu_split(ncu, args.front_cus)  # whole XCDs per side (ME_CU_SPLIT=interleaved: shared)
+        tctx.set_cu_mask(front if on else None)
+        ctx.set_cu_mask(back if on else None)
     if not args.no_pipeline:
         tctx = Context(local_rank)  # tracker context: its own HIP stream and scratch
         pipe = FramePipeline(ctx, tctx, _Hip(), args.overlap)

@@ -261,6 +261,22 @@ def vptr(a):
     return c_void_p(a.ctypes.data)
 
 
+def cu_split(ncu: int, front_of_16: int, mode: str | None = None):
+    """Disjoint CU sets (front, back) for two contexts, front_of_16 of every 16
+    CUs to the front.  mode "xcd" (default; ME_CU_SPLIT overrides) gives each
+    side whole XCDs: logical CU i sits on XCD i mod 8 (measured: the split by
+    i mod 8 keeps the BA's L2 apart from the front end's, the split by
+    i // 32 does not), so front = {i : i mod 8 < front_of_16 / 2}.  mode
+    "interleaved": front = {i : i mod 16 < front_of_16}, every XCD shared."""
+    mode = mode or os.environ.get("ME_CU_SPLIT", "xcd")
+    if mode == "xcd" and front_of_16 % 2 == 0:
+        front = [i for i in range(ncu) if i % 8 < front_of_16 // 2]
+    else:
+        front = [i for i in range(ncu) if i % 16 < front_of_16]
+    fs = set(front)
+    return front, [i for i in range(ncu) if i not in fs]
+
+
 class Context:
     """One me_ctx (HIP device + stream + scratch).  One per host thread."""
 

@@ -275,17 +275,19 @@ class GPUBackend(Backend):
         self.ctx = ctx or default_context()
         self._own_t = tctx is None and overlap
         self.tctx = tctx or (Context(self.ctx.device) if overlap else self.ctx)
-        # the two contexts run side by side on disjoint CU sets (CU i with
-        # i % 16 < front_cus: front end; every XCD keeps CUs of both): the
+        # the two contexts run side by side on disjoint CU sets (front_cus of
+        # every 16 CUs to the front end, whole XCDs: _lib.cu_split): the
         # persistent scale-LM kernel needs its workgroups co-resident, which
         # the BA's kernels on shared CUs would not leave room for
         self._masked = False
         if self.tctx is not self.ctx and 0 < front_cus < 16:
             import torch
 
+            from ._lib import cu_split
             ncu = torch.cuda.get_device_properties(self.ctx.device).multi_processor_count
-            self.tctx.set_cu_mask([i for i in range(ncu) if i % 16 < front_cus])
-            self.ctx.set_cu_mask([i for i in range(ncu) if i % 16 >= front_cus])
+            front, back = cu_split(ncu, front_cus)
+            self.tctx.set_cu_mask(front)
+            self.ctx.set_cu_mask(back)
             self._masked = True
         # the matchers sit on the loop's critical path between two BAs, when
         # the BA context is idle: they run there (its larger CU share)
