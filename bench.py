@@ -403,7 +403,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MI_COUNTERS = "r03_b_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
+MI_COUNTERS = "r03_c_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
@@ -523,7 +523,7 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
     cpath = os.path.join(ROOT, "profiles", MI_COUNTERS + ".json")
     if os.path.exists(cpath):
         cnt = json.load(open(cpath))
-        if cnt.get("kernel", "").startswith(kernel):
+        if kernel in cnt.get("kernel", ""):
             peak = 1024 * 2.4e9 / 4 / 1e9
             ach = cnt["valu_insts_per_pair"] * n_pairs / (avg * 1e-3) / 1e9
             out["valu_issue"] = {"bound": "valu-issue", "achieved": round(ach, 1), "peak": round(peak, 1),

@@ -30,10 +30,12 @@ def test_mi_scores_bit_exact(ctx, oracle, patch):
     assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
 
 
-@pytest.mark.parametrize("patch", [(11, 11), (10, 10), (12, 12), (13, 13), (3, 7), (1, 1)])
+@pytest.mark.parametrize("patch", [(11, 11), (10, 10), (12, 12), (13, 13), (3, 7), (1, 1), (12, 15), (9, 14)])
 def test_mi_large_batch_bit_exact(ctx, oracle, patch):
-    """>= 32768 pairs take the 8-lane table-driven batch kernel; corners hug the
-    right / bottom image edges so the realigned row loads hit their bounds."""
+    """>= 32768 pairs take the four-lanes-per-pair table-driven batch kernel
+    (11x11, 10x10 compiled shapes; any other <= 12 px wide shape the generic
+    instance, taller ones included); corners hug the right / bottom image edges
+    so the realigned row loads hit their bounds."""
     from uasl_motion_estimation_amd.mutual_information import mi_scores
 
     pw, ph = patch

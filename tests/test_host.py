@@ -134,3 +134,18 @@ def test_mi_table_index_arithmetic_is_exact():
     assert np.array_equal(q, p // 6)
     code = np.arange(400)
     assert np.array_equal((code * 205) >> 12, code // 20)
+
+
+@pytest.mark.parametrize("front", [2, 4, 6, 8, 10, 3])
+@pytest.mark.parametrize("mode", ["xcd", "interleaved"])
+def test_cu_split_is_a_disjoint_cover(front, mode):
+    """_lib.cu_split: the two contexts' CU sets are disjoint, cover the device
+    and give the front end front/16 of it; the XCD mode (CU i on XCD i mod 8)
+    never puts both sides on one XCD (odd shares fall back to interleaving)."""
+    ncu = 256
+    f, b = _lib.cu_split(ncu, front, mode)
+    assert not set(f) & set(b) and sorted(f + b) == list(range(ncu))
+    assert len(f) == ncu * front // 16
+    if mode == "xcd" and front % 2 == 0:
+        xf, xb = {i % 8 for i in f}, {i % 8 for i in b}
+        assert not xf & xb and len(xf) == front // 2

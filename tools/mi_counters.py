@@ -9,6 +9,7 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
 
 name = sys.argv[1]
@@ -21,7 +22,7 @@ for p in ("p1", "p2"):
         k = r["Kernel_Name"]
         if "mi_quad_kernel" not in k and "mi_lane_kernel" not in k:
             continue
-        kname = k.split("(")[0].replace("void ", "").replace("anonymous namespace)::", "").strip()
+        kname = re.sub(r"^void |\(anonymous namespace\)::", "", k).split("(")[0].strip()
         agg[r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[r["Counter_Name"]] += 1
 c = {k: agg[k] / cnt[k] for k in agg}
