@@ -280,6 +280,7 @@ class GPUBackend(Backend):
         # persistent scale-LM kernel needs its workgroups co-resident, which
         # the BA's kernels on shared CUs would not leave room for
         self._masked = False
+        front_cus = int(os.environ.get("ME_VO_FRONT_CUS", front_cus))  # A/B timing
         if self.tctx is not self.ctx and 0 < front_cus < 16:
             import torch
 
