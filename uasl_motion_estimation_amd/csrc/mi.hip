@@ -30,6 +30,9 @@ using namespace me_dev;
 #ifndef QUAD_EXP
 #define QUAD_EXP 0  // quad kernel timing variants (tools/build_variant.sh): 1 no walk, 2 no histogram updates, 4 no gathers
 #endif
+#ifndef QUAD_U
+#define QUAD_U 4  // quad kernel: walk iterations in flight per lane (table gathers overlapped)
+#endif
 #ifndef MI_PERM
 #define MI_PERM 37  // histogram update order: pixel p = (k * MI_PERM) mod (PW PH), 1 = row-major
 #endif
@@ -582,7 +585,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     nxt = rowtab[16 * (e + 1)];
     ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
     int rowb = 64 * 5 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
-    constexpr int kU = 4;
+    constexpr int kU = QUAD_U;
     float vp[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
