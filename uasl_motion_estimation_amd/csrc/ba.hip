@@ -241,7 +241,10 @@ constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups ove
 // observations over every CU (config 3: 22k observations = 344 workgroups,
 // 13.6 -> 11.0 us), 256 threads for large ones (config 4: 100k observations,
 // 34.4 us vs 38.6 with one-wave workgroups)
-constexpr int kLinSmall = 64, kLinSmallMaxObs = 64 * 512;
+#ifndef ME_LIN_SMALL
+#define ME_LIN_SMALL 64  // linearize workgroup for small windows (A/B builds)
+#endif
+constexpr int kLinSmall = ME_LIN_SMALL, kLinSmallMaxObs = 64 * 512;
 __host__ __device__ inline int lin_block(int no) { return no <= kLinSmallMaxObs ? kLinSmall : kBlock; }
 template <int OD, int BLK>
 __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
