@@ -493,3 +493,28 @@ def test_ba_async_two_queued_windows(ctx):
             d.reset()
     for d in ds:
         d.close()
+
+
+def test_mi_lane_kernel_still_bit_exact():
+    """The one-lane-per-pair batch kernel (ME_MI_KERNEL=lane, the A/B
+    alternative of mi_quad_kernel; the switch is read once per process, so a
+    child process runs it) still matches the oracle bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = (
+        "import sys, numpy as np; sys.path[:0] = [%r, %r]\n"
+        "import oracle as O\n"
+        "from uasl_motion_estimation_amd import synthetic as S\n"
+        "from uasl_motion_estimation_amd.mutual_information import mi_scores\n"
+        "for pw, ph in ((11, 11), (10, 10), (7, 9)):\n"
+        "    L, R, xyL, xyR = S.random_patches(300 + pw, 161, 97, 40000, pw, ph)\n"
+        "    got = mi_scores(L, R, xyL, xyR, (pw, ph))\n"
+        "    ref = O.mi_scores(L, R, xyL, xyR, pw, ph)\n"
+        "    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (pw, ph)\n"
+        "print('lane ok')\n" % (root, os.path.join(root, "tests")))
+    env = dict(os.environ, ME_MI_KERNEL="lane")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "lane ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
