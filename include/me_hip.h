@@ -372,6 +372,20 @@ int me_ba_solve_comm(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_c
    gradient max-norm then travels in a separate max all-reduce. */
 int me_ba_solve_sharded(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn allreduce,
                         void* user, me_ba_summary* s);
+/* Landmark-count gate of the sharded solve (shard "only when the
+   landmark count warrants it").  Every rank solves the camera system
+   redundantly, so sharding saves only landmark-kernel time (linearisation,
+   Schur pass, point step) and costs two all-reduces per LM iteration.  Model
+   per LM iteration: t(n) = max(ME_SHARD_FLOOR_US, n * ME_SHARD_OBS_NS / 1000)
+   microseconds for n observations (fitted to the one-GPU shard timings of
+   bench.py's sharded_ba.crossover_model); returns 1 when
+   t(n_obs) - t(ceil(n_obs / world)) > 2 * xch_us, else 0 (world <= 1: 0).
+   xch_us <= 0 takes the built-in per-exchange estimate for `world`
+   (me_ba_shard_exchange_us).  Host only: no device, no ctx. */
+#define ME_SHARD_OBS_NS 1.0
+#define ME_SHARD_FLOOR_US 40.0
+int me_ba_shard_worthwhile(long n_obs, int world, double xch_us);
+double me_ba_shard_exchange_us(int world);
 
 /* ---- A12: KLT feature tracking (build-defined; no reference) ---------- */
 typedef struct { int win; int max_level; int max_iters; double eps; double min_eig; } me_klt_params;

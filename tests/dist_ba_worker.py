@@ -25,9 +25,15 @@ def main():
     ctx = Context(0)
     c = S.CONFIGS[2]
     bp = S.ba_problem(S.SEED0 + 2, c["n_feats"], c["window"], c["width"], c["height"])
-    cams, pts, (lo, hi), s = ba_solve_distributed(bp, SolverOptions.fixed_iterations(iters), ctx=ctx)
+    opts = SolverOptions.fixed_iterations(iters)
+    cams, pts, (lo, hi), s = ba_solve_distributed(bp, opts, ctx=ctx, shard=True)
+    # the landmark-count gate: config 2 (~5k observations) is below the
+    # crossover, so "auto" solves the whole window on every rank, no exchange
+    gcams, gpts, grng, gs = ba_solve_distributed(bp, opts, ctx=ctx)
     np.savez(os.path.join(out, f"rank{rank}.npz"), cams=cams, pts=pts, lo=lo, hi=hi, iterations=s["iterations"],
-             successful=s["successful_steps"], backend=dist.get_backend(), world=dist.get_world_size())
+             successful=s["successful_steps"], backend=dist.get_backend(), world=dist.get_world_size(),
+             sharded=s["sharded"], gate_sharded=gs["sharded"], gate_cams=gcams, gate_pts=gpts,
+             gate_rng=np.array(grng), gate_iterations=gs["iterations"])
     dist.barrier()
     dist.destroy_process_group()
     ctx.close()

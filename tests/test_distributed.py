@@ -38,6 +38,36 @@ def test_shard_partition_covers_every_landmark_once(world):
     assert max(sizes) - min(sizes) <= 2 * S.CONFIGS[2]["window"]  # balanced to within a track or two
 
 
+def test_shard_gate_model():
+    """The landmark-count gate (me_ba_shard_worthwhile, host only): the
+    windows the bench's crossover model measured -- config 3 (19k
+    observations) never shards, config 4 (100k) and the W = 50 VO window
+    (134k) shard at 2 ranks; one rank never; a slow exchange closes it."""
+    from uasl_motion_estimation_amd._lib import load_library
+    from uasl_motion_estimation_amd.optimisation import shard_worthwhile
+
+    lib = load_library()
+    assert lib.me_ba_shard_exchange_us(1) == 0.0
+    us = [lib.me_ba_shard_exchange_us(w) for w in (2, 4, 8)]
+    assert 0 < us[0] < us[1] < us[2]
+    for w in (1, 2, 4, 8):
+        assert not shard_worthwhile(19012, w)  # config 3
+        assert not shard_worthwhile(0, w)
+    assert not shard_worthwhile(100010, 1)
+    assert shard_worthwhile(100010, 2) and shard_worthwhile(134053, 2)
+    assert not shard_worthwhile(100010, 2, xch_us=1000.0)
+    # monotone in the observation count at fixed world size and exchange cost
+    dec = [shard_worthwhile(n, 4, 25.0) for n in range(0, 400000, 5000)]
+    assert dec == sorted(dec) and dec[-1] and not dec[0]
+    # the model itself: t(n) - t(n / world) > 2 xch_us, t(n) = max(floor, n * ns / 1000)
+    def model(n, w, x):
+        t = lambda m: max(40.0, m * 1.0e-3)  # ME_SHARD_FLOOR_US, ME_SHARD_OBS_NS
+        return t(n) - t(-(-n // w)) > 2 * x
+    for n in (30000, 60000, 90000, 150000, 1000000):
+        for w in (2, 4, 8):
+            assert shard_worthwhile(n, w, 20.0) == model(n, w, 20.0)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -161,6 +191,11 @@ def test_ba_solve_distributed_world2_on_device0(tmp_path, oracle):
         assert int(d["iterations"]) == rs["iterations"] and int(d["successful"]) == rs["successful_steps"]
         np.testing.assert_allclose(d["cams"], rc, rtol=1e-6, atol=1e-9)
         pts[int(d["lo"]):int(d["hi"])] = d["pts"]
+        # gate: below the crossover every rank solved the whole window itself
+        assert bool(d["sharded"]) and not bool(d["gate_sharded"])
+        assert list(d["gate_rng"]) == [int(d["lo"]), int(d["hi"])] and int(d["gate_iterations"]) == rs["iterations"]
+        np.testing.assert_allclose(d["gate_cams"], rc, rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(d["gate_pts"], rp[int(d["lo"]):int(d["hi"])], rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(pts, rp, rtol=1e-6, atol=1e-9)
 
 
@@ -309,3 +344,90 @@ def test_gpu_sharded_infeasible_shard_fails_every_rank(ctx):
     cams, pts, summ = _two_ctx_comm_solve(bp, SolverOptions.fixed_iterations(4))
     for s in summ:
         assert s["status"] == 3 and s["iterations"] == 0
+
+
+_C4 = {}
+
+
+def _config4_refs(ctx, oracle):
+    """Config 4 window, its unsharded device solve and the oracle's (10 fixed
+    LM iterations), computed once for the N-rank tests."""
+    if not _C4:
+        from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+        c = S.CONFIGS[4]
+        bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
+        opts = SolverOptions.fixed_iterations(10)
+        _C4["bp"], _C4["opts"] = bp, opts
+        _C4["dev"] = ba_solve(bp.copy(), opts, ctx=ctx)
+        _C4["oracle"] = oracle.ba_solve(bp, max_num_iterations=10, function_tolerance=0.0, gradient_tolerance=0.0,
+                                        parameter_tolerance=0.0)
+    return _C4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [4, 8])
+def test_gpu_comm_sharded_config4_n_ranks(ctx, oracle, world):
+    """Config 4 (8000 x 30, 10 LM iterations) landmark-sharded over 4 and 8
+    contexts of one GPU (me_comm_create_callback, thread exchange): the
+    packed exchange's per-rank gradient slots and the partition edges at 4
+    and 8 ranks give the unsharded solve's iterations and successful steps,
+    cameras and points within 1e-6 of it and of the oracle."""
+    r = _config4_refs(ctx, oracle)
+    ref_c, ref_p, ref_s = r["dev"]
+    oc, op, os_ = r["oracle"]
+    cams, pts, summ = _two_ctx_comm_solve(r["bp"], r["opts"], world=world)
+    assert not np.isnan(pts).any()  # every landmark is in exactly one shard
+    for cm, s in zip(cams, summ):
+        assert np.array_equal(cm, cams[0])  # the redundant camera solve is identical on every rank
+        for rc, rs in ((ref_c, ref_s), (oc, os_)):
+            np.testing.assert_allclose(cm, rc, rtol=1e-6, atol=1e-9)
+            assert (s["iterations"], s["successful_steps"]) == (rs["iterations"], rs["successful_steps"])
+    np.testing.assert_allclose(pts, ref_p, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(pts, op, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_handoff_timeout_on_one_rank_fails_every_rank(ctx):
+    """a camera-solve hand-off that times out on ONE rank of a
+    sharded solve (forced through the test hook me_debug_solve_flags(512):
+    the fused-assembly wait gives up at once) must not leave the other rank
+    waiting in a collective: both ranks return ME_ERR_STATE, neither hangs."""
+    import ctypes
+
+    from uasl_motion_estimation_amd._lib import Context, MEError
+    from uasl_motion_estimation_amd.optimisation import Comm, SolverOptions, ThreadAllReduce, ba_solve_comm
+
+    bp = _problem()
+    world = 2
+    ar = ThreadAllReduce(world)
+    ctxs = [Context(0) for _ in range(world)]
+    hook = ctxs[1].lib.me_debug_solve_flags
+    hook.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert hook(ctxs[1].h, 512) == 0
+    out = [None] * world
+
+    def run(r):
+        local, _ = shard_landmarks(bp, r, world)
+        comm = Comm.callback(ctxs[r], world, r, ar.callback(r, ctxs[r]))
+        try:
+            ba_solve_comm(local, comm, SolverOptions.fixed_iterations(6), ctx=ctxs[r])
+            out[r] = "ok"
+        except MEError as e:
+            out[r] = e.code
+        finally:
+            comm.close()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    alive = [t.is_alive() for t in th]
+    hook(ctxs[1].h, 0)
+    if not any(alive):
+        for c in ctxs:
+            c.close()
+    assert not any(alive), "a rank is stuck in the exchange"
+    ME_ERR_STATE = -5
+    assert out == [ME_ERR_STATE, ME_ERR_STATE], out

@@ -125,7 +125,7 @@ EXPORTS = [
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
     "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_window_indices",
     "me_comm_unique_id", "me_comm_create_rccl", "me_comm_create_callback", "me_comm_destroy", "me_comm_info",
-    "me_comm_allreduce", "me_ba_solve_comm",
+    "me_comm_allreduce", "me_ba_solve_comm", "me_ba_shard_worthwhile", "me_ba_shard_exchange_us",
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
@@ -225,6 +225,8 @@ def load_library(path: str = LIB_PATH):
         "me_comm_info": (c_int, [c_void_p, P(c_int), P(c_int), P(c_int)]),
         "me_comm_allreduce": (c_int, [c_void_p, c_void_p, c_long, c_int]),
         "me_ba_solve_comm": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), c_void_p, P(BASummaryC)]),
+        "me_ba_shard_worthwhile": (c_int, [c_long, c_int, c_double]),
+        "me_ba_shard_exchange_us": (c_double, [c_int]),
         "me_klt_default_params": (None, [P(KLTParamsC)]),
         "me_klt_track": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_int, P(KLTParamsC)]),

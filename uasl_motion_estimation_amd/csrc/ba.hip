@@ -6,6 +6,7 @@
 // a caller-provided all-reduce.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -1126,6 +1127,55 @@ constexpr int kLoadBatch = 32;
     if ((skip & 256) && tid == 0) st->stamps[(i)] -= (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
+#ifdef ME_SOLVE_TS  // timing experiment only (tools/solve_ts.py): wall-clock phases of cam_solve, 100 MHz ticks
+// [1] lin_finalize, [2] assembly wait, [3] load, [4] factorisation, [5] backward
+// solve, [6] candidate / cost tail, [8] last assembler exit - wg 0 entry,
+// [9] first assembler entry - wg 0 entry, [10] s_memtime ticks of [1..6], [15] calls
+__device__ long long g_solve_ts[16];
+__device__ unsigned long long g_asm_first = ~0ull, g_asm_last = 0ull;
+#define STS_DECL long long sts_prev_ = 0, sts_t0_ = 0, sts_c0_ = 0
+#define STS_BEGIN()                                                        \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      sts_t0_ = sts_prev_ = (long long)__builtin_amdgcn_s_memrealtime();   \
+      sts_c0_ = (long long)__builtin_amdgcn_s_memtime();                   \
+    }                                                                      \
+  } while (0)
+#define STS(k)                                                             \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      const long long t_ = (long long)__builtin_amdgcn_s_memrealtime();    \
+      atomicAdd((unsigned long long*)&g_solve_ts[(k)], (unsigned long long)(t_ - sts_prev_)); \
+      sts_prev_ = t_;                                                      \
+    }                                                                      \
+  } while (0)
+#define STS_END()                                                          \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      atomicAdd((unsigned long long*)&g_solve_ts[10],                      \
+                (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - sts_c0_)); \
+      atomicAdd((unsigned long long*)&g_solve_ts[15], 1ull);               \
+    }                                                                      \
+  } while (0)
+#define STS_ASM()                                                          \
+  do {                                                                     \
+    if (threadIdx.x == 0) {                                                \
+      const unsigned long long a_ = atomicExch(&g_asm_last, 0ull);         \
+      const unsigned long long f_ = atomicExch(&g_asm_first, ~0ull);       \
+      if (a_) {                                                            \
+        atomicAdd((unsigned long long*)&g_solve_ts[8], (unsigned long long)((long long)a_ - sts_t0_)); \
+        atomicAdd((unsigned long long*)&g_solve_ts[9], (unsigned long long)((long long)f_ - sts_t0_)); \
+      }                                                                    \
+    }                                                                      \
+  } while (0)
+#else
+#define STS_DECL
+#define STS_BEGIN() do {} while (0)
+#define STS(k) do {} while (0)
+#define STS_END() do {} while (0)
+#define STS_ASM() do {} while (0)
+#endif
+
 __host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
 // dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
 #ifndef ME_CHOL_PB
@@ -1415,6 +1465,23 @@ __device__ __forceinline__ double4_t trailing_diag_acc(const double* A, int ld, 
   return acc;
 }
 
+// A bounded cross-workgroup wait of the camera solve timed out (a partner
+// not co-resident): me_ba_* returns ME_ERR_STATE.  One GPU: the solve ends
+// here.  Sharded: the rank must keep issuing the same collectives
+// as its peers, so it only fails its steps -- st->fail reaches every rank
+// through the step exchange (R_COUNT), the camera solve keeps failing while
+// spin_err is set, and every rank ends alike after max_invalid rejected steps
+// (decide, on exchanged values).
+__device__ __forceinline__ void spin_timeout(const Bufs& b) {
+  State* st = b.st;
+  st->spin_err = 1;
+  st->fail = 1;
+  if (!b.xch) {
+    st->done = 1;
+    st->termination = 2;
+  }
+}
+
 // Workers of the multi-workgroup solve.  Tile (I, K), 1 <= K <= I < Ts, is
 // owned by one wave of one worker for the whole solve (linear index
 // (I-1) I / 2 + K - 1, dealt round-robin over the workers' waves), so its
@@ -1496,21 +1563,30 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   }
   unsigned* asm_cnt = b.cnt + g.m + 3;
   if (kMode != 2 && nasm > 0 && blockIdx.x > 0) {
+#ifdef ME_SOLVE_TS
+    if (threadIdx.x == 0) atomicMin(&g_asm_first, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     // (sharded: the assemblers unpack the all-reduced exchange instead of summing partials)
     s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM);
     drain_and_barrier();  // every wave's written-through stores have left
+#ifdef ME_SOLVE_TS
+    if (threadIdx.x == 0) atomicMax(&g_asm_last, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
     if (threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   State* st = b.st;
   const bool fused = kMode != 2 && nasm > 0;
+  STS_DECL;
+  STS_BEGIN();
   if (fused) {
     lin_finalize_body(g, b, o, gc_raw, red);
+    STS(1);
     if (threadIdx.x == 0) {
       const int live = !st->done;
       // (what s_assemble's first block writes in the unfused form; read by decide)
       b.scal[R_COUNT] = (st->fail || (b.xch && b.xch[xo_fail(g)] != 0.0)) ? 1.0 : 0.0;
-      long k = 0;
+      long k = (skip & 512) ? kSolveSpin : 0;  // (512: test hook, a forced timeout on this ctx)
       if (live) {
         for (; k < kSolveSpin; ++k) {
           if (__hip_atomic_load(asm_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nasm) break;
@@ -1519,9 +1595,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         if (k == kSolveSpin) {
           // a missing assembler: the solve ends in error (a late one may still
           // arrive, so the counter is not re-armed: the next plan clears it)
-          st->spin_err = 1;
-          st->done = 1;
-          st->termination = 2;
+          spin_timeout(b);
         } else {
           __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
         }
@@ -1529,6 +1603,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
     __syncthreads();
+    STS(2);
+    STS_ASM();
   }
   const int n = g.n6, Ts = g.Ts, N = 16 * Ts;
   const int ld = solve_ld(Ts);
@@ -1541,7 +1617,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
-  const int fail_in = st->fail || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0);
+  const int fail_in = st->fail || st->spin_err || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0);
   const double radius = st->radius;
   // the candidate-camera inputs (current cameras, Jacobi scales) are requested
   // now; they are consumed after the factorisation, which hides their latency
@@ -1592,6 +1668,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   if ((skip & 256) && tid == 0) st->stamps[15] += 1;
   SOLVE_START(0);
   __syncthreads();
+  STS(3);
   if (sfail) {
     if (tid == 0) st->fail = 1;
     return;
@@ -1794,13 +1871,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     }
     SOLVE_STAMP(3);
   }
+  STS(4);
   if (sfail) {
     if (tid == 0) {
       st->fail = 1;
-      if (st->spin_err) {  // a hand-off timed out: not a numerical failure, the solve ends (me_ba_* returns an error)
-        st->done = 1;
-        st->termination = 2;
-      }
+      if (st->spin_err) spin_timeout(b);  // not a numerical failure: me_ba_* returns an error
       if (kMode == 2 && nworkers > 0) __hip_atomic_store(b.ssync, kSolveTerm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
@@ -1841,6 +1916,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     __syncthreads();
   }
   SOLVE_STAMP(5);
+  STS(5);
   for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
   // candidate cameras
   const double* x = b.cams[cur];
@@ -1877,6 +1953,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     st->cam_xn2 = out[1];
     st->cam_model = out[2];
   }
+  STS(6);
+  STS_END();
 }
 
 // Point back-substitution and step evaluation, 16 lanes per point (one
@@ -1890,9 +1968,21 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 // Step partials -> scal (fixed order).  In single-GPU mode the same workgroup
 // then runs the Ceres step handling (decide); in sharded mode the host
 // all-reduces scal between step_partials and a decide-only launch.
+// R_COUNT of a step whose camera solve hit a hand-off timeout: summed over
+// the ranks it stays >= kSpinFlag, so every rank of a sharded solve ends at
+// the same iteration with spin_err (ME_ERR_STATE) -- no rank is left waiting
+// in a collective the others no longer issue.
+constexpr double kSpinFlag = 65536.0;
+
 __device__ void decide(Bufs& b, const Opts& o) {
   State* st = b.st;
   st->accepted = 0;
+  if (b.scal[R_COUNT] >= kSpinFlag) {
+    st->spin_err = 1;
+    st->done = 1;
+    st->termination = 2;
+    return;
+  }
   const double model_change = b.scal[R_MODEL];
   const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
   st->fail = 0;  // consumed: the next iteration starts clean
@@ -1958,7 +2048,7 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
     b.scal[R_CAND] = out[1];
     b.scal[R_STEP2] = out[2];
     b.scal[R_XN2] = out[3];
-    b.scal[R_COUNT] = st->fail ? 1.0 : 0.0;
+    b.scal[R_COUNT] = st->fail ? (st->spin_err ? kSpinFlag : 1.0) : 0.0;
     if (do_decide) decide(b, o);
   }
 }
@@ -2615,6 +2705,7 @@ struct Plan {
   bool full_S = false;      // assemble both block triangles of S (reduced-system / covariance read-back)
   int solve_workers = -1;   // global-memory camera solve: trailing-update workgroups (-1: by size; ME_SOLVE_WORKERS)
   int solve_cap = 0;        // co-resident cam_solve_kernel<2> workgroups on the ctx's CUs (0: not queried)
+  int warned_workers = 0;   // an explicit worker count was clamped (reported once per plan)
   me_comm* comm = nullptr;  // sharded solve: the exchange (null: one GPU)
   bool xmax_separate = false;  // ABI-v2 callback (no rank): the gradient max-norm travels in its own max all-reduce
 };
@@ -2647,6 +2738,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   P.c = c;
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
+  P.diag_skip |= c->dbg_solve_flags;
   if (const char* sw = getenv("ME_SOLVE_WORKERS")) P.solve_workers = atoi(sw);  // A/B timing (0: one workgroup)
   if (const char* sq = getenv("ME_BA_SEQUENTIAL")) P.sequential = atoi(sq) != 0;
   if (const char* fa = getenv("ME_BA_NOFUSEASM")) P.no_fused_asm = atoi(fa) != 0;
@@ -2890,10 +2982,26 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   // the multi-workgroup camera solve needs block 0 and every worker resident
   // at once: the workers it may use are capped by the co-resident count on
   // the ctx's CUs; a hand-off that still times out is an error
-  if (!P.use_lds && g.Ts >= kSolveMwMinTs) {
+  // (queried for every global-memory solve: an explicit worker count is
+  // clamped by it too)
+  if (!P.use_lds) {
     int per_cu = 0;
     ME_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cam_solve_kernel<2>, kSolveBlock, P.solve_lds));
     P.solve_cap = std::max(0, per_cu) * (c->cu_active > 0 ? c->cu_active : c->num_cu);
+    if (P.comm && (g.Ts >= kSolveMwMinTs || P.solve_workers > 0)) {
+      // Sharded: every rank solves the camera system redundantly and must run
+      // the same solve form (worker count) on the same operands, whatever its
+      // own CU mask: the smallest capacity over the ranks (one max exchange of
+      // -cap at plan time; the result is read back before any iteration).
+      double* d = P.b.scal;  // (free until the first linearisation)
+      const double v = -(double)P.solve_cap;
+      ME_HIP(c, hipMemcpyAsync(d, &v, 8, hipMemcpyHostToDevice, c->stream));
+      ME_TRY(me_comm_allreduce_impl(P.comm, d, 1, ME_COMM_MAX));
+      double r = 0.0;
+      ME_HIP(c, hipMemcpyAsync(&r, d, 8, hipMemcpyDeviceToHost, c->stream));
+      ME_HIP(c, hipStreamSynchronize(c->stream));
+      P.solve_cap = (int)-r;
+    }
   }
   return ME_OK;
 }
@@ -3022,7 +3130,14 @@ int enqueue_iteration(Plan& P, bool last = false) {
             : P.solve_workers >= 0 ? P.solve_workers
             : g.Ts >= kSolveMwMinTs ? std::min(64, std::max(1, (np0 + kSolveBlock / 64 - 1) / (kSolveBlock / 64)))
                                     : 0;
-  if (nwk > 0) nwk = std::max(0, std::min(nwk, P.solve_cap - 1));
+  if (nwk > 0) {
+    const int cap = std::max(0, std::min(nwk, P.solve_cap - 1));
+    if (P.solve_workers > 0 && cap != nwk && !P.warned_workers) {  // an explicit count the CUs cannot host
+      std::fprintf(stderr, "me_ba: ME_SOLVE_WORKERS=%d exceeds the co-resident capacity, using %d\n", nwk, cap);
+      P.warned_workers = 1;
+    }
+    nwk = cap;
+  }
   // S = U - sum of the Schur partials is assembled by wide workgroups
   // (coalesced, all CUs) rather than by the one-workgroup solve, whose
   // dependent cross-XCD loads would otherwise dominate the iteration.  Modes
@@ -3294,6 +3409,18 @@ extern "C" int me_round_stamps(unsigned long long* out, int reset) {
 }
 #endif
 
+#ifdef ME_SOLVE_TS
+extern "C" int me_solve_ts(long long* out, int reset) {
+  hipDeviceSynchronize();
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_ts), sizeof(g_solve_ts));
+  if (reset) {
+    long long z[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_solve_ts), z, sizeof(z));
+  }
+  return 0;
+}
+#endif
+
 extern "C" int me_ba_solve_comm(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_comm* comm,
                                 me_ba_summary* s) {
   if (!c) return ME_ERR_INVALID;
@@ -3304,6 +3431,25 @@ extern "C" int me_ba_solve_comm(me_ctx* c, me_ba_problem* p, const me_ba_options
 
 // ABI-v2 form: a callback without rank information (world 0: one gradient
 // max-norm slot, reduced by its own max all-reduce)
+// Per-exchange estimate (µs) of the packed all-reduce at `world` ranks: the
+// one-rank RCCL exchange measured on MI355X (~14 µs each, bench
+// sharded_ba.rccl_1rank, r03) is the floor; every doubling of the ring adds a
+// latency step over xGMI (an estimate until the driver's 8-GPU line measures it).
+extern "C" double me_ba_shard_exchange_us(int world) {
+  if (world <= 1) return 0.0;
+  double us = 14.0;
+  for (int w = 2; w <= world; w *= 2) us += 4.0;
+  return us;
+}
+
+extern "C" int me_ba_shard_worthwhile(long n_obs, int world, double xch_us) {
+  if (world <= 1 || n_obs <= 0) return 0;
+  if (!(xch_us > 0.0)) xch_us = me_ba_shard_exchange_us(world);
+  auto t = [](double n) { return std::max(ME_SHARD_FLOOR_US, n * ME_SHARD_OBS_NS * 1e-3); };
+  const double saved = t((double)n_obs) - t(std::ceil((double)n_obs / world));
+  return saved > 2.0 * xch_us ? 1 : 0;
+}
+
 extern "C" int me_ba_solve_sharded(me_ctx* c, me_ba_problem* p, const me_ba_options* o, me_allreduce_fn ar,
                                    void* user, me_ba_summary* s) {
   if (!c) return ME_ERR_INVALID;
@@ -3463,6 +3609,15 @@ extern "C" int me_ba_window_indices(me_ctx* c, const int32_t* frame, const int32
   hipLaunchKernelGGL(window_indices_kernel, dim3(blocks(n_obs, kBlock)), dim3(kBlock), 0, c->stream, frame, ids, n_obs,
                      first_frame, win_ids, n_pts, cam_idx, pt_idx);
   return me_check_launch(c, "window_indices_kernel");
+}
+
+// Test hook (not part of the drop-in ABI): flags OR-ed into this ctx's camera
+// solve diagnostics; 512 forces the fused-assembly wait to time out
+// (tests/test_distributed.py: a hand-off timeout on one rank of a sharded solve).
+extern "C" int me_debug_solve_flags(me_ctx* c, int flags) {
+  if (!c) return ME_ERR_INVALID;
+  c->dbg_solve_flags = flags;
+  return ME_OK;
 }
 
 extern "C" int me_debug_read(me_ctx* c, long long* out, int n) {

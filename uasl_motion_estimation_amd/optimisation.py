@@ -724,8 +724,19 @@ def rccl_comm(ctx: Context, group=None, key: str = "me_rccl_uid") -> "Comm":
     return Comm.rccl(ctx, world, rank, uid)
 
 
+def shard_worthwhile(n_obs: int, world: int, xch_us: float = 0.0) -> bool:
+    """The landmark-count gate of the sharded solve (me_ba_shard_worthwhile,
+    include/me_hip.h): True when splitting n_obs observations over `world`
+    ranks is predicted to save more landmark-kernel time per LM iteration
+    than its two all-reduces cost (xch_us per exchange; <= 0: the built-in
+    estimate).  Host only."""
+    from ._lib import load_library
+
+    return bool(load_library().me_ba_shard_worthwhile(int(n_obs), int(world), float(xch_us)))
+
+
 def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context | None = None, group=None,
-                         allreduce=None, comm: "Comm | None" = None):
+                         allreduce=None, comm: "Comm | None" = None, shard="auto", xch_us: float = 0.0):
     """Landmark-sharded BA over torch.distributed: each rank holds
     the cameras and a contiguous, observation-balanced landmark range; the
     packed reduced camera system (S, b, gradient, LM scalars) is summed across
@@ -734,13 +745,26 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     its own landmarks.  The exchange is the library's native RCCL communicator
     for the nccl backend (``comm``, or one created here), host-staged through
     the group for gloo, or the given ``allreduce(dev_ptr, n)`` callback.
-    Returns (cams, local pts, (lo, hi), summary)."""
+
+    ``shard``: "auto" applies the landmark-count gate (shard_worthwhile on
+    the window's observation count, the same decision on every rank); below
+    it -- or with shard=False -- every rank solves the whole window on its own
+    GPU (replicated, no collective; the same deterministic solve on every
+    rank) and returns its landmark range of the result.  True always shards.
+    Returns (cams, local pts, (lo, hi), summary); summary["sharded"] says
+    which ran."""
     import torch
     import torch.distributed as dist
 
     ctx = ctx or default_context()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     local, rng = shard_landmarks(bp, rank, world)
+    if shard == "auto":
+        shard = shard_worthwhile(len(bp.obs), world, xch_us)
+    if not shard:
+        cams, pts, summ = ba_solve(bp.copy(), options, ctx)
+        summ = dict(summ, sharded=False)
+        return cams, pts[rng[0]:rng[1]], rng, summ
     own = False
     if comm is None:
         if allreduce is None and dist.get_backend(group) != "gloo":
@@ -765,7 +789,7 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     finally:
         if own:
             comm.close()
-    return cams, pts, rng, summ
+    return cams, pts, rng, dict(summ, sharded=True)
 
 
 def ba_cost(bp, ctx: Context | None = None) -> float:
