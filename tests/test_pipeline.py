@@ -155,6 +155,12 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
         n = 600
         uv = np.stack([rng.uniform(PL.MARGIN, 1280 - PL.MARGIN, n), rng.uniform(PL.MARGIN, 720 - PL.MARGIN, n)],
                       -1).astype(np.float32)
+        # features whose patch leaves the image: scored -inf on both sides, never read
+        e = 48
+        uv[:e // 4, 0] = rng.uniform(0, 6, e // 4)
+        uv[e // 4:e // 2, 0] = rng.uniform(1274, 1280, e // 4)
+        uv[e // 2:3 * e // 4, 1] = rng.uniform(0, 6, e // 4)
+        uv[3 * e // 4:e, 1] = rng.uniform(714, 720, e // 4)
         if unique:
             lo, nd, dvalid = np.full(n, 2, np.int64), 127, None
             got = be.match(imgs, uv, lo, nd, True)
@@ -182,3 +188,4 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
     assert np.array_equal(got[1], ref[1])
     assert np.array_equal(got[0][ref[1]].view(np.uint32), ref[0][ref[1]].view(np.uint32))
     assert ref[1].sum() > n // 4  # the comparison covers many accepted matches
+    assert not ref[1][:e].any()  # the border features match nothing

@@ -197,7 +197,9 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
         fv = fv && em.status[f] == 1 && u >= em.margin && u < (float)em.width - em.margin && v >= em.margin &&
              v < (float)em.height - em.margin;
       const int d = em.lo[f] + c, xr = x0 - d;
-      live = fv && xr >= 0 && d <= em.d_max;
+      // (inside the image: the left patch, and the right one (x >= 0) -- ADVICE r3)
+      live = fv && xr >= 0 && d <= em.d_max && x0 >= 0 && y0 >= 0 && x0 + 2 * em.half + 1 <= em.width &&
+             y0 + 2 * em.half + 1 <= em.height;
       oL = (long)y0 * strideL + x0;
       oR = (long)y0 * strideR + xr;
     } else if (!EPI && live) {
@@ -484,7 +486,9 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         fv = fv && em.status[f] == 1 && u >= em.margin && u < (float)em.width - em.margin && v >= em.margin &&
              v < (float)em.height - em.margin;
       const int d = em.lo[f] + c, xr = x0 - d;
-      live = fv && xr >= 0 && d <= em.d_max;
+      // (inside the image: the left patch, and the right one (x >= 0) -- ADVICE r3)
+      live = fv && xr >= 0 && d <= em.d_max && x0 >= 0 && y0 >= 0 && x0 + 2 * em.half + 1 <= em.width &&
+             y0 + 2 * em.half + 1 <= em.height;
       oL = (long)y0 * strideL + x0;
       oR = (long)y0 * strideR + xr;
     } else if (!EPI && live) {
@@ -772,7 +776,8 @@ __global__ __launch_bounds__(kEpiBlock) void mi_epi_score_kernel(
       fv = fv && status[f] == 1 && u >= margin && u < (float)width - margin && v >= margin &&
            v < (float)height - margin;
     const int d = lo[f] + c, xr = x0 - d;
-    const bool ok = fv && xr >= 0 && d <= d_max;  // (group-uniform)
+    const bool ok = fv && xr >= 0 && d <= d_max && x0 >= 0 && y0 >= 0 && x0 + patch <= width &&
+                    y0 + patch <= height;  // (group-uniform; both patches inside the image)
     float s = 0.0f;
     if (ok) s = group_mi<false>(h, L + (long)y0 * stride + x0, stride, R + (long)y0 * stride + xr, stride, patch, patch,
                                 invN);

@@ -113,12 +113,16 @@ def match_host(be, imgs, uv, lo, nd, dvalid, unique: bool, d_max: int, ratio: fl
     y0 = np.floor(uv[:, 1].astype(np.float64) - W_SCALE).astype(np.int64)
     d = lo[:, None] + np.arange(nd, dtype=np.int64)[None, :]
     xr = x0[:, None] - d
-    valid = (xr >= 0) & (d <= d_max)
+    P = 2 * W_SCALE + 1  # both patches inside the image (the right one: xr >= 0)
+    H, W = imgs[2][:2]
+    inside = (x0 >= 0) & (y0 >= 0) & (x0 + P <= W) & (y0 + P <= H)
+    valid = (xr >= 0) & (d <= d_max) & inside[:, None]
     if dvalid is not None:
         valid &= dvalid[:, None]
     xr_c = np.where(valid, xr, 0)
-    xyL = np.stack([np.repeat(x0, nd), np.repeat(y0, nd)], -1)
-    xyR = np.stack([xr_c.ravel(), np.repeat(y0, nd)], -1)
+    x0c, y0c = np.where(inside, x0, 0), np.where(inside, y0, 0)  # (scored -inf below: any in-image corner)
+    xyL = np.stack([np.repeat(x0c, nd), np.repeat(y0c, nd)], -1)
+    xyR = np.stack([xr_c.ravel(), np.repeat(y0c, nd)], -1)
     sc = be.mi_scores(imgs, xyL, xyR).reshape(n, nd).astype(np.float64)
     sc = np.where(valid, sc, -np.inf)
     with np.errstate(invalid="ignore", divide="ignore"):  # -inf candidates (outside the image)
@@ -322,8 +326,9 @@ class GPUBackend(Backend):
     def _hbuf(self, name, nbytes):
         b = self._pin.get(name)
         if b is None or b[1] < nbytes:
-            if b is not None:
+            if b is not None:  # (both contexts copy from / to staging buffers, as _dbuf)
                 self.tctx.synchronize()
+                self.ctx.synchronize()
                 self._hview.pop(b[0], None)
                 self.tctx.host_free(b[0])
             nb = max(4096, int(nbytes * 1.5))
