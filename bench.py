@@ -337,14 +337,40 @@ def cpu_frame(payload, ba_iters, scale_iters):
     return dict(klt=kp, klt_status=kst, scale=sc, cams=cams, pts=pps, ba=s)
 
 
+def _pin_init(cores):
+    """Pool initializer: pin this worker process to one core of the shared
+    queue (the `taskset -c` of BASELINE.md / SURVEY §8d, done in-process)."""
+    try:
+        core = cores.get(timeout=5)
+        os.sched_setaffinity(0, {core})
+    except Exception:  # pragma: no cover  (affinity not permitted: unpinned, reported as such)
+        pass
+
+
 def _cpu_worker(args):
     """All-cores leg: one process runs its frames back to back (spawned before
-    this bench touched the GPU)."""
+    this bench touched the GPU, pinned to its own core)."""
     payloads, ba_iters, scale_iters = args
     t0 = time.perf_counter()
     for pl in payloads:
         cpu_frame(pl, ba_iters, scale_iters)
     return len(payloads), time.perf_counter() - t0
+
+
+def _cpu_single(args):
+    """1-thread leg in a process pinned to one core: one warm-up frame, then
+    `runs` passes over the distinct frames; per-pass frames/s."""
+    pls, ba_iters, scale_iters, runs = args
+    cpu_frame(pls[0], ba_iters, scale_iters)
+    rates, tot_t, ba_it = [], 0.0, 0
+    for _ in range(max(1, runs)):
+        t1 = time.perf_counter()
+        for pl in pls:
+            ba_it += cpu_frame(pl, ba_iters, scale_iters)["ba"]["iterations"]
+        dt = time.perf_counter() - t1
+        rates.append(len(pls) / dt)
+        tot_t += dt
+    return rates, tot_t, ba_it, sorted(os.sched_getaffinity(0))
 
 
 def host_cpu():
@@ -581,16 +607,22 @@ def _parity_ok(p):
     return bool(p["same_iterations"] and p["cams_max_rel"] <= 1e-6 and p["pts_max_rel"] <= 1e-6)
 
 
-def crossover_model(ctx, opts, reps, ar_us=(25.0, 30.0, 40.0)):
+def crossover_model(ctx, opts, reps, xch_lb_us=None):
     """Where landmark sharding pays, from one GPU: the device time of the
     largest rank's shard (1/G of the landmarks, all cameras, the same fixed
-    LM iterations) plus two all-reduces per iteration at an ASSUMED RCCL
-    latency over xGMI (ar_us for G = 2, 4, 8: small-message all-reduce of the
-    packed S (<= 370 KB)); the measured 1-rank RCCL overhead is in
-    rccl_1rank.  A prediction for the driver's 8-GPU run, not a measurement."""
+    LM iterations) plus two all-reduces per iteration, priced two ways:
+    (a) at the MEASURED per-exchange cost of the 1-rank RCCL communicator on
+    this GPU (xch_lb_us, from rccl_1rank: a lower bound -- a real ring over
+    xGMI adds hops), and (b) at the library gate's per-exchange estimate
+    (me_ba_shard_exchange_us); `gate` is me_ba_shard_worthwhile's decision
+    for the window at G ranks.  A prediction for the driver's 8-GPU run, not
+    a measurement."""
     from uasl_motion_estimation_amd import synthetic as S
-    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, shard_landmarks
+    from uasl_motion_estimation_amd._lib import load_library
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, shard_landmarks, shard_worthwhile
 
+    lib = load_library()
+    est = {G: lib.me_ba_shard_exchange_us(G) for G in (2, 4, 8)}
     rows = []
     for name, (npts, win, w, h, seed) in {"config 3 (2000 x 20)": (2000, 20, 1280, 720, 3),
                                           "config 4 (8000 x 30)": (8000, 30, 3840, 2160, 4),
@@ -613,12 +645,60 @@ def crossover_model(ctx, opts, reps, ar_us=(25.0, 30.0, 40.0)):
                 t1 = el
                 row["ms_1gpu"] = round(1e3 * el, 3)
                 continue
-            pred = el + 2 * s1["iterations"] * ar_us[(2, 4, 8).index(G)] * 1e-6
             row[f"ms_shard_{G}"] = round(1e3 * el, 3)
+            if xch_lb_us is not None:
+                pred = el + 2 * s1["iterations"] * xch_lb_us * 1e-6
+                row[f"predicted_speedup_{G}gpu_measured_1rank_xch"] = round(t1 / pred, 2)
+            pred = el + 2 * s1["iterations"] * est[G] * 1e-6
             row[f"predicted_ms_{G}gpu"] = round(1e3 * pred, 3)
             row[f"predicted_speedup_{G}gpu"] = round(t1 / pred, 2)
+            row[f"gate_{G}gpu"] = shard_worthwhile(len(bp.obs), G)
         rows.append(row)
-    return {"assumed_allreduce_us": dict(zip(("2", "4", "8"), ar_us)), "rows": rows}
+    return {"xch_us_measured_1rank_lower_bound": None if xch_lb_us is None else round(xch_lb_us, 2),
+            "xch_us_gate_estimate": {str(G): v for G, v in est.items()}, "rows": rows}
+
+
+def hbm_copy_gbs(device: int, nbytes: int = 1 << 30, reps: int = 10):
+    """Measured device-to-device copy bandwidth (read + write bytes / time) of
+    a 1 GiB buffer on this GPU: the measured HBM denominator beside the 8 TB/s
+    datasheet peak."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{device}")
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
+def exchange_us(ctx, comm, barrier, sizes, reps=50):
+    """Measured cost (us) of one in-place sum all-reduce of n doubles through
+    the library's communicator on the ctx stream, per size: the packed
+    camera-system exchange (~17k doubles at W = 30) and the step scalars (5)."""
+    out = {}
+    for n in sizes:
+        d = ctx.malloc(8 * n)
+        ctx.h2d(d, np.zeros(n))
+        for _ in range(5):
+            comm.allreduce(d, n)
+        ctx.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            comm.allreduce(d, n)
+        ctx.synchronize()
+        out[str(n)] = round((time.perf_counter() - t0) / reps * 1e6, 2)
+        ctx.free(d)
+    return out
 
 
 def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
@@ -638,7 +718,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     from uasl_motion_estimation_amd import synthetic as S
     from uasl_motion_estimation_amd._lib import Context
     from uasl_motion_estimation_amd.optimisation import (Comm, DeviceBAProblem, SolverOptions, ThreadAllReduce,
-                                                         rccl_comm, shard_landmarks)
+                                                         rccl_comm, shard_landmarks, shard_worthwhile)
 
     c = S.CONFIGS[4]
     bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
@@ -677,6 +757,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
         comm = rccl_comm(ctx)
         el, ss = timed_comm(d, comm)
         cams, pts = d.download()
+        xus = exchange_us(ctx, comm, barrier, [17000, 5])
         comm.close()
         d.close()
         par = _shard_parity(cams, pts, lo, hi, ss, ref_cams, ref_pts, s1)
@@ -689,6 +770,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
         par["ok"] = _parity_ok(par)
         out.update({"mode": f"landmark-sharded over native RCCL (me_comm), {world} ranks, one GPU each",
                     "ranks": world, "sharded_ms": round(1e3 * el, 3),
+                    "gate_would_shard": shard_worthwhile(len(bp.obs), world), "exchange_us": xus,
                     "sharded_ba_iter_per_s": round(ss["iterations"] / el, 1),
                     "speedup_vs_single_gpu": round(t_single / el, 3), "landmarks_rank0": hi - lo if rank == 0 else None,
                     "parity_vs_single_gpu": par})
@@ -700,13 +782,17 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
         el1, ss1 = timed_comm(d, comm)
         cams, pts = d.download()
         d.close()
+        xus1 = exchange_us(ctx, comm, barrier, [17000, 5])
         comm.close()
         par = _shard_parity(cams, pts, 0, len(bp.pts), ss1, ref_cams, ref_pts, s1)
         par = {k: (float("%.3g" % v) if isinstance(v, float) else v) for k, v in par.items()}
         par["ok"] = _parity_ok(par)
+        xch_lb = max(0.0, (el1 - t_single) / max(1, 2 * ss1["iterations"])) * 1e6
         out["rccl_1rank"] = {"ms": round(1e3 * el1, 3), "overhead_vs_single_gpu": round(el1 / t_single - 1.0, 4),
+                             "us_per_exchange_in_solve": round(xch_lb, 2), "exchange_us": xus1,
                              "parity_vs_single_gpu": par}
     except Exception as e:  # reported, never fatal
+        xch_lb = None
         out["rccl_1rank"] = {"error": f"{type(e).__name__}: {e}"}
     # (b) two contexts on this GPU, threads + host exchange (the crossover point)
     ranks = 2
@@ -753,7 +839,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
            "pts_max_rel": float("%.3g" % max(p["pts_max_rel"] for p in pars)),
            "same_iterations": all(p["same_iterations"] for p in pars)}
     par["ok"] = _parity_ok(par)
-    out["crossover_model"] = crossover_model(ctx, opts, reps)
+    out["crossover_model"] = crossover_model(ctx, opts, reps, xch_lb)
     out.update({"mode": "landmark-sharded over 2 contexts of one GPU (threads, host-staged exchange through "
                         "me_comm_create_callback)", "ranks": ranks,
                 "sharded_ms": round(1e3 * el, 3), "sharded_ba_iter_per_s": round(res[0]["iterations"] / el, 1),
@@ -761,7 +847,7 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     return out
 
 
-def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
+def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_prefix: int = 0):
     """The windowed stereo VO loop itself (uasl_motion_estimation_amd/
     pipeline.py) on one synthetic stream of config c: per keyframe KLT, the
     epipolar MI matcher (tracked and new features), the WBA_Point
@@ -774,7 +860,11 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
     calls, wait = time blocked on device results; a second, event-timed pass
     gives the device time per kernel family.  With cpu=True the same loop runs
     sequentially on the oracle backend (1 thread) and its track IDs, feature
-    positions and poses are compared with the GPU's."""
+    positions and poses are compared with the GPU's.  parity_prefix = P > 0
+    (cpu=False): the oracle runs the first P keyframes only and the GPU run's
+    keyframe records (WBA_Point events, per-keyframe results and poses at
+    completion) of those keyframes are compared with it -- keyframe k's
+    decisions depend only on keyframes <= k + 1."""
     from uasl_motion_estimation_amd import pipeline as PL
 
     t0 = time.perf_counter()
@@ -787,10 +877,11 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
         for t in range(n):
             be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
         ctx.synchronize()
-        vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=cpu, overlap=True)
+        vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=cpu or parity_prefix > 0, overlap=True)
         for t in range(warm):
             vo.process(t, fr[t].left, fr[t].right)
-        vo.finish()  # (the warm-up keyframes complete outside the timed span)
+        # (no finish() here: the loop applies BA(t-1) after keyframe t's matching, so the timed span
+        # starts in steady state, with the last warm-up keyframe's BA in flight)
         for cc in (ctx, be.tctx):
             cc.timing_reset()
             cc.timing(timed_families)
@@ -844,6 +935,27 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6):
                                          f"{ct:.1f} s"}
         out["parity"] = {"events_bit_exact": vo.events == ov.events, "track_ids_equal": bool(np.array_equal(vo.ids, ov.ids)),
                          "pose_max_rel_diff": float("%.3g" % pose_rel)}
+    elif parity_prefix > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from pipeline_oracle import OracleBackend  # parity leg only
+        P = min(parity_prefix, n)
+        ov = PL.WindowedStereoVO(cfg, OracleBackend(), K, p0, v, log_events=True)
+        for t in range(P):
+            ov.process(t, fr[t].left, fr[t].right)
+        ov.finish()
+        frames_g = [e for e in vo._ev if e[0] == "frame" and e[2] < P]
+        frames_o = [e for e in ov._ev if e[0] == "frame"]
+        ev_ok = len(frames_g) == len(frames_o) and all(
+            np.array_equal(a[1], b[1]) and a[2] == b[2] and np.array_equal(a[3].view(np.uint32), b[3].view(np.uint32))
+            and np.array_equal(a[4], b[4]) for a, b in zip(frames_g, frames_o))
+        rg, ro = vo.results[:P], ov.results[:P]
+        same = all((a.n_tracked, a.n_new, a.n_window_pts, a.n_window_obs, a.ba_iters, a.scale_stop, a.scale_iters)
+                   == (b.n_tracked, b.n_new, b.n_window_pts, b.n_window_obs, b.ba_iters, b.scale_stop, b.scale_iters)
+                   for a, b in zip(rg, ro)) and len(rg) == len(ro) == P
+        pose_rel = max(float(np.max(np.abs(a.pose - b.pose) / (np.abs(b.pose) + 1e-3))) for a, b in zip(rg, ro))
+        out["parity"] = {"keyframes_checked": P, "events_bit_exact": bool(ev_ok), "results_equal": bool(same),
+                         "pose_max_rel_diff": float("%.3g" % pose_rel),
+                         "ok": bool(ev_ok and same and pose_rel <= 1e-6)}
     return out
 
 
@@ -901,14 +1013,25 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    pool = None
+    pool = pool1 = None
     model, ncpu, avail = host_cpu()
     cpu_workers = args.cpu_workers or min(16, avail)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and cpu_workers > 1:
-        # all-cores CPU leg: worker processes started before anything touches the GPU
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # CPU legs: worker processes started before anything touches the GPU,
+        # each pinned to its own core (1-thread leg: the first allowed core;
+        # all-cores leg: the next cpu_workers cores)
         import multiprocessing as mp
 
-        pool = mp.get_context("spawn").Pool(cpu_workers)
+        mpc = mp.get_context("spawn")
+        cores = sorted(os.sched_getaffinity(0))
+        q1 = mpc.Queue()
+        q1.put(cores[0])
+        pool1 = mpc.Pool(1, initializer=_pin_init, initargs=(q1,))
+        if cpu_workers > 1:
+            qa = mpc.Queue()
+            for k in range(cpu_workers):
+                qa.put(cores[k % len(cores)])
+            pool = mpc.Pool(cpu_workers, initializer=_pin_init, initargs=(qa,))
     import torch
 
     dist = None
@@ -1062,14 +1185,22 @@ def main():
                              "us_per_frame": b["us_per_frame"],
                              "share_of_step": round(b["us_per_frame"] * 1e-3 / (t_max * 1e3 / max(frames_total, 1)
                                                                                   * max(world, 1)), 4)}
+    copy_gbs = hbm_copy_gbs(local_rank)
+    if unit == "GB/s":
+        roofline["peak_measured_copy"] = copy_gbs
+        roofline["frac_vs_measured_copy"] = round(achieved / copy_gbs, 5)
     mi_rl = mi_batch_roofline(ctx, frames, args.mi_pairs) if args.mi_pairs > 0 else None
+    for r_ in (mi_rl, mi_in_frame):
+        if r_ is not None:
+            r_["peak_measured_copy"] = copy_gbs
+            r_["frac_vs_measured_copy"] = round(r_["achieved"] / copy_gbs, 5)
     multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
     pipe_line = pipe_c5 = None
     if args.pipeline_frames > 0 and rank == 0:
         cpu_leg = world == 1 and not args.no_cpu_baseline
         pipe_line = pipeline_line(args, ctx, cpu_leg, args.config, args.pipeline_frames)
         if args.pipeline_c5_frames > 0:
-            pipe_c5 = pipeline_line(args, ctx, False, 5, args.pipeline_c5_frames)
+            pipe_c5 = pipeline_line(args, ctx, False, 5, args.pipeline_c5_frames, parity_prefix=16)
     sharded = None
     if args.sharded_ba:
         try:
@@ -1088,22 +1219,16 @@ def main():
                   "scale_match": all(c["scale_match"] for c in cmp), "ba_match": all(c["ba_match"] for c in cmp),
                   "ba_max_rel_diff": float("%.3g" % max(c["ba_max_rel"] for c in cmp))}
         parity["ok"] = parity["klt_bit_exact"] and parity["scale_match"] and parity["ba_match"]
-        # 1 thread: median of cpu_runs runs over the distinct frames (one warm-up frame first)
+        # 1 thread, pinned to one core: median of cpu_runs runs over the distinct frames (one warm-up frame first)
         pls = [cpu_payload(fd) for fd in frames]
-        cpu_frame(pls[0], args.ba_iters, args.scale_iters)
-        rates, tot_t, tot_f, ba_it = [], 0.0, 0, 0
-        for _ in range(max(1, args.cpu_runs)):
-            t1 = time.perf_counter()
-            for pl in pls:
-                ba_it += cpu_frame(pl, args.ba_iters, args.scale_iters)["ba"]["iterations"]
-            dt = time.perf_counter() - t1
-            rates.append(len(pls) / dt)
-            tot_t += dt
-            tot_f += len(pls)
+        rates, tot_t, ba_it, pinned = pool1.apply(_cpu_single, ((pls, args.ba_iters, args.scale_iters,
+                                                                args.cpu_runs),))
         cpu = {"value": round(float(np.median(rates)), 4), "unit": "frames/s", "cores": 1, "kind": "port",
                "sample": f"median of {len(rates)} runs x {len(pls)} config-{args.config} frames (KLT + MI scale LM "
                          f"(<= {args.scale_iters} it.) + {args.ba_iters}-iteration BA) on the oracle restatement, "
-                         f"1 thread, after 1 warm-up frame; {tot_t:.1f} s",
+                         f"1 thread pinned to core {pinned if len(pinned) > 1 else pinned[0]}, after 1 warm-up "
+                         f"frame; {tot_t:.1f} s",
+               "pinned_cores": pinned,
                "runs_frames_per_s": [round(r, 4) for r in rates],
                "ba_iter_per_s": round(ba_it / tot_t, 3), "cpu_model": model, "nproc": ncpu,
                "cores_available": avail}
@@ -1115,16 +1240,18 @@ def main():
             nf_all = sum(r[0] for r in res)
             cpu["all_cores"] = {"value": round(nf_all / wall, 3), "unit": "frames/s", "cores": cpu_workers,
                                 "sample": f"{cpu_workers} processes x {2 * len(pls)} frames (independent frames, "
-                                          f"one process per core: an upper bound for a multi-threaded CPU path); "
+                                          f"one process pinned per core: an upper bound for a multi-threaded "
+                                          f"CPU path); "
                                           f"{wall:.1f} s"}
             if avail > cpu_workers:
                 # the GPU box grants one GPU's job 16 cores; the frames are independent, so the
                 # host's other cores would add linearly at best: a stated upper bound, not a run
                 cpu["all_cores"]["linear_extrapolation_to_cores_available"] = {
                     "value": round(nf_all / wall * avail / cpu_workers, 3), "cores": avail}
-    if pool is not None:
-        pool.close()
-        pool.join()
+    for pl_ in (pool, pool1):
+        if pl_ is not None:
+            pl_.close()
+            pl_.join()
     if rank == 0:
         out = {
             "metric": "frames/sec + BA iter/sec, 2000 feats x 20-keyframe window, 1/2/4/8 MI355X",
@@ -1164,6 +1291,7 @@ def main():
             "pipeline_config5": pipe_c5,
             "stereo_vo": vo_line,
             "cpu_baseline": cpu,
+            "hbm_copy_GBs_measured": copy_gbs,
             "kernel_ms_profile": {f: [prof[f][0], round(prof[f][1], 3)] for f in prof},
             "kernel_budget_per_frame": budget,
             "mi_in_frame": mi_in_frame,

@@ -117,10 +117,10 @@ def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window, n):
 
     be = PL.GPUBackend(ctx)  # front end on its own context, the loop pipelined
     try:
-        g = _run(5, n, be, window=window, frames=seq5, overlap=True)
+        g = _run(5, n, be, window=window, frames=seq5, overlap=True, ba_iters=10)
     finally:
         be.close()
-    o = _run(5, n, OracleBackend(), window=window, frames=seq5)
+    o = _run(5, n, OracleBackend(), window=window, frames=seq5, ba_iters=10)
     if window == 50:  # the window slid: its oldest keyframe is n - 50, and pops happened
         assert min(g.obs) == n - window and any(ev[0] == "pop" for ev in g.events)
     assert g.events == o.events  # track IDs, frames and feature positions, bit for bit
@@ -157,10 +157,11 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
                       -1).astype(np.float32)
         # features whose patch leaves the image: scored -inf on both sides, never read
         e = 48
-        uv[:e // 4, 0] = rng.uniform(0, 6, e // 4)
-        uv[e // 4:e // 2, 0] = rng.uniform(1274, 1280, e // 4)
-        uv[e // 2:3 * e // 4, 1] = rng.uniform(0, 6, e // 4)
-        uv[3 * e // 4:e, 1] = rng.uniform(714, 720, e // 4)
+        # (patch corner floor(u - 5): x0 < 0 for u < 5, x0 + 11 > 1280 for u >= 1275)
+        uv[:e // 4, 0] = rng.uniform(0, 4.9, e // 4)
+        uv[e // 4:e // 2, 0] = rng.uniform(1275, 1280, e // 4)
+        uv[e // 2:3 * e // 4, 1] = rng.uniform(0, 4.9, e // 4)
+        uv[3 * e // 4:e, 1] = rng.uniform(715, 720, e // 4)
         if unique:
             lo, nd, dvalid = np.full(n, 2, np.int64), 127, None
             got = be.match(imgs, uv, lo, nd, True)

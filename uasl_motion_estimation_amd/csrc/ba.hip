@@ -1003,10 +1003,12 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
     // grp + 8, ... added in order; their loads issued 8 at a time
     // (independent addresses: one memory latency per batch, not per add)
 #ifndef ME_SA_BATCH
-#define ME_SA_BATCH 8
+#define ME_SA_BATCH 16
 #endif
     if (g.sorted) {
-      const int cnt = b.tcnt[idx >> 8];
+      // whole lists (padded with -1 at plan time): no wait for the tile's count
+      // before the list loads -- two rounds of latency (list, partials) per batch
+      const int cnt = g.nruns;
       const int* tl = b.tl + (long)(idx >> 8) * g.nruns;
       const double* src = b.Spart + (idx & 255);
       for (int q0 = grp; q0 < cnt; q0 += ME_SA_BATCH * kSaGroups) {
@@ -1579,6 +1581,17 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const bool fused = kMode != 2 && nasm > 0;
   STS_DECL;
   STS_BEGIN();
+  // the tail's camera part of the model cost change needs row r of U and
+  // g_c[r] (earlier launches): requested now, consumed after the backward
+  // solve, off its latency
+  const bool upre = g.n6 <= (int)blockDim.x;
+  double urow[6] = {0, 0, 0, 0, 0, 0}, gcr = 0.0;
+  if (upre && (int)threadIdx.x < g.n6) {
+    const double* Ur = b.U + 36 * (long)(threadIdx.x / 6) + 6 * (threadIdx.x % 6);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) urow[k] = Ur[k];
+    gcr = b.gcs[threadIdx.x];
+  }
   if (fused) {
     lin_finalize_body(g, b, o, gc_raw, red);
     STS(1);
@@ -1605,6 +1618,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     __syncthreads();
     STS(2);
     STS_ASM();
+    STS(11);
   }
   const int n = g.n6, Ts = g.Ts, N = 16 * Ts;
   const int ld = solve_ld(Ts);
@@ -1629,34 +1643,60 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     x_pre = b.cams[cur][tid];
     if (tid >= 6 * g.nf) cs_pre = b.csc[tid - 6 * g.nf];
   }
-  // the system written through by this launch's assemblers is read through (sc1)
-  auto ld_sys = [&](const double* p) { return fused ? a_ld<true>(p) : *p; };
+  // [S + D; -b^T]: every load of a batch is issued from a computed index
+  // before the first use, so a batch costs one round of global latency.
+  // (Per-element branches with the use inside them made the compiler wait on
+  // every load: the load phase took 15.2 of the 45 us launch at config 3 and
+  // 100 of 265 us at config 5, tools/solve_ts.py.)  S | b | diag(U) are one
+  // allocation (plan), so every element is an index off b.S.  The LM diagonal
+  // (Ceres: clamp(diag(U)) / radius) goes through LDS (u, free until the
+  // backward solve), loaded beside the first batch.  Loads are coherent (sc1):
+  // the system is written through by this launch's assemblers, or by the
+  // previous launch.
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
+  const double* S0 = b.S;
+  const int nn = n * n;
   for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
-    double v[kLoadBatch];
+    double xv[kLoadBatch];
+    const int tb = q0 / CC, ub = q0 - tb * CC;  // (t, uu) of the batch's first element, stepped below
+    int t = tb, uu = ub;
 #pragma unroll
     for (int k = 0; k < kLoadBatch; ++k) {
-      const int q = q0 + k, t = q / CC, uu = q - t * CC;
+      const int q = q0 + k;
       const int r = wave + nw * t, c = lane + 64 * uu;
-      v[k] = 0.0;
-      if (q < NQ && r < N && c < n && (c >> 4) <= (r >> 4)) {
-        if (r < n) {
-          v[k] = ld_sys(&b.S[r * n + c]);
-          // LM diagonal (Ceres: clamp(diag(U)) / radius), loaded in the same round
-          if (r == c) v[k] += fmin(fmax(ld_sys(&b.diagU[r]), o.min_diag), o.max_diag) / radius;
-        } else if (r == n) {
-          v[k] = -ld_sys(&b.bvec[c]);
-        }
-      } else if (q < NQ && c == n && r < n && (r >> 4) == (n >> 4)) {
-        v[k] = -ld_sys(&b.bvec[r]);  // the diagonal block must stay symmetric
+      if (++uu == CC) {
+        uu = 0;
+        ++t;
       }
+      // element class, branch-free: S (r, c < n), b as row n, b as column n
+      // of the last diagonal block (it must stay symmetric); others load S[0]
+      const bool in = q < NQ && r < N && c < n && (c >> 4) <= (r >> 4);
+      const bool colb = q < NQ && c == n && r < n && (r >> 4) == (n >> 4);
+      const int ix = in ? (r < n ? r * n + c : (r == n ? nn + c : 0)) : (colb ? nn + r : 0);
+      xv[k] = a_ld<true>(S0 + ix);
+    }
+    if (q0 == 0) {
+      STS(12);
+      for (int r = tid; r < n; r += nt) u[r] = fmin(fmax(a_ld<true>(S0 + nn + n + r), o.min_diag), o.max_diag) / radius;
+      __syncthreads();
+      STS(13);
     }
     if (done) return;
+    t = tb;
+    uu = ub;
 #pragma unroll
     for (int k = 0; k < kLoadBatch; ++k) {
-      const int q = q0 + k, t = q / CC, uu = q - t * CC;
+      const int q = q0 + k;
       const int r = wave + nw * t, c = lane + 64 * uu;
-      if (q < NQ && r < N && c < N && (c >> 4) <= (r >> 4)) a_st<kSc1>(&A[r * ld + c], (r == c && r >= n) ? 1.0 : v[k]);
+      if (++uu == CC) {
+        uu = 0;
+        ++t;
+      }
+      const bool in = q < NQ && r < N && c < n && (c >> 4) <= (r >> 4);
+      const bool colb = q < NQ && c == n && r < n && (r >> 4) == (n >> 4);
+      double v = (in && r < n) ? xv[k] : ((in && r == n) || colb) ? -xv[k] : 0.0;
+      if (in && r < n && r == c) v += u[r];
+      if (q < NQ && r < N && c < N && (c >> 4) <= (r >> 4)) a_st<kSc1>(&A[r * ld + c], (r == c && r >= n) ? 1.0 : v);
     }
   }
   if (done) return;
@@ -1943,8 +1983,9 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     const double* U = b.U + 36 * (long)(r / 6) + 6 * (r % 6);
     const int c0 = r - r % 6;
     double uy = 0.0;
-    for (int k = 0; k < 6; ++k) uy += U[k] * u[c0 + k];
-    cm += b.gcs[r] * u[r] + 0.5 * u[r] * uy;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) uy += (upre ? urow[k] : U[k]) * u[c0 + k];
+    cm += (upre ? gcr : b.gcs[r]) * u[r] + 0.5 * u[r] * uy;
   }
   double v2[3] = {s2, xn2, -cm}, out[3];
   block_sum<3>(v2, out, red);
@@ -2668,6 +2709,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_order_kernel(Geo g, Bufs b) {
       b.tl[(long)p * g.nruns + cnt++] = r * g.npairs + ka * ns - ka * (ka - 1) / 2 + (kb - ka);
     }
     b.tcnt[p] = cnt;
+    for (int q = cnt; q < g.nruns; ++q) b.tl[(long)p * g.nruns + q] = -1;  // (the assembly reads whole lists)
   }
 }
 

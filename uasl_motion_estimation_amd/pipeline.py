@@ -273,7 +273,7 @@ class GPUBackend(Backend):
     and page-locked staging are persistent (grow-only); per stage one H2D and
     one D2H."""
 
-    def __init__(self, ctx=None, tctx=None, overlap: bool = True, front_cus: int = 4, match_on_ba: bool = True):
+    def __init__(self, ctx=None, tctx=None, overlap: bool = True, front_cus: int = 4, match_on_ba: bool = False):
         from ._lib import Context, default_context
 
         self.ctx = ctx or default_context()
@@ -294,8 +294,8 @@ class GPUBackend(Backend):
             self.tctx.set_cu_mask(front)
             self.ctx.set_cu_mask(back)
             self._masked = True
-        # the matchers sit on the loop's critical path between two BAs, when
-        # the BA context is idle: they run there (its larger CU share)
+        # the matchers run on the front end beside the BA of the previous
+        # keyframe (the loop applies that BA only after the matching)
         self.mctx = self.ctx if match_on_ba else self.tctx
         self._imgs = {}
         # device-resident BA window: obs (4 doubles) | frame | track ID per
@@ -724,12 +724,13 @@ class WindowedStereoVO:
     (("new", id, t, (l, r)), ("add", id, t, (l, r)), ("pop", id), ("del", id))
     when log_events is set.
 
-    overlap=True pipelines the loop without changing any decision: process(t)
-    queues the KLT of frame t first, then completes frame t - 1 (queues its
-    scale LM behind that KLT, both beside frame t - 1's BA, then waits for the
-    BA result; pops; its FrameResult), then matches, books and queues the BA
-    of frame t; call finish() after the last frame.  With overlap=False every
-    process(t) completes frame t before returning."""
+    The loop is lagged by definition (process): BA(t - 1) enters the state
+    after keyframe t is matched and booked, so on the GPU the BA of t - 1 runs
+    while the host tracks, matches and books t, and the BA context idles only
+    while BA(t - 1) is applied and BA(t) queued.  Every backend takes the same
+    decisions; `overlap` only tells the GPU backend to run the front end on its
+    own context (overlap=False: one stream, everything in order).  Call
+    finish() after the last keyframe."""
 
     def __init__(self, cfg: PipelineConfig, backend: Backend, K=None, first_pose=None, velocity=None,
                  log_events: bool = False, overlap: bool = False):
@@ -850,6 +851,24 @@ class WindowedStereoVO:
 
     # ---------------------------------------------------------------- one keyframe
     def process(self, t: int, left: np.ndarray, right: np.ndarray):
+        """Keyframe t.  The loop definition (both backends, overlap or not):
+        the BA of keyframe t - 1 enters the state (poses, landmarks) only after
+        keyframe t is matched and booked -- keyframe t's prediction, matching
+        and new tracks use the state after BA(t - 2) -- so BA(t - 1) runs on
+        the device while the host tracks, matches and books keyframe t, and
+        BA(t) is queued as soon as BA(t - 1) is applied:
+          1. KLT of the active tracks (L(t-1) -> L(t)) queued;
+          2. pops of keyframe t-1's completion (features leaving the window);
+          3. pose(t) predicted (constant velocity, lagged state);
+          4. KLT gate + MI matching of the tracked features, new features of
+             the cells they leave empty (one round trip);
+          5. WBA_Point bookkeeping of t (addMatch, new tracks triangulated at
+             the predicted pose);
+          6. scale LM of keyframe t-1 (front end, beside BA(t-1));
+          7. BA(t-1) applied, keyframe t-1's FrameResult; pose(t) predicted
+             again from the refined poses and t's new landmarks moved with
+             it (camera-frame coordinates kept);
+          8. keyframe t's observations appended, BA(t) queued."""
         import time
         t_in = time.perf_counter()
         w0 = self.stage_s["wait"]
@@ -862,7 +881,10 @@ class WindowedStereoVO:
             pid, puv = self.obs[self.prev_t]
             pos = np.searchsorted(pid, self.ids[act])
             kh = self.be.klt_submit(self.prev_imgs, imgs, np.ascontiguousarray(puv[pos, :2]))
-        self._complete()  # frame t-1: BA result, pops (active tracks keep their order)
+        # 2. pops of frame t-1's completion (active tracks keep their order)
+        if self._pending is not None:
+            self._pop(self._pending[0] + 1 - cfg.window)
+        # 3. prediction from the lagged state
         pose = self._predict_pose(t)
         self.poses[t] = pose
         trk_idx = np.zeros(0, np.int64)
@@ -871,8 +893,8 @@ class WindowedStereoVO:
         grid = (self.nx, self.ny, self.cw, self.ch, cfg.n_feats)
         _, nd_new, _ = self.search_window()
         if kh is not None:
-            # 2. KLT gate + stereo matching of the tracked features (around their predicted disparity),
-            # 3a. then the new features of the cells they leave empty -- one backend round trip
+            # 4. KLT gate + stereo matching of the tracked features (around their predicted disparity),
+            # then the new features of the cells they leave empty -- one backend round trip
             act = np.flatnonzero(self.active)
             lo, nd, dvalid = self.search_window(self._predicted_disparity(act, pose))
             uv, st, xr_all, ok, nuv, nxr, nok = self._wait(self.be.klt_match_new, kh, imgs, lo, nd, dvalid, t, grid,
@@ -885,8 +907,8 @@ class WindowedStereoVO:
             nxr, nok = self._wait(self.be.match, imgs, nuv, np.full(len(nuv), cfg.d_min, np.int64), nd_new, True)
         n_tracked = len(trk_idx)
         nuv, nxr = nuv[nok], nxr[nok]
+        # 5. bookkeeping: new tracks, this frame's features (tracked first, then new; sorted by track = ID order)
         new_idx = self._add_tracks(t, nuv, nxr, pose)
-        # 3b. this frame's features (tracked first, then new; sorted by track = ID order)
         idx = np.concatenate([trk_idx, new_idx])
         feats = np.concatenate([np.concatenate([trk_uv, xr[:, None], trk_uv[:, 1:2]], 1),
                                 np.concatenate([nuv, nxr[:, None], nuv[:, 1:2]], 1)]).astype(np.float32)
@@ -895,30 +917,43 @@ class WindowedStereoVO:
         fid = self.ids[idx]
         self.obs[t] = (fid, feats)
         self.last[idx] = t
-        self.be.window_add(t, fid.astype(np.int32), feats)
         if self.log_events:
             is_new = np.zeros(len(self.ids), bool)
             is_new[new_idx] = True
             self._ev.append(("frame", self.ids[idx].copy(), t, feats.copy(), is_new[idx]))
-        # 5./6. windowed BA queued; the scale LM over the tracks seen in t is queued by the next
-        # keyframe behind its KLT (both beside this BA; the scale only enters the frame's result)
+        new_ids = self.ids[new_idx]
+        # 6./7. frame t-1: its scale LM (front end, beside its BA), then its BA applied
+        self._complete()
+        # pose(t) again from the refined poses; the new landmarks of t keep their camera-frame coordinates
+        pose2 = self._predict_pose(t)
+        if not np.array_equal(pose2, pose) and len(new_ids):
+            j = np.searchsorted(self.ids, new_ids)
+            R, R2 = aa_to_R(pose[3:]), aa_to_R(pose2[3:])
+            pc = self.X[j] @ R.T + pose[:3][None, :]
+            self.X[j] = (pc - pose2[:3][None, :]) @ R2
+        self.poses[t] = pose2
+        # 8. the window's observations, BA(t) queued; the scale LM over the tracks seen in t is queued by
+        # the next keyframe (beside this BA; the scale only enters the frame's result)
+        self.be.window_add(t, fid.astype(np.int32), feats)
         ba = self._ba_submit(t)
-        self._scale_args = (t, imgs, idx)
+        self._scale_args = (t, imgs, fid.copy())
         self._pending = (t, n_tracked, len(new_idx), int(self.active.sum()), ba)
         self.prev_imgs, self.prev_t = imgs, t
-        if not self.overlap:
-            self._complete()
         self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
 
     def finish(self):
-        """Complete the last queued frame (overlap mode)."""
+        """Complete the last queued keyframe (its pops, scale LM, BA)."""
         import time
         t_in = time.perf_counter()
         w0 = self.stage_s["wait"]
+        if self._pending is not None:
+            self._pop(self._pending[0] + 1 - self.cfg.window)
         self._complete()
         self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
 
     def _complete(self):
+        """Frame t-1 (the pending one): scale LM, then its BA result applied
+        and its FrameResult (its pops ran before the next keyframe's matching)."""
         if self._pending is None:
             return
         t, n_tracked, n_new, n_active, ba = self._pending
@@ -927,15 +962,14 @@ class WindowedStereoVO:
         self._scale_args = None
         sc = self._wait(self.be.scale_result)
         nwp, nwo, bs = self._ba_finish(ba)
-        # 3c. pop the features that leave the window with the next keyframe
-        self._pop(t + 1 - self.cfg.window)
         self.results.append(FrameResult(t, n_tracked, n_new, n_active, nwp, nwo, sc["scale"], int(sc["stop"]),
                                         int(sc["iterations"]), int(bs["iterations"]), float(bs["final_cost"]),
                                         self.poses[t].copy()))
 
-    def _scale_submit(self, t, imgs, idx):
+    def _scale_submit(self, t, imgs, tids):
         from .optimisation import OptimisationParams
 
+        idx = np.searchsorted(self.ids, tids)  # (tracks seen in t are alive: their last frame is t)
         pose = self.poses[t]
         R = aa_to_R(pose[3:])
         q = R_to_quat(R)
@@ -967,10 +1001,10 @@ class WindowedStereoVO:
             self.be._K, self.be._calib = self.K, (cfg.baseline, cfg.feat_var, cfg.fixed_frames)
             n_obs = self._wait(self.be.ba_submit_window, t, f0, self.ids[upts].astype(np.int32), self.X[upts], cams,
                                cfg.ba_iters)
-            return (t, f0, upts, n_obs)
+            return (t, f0, self.ids[upts].copy(), n_obs)
         bp = self.ba_problem(t, f0, upts)
         self._wait(self.be.ba_submit, bp, cfg.ba_iters)
-        return (t, f0, upts, len(bp.obs))
+        return (t, f0, self.ids[upts].copy(), len(bp.obs))
 
     def ba_problem(self, t, f0, upts):
         """The window [f0, t]'s BA problem on the host (host-path backends;
@@ -1004,9 +1038,14 @@ class WindowedStereoVO:
     def _ba_finish(self, ba):
         if ba is None:
             return 0, 0, {"iterations": 0, "final_cost": float("nan")}
-        t, f0, upts, nobs = ba
+        t, f0, wids, nobs = ba
         c, p, s = self._wait(self.be.ba_result)
+        # the window's tracks by ID (pops may have compacted the table since the submit; a track
+        # popped out of the table, seen only in the window's first keyframe, needs no landmark)
+        j = np.minimum(np.searchsorted(self.ids, wids), max(len(self.ids) - 1, 0))
+        live = (self.ids[j] == wids) if len(self.ids) else np.zeros(len(wids), bool)
         if s.get("status", 2) != 2 and os.environ.get("ME_VO_DUMP_FAILED"):  # diagnostics: the failed window
+            upts = j[live]
             bp = self.ba_problem(t, f0, upts)
             np.savez(os.environ["ME_VO_DUMP_FAILED"], cams=bp.cams, pts=bp.pts, obs=bp.obs, cam_idx=bp.cam_idx,
                      pt_idx=bp.pt_idx, K=bp.K0, t=t, f0=f0, ids=self.ids[upts], first=self.first[upts],
@@ -1015,8 +1054,8 @@ class WindowedStereoVO:
         if s.get("status", 2) == 2:
             for k, f in enumerate(range(f0, t + 1)):
                 self.poses[f] = np.asarray(c[k], np.float64).copy()
-            self.X[upts] = p
-        return len(upts), nobs, s
+            self.X[j[live]] = np.asarray(p)[live]
+        return len(wids), nobs, s
 
     def _pop(self, new_first):
         """WBA_Point::pop() of every feature older than `new_first`; empty tracks deleted."""
