@@ -668,6 +668,72 @@ class StereoVisualOdometry {
   std::vector<int> m_inliers;
 };
 
+// me::MonoVisualOdometry (include/MotionEstimation/vo/MonoVisualOdometry.h:18-57,
+// src/vo/MonoVisualOdometry.cpp:7-73): findEssentialMat + recoverPose on the
+// device (me_mono_vo_process).  Matches are StereoMatch<Point2f> {f1, f2}.
+template <class T>
+struct StereoMatch {
+  T f1, f2;
+  float m_score = -1.0f;
+};
+class MonoVisualOdometry {
+ public:
+  struct parameters {  // MonoVisualOdometry::parameters (MonoVisualOdometry.h:21-28) + the fields of the base it reads
+    bool ransac;
+    double inlier_threshold;
+    double prob;
+    double fu, fv, cu, cv;
+    parameters() : ransac(true), inlier_threshold(2.0), prob(0.99), fu(1.0), fv(1.0), cu(0.0), cv(0.0) {}
+  };
+  explicit MonoVisualOdometry(const parameters& param = parameters(),
+                              amd::Context& ctx = amd::Context::thread_default())
+      : m_param(param), m_ctx(&ctx) {
+    for (int i = 0; i < 16; ++i) m_Rt[i] = (i % 5 == 0) ? 1.0 : 0.0;
+  }
+  bool process(const std::vector<StereoMatch<Point2f>>& matches) {
+    const int n = (int)matches.size();
+    std::vector<float> f1(2 * (size_t)n), f2(2 * (size_t)n);
+    for (int i = 0; i < n; ++i) {
+      f1[2 * i] = matches[i].f1.x;
+      f1[2 * i + 1] = matches[i].f1.y;
+      f2[2 * i] = matches[i].f2.x;
+      f2[2 * i + 1] = matches[i].f2.y;
+    }
+    me_mono_params p;
+    me_mono_default_params(&p);
+    p.fu = m_param.fu;
+    p.fv = m_param.fv;
+    p.cu = m_param.cu;
+    p.cv = m_param.cv;
+    p.prob = m_param.prob;
+    p.inlier_threshold = m_param.inlier_threshold;
+    p.ransac = m_param.ransac ? 1 : 0;
+    std::vector<int32_t> inl((size_t)std::max(n, 1));
+    int ni = 0, ok = 0;
+    m_ctx->check(me_mono_vo_process(m_ctx->get(), f1.data(), f2.data(), n, &p, m_Rt.data(), m_E.data(), inl.data(),
+                                    &ni, &ok),
+                 "MonoVisualOdometry::process");
+    m_inliers.assign(inl.begin(), inl.begin() + ni);
+    m_outliers.clear();
+    for (int i = 0, k = 0; i < n; ++i) {
+      if (k < ni && inl[k] == i) ++k;
+      else m_outliers.push_back(i);
+    }
+    return ok != 0;
+  }
+  const std::array<double, 16>& getMotion() const { return m_Rt; }
+  const std::array<double, 9>& getEssentialMat() const { return m_E; }
+  const std::vector<int>& getInliersIdx() const { return m_inliers; }
+  const std::vector<int>& getOutliersIdx() const { return m_outliers; }
+
+ private:
+  parameters m_param;
+  amd::Context* m_ctx;
+  std::array<double, 16> m_Rt{};
+  std::array<double, 9> m_E{};
+  std::vector<int> m_inliers, m_outliers;
+};
+
 // Pyramidal LK tracking of n points from prev to next (A12, no reference
 // counterpart: the application's feature tracker).  status[i] = 1 tracked.
 inline void calcOpticalFlowPyrLK(const amd::ImageView& prev, const amd::ImageView& next,

@@ -434,6 +434,28 @@ int me_vo_process(me_ctx* ctx, const float* matches, int n, const double* init6,
                   int max_outer, double* motion, double* state, double* pts3d, int* inliers, int* n_inliers,
                   int* ok);
 
+/* ---- §8f-4: monocular VO -----------------------------------------------
+ * Replaces bool me::MonoVisualOdometry::process(const std::vector<StereoMatch<
+ * cv::Point2f>>&) (src/vo/MonoVisualOdometry.cpp:7-73) with getMotion(),
+ * getEssentialMat(), getInliersIdx() (MonoVisualOdometry.h:35-41).  The
+ * reference's OpenCV findEssentialMat (five-point + RANSAC at prob, or LMedS
+ * when ransac = 0; threshold <= 0 -> 1 px) and recoverPose (distance 500) are
+ * restated on the device (csrc/mono.hip; parity unpinned: OpenCV absent).
+ * f1, f2: n (x, y) floats (StereoMatch f1 / f2; a match with f1.x <= 0 or
+ * f2.x <= 0 is skipped as in the reference).  ok = process()'s result; Rt =
+ * getMotion() (4x4 row-major, identity when ok = 0); E = getEssentialMat()
+ * (3x3, zero when none; may be NULL); inliers = getInliersIdx() (indices into
+ * the matches, capacity n; may be NULL). */
+typedef struct {
+  double fu, fv, cu, cv;     /* MonoVisualOdometry::parameters (MonoVisualOdometry.h:21-28) */
+  double prob;               /* 0.99 */
+  double inlier_threshold;   /* VisualOdometry::parameters: 2.0 */
+  int ransac;                /* 1: RANSAC, 0: LMedS */
+} me_mono_params;
+void me_mono_default_params(me_mono_params* p);
+int me_mono_vo_process(me_ctx* ctx, const float* f1, const float* f2, int n, const me_mono_params* p, double* Rt,
+                       double* E, int32_t* inliers, int* n_inliers, int* ok);
+
 #ifdef __cplusplus
 }
 #endif

@@ -152,6 +152,24 @@ int oracle_vo_process(const float* matches, int n, const double* init6, const or
                       const int* rand_seq, int rand_len, double* motion, int* inliers, int* n_inliers,
                       int max_outer);
 
+/* ---- Mono VO (src/vo/MonoVisualOdometry.cpp:7-73): OpenCV findEssentialMat
+   (five-point + RANSAC / LMedS) + recoverPose restated (oracle/mono.cpp) ---- */
+typedef struct {
+  double fu, fv, cu, cv;     /* MonoVisualOdometry::parameters (MonoVisualOdometry.h:21-28) */
+  double prob;               /* 0.99 */
+  double inlier_threshold;   /* VisualOdometry::parameters, 2.0 (<= 0 -> 1.0) */
+  int ransac;                /* 1 RANSAC, 0 LMedS */
+} oracle_mono_params;
+/* f1, f2: n matches (x, y) float; Rt 16 (row-major 4x4), E 9; inliers: indices
+   into the matches; stats (optional): iterations run, best inlier count,
+   recoverPose branch.  Returns process(): 1 / 0. */
+int oracle_mono_vo_process(const float* f1, const float* f2, int n, const oracle_mono_params* p, double* Rt,
+                           double* E, int32_t* inliers, int* n_inliers, int* stats);
+int oracle_five_point(const double* x1, const double* x2, double* E_out /* 90 */);
+float oracle_sampson(const double* E, const double* x1, const double* x2);
+/* the first n_sets RANSAC subsets (5 indices each) of cv::RNG((uint64)-1) */
+int oracle_cv_rng_subsets(int count, int n_sets, int32_t* idx);
+
 /* ---- pose-covariance propagation (src/core/feature_types.cpp:171-251) ---- */
 void oracle_pose_mul_cov(const double* q1, const double* t1, const double* c1, const double* q2, const double* t2,
                          const double* c2, int reverse, double* q3, double* t3, double* c3);

@@ -245,11 +245,35 @@ int run_vo(Reader& in, FILE* out) {
   fwrite(vo.getInliers_idx().data(), 4, vo.getInliers_idx().size(), out);
   return 0;
 }
+int run_mono(Reader& in, FILE* out) {
+  const int n = in.get<int32_t>();
+  me::MonoVisualOdometry::parameters prm;
+  prm.ransac = in.get<int32_t>() != 0;
+  prm.fu = in.get<double>();
+  prm.fv = in.get<double>();
+  prm.cu = in.get<double>();
+  prm.cv = in.get<double>();
+  std::vector<me::StereoMatch<me::Point2f>> m((size_t)n);
+  for (auto& q : m) {
+    float v[4];
+    in.get(v, 4);
+    q.f1 = {v[0], v[1]};
+    q.f2 = {v[2], v[3]};
+  }
+  me::MonoVisualOdometry vo(prm);
+  const int32_t ok = vo.process(m) ? 1 : 0;
+  fwrite(&ok, 4, 1, out);
+  fwrite(vo.getMotion().data(), 8, 16, out);
+  const int32_t ninl = (int32_t)vo.getInliersIdx().size();
+  fwrite(&ninl, 4, 1, out);
+  fwrite(vo.getInliersIdx().data(), 4, vo.getInliersIdx().size(), out);
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc != 4) {
-    std::fprintf(stderr, "usage: %s ba|mi|nms|scale|vo in.bin out.bin\n", argv[0]);
+    std::fprintf(stderr, "usage: %s ba|mi|nms|scale|vo|mono in.bin out.bin\n", argv[0]);
     return 2;
   }
   Reader in = read_file(argv[2]);
@@ -263,6 +287,7 @@ int main(int argc, char** argv) {
     else if (!std::strcmp(argv[1], "nms")) rc = run_nms(in, out);
     else if (!std::strcmp(argv[1], "scale")) rc = run_scale(in, out);
     else if (!std::strcmp(argv[1], "vo")) rc = run_vo(in, out);
+    else if (!std::strcmp(argv[1], "mono")) rc = run_mono(in, out);
   } catch (const std::exception& e) {
     std::fprintf(stderr, "adapter_cli: %s\n", e.what());
     rc = 1;

@@ -538,3 +538,65 @@ def vo_process(matches, params: dict, rand_seq=None, init=None, max_outer=10000)
                              rs.ctypes.data, len(rs), motion.ctypes.data, inl.ctypes.data, ctypes.byref(nin),
                              max_outer)
     return rc, motion.reshape(4, 4), inl[:nin.value].copy()
+
+
+# ------------------------------------------------------------------ Mono VO (oracle/mono.cpp)
+class OMonoParams(ctypes.Structure):
+    _fields_ = [("fu", c_double), ("fv", c_double), ("cu", c_double), ("cv", c_double), ("prob", c_double),
+                ("inlier_threshold", c_double), ("ransac", c_int)]
+
+
+def _mono_decl(L):
+    if getattr(L, "_mono_decl", False):
+        return
+    L.oracle_mono_vo_process.argtypes = [c_void_p, c_void_p, c_int, POINTER(OMonoParams), c_void_p, c_void_p,
+                                         c_void_p, POINTER(c_int), c_void_p]
+    L.oracle_mono_vo_process.restype = c_int
+    L.oracle_five_point.argtypes = [c_void_p, c_void_p, c_void_p]
+    L.oracle_five_point.restype = c_int
+    L.oracle_sampson.argtypes = [c_void_p, c_void_p, c_void_p]
+    L.oracle_sampson.restype = c_float
+    L.oracle_cv_rng_subsets.argtypes = [c_int, c_int, c_void_p]
+    L.oracle_cv_rng_subsets.restype = c_int
+    L._mono_decl = True
+
+
+def mono_params(**kw) -> OMonoParams:
+    d = dict(fu=1.0, fv=1.0, cu=0.0, cv=0.0, prob=0.99, inlier_threshold=2.0, ransac=1)
+    d.update(kw)
+    return OMonoParams(**{k: (int(v) if k == "ransac" else float(v)) for k, v in d.items()})
+
+
+def mono_vo_process(f1, f2, **params):
+    """oracle_mono_vo_process: (ok, Rt (4,4), E (3,3), inlier indices, stats (iters, best count, pose branch))."""
+    L = lib()
+    _mono_decl(L)
+    a = np.ascontiguousarray(f1, np.float32).reshape(-1, 2)
+    b = np.ascontiguousarray(f2, np.float32).reshape(-1, 2)
+    n = len(a)
+    Rt, E = np.zeros(16), np.zeros(9)
+    inl = np.zeros(max(n, 1), np.int32)
+    ni = c_int(0)
+    st = np.zeros(3, np.int32)
+    p = mono_params(**params)
+    ok = L.oracle_mono_vo_process(a.ctypes.data, b.ctypes.data, n, ctypes.byref(p), Rt.ctypes.data, E.ctypes.data,
+                                  inl.ctypes.data, ctypes.byref(ni), st.ctypes.data)
+    return ok, Rt.reshape(4, 4), E.reshape(3, 3), inl[:ni.value].copy(), st
+
+
+def five_point(x1, x2):
+    L = lib()
+    _mono_decl(L)
+    a = np.ascontiguousarray(x1, np.float64).reshape(5, 2)
+    b = np.ascontiguousarray(x2, np.float64).reshape(5, 2)
+    E = np.zeros(90)
+    n = L.oracle_five_point(a.ctypes.data, b.ctypes.data, E.ctypes.data)
+    return E[:9 * n].reshape(n, 3, 3)
+
+
+def cv_rng_subsets(count: int, n_sets: int) -> np.ndarray:
+    L = lib()
+    _mono_decl(L)
+    idx = np.zeros(5 * n_sets, np.int32)
+    k = L.oracle_cv_rng_subsets(count, n_sets, idx.ctypes.data)
+    return idx[:5 * k].reshape(k, 5)

@@ -200,3 +200,21 @@ def test_cpp_stereo_vo_matches_oracle(tmp_path, oracle):
     assert rc in (0, 1) and bool(ok) == bool(rc)
     assert np.array_equal(inl, rinl)
     np.testing.assert_allclose(motion, rM, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_cpp_mono_vo_matches_oracle(tmp_path, oracle):
+    """me::MonoVisualOdometry (the C++ mirror of MonoVisualOdometry.h) over the
+    C ABI = the oracle's restated findEssentialMat + recoverPose."""
+    f1, f2, p, R, t = S.mono_matches(31, 500, noise=0.4, n_outliers=80, n_invalid=4)
+    b = struct.pack("<ii", len(f1), 1) + struct.pack("<4d", p["fu"], p["fv"], p["cu"], p["cv"])
+    b += np.ascontiguousarray(np.concatenate([f1, f2], 1), np.float32).tobytes()
+    _, out = _run("mono", b, tmp_path)
+    (ok,) = struct.unpack_from("<i", out)
+    motion = np.frombuffer(out, np.float64, 16, 4).reshape(4, 4)
+    (ninl,) = struct.unpack_from("<i", out, 4 + 128)
+    inl = np.frombuffer(out, np.int32, ninl, 8 + 128)
+    rok, rRt, rE, rinl, _ = oracle.mono_vo_process(f1, f2, **p)
+    assert ok == rok == 1
+    assert np.array_equal(inl, rinl)
+    np.testing.assert_allclose(motion, rRt, rtol=0, atol=1e-9)

@@ -129,7 +129,14 @@ EXPORTS = [
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
+    "me_mono_default_params", "me_mono_vo_process",
 ]
+
+class MonoParamsC(ctypes.Structure):
+    """me_mono_params (include/me_hip.h)."""
+    _fields_ = [("fu", c_double), ("fv", c_double), ("cu", c_double), ("cv", c_double), ("prob", c_double),
+                ("inlier_threshold", c_double), ("ransac", c_int)]
+
 
 class VOParamsC(ctypes.Structure):
     """me_vo_params (include/me_hip.h)."""
@@ -237,6 +244,9 @@ def load_library(path: str = LIB_PATH):
         "me_vo_rand": (c_int, [c_void_p, P(c_int)]),
         "me_vo_process": (c_int, [c_void_p, c_void_p, c_int, P(c_double), P(VOParamsC), c_int, P(c_double),
                                   P(c_double), P(c_double), P(c_int), P(c_int), P(c_int)]),
+        "me_mono_default_params": (None, [P(MonoParamsC)]),
+        "me_mono_vo_process": (c_int, [c_void_p, c_void_p, c_void_p, c_int, P(MonoParamsC), P(c_double),
+                                       P(c_double), c_void_p, P(c_int), P(c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

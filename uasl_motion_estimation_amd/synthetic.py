@@ -701,3 +701,41 @@ def vo_matches(seed: int, n: int, width: int = 1280, height: int = 720, noise: f
         k += 1
     params = dict(baseline=b, fu1=f, fv1=f, fu2=f, fv2=f, cu1=cu, cu2=cu, cv1=cv, cv2=cv)
     return out, params
+
+
+def mono_matches(seed: int, n: int, width: int = 1280, height: int = 720, noise: float = 0.3,
+                 aa=(0.01, -0.02, 0.005), t=(0.3, -0.05, 1.0), n_outliers: int = 0, n_invalid: int = 0):
+    """Two-view matches (f1 in view 1, f2 in view 2; the MonoVisualOdometry
+    input, MonoVisualOdometry.cpp:7-17) of points 4-40 m in front of a
+    camera that moves by X2 = R(aa) X1 + t (t normalised to 1 m: the mono scale
+    is unobservable).  `noise` px Gaussian on both views; the first
+    `n_outliers` matches get f2 shifted 15-60 px; the last `n_invalid` get
+    f1.x = -1 (dropped by the reference's f1.x > 0 test).  Returns
+    (f1 (n, 2) float32, f2 (n, 2) float32, params dict, R, t unit)."""
+    rng = np.random.default_rng(seed)
+    K = intrinsics(width, height)
+    f, cu, cv = K[0, 0], K[0, 2], K[1, 2]
+    R = aa_to_R(np.asarray(aa, np.float64))
+    tv = np.asarray(t, np.float64)
+    tv = tv / np.linalg.norm(tv)
+    f1 = np.zeros((n, 2), np.float32)
+    f2 = np.zeros((n, 2), np.float32)
+    k = 0
+    while k < n:
+        u, v, Z = rng.uniform(10, width - 10), rng.uniform(10, height - 10), rng.uniform(4.0, 40.0)
+        X1 = np.array([(u - cu) * Z / f, (v - cv) * Z / f, Z])
+        X2 = R @ X1 + tv
+        if X2[2] < 1.0:
+            continue
+        u2, v2 = f * X2[0] / X2[2] + cu, f * X2[1] / X2[2] + cv
+        if not (0 <= u2 < width and 0 <= v2 < height):
+            continue
+        a = np.array([u, v]) + (rng.normal(0, noise, 2) if noise else 0)
+        b = np.array([u2, v2]) + (rng.normal(0, noise, 2) if noise else 0)
+        if k < n_outliers:
+            b = b + rng.uniform(15, 60, 2) * rng.choice([-1, 1], 2)
+        f1[k], f2[k] = a, b
+        k += 1
+    if n_invalid:
+        f1[n - n_invalid:, 0] = -1.0
+    return f1, f2, dict(fu=f, fv=f, cu=cu, cv=cv), R, tv

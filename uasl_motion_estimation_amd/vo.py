@@ -147,3 +147,80 @@ class StereoVisualOdometry:
 
     def getParams(self) -> Parameters:
         return self.m_param
+
+
+# ------------------------------------------------------------------ monocular VO (§8f-4)
+@dataclass
+class MonoParameters:
+    """MonoVisualOdometry::parameters with the VisualOdometry::parameters base
+    (MonoVisualOdometry.h:21-28, VisualOdometry.h:19-33); the fields the mono
+    path reads, same defaults."""
+    prob: float = 0.99
+    fu: float = 1.0
+    fv: float = 1.0
+    cu: float = 0.0
+    cv: float = 0.0
+    ransac: bool = True
+    inlier_threshold: float = 2.0
+
+    def to_c(self):
+        from ._lib import MonoParamsC
+
+        return MonoParamsC(self.fu, self.fv, self.cu, self.cv, self.prob, self.inlier_threshold, int(bool(self.ransac)))
+
+
+class MonoVisualOdometry:
+    """Mirror of me::MonoVisualOdometry (include/MotionEstimation/vo/
+    MonoVisualOdometry.h:18-57, src/vo/MonoVisualOdometry.cpp:7-73).
+    process() hands the matches to me_mono_vo_process: the five-point solve of
+    every RANSAC sample on its own GPU lane, the Sampson scores of every
+    model by a wave, the best model's recoverPose (decomposition, DLT
+    triangulation and cheirality of every match under the four poses) on the
+    device.  OpenCV's findEssentialMat / recoverPose are restated (parity
+    unpinned); the RANSAC samples follow OpenCV's cv::RNG((uint64)-1)."""
+
+    def __init__(self, param: MonoParameters | None = None, ctx: Context | None = None):
+        self.param = param or MonoParameters()
+        self.ctx = ctx or default_context()
+        self._Rt = np.eye(4)
+        self._E = np.eye(4)  # (the reference's ctor sets m_E = eye(4, 4))
+        self._inliers: list = []
+        self._outliers: list = []
+
+    def process(self, matches) -> bool:
+        """matches: (n, 4) {f1.x, f1.y, f2.x, f2.y} or a pair (f1 (n, 2), f2 (n, 2))."""
+        if isinstance(matches, tuple):
+            f1 = np.ascontiguousarray(matches[0], np.float32).reshape(-1, 2)
+            f2 = np.ascontiguousarray(matches[1], np.float32).reshape(-1, 2)
+        else:
+            m = np.asarray(matches, np.float32).reshape(-1, 4)
+            f1, f2 = np.ascontiguousarray(m[:, :2]), np.ascontiguousarray(m[:, 2:])
+        n = len(f1)
+        p = self.param.to_c()
+        Rt, E = np.zeros(16), np.zeros(9)
+        inl = np.zeros(max(n, 1), np.int32)
+        ni, ok = ctypes.c_int(0), ctypes.c_int(0)
+        c = self.ctx
+        c.check(c.lib.me_mono_vo_process(c.h, f1.ctypes.data, f2.ctypes.data, n, ctypes.byref(p),
+                                         Rt.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                         E.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), inl.ctypes.data,
+                                         ctypes.byref(ni), ctypes.byref(ok)), "me_mono_vo_process")
+        self._Rt = Rt.reshape(4, 4)
+        if n >= 8 and np.any(E):
+            self._E = E.reshape(3, 3)
+        self._inliers = [int(i) for i in inl[:ni.value]]
+        s = set(self._inliers)
+        self._outliers = [i for i in range(n) if i not in s] if n >= 8 and np.any(E) else self._outliers
+        return bool(ok.value)
+
+    def getMotion(self) -> np.ndarray:
+        return self._Rt.copy()
+
+    def getEssentialMat(self) -> np.ndarray:
+        return self._E.copy()
+
+    def getInliersIdx(self) -> list:
+        return list(self._inliers)
+
+    def getOutliersIdx(self) -> list:
+        return list(self._outliers)
