@@ -971,9 +971,18 @@ constexpr int kSaElems = 32, kSaGroups = kBlock / kSaElems;
 // into the exchange buffer in the tile layout (element idx of [S | b] at
 // xch[idx], diag(U) in the tail) instead of S; SA_UNPACK reads the all-reduced
 // exchange (no partials, no U) and stores S / b / diag(U) exactly as SA_SUM.
+__host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
 enum { SA_SUM = 0, SA_PACK = 1, SA_UNPACK = 2 };
+// img (fused camera solve, LDS form): instead of S | b | diag(U), the
+// assembly writes the solver's image of [S + D; -b^T] itself -- the lower
+// block triangle of the N x ld padded matrix the factorisation runs on (the
+// LM diagonal clamp(diag U) / radius added, row n = -b^T, the last diagonal
+// block symmetric, identity padding), written through -- so the solve copies
+// it into LDS with a few LDS-DMA instructions instead of an element-wise load
+// (whose one-time code dominated the launch, tools/solve_ts.py).
 template <int NTH, bool SC1>
-__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, int mode = SA_SUM) {
+__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, int mode = SA_SUM,
+                                double* img = nullptr, const Opts* o = nullptr) {
   constexpr int EL = NTH / kSaGroups;
   __shared__ double part[kSaGroups][EL];
   const State* st = b.st;
@@ -1043,6 +1052,41 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
   }
   part[grp][e] = acc;
   __syncthreads();
+  if (img != nullptr) {
+    // every element of the tile pair when live (padding included): the image
+    // is complete without any other writer
+    if (grp == 0 && live && gr >= 0) {
+      const int ld = solve_ld(g.Ts);
+      double sum = 0.0;
+      if (mode == SA_UNPACK) {
+        sum = b.xch[idx];
+      } else {
+#pragma unroll
+        for (int k = 0; k < kSaGroups; ++k) sum += part[k][e];
+      }
+      double v;
+      if (gr < n && gc < n) {
+        if (mode == SA_UNPACK) {
+          v = fail ? 0.0 : sum;
+        } else {
+          v = 0;
+          if (gr / 6 == gc / 6) v = b.U[36 * (gr / 6) + (gr % 6) * 6 + (gc % 6)];
+          v = fail ? 0.0 : v - sum;
+        }
+        if (gr == gc) {
+          const double du = mode == SA_UNPACK ? b.xch[xo_diag(g) + gr] : b.U[36 * (gr / 6) + (gr % 6) * 7];
+          v += fmin(fmax(du, o->min_diag), o->max_diag) / b.st->radius;
+        }
+      } else if ((gr < n && gc == n) || (gr == n && gc < n)) {
+        const int r = gr < n ? gr : gc;  // (the (n, c) partial equals the (c, n) one bit for bit: Y^T Y)
+        v = -(fail ? 0.0 : mode == SA_UNPACK ? sum : b.gcs[r] - sum);
+      } else {
+        v = gr == gc ? 1.0 : 0.0;  // (n, n) and the padding: identity
+      }
+      a_st<SC1>(&img[diag ? (long)gr * ld + gc : (long)gc * ld + gr], v);
+    }
+    return;
+  }
   if (grp == 0 && use) {
     double sum = 0.0;
     if (mode == SA_UNPACK) {
@@ -1133,7 +1177,7 @@ constexpr int kLoadBatch = 32;
 // [1] lin_finalize, [2] assembly wait, [3] load, [4] factorisation, [5] backward
 // solve, [6] candidate / cost tail, [8] last assembler exit - wg 0 entry,
 // [9] first assembler entry - wg 0 entry, [10] s_memtime ticks of [1..6], [15] calls
-__device__ long long g_solve_ts[16];
+__device__ long long g_solve_ts[24];
 __device__ unsigned long long g_asm_first = ~0ull, g_asm_last = 0ull;
 #define STS_DECL long long sts_prev_ = 0, sts_t0_ = 0, sts_c0_ = 0
 #define STS_BEGIN()                                                        \
@@ -1178,7 +1222,6 @@ __device__ unsigned long long g_asm_first = ~0ull, g_asm_last = 0ull;
 #define STS_ASM() do {} while (0)
 #endif
 
-__host__ __device__ inline int solve_ld(int Ts) { return ((16 * Ts + 31) / 32) * 32 + 2; }  // == 2 mod 32
 // dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
 #ifndef ME_CHOL_PB
 #define ME_CHOL_PB 4
@@ -1569,7 +1612,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     if (threadIdx.x == 0) atomicMin(&g_asm_first, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
     // (sharded: the assemblers unpack the all-reduced exchange instead of summing partials)
-    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM);
+    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM, kLds ? b.Abuf : nullptr,
+                                       &o);
     drain_and_barrier();  // every wave's written-through stores have left
 #ifdef ME_SOLVE_TS
     if (threadIdx.x == 0) atomicMax(&g_asm_last, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1656,6 +1700,20 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
   const double* S0 = b.S;
   const int nn = n * n;
+  if (kLds && fused) {
+    // the assemblers wrote the solver's image (s_assemble_body img): N x ld
+    // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
+    // coherent reads (sc1); the barrier below retires them (vmcnt)
+    const int nbytes = N * ld * 8, nchunk = (nbytes + 1023) >> 10;
+    if (!done)
+      for (int k = wave; k < nchunk; k += nw) {
+        const int off = (k << 10) + 16 * lane;
+        if (off < nbytes)
+          __builtin_amdgcn_global_load_lds((const void*)((const char*)b.Abuf + off),
+                                           (__attribute__((address_space(3))) void*)((char*)A + (k << 10)), 16, 0,
+                                           16 /* sc1 */);
+      }
+  } else
   for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
     double xv[kLoadBatch];
     const int tb = q0 / CC, ub = q0 - tb * CC;  // (t, uu) of the batch's first element, stepped below
@@ -1775,9 +1833,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
     if (wave == 0) diag_block(0);
+    STS(19);
     __syncthreads();
     for (int J = 0; J + 1 < Ts; ++J) {
       if (sfail) break;
+      STS(18);
       if (wave == 0) {
         panel_tile(J, J + 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -1786,7 +1846,9 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         // (its updated values are read by no one else: the factorisation
         // overwrites the lower triangle with L, the upper one is never read)
         solve_wave_sync();  // the panel tile just stored is an operand
+        STS(16);
         diag_factor(J + 1, trailing_diag_acc(A, ld, J, J + 1, lane));
+        STS(17);
       } else if (worker) {
         for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -3456,7 +3518,7 @@ extern "C" int me_solve_ts(long long* out, int reset) {
   hipDeviceSynchronize();
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solve_ts), sizeof(g_solve_ts));
   if (reset) {
-    long long z[16] = {0};
+    long long z[24] = {0};
     hipMemcpyToSymbol(HIP_SYMBOL(g_solve_ts), z, sizeof(z));
   }
   return 0;

@@ -297,6 +297,9 @@ class GPUBackend(Backend):
         # the matchers run on the front end beside the BA of the previous
         # keyframe (the loop applies that BA only after the matching)
         self.mctx = self.ctx if match_on_ba else self.tctx
+        self._scale_pool = None  # worker thread of the asynchronous scale LM
+        self._ba_pool = self._ba_fut = None  # worker thread queueing the BA launches
+        self.async_enqueue = os.environ.get("ME_VO_ASYNC_ENQUEUE", "1") == "1"
         self._imgs = {}
         # device-resident BA window: obs (4 doubles) | frame | track ID per
         # observation, frame by frame; [_wstart, _wend) live in store _wcur
@@ -358,9 +361,10 @@ class GPUBackend(Backend):
             return self._imgs[t]
         L = np.ascontiguousarray(left, np.uint8)
         R = np.ascontiguousarray(right, np.uint8)
-        dL, dR = self.ctx.malloc(L.nbytes), self.ctx.malloc(R.nbytes)
-        self.ctx.h2d(dL, L)
-        self.ctx.h2d(dR, R)
+        # (on the front-end context: the BA context may be in use by the enqueue worker)
+        dL, dR = self.tctx.malloc(L.nbytes), self.tctx.malloc(R.nbytes)
+        self.tctx.h2d(dL, L)
+        self.tctx.h2d(dR, R)
         h = (dL, dR, L.shape, L, R)
         self._imgs[t] = h
         return h
@@ -380,12 +384,20 @@ class GPUBackend(Backend):
     def release(self, t):
         h = self._imgs.pop(t, None)
         if h is not None and len(h) == 5:  # (device-resident inputs of frame_images_device are the caller's)
-            self.ctx.free(h[0])
-            self.ctx.free(h[1])
+            self.tctx.free(h[0])
+            self.tctx.free(h[1])
 
     def close(self):
+        if self._scale_res is not None:
+            self.scale_result()
+        if self._scale_pool is not None:
+            self._scale_pool.shutdown()
+            self._scale_pool = None
         if self._ba is not None:
             self.ba_result()
+        if self._ba_pool is not None:
+            self._ba_pool.shutdown()
+            self._ba_pool = None
         for st in self._wstore:
             if st is not None:
                 self.ctx.free(st)
@@ -573,7 +585,18 @@ class GPUBackend(Backend):
         return self._view(ho, np.float32, n).copy(), self._view(ho, np.uint8, n, 4 * n).astype(bool)
 
     def scale_submit(self, sp, params):
-        self._scale_res = self.scale_optimise(sp, params)
+        """The scale LM on the front-end context, run by a worker thread (the
+        C call releases the GIL): the loop books the keyframe and queues the
+        next BA meanwhile; scale_result joins it."""
+        if self._scale_pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._scale_pool = ThreadPoolExecutor(max_workers=1)
+        self._scale_res = self._scale_pool.submit(self.scale_optimise, sp, params)
+
+    def scale_result(self) -> dict:
+        r, self._scale_res = self._scale_res, None
+        return r.result() if r is not None else None
 
     # ---- device-resident BA window
     device_window = True
@@ -648,12 +671,8 @@ class GPUBackend(Backend):
         self._view(hp, np.float64, 3 * npts, 48 * nc)[:] = np.asarray(X, np.float64).ravel()
         self._view(hp, np.int32, npts, 48 * nc + 24 * npts)[:] = win_ids
         d = self._dbuf("bw", nb)
-        c.copy_async(d, hp, nb)
         di = self._dbuf("bw_idx", 8 * max(n_obs, 1))
         o, f, i = self._wview(self._wcur)
-        c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
-                                           V(d + 48 * nc + 24 * npts), npts, V(di), V(di + 4 * n_obs)),
-                "me_ba_window_indices")
         p = BAProblemC()
         p.n_cams, p.n_pts, p.n_obs = nc, npts, n_obs
         p.cams = ctypes.cast(d, ctypes.POINTER(ctypes.c_double))
@@ -667,7 +686,25 @@ class GPUBackend(Backend):
         p.baseline, p.feat_var, p.fixed_frames = self._calib
         p.mem, p.obs_dim = ME_DEVICE, 4
         opt = SolverOptions.fixed_iterations(iters).to_c()
-        c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(opt)), "me_ba_solve_async")
+
+        def enqueue():  # H2D, the window's indices, the solve (~50 launches of host time)
+            c.copy_async(d, hp, nb)
+            c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
+                                               V(d + 48 * nc + 24 * npts), npts, V(di), V(di + 4 * n_obs)),
+                    "me_ba_window_indices")
+            c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(opt)), "me_ba_solve_async")
+
+        # The launches are queued by a worker thread (the C calls release the
+        # GIL): the loop goes on with the next keyframe's front end, which uses
+        # the other context; ba_result joins the worker before touching this one.
+        if self.async_enqueue:
+            if self._ba_pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._ba_pool = ThreadPoolExecutor(max_workers=1)
+            self._ba_fut = self._ba_pool.submit(enqueue)
+        else:
+            enqueue()
         self._ba = ("dev", p, opt, d, nc, npts)
         return n_obs
 
@@ -691,6 +728,9 @@ class GPUBackend(Backend):
         from ._lib import BASummaryC
         from .optimisation import _summary
 
+        if self._ba_fut is not None:  # the worker's enqueue (and its errors)
+            fut, self._ba_fut = self._ba_fut, None
+            fut.result()
         rec = self._ba
         self._ba = None
         s = BASummaryC()
@@ -764,6 +804,7 @@ class WindowedStereoVO:
         self._pending = None                 # frame whose BA (and, once _complete runs, scale LM) are queued
         self._scale_args = None
         self.stage_s = {"host": 0.0, "wait": 0.0}  # host bookkeeping vs time blocked in the backend
+        self.wait_by_stage = {}  # backend call -> seconds blocked in it
 
     @property
     def events(self):
@@ -844,9 +885,12 @@ class WindowedStereoVO:
 
         from ._lib import roctx_range
         t0 = time.perf_counter()
-        with roctx_range(getattr(fn, "__name__", "stage"), ROCTX):
+        name = getattr(fn, "__name__", "stage")
+        with roctx_range(name, ROCTX):
             r = fn(*a)
-        self.stage_s["wait"] += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.stage_s["wait"] += dt
+        self.wait_by_stage[name] = self.wait_by_stage.get(name, 0.0) + dt
         return r
 
     # ---------------------------------------------------------------- one keyframe
@@ -905,6 +949,11 @@ class WindowedStereoVO:
         else:
             nuv = new_cells(t, trk_uv, grid)
             nxr, nok = self._wait(self.be.match, imgs, nuv, np.full(len(nuv), cfg.d_min, np.int64), nd_new, True)
+        # 6. frame t-1's scale LM queued now (front end, beside BA(t-1); its inputs are the lagged state,
+        # untouched by this frame's bookkeeping): the GPU backend runs it on a worker thread
+        if self._scale_args is not None:
+            self._scale_submit(*self._scale_args)
+            self._scale_args = None
         n_tracked = len(trk_idx)
         nuv, nxr = nuv[nok], nxr[nok]
         # 5. bookkeeping: new tracks, this frame's features (tracked first, then new; sorted by track = ID order)
@@ -922,8 +971,8 @@ class WindowedStereoVO:
             is_new[new_idx] = True
             self._ev.append(("frame", self.ids[idx].copy(), t, feats.copy(), is_new[idx]))
         new_ids = self.ids[new_idx]
-        # 6./7. frame t-1: its scale LM (front end, beside its BA), then its BA applied
-        self._complete()
+        # 7. frame t-1's BA applied
+        done = self._complete_ba()
         # pose(t) again from the refined poses; the new landmarks of t keep their camera-frame coordinates
         pose2 = self._predict_pose(t)
         if not np.array_equal(pose2, pose) and len(new_ids):
@@ -939,6 +988,8 @@ class WindowedStereoVO:
         self._scale_args = (t, imgs, fid.copy())
         self._pending = (t, n_tracked, len(new_idx), int(self.active.sum()), ba)
         self.prev_imgs, self.prev_t = imgs, t
+        # 9. frame t-1's FrameResult (its scale LM result), while BA(t) runs
+        self._complete_result(done)
         self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
 
     def finish(self):
@@ -948,20 +999,28 @@ class WindowedStereoVO:
         w0 = self.stage_s["wait"]
         if self._pending is not None:
             self._pop(self._pending[0] + 1 - self.cfg.window)
-        self._complete()
+        if self._scale_args is not None:
+            self._scale_submit(*self._scale_args)
+            self._scale_args = None
+        self._complete_result(self._complete_ba())
         self.stage_s["host"] += (time.perf_counter() - t_in) - (self.stage_s["wait"] - w0)
 
-    def _complete(self):
-        """Frame t-1 (the pending one): scale LM, then its BA result applied
-        and its FrameResult (its pops ran before the next keyframe's matching)."""
+    def _complete_ba(self):
+        """Frame t-1 (the pending one): its BA result applied (its pops ran
+        before the next keyframe's matching, its scale LM is queued)."""
         if self._pending is None:
-            return
+            return None
         t, n_tracked, n_new, n_active, ba = self._pending
         self._pending = None
-        self._scale_submit(*self._scale_args)
-        self._scale_args = None
-        sc = self._wait(self.be.scale_result)
         nwp, nwo, bs = self._ba_finish(ba)
+        return (t, n_tracked, n_new, n_active, nwp, nwo, bs)
+
+    def _complete_result(self, done):
+        """Frame t-1's FrameResult: its scale LM result and its BA summary."""
+        if done is None:
+            return
+        t, n_tracked, n_new, n_active, nwp, nwo, bs = done
+        sc = self._wait(self.be.scale_result)
         self.results.append(FrameResult(t, n_tracked, n_new, n_active, nwp, nwo, sc["scale"], int(sc["stop"]),
                                         int(sc["iterations"]), int(bs["iterations"]), float(bs["final_cost"]),
                                         self.poses[t].copy()))
