@@ -235,6 +235,39 @@ __device__ __forceinline__ void drain_and_barrier() {
 // ---------------------------------------------------------------- kernels
 constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups over the CUs
 
+// One observation's linearisation (Huber-corrected residual and Jacobians ->
+// V_o | g_o at its CSR slot, W_o when its camera is variable); returns the
+// cost term.  (Measured and dropped: the point step linearising speculatively
+// at its candidate into a second obsx / Wo set, which removes the linearize
+// launch of every accepted step -- the step went 15.1 -> 28.7 us for 9.3 us
+// saved, config 3 BA 0.821 -> 0.894 ms.)
+__device__ __forceinline__ double lin_store(const Geo& g, double* obsx, double* Wo, long slot, bool var_cam,
+                                            double* r, double* Jc, double* Jp) {
+  const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+  double rho0, sc;
+  huber(s, &rho0, &sc);
+  for (int k = 0; k < 4; ++k) r[k] *= sc;
+  for (int k = 0; k < 24; ++k) Jc[k] *= sc;
+  for (int k = 0; k < 12; ++k) Jp[k] *= sc;
+  double* X = obsx + slot * kObsxStride;
+  X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
+  X[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
+  X[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
+  X[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
+  X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
+  X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
+  for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
+  // (the camera normal-equation pieces are formed by cam_assemble from the
+  // same residual and Jacobian: no 216 B per observation through HBM)
+  if (var_cam) {
+    double* W = Wo + 18 * slot;
+    for (int a = 0; a < 6; ++a)
+      for (int c = 0; c < 3; ++c)
+        W[a * 3 + c] = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
+  }
+  return 0.5 * rho0;
+}
+
 // Per observation: corrected residual / Jacobian, cost, and the unscaled
 // per-observation normal-equation pieces W_o = Jc^T Jp (6x3), V_o = Jp^T Jp
 // (6 unique), g_o = Jp^T r, so the per-point stage only sums.
@@ -259,30 +292,7 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
     const int ci = b.cam_idx[o], pi = b.pt_idx[o];
     double r[4], Jc[24], Jp[12];
     obs_residual<OD>(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
-    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
-    double rho0, sc;
-    huber(s, &rho0, &sc);
-    cost = 0.5 * rho0;
-    for (int k = 0; k < 4; ++k) r[k] *= sc;
-    for (int k = 0; k < 24; ++k) Jc[k] *= sc;
-    for (int k = 0; k < 12; ++k) Jp[k] *= sc;
-    const long slot = b.pos[o];  // CSR-by-point slot: per-point stages read contiguously
-    double* X = b.obsx + slot * kObsxStride;
-    X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
-    X[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
-    X[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
-    X[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
-    X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
-    X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
-    for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
-    // (the camera normal-equation pieces are formed by cam_assemble from the
-    // same residual and Jacobian: no 216 B per observation through HBM)
-    if (ci - g.nf >= 0) {
-      double* W = b.Wo + 18 * slot;
-      for (int a = 0; a < 6; ++a)
-        for (int c = 0; c < 3; ++c)
-          W[a * 3 + c] = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
-    }
+    cost = lin_store(g, b.obsx, b.Wo, b.pos[o], ci - g.nf >= 0, r, Jc, Jp);
   }
   double v[1] = {cost};
   double out[1];
@@ -578,6 +588,8 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
 #endif
   SCHUR_T(0);
   const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
+  const double* obsx = b.obsx;
+  const double* Wo = b.Wo;
   const double radius = st->radius;
   // all allowed steps taken: this pass only evaluates the gradient for the
   // closing test (Ceres HandleSuccessfulStep); no Schur complement is needed
@@ -634,9 +646,9 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         if (q0 > beg) cprev0 = b.p_cam[q0 - 1];
         if (q0 + 1 < end) cnext0 = b.p_cam[q0 + 1];  // duplicate test of phase B, requested with the rest
         if (need_lin)
-          for (int i = 0; i < 9; ++i) X0[i] = b.obsx[(long)q0 * kObsxStride + i];
+          for (int i = 0; i < 9; ++i) X0[i] = obsx[(long)q0 * kObsxStride + i];
         if (ci0 >= 0) {
-          for (int i = 0; i < 18; ++i) w0[i] = b.Wo[18 * (long)q0 + i];
+          for (int i = 0; i < 18; ++i) w0[i] = Wo[18 * (long)q0 + i];
           for (int a = 0; a < 6; ++a) cs0[a] = b.csc[6 * ci0 + a];
         }
       }
@@ -648,7 +660,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         double V[9];  // V_o (6 unique) | g_o (3)
         for (int i = 0; i < 9; ++i) V[i] = X0[i];
         for (int q = q0 + SL; q < end; q += SL)
-          for (int i = 0; i < 9; ++i) V[i] += b.obsx[(long)q * kObsxStride + i];
+          for (int i = 0; i < 9; ++i) V[i] += obsx[(long)q * kObsxStride + i];
         SCHUR_T(1);  // loads of phase A issued and returned (first use)
       for (int i = 0; i < 9; ++i) V[i] = group_sum<SL>(V[i]);
         if (!scaled) {
@@ -713,7 +725,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
           ci = b.p_cam[q];
           cp = b.p_cam[q - 1];
           if (ci >= 0) {
-            for (int i = 0; i < 18; ++i) w[i] = b.Wo[18 * (long)q + i];
+            for (int i = 0; i < 18; ++i) w[i] = Wo[18 * (long)q + i];
             for (int a = 0; a < 6; ++a) cs[a] = b.csc[6 * ci + a];
           }
         }
@@ -723,7 +735,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         if (cp == ci) continue;  // not the first slot of its camera run
         if (q != q0 || cnext0 == ci)  // (the first slot's next camera came with phase A's loads)
           for (int r = q + 1; r < end && b.p_cam[r] == ci; ++r)
-            for (int i = 0; i < 18; ++i) w[i] += b.Wo[18 * (long)r + i];
+            for (int i = 0; i < 18; ++i) w[i] += Wo[18 * (long)r + i];
         for (int a = 0; a < 6; ++a) {
           const int col = 6 * ci + a;
           const double wa[3] = {w[3 * a] * cs[a] * pv[0], w[3 * a + 1] * cs[a] * pv[1], w[3 * a + 2] * cs[a] * pv[2]};
@@ -1400,6 +1412,32 @@ constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 #ifndef ME_SOLVE_PIPE
 #define ME_SOLVE_PIPE 1
 #endif
+#ifndef ME_SOLVE_BWD1
+// LDS form without ME_SOLVE_INVE: backward solve on wave 0, u in registers
+// (0: all waves, two barriers per block).  Measured: 4.7 vs 3.8 us; off.
+#define ME_SOLVE_BWD1 0
+#endif
+#ifndef ME_SOLVE_INVE
+// LDS form: the worker waves accumulate E = L^-T in the (otherwise unused)
+// upper block triangle during the factorisation, so the backward solve is
+// one product y = E z (see the kPipe loop).  Measured (config 3 stamps):
+// backward 3.78 -> 1.45 us, but wave 0's panels 4.22 -> 5.59 and the step
+// barriers 1.60 -> 2.87 us (the workers' extra tiles), +1.2 us for E's last
+// column: 37.0 vs 35.5 us per solve; off.
+#define ME_SOLVE_INVE 0
+#endif
+#ifndef ME_SOLVE_PANEL_REG
+// wave 0's panel tile kept in registers for the diagonal update (0: through
+// LDS).  Measured (config 3 stamps): panel 4.23 -> 4.97 us, diagonal 12.50 ->
+// 11.81 us per solve -- no gain; off.
+#define ME_SOLVE_PANEL_REG 0
+#endif
+#ifndef ME_SOLVE_EARLY0
+// fused LDS form: wave 0 copies rows 0-15 itself and factors block 0 while
+// the rest arrives.  Measured: no gain (one wave's 17 KiB copy takes as long
+// as the whole 133 KiB over eight waves, 2.5 us); off.
+#define ME_SOLVE_EARLY0 0
+#endif
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
 constexpr int kSolveMwMinTs = 16;             // block steps from which the trailing workers are used
 
@@ -1575,6 +1613,33 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
   }
 }
 
+// Diagonal block Jd of the LDS-resident system on one wave, from its updated
+// values in the accumulator layout (lane l, register r: row (l >> 4) + 4 r,
+// column l & 15); false on a non-positive pivot.
+__device__ __forceinline__ bool diag_factor_wave(double* A, int ld, double* X, double* xch, int n, int Jd,
+                                                 double4_t A4, int lane) {
+  const int jd0 = 16 * Jd;
+  double* Ablk = A + (long)jd0 * ld + jd0;
+  double* XJw = X + 256 * Jd;
+  const int q = lane >> 4, c = lane & 15;
+  bool ok = true;
+  double4_t Y4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+  diag_round_mfma<0>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+  diag_round_mfma<1>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+  diag_round_mfma<2>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+  diag_round_mfma<3>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
+  return ok;
+}
+__device__ __forceinline__ double4_t diag_load_wave(const double* A, int ld, int Jd, int lane) {
+  const double* Ablk = A + (long)(16 * Jd) * ld + 16 * Jd;
+  double4_t A4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) A4[r] = Ablk[((lane >> 4) + 4 * r) * ld + (lane & 15)];
+  return A4;
+}
+
 // kMode: 0 = [S; -b^T] in LDS, one workgroup; 1 = in global memory, one workgroup;
 // 2 = in global memory, trailing updates on `nworkers` more workgroups (sc1 hand-offs)
 template <int kMode>
@@ -1598,6 +1663,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   constexpr bool kLook = ME_DIAG_MFMA && ME_SOLVE_LOOKAHEAD && kMode != 2;
   // LDS-resident system: wave 0 alone on the critical path (see below)
   constexpr bool kPipe = kLook && kLds && ME_SOLVE_PIPE;
+  constexpr bool kInvE = kPipe && ME_SOLVE_INVE;
   __shared__ unsigned pflag, pdone;
   // Measured and dropped (config 3): panel fused with the column-(J+1) update
   // in one phase (transposed panel tiles as MFMA operands, no barrier between;
@@ -1700,13 +1766,19 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
   const double* S0 = b.S;
   const int nn = n * n;
+  const bool early0 = kPipe && ME_SOLVE_EARLY0 && fused;
   if (kLds && fused) {
     // the assemblers wrote the solver's image (s_assemble_body img): N x ld
     // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
     // coherent reads (sc1); the barrier below retires them (vmcnt)
+    // (early0: wave 0 takes the chunks of rows 0-15 -- diagonal block 0 --
+    // and the other waves the rest, round-robin)
     const int nbytes = N * ld * 8, nchunk = (nbytes + 1023) >> 10;
+    const int c0 = early0 ? (16 * ld * 8 + 1023) >> 10 : 0;
+    const int kb = early0 ? (wave == 0 ? 0 : c0 + wave - 1) : wave;
+    const int ke = early0 && wave == 0 ? c0 : nchunk, ks = early0 ? (wave == 0 ? 1 : nw - 1) : nw;
     if (!done)
-      for (int k = wave; k < nchunk; k += nw) {
+      for (int k = kb; k < ke; k += ks) {
         const int off = (k << 10) + 16 * lane;
         if (off < nbytes)
           __builtin_amdgcn_global_load_lds((const void*)((const char*)b.Abuf + off),
@@ -1763,6 +1835,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     pflag = 0u;
     pdone = 0u;
   }
+  if (early0 && wave == 0) {  // block 0 from wave 0's own copies, beside the other waves' copies
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    if (!diag_factor_wave(A, ld, X, xch, n, 0, diag_load_wave(A, ld, 0, lane), lane)) sfail = 1;
+  }
   if ((skip & 256) && tid == 0) st->stamps[15] += 1;
   SOLVE_START(0);
   __syncthreads();
@@ -1787,26 +1863,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     const int widx = wave - 1 - (nw > 4 && wave > 4 ? 1 : 0);
     // diagonal block Jd from its (updated) values in the accumulator layout
     auto diag_factor = [&](int Jd, double4_t A4) {
-      const int jd0 = 16 * Jd;
-      double* Ablk = A + (long)jd0 * ld + jd0;
-      double* XJw = X + 256 * Jd;
-      const int q = lane >> 4, c = lane & 15;
-      bool ok = true;
-      double4_t Y4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
-      diag_round_mfma<0>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
-      diag_round_mfma<1>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
-      diag_round_mfma<2>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
-      diag_round_mfma<3>(A4, Y4, q, c, n - jd0, ok, Ablk, ld, XJw, xch);
-      if (!ok) sfail = 1;  // benign race: every writer stores 1
-    };
-    auto diag_block = [&](int Jd) {
-      const double* Ablk = A + (long)(16 * Jd) * ld + 16 * Jd;
-      double4_t A4;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) A4[r] = Ablk[((lane >> 4) + 4 * r) * ld + (lane & 15)];
-      diag_factor(Jd, A4);
+      if (!diag_factor_wave(A, ld, X, xch, n, Jd, A4, lane)) sfail = 1;  // benign race: every writer stores 1
     };
     auto panel_tile = [&](int J, int I) {  // L_IJ = A_IJ X_J^T on the matrix cores
       const int j0 = 16 * J, i0 = 16 * I;
@@ -1823,6 +1880,37 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) A[(long)(i0 + (lane >> 4) + 4 * q4) * ld + j0 + (lane & 15)] = acc[q4];
     };
+#if ME_SOLVE_PANEL_REG
+    // Wave 0's panel tile of step J, transposed: P = L_{J+1,J}^T = X_J A_{J+1,J}^T
+    // (the operands of panel_tile swapped: the same products and K order, so
+    // the same bits).  In the accumulator layout (lane l, register s holds
+    // P[(l >> 4) + 4 s][l & 15]) P is already both MFMA operands of K-step s
+    // of the diagonal update A_{J+1,J+1} - P^T P: no LDS round trip between
+    // the panel and the factorisation on the critical path.  L_{J+1,J} is
+    // stored (transposed) for the other waves.
+    auto panel_diag = [&](int J) -> double4_t {
+      const int j0 = 16 * J, i0 = 16 * (J + 1);
+      const double* XJ = X + 256 * J;
+      double av[4], bv[4];
+      double4_t D;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        av[s4] = XJ[(lane & 15) * 16 + 4 * s4 + (lane >> 4)];
+        bv[s4] = A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)];
+        D[s4] = A[(long)(i0 + (lane >> 4) + 4 * s4) * ld + i0 + (lane & 15)];
+      }
+      double4_t P = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) P = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], P, 0, 0, 0);
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) A[(long)(i0 + (lane & 15)) * ld + j0 + (lane >> 4) + 4 * q4] = P[q4];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) pflag = (unsigned)(J + 1);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) D = __builtin_amdgcn_mfma_f64_16x16x4f64(-P[s4], P[s4], D, 0, 0, 0);
+      return D;
+    };
+#endif
     auto lds_wait = [&](volatile unsigned* f, unsigned want) {
       long k = 0;
       for (; k < kSolveSpin && *f < want; ++k) __builtin_amdgcn_s_sleep(1);
@@ -1832,32 +1920,72 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
-    if (wave == 0) diag_block(0);
-    STS(19);
-    __syncthreads();
+    if (!early0) {
+      if (wave == 0) diag_factor(0, diag_load_wave(A, ld, 0, lane));
+      STS(19);
+      __syncthreads();
+    }
     for (int J = 0; J + 1 < Ts; ++J) {
       if (sfail) break;
       STS(18);
       if (wave == 0) {
-        panel_tile(J, J + 1);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) pflag = (unsigned)(J + 1);
         // step J on the diagonal tile, handed to the factorisation in registers
         // (its updated values are read by no one else: the factorisation
         // overwrites the lower triangle with L, the upper one is never read)
+#if ME_SOLVE_PANEL_REG
+        const double4_t D = panel_diag(J);
+        STS(16);
+        diag_factor(J + 1, D);
+#else
+        panel_tile(J, J + 1);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) pflag = (unsigned)(J + 1);
         solve_wave_sync();  // the panel tile just stored is an operand
         STS(16);
         diag_factor(J + 1, trailing_diag_acc(A, ld, J, J + 1, lane));
+#endif
         STS(17);
       } else if (worker) {
         for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
+        if (kInvE)  // E panel tiles E_IJ = B_IJ X_J^T, I < J (B: E's rows before step J)
+          for (int I = (widx + nwk - (Ts - J - 2) % nwk) % nwk; I < J; I += nwk) panel_tile(J, I);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) atomicAdd(&pdone, 1u);
         lds_wait(&pflag, (unsigned)(J + 1));
         for (int I = J + 2 + widx; I < Ts; I += nwk) trailing_tile<false>(A, ld, J, I, J + 1, lane);
         lds_wait(&pdone, (unsigned)(nwk * (J + 1)));
         trailing_split<false>(A, ld, Ts, J, false, widx, nwk, lane);  // tiles (I, K), J + 2 <= K <= I
+        if (kInvE) {
+          // E's trailing tiles of step J: E_IK -= E_IJ L_KJ^T, I <= J < K
+          // (I = J: E_JJ = X_J^T, and E_JK starts from 0), continuing the
+          // round-robin of the tiles above
+          const int rem = Ts - J - 1, ntr = rem * (rem - 1) / 2, cnt = (J + 1) * rem;
+          for (int p = (widx + nwk - ntr % nwk) % nwk; p < cnt; p += nwk) {
+            const int I = p / rem, K = J + 1 + p % rem;
+            if (I < J) {
+              trailing_tile<false>(A, ld, J, I, K, lane);
+            } else {
+              const int j0 = 16 * J, k0 = 16 * K;
+              const double* XJ = X + 256 * J;
+              double av[4], bv[4];
+              double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+              for (int s4 = 0; s4 < 4; ++s4) {
+                av[s4] = -XJ[(4 * s4 + (lane >> 4)) * 16 + (lane & 15)];
+                bv[s4] = A[(long)(k0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)];
+              }
+#pragma unroll
+              for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+#pragma unroll
+              for (int q4 = 0; q4 < 4; ++q4) A[(long)(j0 + (lane >> 4) + 4 * q4) * ld + k0 + (lane & 15)] = acc[q4];
+            }
+          }
+        }
       }
+      __syncthreads();
+    }
+    if (kInvE && !sfail) {  // E's last block column, once X_{Ts-1} is formed
+      for (int I = wave; I < Ts - 1; I += nw) panel_tile(Ts - 1, I);
       __syncthreads();
     }
   } else
@@ -1983,8 +2111,91 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     return;
   }
   SOLVE_START(5);
-  // backward solve L^T y = z (z = row n of L), block by block: wave 0 forms
-  // y_J = X_J^T z_J, then every wave updates the entries above the block
+  // backward solve L^T y = z (z = row n of L), block by block.
+  // LDS form (ME_SOLVE_BWD1; Ts <= 8 there, so N <= 128): wave 0 alone, no
+  // workgroup barrier, u in registers -- lane l holds u[l] and u[l + 64].
+  // Per block J: r_J is broadcast from its 16 lanes (readlane), each lane
+  // forms y_J[l & 15] = (X_J^T r_J)[l & 15], y_J is broadcast back, and every
+  // lane subtracts L_{J,K}^T y_J from its own entries below j0 (L rows of
+  // block J, requested before the chain needs them).  (A left-looking form on
+  // wave 0, LDS-resident u: 6.07 vs 3.82 us.)  Otherwise wave 0 forms y_J =
+  // X_J^T z_J and every wave updates the entries above the block (two
+  // barriers per block).
+  if (kInvE) {
+    // y = E z, E = L^-T (upper block triangle of A; diagonal blocks X_J^T),
+    // z = row n of A: four lanes per row, strided over the columns
+    const int i = tid >> 2, gq = tid & 3;
+    double a0 = 0.0, a1 = 0.0;
+    if (i < n && !(skip & 8)) {
+      const int i0 = i & ~15;
+      const double* XJ = X + 16 * i0;  // X_J, J = i >> 4 (256 doubles per block)
+      const double* zr = A + (long)n * ld;
+      int j = i + gq;
+      for (; j < i0 + 16 && j < n; j += 4) a0 = fma(XJ[(j - i0) * 16 + (i - i0)], zr[j], a0);
+      for (; j + 4 < n; j += 8) {
+        a0 = fma(A[(long)i * ld + j], zr[j], a0);
+        a1 = fma(A[(long)i * ld + j + 4], zr[j + 4], a1);
+      }
+      if (j < n) a0 = fma(A[(long)i * ld + j], zr[j], a0);
+    }
+    double acc = a0 + a1;
+    acc += __shfl_xor(acc, 1, 64);
+    acc += __shfl_xor(acc, 2, 64);
+    if (gq == 0 && i < N) u[i] = i < n ? acc : 0.0;
+    for (int c = (nt >> 2) + tid; c < N; c += nt) u[c] = 0.0;  // (N > nt / 4: not in the LDS form)
+    __syncthreads();
+  } else if (kLds && ME_SOLVE_BWD1) {
+    if (wave == 0) {
+      const int t = lane & 15;
+      double u0 = lane < n ? A[(long)n * ld + lane] : 0.0;
+      double u1 = lane + 64 < n ? A[(long)n * ld + lane + 64] : 0.0;
+      for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
+        const int j0 = 16 * J, base = j0 & 63;
+        const double* XJ = X + 256 * J;
+        double xm[16], l0[16], l1[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) xm[m] = XJ[m * 16 + t];
+        if (j0 > 0) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) l0[m] = A[(long)(j0 + m) * ld + lane];
+        }
+        if (j0 > 64) {
+#pragma unroll
+          for (int m = 0; m < 16; ++m) l1[m] = A[(long)(j0 + m) * ld + lane + 64];
+        }
+        const double rj = j0 >= 64 ? u1 : u0;
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int m = 0; m < 16; ++m) s4[m & 3] = fma(xm[m], lane_read(rj, base + m), s4[m & 3]);
+        double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        s = j0 + t < n ? s : 0.0;
+        if (lane >= base && lane < base + 16) {
+          if (j0 >= 64)
+            u1 = s;
+          else
+            u0 = s;
+        }
+        if (j0 > 0) {
+          double y[16];
+#pragma unroll
+          for (int m = 0; m < 16; ++m) y[m] = lane_read(s, m);
+          double a4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int m = 0; m < 16; ++m) a4[m & 3] = fma(l0[m], y[m], a4[m & 3]);
+          if (lane < j0) u0 -= (a4[0] + a4[1]) + (a4[2] + a4[3]);
+          if (j0 > 64) {
+            double b4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int m = 0; m < 16; ++m) b4[m & 3] = fma(l1[m], y[m], b4[m & 3]);
+            if (lane + 64 < j0) u1 -= (b4[0] + b4[1]) + (b4[2] + b4[3]);
+          }
+        }
+      }
+      if (lane < N) u[lane] = u0;
+      if (lane + 64 < N) u[lane + 64] = u1;
+    }
+    __syncthreads();
+  } else {
   for (int c = tid; c < N; c += nt) u[c] = c < n ? a_ld<kSc1>(&A[(long)n * ld + c]) : 0.0;
   __syncthreads();
   for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
@@ -2016,6 +2227,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
     }
     __syncthreads();
+  }
   }
   SOLVE_STAMP(5);
   STS(5);
@@ -2183,6 +2395,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     // any arithmetic; further slots (points with more than 16 observations)
     // load in the loops.
     const int cur = st->cur;
+    const double* Wo = b.Wo;
     double psv[3], gpv[3], Lv[9], xv[3], Vv[9];
     for (int a = 0; a < 3; ++a) {
       psv[a] = b.psc[3 * (long)j + a];
@@ -2201,7 +2414,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     if (has0) {
       ci0 = b.p_cam[q0];
       o0 = b.p_obs[q0];
-      for (int i = 0; i < 18; ++i) W0[i] = b.Wo[18 * (long)q0 + i];  // (unused for a fixed camera)
+      for (int i = 0; i < 18; ++i) W0[i] = Wo[18 * (long)q0 + i];  // (unused for a fixed camera)
     }
     const double* cams_c = b.cams[1 - cur];
     double ys0[6], f0[4];
@@ -2228,7 +2441,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
         for (int i = 0; i < 18; ++i) W[i] = W0[i];
       } else {
         for (int a = 0; a < 6; ++a) ys[a] = b.csc[6 * ci + a] * b.yc[6 * ci + a];
-        for (int i = 0; i < 18; ++i) W[i] = b.Wo[18 * (long)q + i];
+        for (int i = 0; i < 18; ++i) W[i] = Wo[18 * (long)q + i];
       }
       for (int c = 0; c < 3; ++c) {
         double s = 0;
