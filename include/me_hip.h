@@ -307,6 +307,37 @@ int me_ba_solve(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_ba_sum
    readable by me_ba_wait). */
 int me_ba_solve_async(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o);
 int me_ba_wait(me_ctx* ctx, me_ba_summary* s);
+/* me_ba_wait, and for a device-resident problem (ME_DEVICE) its solved cams
+   (6 per camera) / pts (3 per point) copied to host arrays (either may be
+   NULL): read back behind the solve, so the wait does not block on work
+   queued after it. */
+int me_ba_wait_out(me_ctx* ctx, me_ba_summary* s, double* cams, double* pts);
+/* Sizes the ctx's BA scratch and page-locked staging (synchronous and both
+   asynchronous sets) for windows up to these sizes, so a growing window does
+   not reallocate (a reallocation waits for the ctx stream).  No solve may be
+   queued. */
+int me_ba_reserve(me_ctx* ctx, int n_cams, int n_pts, int n_obs, int obs_dim, int fixed_frames);
+/* Windowed VO loop (pipeline.py WindowedStereoVO.process, step 7), no
+   counterpart in the reference (whose loop solves each window before the
+   next keyframe, WBA_Point / BundleAdjuster.h): window t's BA start formed on
+   the device from the last queued device-resident solve (window t-1) before
+   that solve completes.  cams (n_cams x 6) / pts (n_pts x 3), device memory,
+   hold the host's values (the loop state before window t-1's result); camera
+   k / landmark i with cam_src / pt_src >= 0 take that solve's camera / point
+   at the source index when it succeeded (termination != FAILURE); pt_src -2:
+   a landmark new in keyframe t, moved from pose (rotation R, row-major) to
+   the new pose(t) when they differ; camera n_cams - 1 is pose(t):
+   mode 1: c[k1] + (c[k1] - c[k0]), mode 0: c[k1] + vel, mode -1: kept.  The
+   new pose's rotation is a fixed Taylor series in theta^2 (the loop's host
+   code repeats the arithmetic bit for bit).  Asynchronous on the ctx stream. */
+typedef struct me_vo_chain_args {
+  double pose[6];
+  double R[9];
+  double vel[6];
+  int k1, k0, mode;
+} me_vo_chain_args;
+int me_vo_ba_chain(me_ctx* ctx, double* cams, int n_cams, double* pts, int n_pts, const int32_t* cam_src,
+                   const int32_t* pt_src, const me_vo_chain_args* a);
 /* BundleAdjuster<M>::initialiseObservations (BundleAdjuster.h:354-376) for a
    device-resident window: observation i was seen in frame[i] by the track
    ids[i]; cam_idx[i] = frame[i] - first_frame and pt_idx[i] = the position of

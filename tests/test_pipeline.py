@@ -139,6 +139,41 @@ def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window, n):
 
 
 @pytest.mark.gpu
+def test_pipeline_gpu_chained_equals_unchained(ctx, seq5):
+    """BA(t) queued behind BA(t - 1), its start formed on the device from
+    BA(t - 1)'s result (me_vo_ba_chain: refined poses and landmarks, pose(t)
+    predicted again, t's new landmarks moved), is the state the host forms in
+    step 7: events, poses and landmarks bit for bit against the loop that
+    waits for BA(t - 1) before queueing BA(t)."""
+    runs = []
+    for chain in (True, False):
+        be = PL.GPUBackend(ctx)
+        be.chain_window = chain
+        try:
+            runs.append(_run(5, 24, be, window=8, frames=seq5, overlap=True, ba_iters=10))
+        finally:
+            be.close()
+    a, b = runs
+    assert a.events == b.events and np.array_equal(a.ids, b.ids)
+    assert np.array_equal(a.X, b.X)
+    assert all(np.array_equal(a.poses[t], b.poses[t]) for t in a.poses)
+    assert [r.ba_iters for r in a.results] == [r.ba_iters for r in b.results]
+    assert np.array_equal([r.ba_cost for r in a.results], [r.ba_cost for r in b.results], equal_nan=True)
+
+
+def test_rot_series_equals_rodrigues():
+    """The loop's pose(t) re-prediction rotation (pipeline.rot_series: a
+    Taylor series in theta^2, the device chain's arithmetic) against the
+    closed-form Rodrigues rotation, up to pi."""
+    rng = np.random.default_rng(3)
+    for _ in range(500):
+        a = rng.normal(0, 1.0, 3)
+        a *= min(1.0, np.pi / np.linalg.norm(a))
+        np.testing.assert_allclose(PL.rot_series(a), PL.aa_to_R(a), rtol=0, atol=1e-14)
+    assert np.array_equal(PL.rot_series(np.zeros(3)), np.eye(3))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("unique", [False, True])
 def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
     """me_mi_epipolar_match (device MI scores + FP64 pick) = match_host (MI

@@ -106,6 +106,12 @@ class BASummaryC(ctypes.Structure):
     ]
 
 
+class VOChainArgsC(ctypes.Structure):
+    """me_vo_chain_args (include/me_hip.h)."""
+    _fields_ = [("pose", c_double * 6), ("R", c_double * 9), ("vel", c_double * 6), ("k1", c_int), ("k0", c_int),
+                ("mode", c_int)]
+
+
 class KLTParamsC(ctypes.Structure):
     _fields_ = [("win", c_int), ("max_level", c_int), ("max_iters", c_int), ("eps", c_double),
                 ("min_eig", c_double)]
@@ -123,7 +129,8 @@ EXPORTS = [
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
-    "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_window_indices",
+    "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_wait_out", "me_ba_reserve", "me_ba_window_indices",
+    "me_vo_ba_chain",
     "me_comm_unique_id", "me_comm_create_rccl", "me_comm_create_callback", "me_comm_destroy", "me_comm_info",
     "me_comm_allreduce", "me_ba_solve_comm", "me_ba_shard_worthwhile", "me_ba_shard_exchange_us",
     "me_klt_default_params", "me_klt_track",
@@ -217,6 +224,9 @@ def load_library(path: str = LIB_PATH):
         "me_ba_solve": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), P(BASummaryC)]),
         "me_ba_solve_async": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC)]),
         "me_ba_wait": (c_int, [c_void_p, P(BASummaryC)]),
+        "me_ba_wait_out": (c_int, [c_void_p, P(BASummaryC), c_void_p, c_void_p]),
+        "me_ba_reserve": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
+        "me_vo_ba_chain": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, P(VOChainArgsC)]),
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
         "me_ba_window_indices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                                          c_void_p]),

@@ -3012,6 +3012,8 @@ struct Plan {
   double* host = nullptr;  // pinned staging (inputs in, State / results out)
   State* hstate[2] = {nullptr, nullptr};  // pinned slots of the pipelined State polls
   bool dev = false;        // problem arrays are device-resident
+  bool copy_out = false;   // device-resident problem: the solved cams / pts also staged to the host (me_ba_wait_out)
+  bool reserve_only = false;  // me_ba_reserve: size the scratch and staging, queue nothing
   size_t solve_lds = 0;
   size_t schur_lds = 0;
   int use_lds = 0;
@@ -3237,6 +3239,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     ME_TRY(me_pinned(c, hbytes, &hp));
   }
   P.host = (double*)hp;
+  if (P.reserve_only) return ME_OK;
   P.hstate[0] = (State*)((char*)hp + stage);
   P.hstate[1] = (State*)((char*)hp + stage + rup(sizeof(State), 64));
   P.dev = dev;
@@ -3506,6 +3509,12 @@ int enqueue_output(Plan& P, me_ba_problem* p) {
   ME_TRY(me_check_launch(c, "BA output"));
   const size_t bytes = 8 * (P.dev ? nst : nst + 6 * (size_t)g.nc + 3 * (size_t)g.np);
   ME_HIP(c, hipMemcpyAsync(P.host, P.b.out, bytes, hipMemcpyDeviceToHost, c->stream));
+  if (P.dev && P.copy_out) {  // (staging holds State | cams | pts: out_doubles)
+    ME_HIP(c, hipMemcpyAsync(P.host + nst, p->cams, 8 * 6 * (size_t)g.nc, hipMemcpyDeviceToHost, c->stream));
+    if (g.np)
+      ME_HIP(c, hipMemcpyAsync(P.host + nst + 6 * (size_t)g.nc, p->pts, 8 * 3 * (size_t)g.np, hipMemcpyDeviceToHost,
+                               c->stream));
+  }
   return ME_OK;
 }
 
@@ -3659,6 +3668,7 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   A->prob = *p;
   A->set = Q->n == 0 ? 0 : 1 - Q->q[0]->set;
   int rc = plan_build(c, p, opt, A->P, A->set, A->set);
+  A->P.copy_out = A->P.dev;
   if (rc == ME_OK) {
     for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it)
       rc = enqueue_iteration(A->P, it == opt->max_num_iterations);
@@ -3679,7 +3689,7 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   return ME_OK;
 }
 
-extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) {
+extern "C" int me_ba_wait_out(me_ctx* c, me_ba_summary* s, double* cams, double* pts) {
   me_range range_("me_ba_wait");
   if (!c) return ME_ERR_INVALID;
   auto* Q = (AsyncQueue*)c->ba_async;
@@ -3689,11 +3699,164 @@ extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) {
   ME_TRY(ba_complete_one(c, A));
   const int rc = A->rc;
   if (s && rc == ME_OK) *s = A->sum;
+  if (rc == ME_OK && A->P.dev && (cams || pts)) {  // from the staging (read back behind the solve's event)
+    constexpr size_t nst = sizeof(State) / 8;
+    const Geo& g = A->P.g;
+    if (cams) std::memcpy(cams, A->P.host + nst, 8 * 6 * (size_t)g.nc);
+    if (pts && g.np) std::memcpy(pts, A->P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
+  }
   hipEventDestroy(A->ev);
   delete A;
   for (int i = 1; i < Q->n; ++i) Q->q[i - 1] = Q->q[i];
   Q->q[--Q->n] = nullptr;
   return rc;
+}
+
+extern "C" int me_ba_wait(me_ctx* c, me_ba_summary* s) { return me_ba_wait_out(c, s, nullptr, nullptr); }
+
+extern "C" int me_ba_reserve(me_ctx* c, int n_cams, int n_pts, int n_obs, int obs_dim, int fixed_frames) {
+  me_range range_("me_ba_reserve");
+  if (!c || n_cams < 1 || n_pts < 0 || n_obs < 0) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  auto* Q = (AsyncQueue*)c->ba_async;
+  if (Q && Q->n > 0) return me_set_error(c, ME_ERR_STATE, "me_ba_reserve: asynchronous solves are queued");
+  ME_TRY(ba_drain(c));
+  // a problem of these sizes (no arrays: the plan stops once its memory is sized)
+  static const int32_t zero = 0;
+  me_ba_problem p{};
+  p.n_cams = n_cams;
+  p.n_pts = n_pts;
+  p.n_obs = n_obs;
+  p.obs_dim = obs_dim == 2 ? 2 : 4;
+  p.fixed_frames = fixed_frames;
+  p.mem = ME_DEVICE;
+  p.cam_id = &zero;
+  p.feat_var = 1.0;
+  p.baseline = 1.0;
+  const double K[9] = {1, 0, 1, 0, 1, 1, 0, 0, 1};
+  std::memcpy(p.K0, K, sizeof(K));
+  std::memcpy(p.K1, K, sizeof(K));
+  me_ba_options o;
+  me_ba_default_options(&o);
+  for (int set = 0; set < kBaQueue; ++set) {  // the asynchronous solves' two sets
+    Plan P;
+    P.reserve_only = true;
+    ME_TRY(plan_build(c, &p, &o, P, set, set));
+  }
+  Plan P;  // and the synchronous one
+  P.reserve_only = true;
+  return plan_build(c, &p, &o, P, 0);
+}
+
+// ---------------------------------------------------------------- VO chain
+// The windowed VO loop (pipeline.py, WindowedStereoVO.process step 7) forms
+// window t's BA start from window t-1's BA result: the poses and landmarks it
+// solved (when it succeeded, BundleAdjuster status 2), pose(t) predicted again
+// from the refined poses, and the landmarks new in t moved with it (their
+// camera-frame coordinates kept).  On the device the same arithmetic, in the
+// same order (fp-contract off; the rotation of the new pose by a fixed Taylor
+// series in theta^2: no libm), runs behind window t-1's solve, so window t is
+// queued before t-1 completes; the host repeats it on the downloaded result
+// (pipeline.rot_series, bit for bit).
+namespace {
+__device__ __constant__ double kRotA[24] = {
+    1.0, -0.16666666666666666, 0.008333333333333333, -0.0001984126984126984, 2.7557319223985893e-06,
+    -2.505210838544172e-08, 1.6059043836821613e-10, -7.647163731819816e-13, 2.8114572543455206e-15,
+    -8.22063524662433e-18, 1.9572941063391263e-20, -3.868170170630684e-23, 6.446950284384474e-26,
+    -9.183689863795546e-29, 1.1309962886447716e-31, -1.216125041553518e-34, 1.151633562077195e-37,
+    -9.67759295863189e-41, 7.265460179153071e-44, -4.902469756513544e-47, 2.9893108271424046e-50,
+    -1.6552108677421951e-53, 8.359650847182804e-57, -3.866628513960594e-60};  // (-1)^k / (2k+1)!
+__device__ __constant__ double kRotB[24] = {
+    0.5, -0.041666666666666664, 0.001388888888888889, -2.48015873015873e-05, 2.755731922398589e-07,
+    -2.08767569878681e-09, 1.1470745597729725e-11, -4.779477332387385e-14, 1.5619206968586225e-16,
+    -4.110317623312165e-19, 8.896791392450574e-22, -1.6117375710961184e-24, 2.4795962632247976e-27,
+    -3.279889237069838e-30, 3.7699876288159054e-33, -3.8003907548547434e-36, 3.387157535521162e-39,
+    -2.6882202662866363e-42, 1.911963205040282e-45, -1.2256174391283858e-48, 7.117406731291439e-52,
+    -3.7618428812322616e-55, 1.817315401561479e-58, -8.055476070751236e-62};  // (-1)^k / (2k+2)!
+
+// R = I + A [a]x + B [a]x^2, A = sin(th) / th, B = (1 - cos th) / th^2, th = |a|
+__device__ void rot_series(const double* a, double* R) {
+  const double t2 = (a[0] * a[0] + a[1] * a[1]) + a[2] * a[2];
+  double A = kRotA[23], B = kRotB[23];
+  for (int k = 22; k >= 0; --k) {
+    A = A * t2 + kRotA[k];
+    B = B * t2 + kRotB[k];
+  }
+  const double K[9] = {0.0, -a[2], a[1], a[2], 0.0, -a[0], -a[1], a[0], 0.0};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double k2 = a[i] * a[j] - (i == j ? t2 : 0.0);
+      R[3 * i + j] = ((i == j ? 1.0 : 0.0) + A * K[3 * i + j]) + B * k2;
+    }
+}
+
+// One launch over the window's landmarks; every workgroup forms pose(t)
+// itself, workgroup 0 also writes the cameras.  A camera / landmark with a
+// source index takes the previous solve's value when that solve succeeded,
+// else keeps the host's (the loop's state before the solve); pt_src -2 marks a
+// landmark new in t (moved when pose(t) changed).
+__global__ __launch_bounds__(256) void vo_chain_kernel(const double* pc, const double* pp, const State* pst, double* cams,
+                                                       int nc, double* pts, int np, const int* cam_src,
+                                                       const int* pt_src, me_vo_chain_args a) {
+  __shared__ double sh[6 + 9];  // pose(t) | its rotation
+  const bool ok = pst->termination != 2;
+  auto cam = [&](int k, int j) {
+    const int s = cam_src[k];
+    return ok && s >= 0 ? pc[6 * s + j] : cams[6 * k + j];
+  };
+  if (threadIdx.x == 0) {
+    double p2[6];
+    for (int j = 0; j < 6; ++j) {
+      const double c1 = cam(a.k1, j);
+      p2[j] = a.mode == 1 ? c1 + (c1 - cam(a.k0, j)) : a.mode == 0 ? c1 + a.vel[j] : cams[6 * (nc - 1) + j];
+    }
+    for (int j = 0; j < 6; ++j) sh[j] = p2[j];
+    rot_series(p2 + 3, sh + 6);
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {  // (formed in LDS first: cam() reads the fallbacks in place)
+    extern __shared__ double scam[];
+    for (int e = threadIdx.x; e < 6 * nc; e += blockDim.x) scam[e] = e >= 6 * (nc - 1) ? sh[e % 6] : cam(e / 6, e % 6);
+    __syncthreads();
+    for (int e = threadIdx.x; e < 6 * nc; e += blockDim.x) cams[e] = scam[e];
+  }
+  bool moved = false;
+  for (int j = 0; j < 6; ++j) moved = moved || sh[j] != a.pose[j];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= np) return;
+  const int s = pt_src[i];
+  double* X = pts + 3 * (long)i;
+  if (s >= 0) {
+    if (ok)
+      for (int k = 0; k < 3; ++k) X[k] = pp[3 * (long)s + k];
+  } else if (s == -2 && moved) {
+    const double* R = a.R;
+    const double* R2 = sh + 6;
+    double d[3];
+    for (int k = 0; k < 3; ++k) d[k] = (((X[0] * R[3 * k] + X[1] * R[3 * k + 1]) + X[2] * R[3 * k + 2]) + a.pose[k]) - sh[k];
+    double y[3];
+    for (int k = 0; k < 3; ++k) y[k] = (d[0] * R2[k] + d[1] * R2[3 + k]) + d[2] * R2[6 + k];
+    for (int k = 0; k < 3; ++k) X[k] = y[k];
+  }
+}
+}  // namespace
+
+extern "C" int me_vo_ba_chain(me_ctx* c, double* cams, int n_cams, double* pts, int n_pts, const int32_t* cam_src,
+                              const int32_t* pt_src, const me_vo_chain_args* a) {
+  me_range range_("me_vo_ba_chain");
+  if (!c || !a || n_cams < 1 || n_pts < 0 || !cams || !cam_src || (n_pts && (!pts || !pt_src))) return ME_ERR_INVALID;
+  if (a->mode >= 0 && (a->k1 < 0 || a->k1 >= n_cams - 1 || (a->mode == 1 && (a->k0 < 0 || a->k0 >= n_cams - 1))))
+    return me_set_error(c, ME_ERR_INVALID, "me_vo_ba_chain: prediction cameras %d, %d outside the window's first %d",
+                        a->k1, a->k0, n_cams - 1);
+  auto* Q = (AsyncQueue*)c->ba_async;
+  if (!Q || Q->n == 0) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: no queued BA solve to chain from");
+  AsyncSolve* A = Q->q[Q->n - 1];
+  if (!A->P.dev) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: the queued solve is not device-resident");
+  ME_HIP(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(vo_chain_kernel, dim3(blocks(std::max(n_pts, 1), 256)), dim3(256), 48 * (size_t)n_cams, c->stream,
+                     A->prob.cams,
+                     A->prob.pts, A->P.b.st, cams, n_cams, pts, n_pts, (const int*)cam_src, (const int*)pt_src, *a);
+  return me_check_launch(c, "me_vo_ba_chain");
 }
 
 extern "C" void me_ba_default_options(me_ba_options* o) {

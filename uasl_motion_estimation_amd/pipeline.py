@@ -63,6 +63,50 @@ def R_to_quat(R):
     return S.R_to_quat(R)
 
 
+# (-1)^k / (2k+1)! and (-1)^k / (2k+2)!: the same literals as vo_chain_kernel (csrc/ba.hip)
+_ROT_A = (1.0, -0.16666666666666666, 0.008333333333333333, -0.0001984126984126984, 2.7557319223985893e-06,
+          -2.505210838544172e-08, 1.6059043836821613e-10, -7.647163731819816e-13, 2.8114572543455206e-15,
+          -8.22063524662433e-18, 1.9572941063391263e-20, -3.868170170630684e-23, 6.446950284384474e-26,
+          -9.183689863795546e-29, 1.1309962886447716e-31, -1.216125041553518e-34, 1.151633562077195e-37,
+          -9.67759295863189e-41, 7.265460179153071e-44, -4.902469756513544e-47, 2.9893108271424046e-50,
+          -1.6552108677421951e-53, 8.359650847182804e-57, -3.866628513960594e-60)
+_ROT_B = (0.5, -0.041666666666666664, 0.001388888888888889, -2.48015873015873e-05, 2.755731922398589e-07,
+          -2.08767569878681e-09, 1.1470745597729725e-11, -4.779477332387385e-14, 1.5619206968586225e-16,
+          -4.110317623312165e-19, 8.896791392450574e-22, -1.6117375710961184e-24, 2.4795962632247976e-27,
+          -3.279889237069838e-30, 3.7699876288159054e-33, -3.8003907548547434e-36, 3.387157535521162e-39,
+          -2.6882202662866363e-42, 1.911963205040282e-45, -1.2256174391283858e-48, 7.117406731291439e-52,
+          -3.7618428812322616e-55, 1.817315401561479e-58, -8.055476070751236e-62)
+
+
+def rot_series(aa):
+    """Angle-axis -> rotation, R = I + A [a]x + B [a]x^2 with A = sin(th) / th
+    and B = (1 - cos th) / th^2 as Taylor series in th^2 (24 terms, Horner):
+    only +, -, * in a fixed order, so the device (me_vo_ba_chain) forms the
+    same bits.  The loop's pose(t) re-prediction uses it (step 7)."""
+    a0, a1, a2 = float(aa[0]), float(aa[1]), float(aa[2])
+    t2 = (a0 * a0 + a1 * a1) + a2 * a2
+    A, B = _ROT_A[23], _ROT_B[23]
+    for k in range(22, -1, -1):
+        A = A * t2 + _ROT_A[k]
+        B = B * t2 + _ROT_B[k]
+    av = (a0, a1, a2)
+    K = ((0.0, -a2, a1), (a2, 0.0, -a0), (-a1, a0, 0.0))
+    R = np.empty((3, 3))
+    for i in range(3):
+        for j in range(3):
+            k2 = av[i] * av[j] - (t2 if i == j else 0.0)
+            R[i, j] = ((1.0 if i == j else 0.0) + A * K[i][j]) + B * k2
+    return R
+
+
+def move_landmarks(X, R, pose, pose2, R2):
+    """Landmarks triangulated at `pose` (rotation R) moved to `pose2`
+    (rotation R2), camera-frame coordinates kept: x_c = R X + t, then
+    R2^T (x_c - t2) -- elementwise, in the order vo_chain_kernel uses."""
+    d = [(((X[:, 0] * R[k, 0] + X[:, 1] * R[k, 1]) + X[:, 2] * R[k, 2]) + pose[k]) - pose2[k] for k in range(3)]
+    return np.stack([(d[0] * R2[0, k] + d[1] * R2[1, k]) + d[2] * R2[2, k] for k in range(3)], 1)
+
+
 @dataclass
 class PipelineConfig:
     width: int
@@ -305,14 +349,45 @@ class GPUBackend(Backend):
         # observation, frame by frame; [_wstart, _wend) live in store _wcur
         self._wcap = 0
         self._wstore = [None, None]
+        self._wcaps = [0, 0]
         self._wcur = 0
         self._wend = 0
         self._wfrm = {}  # frame -> (offset, count)
         self._dev = {}   # name -> [ptr, bytes] on the device
         self._pin = {}   # name -> [ptr, bytes] page-locked host
         self._hview = {}  # page-locked ptr -> uint8 view of the whole buffer
-        self._ba = None
+        self._baq = []  # queued BA solves, oldest first (at most two: window t chained behind t - 1)
+        self._bw_k = 0  # staging / device buffer set of the next window solve
+        # window t's BA start formed on the device behind window t - 1's solve (me_vo_ba_chain)
+        self.chain_window = os.environ.get("ME_VO_CHAIN", "1") == "1"
+        self.tlog = None  # diagnostics (tools/pipe_run.py): (event, frame, perf_counter) of BA enqueues / completions
         self._scale_res = None
+
+    def reserve(self, cfg):
+        """Size the BA side for the configuration's fullest window up front:
+        the window stores, both solve buffer sets and the BA scratch (a buffer
+        that grows mid-run waits for both contexts).  Bounds: every keyframe of
+        the window contributes at most n_feats observations (tracked + new),
+        and a landmark has at least one."""
+        n_obs = cfg.window * cfg.n_feats + cfg.n_feats
+        n_pts = n_obs
+        nc = cfg.window
+        cap = 2 * n_obs
+        if self._wend == 0 and self._wcap < cap:
+            for k in (0, 1):
+                if self._wstore[k] is not None:
+                    self.ctx.free(self._wstore[k])
+                self._wstore[k] = self.ctx.malloc(40 * cap)
+                self._wcaps[k] = cap
+            self._wcap = cap
+        nb = 48 * nc + 24 * n_pts + 4 * n_pts + 4 * nc + 4 * n_pts
+        for k in (0, 1):
+            self._hbuf(f"bw{k}", nb)
+            self._dbuf(f"bw{k}", nb)
+            self._dbuf(f"bw_idx{k}", 8 * n_obs)
+        for k in (0, 1):
+            self._hbuf(f"w_add{k}", 40 * cfg.n_feats)
+        self.ctx.check(self.ctx.lib.me_ba_reserve(self.ctx.h, nc, n_pts, n_obs, 4, cfg.fixed_frames), "me_ba_reserve")
 
     # ---- persistent buffers
     def _dbuf(self, name, nbytes):
@@ -393,7 +468,7 @@ class GPUBackend(Backend):
         if self._scale_pool is not None:
             self._scale_pool.shutdown()
             self._scale_pool = None
-        if self._ba is not None:
+        while self._baq:
             self.ba_result()
         if self._ba_pool is not None:
             self._ba_pool.shutdown()
@@ -402,6 +477,7 @@ class GPUBackend(Backend):
             if st is not None:
                 self.ctx.free(st)
         self._wstore = [None, None]
+        self._wcaps = [0, 0]
         for t in list(self._imgs):
             self.release(t)
         self.tctx.synchronize()
@@ -459,6 +535,7 @@ class GPUBackend(Backend):
         return scale_optimise(sp, params, ctx=self.tctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
 
     def ba_solve(self, bp, iters):
+        assert not self._baq, "ba_solve with window solves queued"
         self.ba_submit(bp, iters)
         return self.ba_result()
 
@@ -608,8 +685,12 @@ class GPUBackend(Backend):
 
     def window_add(self, t, ids, feats):
         """Append keyframe t's observations (one H2D); the live window is
-        compacted into the other store when the tail is full (no BA is in
-        flight here: the loop completes frame t - 1 first)."""
+        compacted into the other store when the tail is full (stream-ordered
+        copies; a BA in flight reads the current store, which the compaction
+        only reads, and the other store's last solve has completed).  The
+        staging alternates by keyframe parity: the copy from the other set,
+        two keyframes back, ran before that keyframe's BA, which the loop has
+        waited for."""
         n = len(ids)
         live0 = min((o for o, _ in self._wfrm.values()), default=self._wend)
         live = self._wend - live0
@@ -617,10 +698,13 @@ class GPUBackend(Backend):
         if self._wend + n > self._wcap:
             cap = max(1 << 16, 2 * (live + n), self._wcap)
             k = 1 - self._wcur
-            if self._wstore[k] is not None:
-                c.free(self._wstore[k])
+            if self._wcaps[k] < cap:  # (the other store is reused when it is large enough: a free waits for the device)
+                if self._wstore[k] is not None:
+                    c.free(self._wstore[k])
+                self._wstore[k] = c.malloc(40 * cap)
+                self._wcaps[k] = cap
+            cap = self._wcaps[k]
             old = self._wcap
-            self._wstore[k] = c.malloc(40 * cap)
             if live:
                 ob, fb, ib = self._wstore[self._wcur], self._wstore[self._wcur] + 32 * old, \
                     self._wstore[self._wcur] + 36 * old
@@ -634,7 +718,7 @@ class GPUBackend(Backend):
             self._wfrm = {f: (o - live0, m) for f, (o, m) in self._wfrm.items()}
             self._wend = live
         if n:
-            hp = self._hbuf("w_add", 40 * n)
+            hp = self._hbuf(f"w_add{t & 1}", 40 * n)
             self._view(hp, np.float64, 4 * n)[:] = np.asarray(feats, np.float64).ravel()
             self._view(hp, np.int32, n, 32 * n)[:] = t
             self._view(hp, np.int32, n, 36 * n)[:] = ids
@@ -649,14 +733,20 @@ class GPUBackend(Backend):
     def window_pop(self, t):
         self._wfrm.pop(t, None)
 
-    def ba_submit_window(self, t, f0, win_ids, X, cams, iters):
+    def ba_submit_window(self, t, f0, win_ids, X, cams, iters, chain=None):
         """Queue the BA of the device-resident window [f0, t]: the window's
         track IDs, points and cameras go up (one H2D), the observation indices
         are built on the device (me_ba_window_indices), the solve runs on the
-        device-resident problem (me_ba_solve_async, ME_DEVICE)."""
+        device-resident problem (me_ba_solve_async, ME_DEVICE).  `chain`
+        (WindowedStereoVO._chain_args): the cameras and points sent are the
+        loop's state before the previous window's result, which
+        me_vo_ba_chain applies on the device behind that window's solve, so
+        this solve is queued before the previous one completes.  Two buffer
+        sets alternate (the previous window's stays in use until its wait)."""
         import ctypes
+        import time
 
-        from ._lib import ME_DEVICE, BAProblemC
+        from ._lib import ME_DEVICE, BAProblemC, VOChainArgsC
         from .optimisation import SolverOptions
 
         off0 = self._wfrm[f0][0]
@@ -664,14 +754,29 @@ class GPUBackend(Backend):
         npts, nc = len(win_ids), len(cams)
         c = self.ctx
         V = ctypes.c_void_p
-        # cams | pts (solved in place) | win_ids, one page-locked block and one H2D
-        nb = 48 * nc + 24 * npts + 4 * npts
-        hp = self._hbuf("bw", nb)
+        k = self._bw_k
+        self._bw_k ^= 1
+        # cams | pts (solved in place) | win_ids | chain: cam_src | pt_src -- one page-locked block, one H2D
+        o_ids = 48 * nc + 24 * npts
+        o_cs = o_ids + 4 * npts
+        o_ps = o_cs + 4 * nc
+        nb = o_ps + 4 * npts
+        hp = self._hbuf(f"bw{k}", nb)
         self._view(hp, np.float64, 6 * nc)[:] = np.asarray(cams, np.float64).ravel()
         self._view(hp, np.float64, 3 * npts, 48 * nc)[:] = np.asarray(X, np.float64).ravel()
-        self._view(hp, np.int32, npts, 48 * nc + 24 * npts)[:] = win_ids
-        d = self._dbuf("bw", nb)
-        di = self._dbuf("bw_idx", 8 * max(n_obs, 1))
+        self._view(hp, np.int32, npts, o_ids)[:] = win_ids
+        args = None
+        if chain is not None:
+            assert chain["nc"] == nc and len(chain["pt_src"]) == npts
+            self._view(hp, np.int32, nc, o_cs)[:] = chain["cam_src"]
+            self._view(hp, np.int32, npts, o_ps)[:] = chain["pt_src"]
+            args = VOChainArgsC()
+            args.pose[:] = [float(x) for x in chain["pose"]]
+            args.R[:] = [float(x) for x in np.asarray(chain["R"], np.float64).ravel()]
+            args.vel[:] = [float(x) for x in chain["vel"]]
+            args.k1, args.k0, args.mode = chain["k1"], chain["k0"], chain["mode"]
+        d = self._dbuf(f"bw{k}", nb)
+        di = self._dbuf(f"bw_idx{k}", 8 * max(n_obs, 1))
         o, f, i = self._wview(self._wcur)
         p = BAProblemC()
         p.n_cams, p.n_pts, p.n_obs = nc, npts, n_obs
@@ -687,12 +792,21 @@ class GPUBackend(Backend):
         p.mem, p.obs_dim = ME_DEVICE, 4
         opt = SolverOptions.fixed_iterations(iters).to_c()
 
-        def enqueue():  # H2D, the window's indices, the solve (~50 launches of host time)
-            c.copy_async(d, hp, nb)
+        def enqueue():  # H2D, the chained start, the window's indices, the solve (~50 launches of host time)
+            if self.tlog is not None:
+                self.tlog.append(("enq0", t, time.perf_counter()))
+            c.copy_async(d, hp, nb if args is not None else o_cs)
+            if args is not None:
+                c.check(c.lib.me_vo_ba_chain(c.h, V(d), nc, V(d + 48 * nc), npts, V(d + o_cs), V(d + o_ps),
+                                             ctypes.byref(args)), "me_vo_ba_chain")
             c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
-                                               V(d + 48 * nc + 24 * npts), npts, V(di), V(di + 4 * n_obs)),
+                                               V(d + o_ids), npts, V(di), V(di + 4 * n_obs)),
                     "me_ba_window_indices")
+            if self.tlog is not None:
+                self.tlog.append(("solve0", t, time.perf_counter()))
             c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(opt)), "me_ba_solve_async")
+            if self.tlog is not None:
+                self.tlog.append(("enq", t, time.perf_counter()))
 
         # The launches are queued by a worker thread (the C calls release the
         # GIL): the loop goes on with the next keyframe's front end, which uses
@@ -702,10 +816,12 @@ class GPUBackend(Backend):
                 from concurrent.futures import ThreadPoolExecutor
 
                 self._ba_pool = ThreadPoolExecutor(max_workers=1)
+            if self._ba_fut is not None:  # (one enqueue at a time on the ctx)
+                self._ba_fut.result()
             self._ba_fut = self._ba_pool.submit(enqueue)
         else:
             enqueue()
-        self._ba = ("dev", p, opt, d, nc, npts)
+        self._baq.append(("dev", p, opt, args, nc, npts))
         return n_obs
 
     def ba_submit(self, bp, iters):
@@ -719,10 +835,16 @@ class GPUBackend(Backend):
         o = SolverOptions.fixed_iterations(iters).to_c()
         c = self.ctx
         import ctypes
+        if self._ba_fut is not None:
+            fut, self._ba_fut = self._ba_fut, None
+            fut.result()
         c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(o)), "me_ba_solve_async")
-        self._ba = ("host", p, o, cams, pts, keep)
+        self._baq.append(("host", p, o, cams, pts, keep))
 
     def ba_result(self):
+        """The oldest queued solve: (cams, pts, summary).  A device-resident
+        window's result comes from the staging its solve read back into
+        (me_ba_wait_out): no wait on a solve queued behind it."""
         import ctypes
 
         from ._lib import BASummaryC
@@ -731,20 +853,21 @@ class GPUBackend(Backend):
         if self._ba_fut is not None:  # the worker's enqueue (and its errors)
             fut, self._ba_fut = self._ba_fut, None
             fut.result()
-        rec = self._ba
-        self._ba = None
+        rec = self._baq.pop(0)
         s = BASummaryC()
         c = self.ctx
-        c.check(c.lib.me_ba_wait(c.h, ctypes.byref(s)), "me_ba_wait")
-        if rec[0] == "dev":  # device-resident window: cams | pts back in one D2H
-            _, p, o, d, nc, npts = rec
-            nb = 48 * nc + 24 * npts
-            hp = self._hbuf("bw_out", nb)
-            c.copy_async(hp, d, nb)
-            c.synchronize()
-            cams = self._view(hp, np.float64, 6 * nc).reshape(nc, 6).copy()
-            pts = self._view(hp, np.float64, 3 * npts, 48 * nc).reshape(npts, 3).copy()
+        if rec[0] == "dev":
+            _, p, o, args, nc, npts = rec
+            cams = np.empty((nc, 6), np.float64)
+            pts = np.empty((npts, 3), np.float64)
+            c.check(c.lib.me_ba_wait_out(c.h, ctypes.byref(s), cams.ctypes.data_as(ctypes.c_void_p),
+                                         pts.ctypes.data_as(ctypes.c_void_p)), "me_ba_wait_out")
+            if self.tlog is not None:
+                import time
+
+                self.tlog.append(("done", None, time.perf_counter()))
             return cams, pts, _summary(s)
+        c.check(c.lib.me_ba_wait(c.h, ctypes.byref(s)), "me_ba_wait")
         _, p, o, cams, pts, keep = rec
         return cams, pts, _summary(s)
 
@@ -777,6 +900,8 @@ class WindowedStereoVO:
         self.cfg = cfg
         self.be = backend
         self.be.d_max = cfg.d_max
+        if hasattr(backend, "reserve"):
+            backend.reserve(cfg)
         self.K = np.asarray(S.intrinsics(cfg.width, cfg.height) if K is None else K, np.float64)
         self.f, self.cx, self.cy = self.K[0, 0], self.K[0, 2], self.K[1, 2]
         # grid of feature cells over the margin-free interior
@@ -971,20 +1096,26 @@ class WindowedStereoVO:
             is_new[new_idx] = True
             self._ev.append(("frame", self.ids[idx].copy(), t, feats.copy(), is_new[idx]))
         new_ids = self.ids[new_idx]
+        R_pose = aa_to_R(pose[3:])
+        # 8 (chained). A backend that can form BA(t)'s start on the device from BA(t-1)'s result queues
+        # BA(t) now, behind BA(t-1): the same values as step 7 forms on the host below
+        chain = self._chain_args(t, pose, R_pose, new_ids)
+        if chain is not None:
+            self.be.window_add(t, fid.astype(np.int32), feats)
+            ba = self._ba_submit(t, chain)
         # 7. frame t-1's BA applied
         done = self._complete_ba()
         # pose(t) again from the refined poses; the new landmarks of t keep their camera-frame coordinates
         pose2 = self._predict_pose(t)
         if not np.array_equal(pose2, pose) and len(new_ids):
             j = np.searchsorted(self.ids, new_ids)
-            R, R2 = aa_to_R(pose[3:]), aa_to_R(pose2[3:])
-            pc = self.X[j] @ R.T + pose[:3][None, :]
-            self.X[j] = (pc - pose2[:3][None, :]) @ R2
+            self.X[j] = move_landmarks(self.X[j], R_pose, pose, pose2, rot_series(pose2[3:]))
         self.poses[t] = pose2
         # 8. the window's observations, BA(t) queued; the scale LM over the tracks seen in t is queued by
         # the next keyframe (beside this BA; the scale only enters the frame's result)
-        self.be.window_add(t, fid.astype(np.int32), feats)
-        ba = self._ba_submit(t)
+        if chain is None:
+            self.be.window_add(t, fid.astype(np.int32), feats)
+            ba = self._ba_submit(t)
         self._scale_args = (t, imgs, fid.copy())
         self._pending = (t, n_tracked, len(new_idx), int(self.active.sum()), ba)
         self.prev_imgs, self.prev_t = imgs, t
@@ -1041,7 +1172,40 @@ class WindowedStereoVO:
         sp.imgs_handle = imgs
         self._wait(self.be.scale_submit, sp, OptimisationParams.fixed_iterations(self.cfg.scale_iters))
 
-    def _ba_submit(self, t):
+    def _chain_args(self, t, pose, R_pose, new_ids):
+        """Step 7's inputs for a backend that chains BA(t) behind BA(t-1) on
+        the device (None: step 7 on the host, then BA(t) queued): per window
+        camera / landmark its source in BA(t-1)'s result (-1 none, -2 new in
+        t), the pose(t) prediction form, the first prediction and its rotation."""
+        if not getattr(self.be, "chain_window", False) or self._pending is None or self._pending[4] is None:
+            return None
+        cfg = self.cfg
+        f0 = max(0, t - cfg.window + 1)
+        if t - f0 + 1 <= cfg.fixed_frames:
+            return None
+        pt, pf0, pwids, _ = self._pending[4]
+        nc = t - f0 + 1
+        k1 = t - 1 - f0
+        if t == 1 or (t - 2) not in self.poses:
+            mode, k0 = 0, -1
+            vel = np.zeros(6) if self.velocity is None else np.asarray(self.velocity, np.float64)
+        elif t - 2 >= f0:
+            mode, k0, vel = 1, t - 2 - f0, np.zeros(6)
+        else:
+            return None
+        if k1 < 0 or pt != t - 1:
+            return None
+        cam_src = np.array([f - pf0 if pf0 <= f <= pt else -1 for f in range(f0, t)] + [-1], np.int32)
+        upts = np.flatnonzero(self.last >= f0)
+        wid = self.ids[upts]
+        pos = np.minimum(np.searchsorted(pwids, wid), max(len(pwids) - 1, 0))
+        hit = (pwids[pos] == wid) if len(pwids) else np.zeros(len(wid), bool)
+        pt_src = np.where(hit, pos, -1).astype(np.int32)
+        pt_src[np.isin(wid, new_ids)] = -2
+        return dict(cam_src=cam_src, pt_src=pt_src, pose=np.asarray(pose, np.float64), R=R_pose, vel=vel, k1=k1,
+                    k0=k0, mode=mode, nc=nc)
+
+    def _ba_submit(self, t, chain=None):
         """The window's BA problem in initialiseObservations order
         (BundleAdjuster.h:354-376: points in track order, each track's
         features in frame order), built in O(observations): the window's
@@ -1059,7 +1223,7 @@ class WindowedStereoVO:
             assert self.latest_id < 2 ** 31
             self.be._K, self.be._calib = self.K, (cfg.baseline, cfg.feat_var, cfg.fixed_frames)
             n_obs = self._wait(self.be.ba_submit_window, t, f0, self.ids[upts].astype(np.int32), self.X[upts], cams,
-                               cfg.ba_iters)
+                               cfg.ba_iters, chain)
             return (t, f0, self.ids[upts].copy(), n_obs)
         bp = self.ba_problem(t, f0, upts)
         self._wait(self.be.ba_submit, bp, cfg.ba_iters)
