@@ -226,7 +226,8 @@ def load_library(path: str = LIB_PATH):
         "me_ba_wait": (c_int, [c_void_p, P(BASummaryC)]),
         "me_ba_wait_out": (c_int, [c_void_p, P(BASummaryC), c_void_p, c_void_p]),
         "me_ba_reserve": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
-        "me_vo_ba_chain": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, P(VOChainArgsC)]),
+        "me_vo_ba_chain": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                                   ctypes.c_int32, P(VOChainArgsC)]),
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),
         "me_ba_window_indices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p,
                                          c_void_p]),

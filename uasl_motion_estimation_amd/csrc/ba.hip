@@ -3791,13 +3791,15 @@ __device__ void rot_series(const double* a, double* R) {
 }
 
 // One launch over the window's landmarks; every workgroup forms pose(t)
-// itself, workgroup 0 also writes the cameras.  A camera / landmark with a
-// source index takes the previous solve's value when that solve succeeded,
-// else keeps the host's (the loop's state before the solve); pt_src -2 marks a
-// landmark new in t (moved when pose(t) changed).
+// itself, workgroup 0 also writes the cameras.  A camera with a source index
+// / a landmark whose track ID the previous window holds takes the previous
+// solve's value when that solve succeeded, else keeps the host's (the loop's
+// state before the solve); a landmark with ID >= new_from is new in t (moved
+// when pose(t) changed).
 __global__ __launch_bounds__(256) void vo_chain_kernel(const double* pc, const double* pp, const State* pst, double* cams,
                                                        int nc, double* pts, int np, const int* cam_src,
-                                                       const int* pt_src, me_vo_chain_args a) {
+                                                       const int* win_ids, const int* prev_ids, int n_prev,
+                                                       int new_from, me_vo_chain_args a) {
   __shared__ double sh[6 + 9];  // pose(t) | its rotation
   const bool ok = pst->termination != 2;
   auto cam = [&](int k, int j) {
@@ -3824,7 +3826,20 @@ __global__ __launch_bounds__(256) void vo_chain_kernel(const double* pc, const d
   for (int j = 0; j < 6; ++j) moved = moved || sh[j] != a.pose[j];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= np) return;
-  const int s = pt_src[i];
+  // landmark i's source: its track ID in the previous window's ascending IDs
+  const int id = win_ids[i];
+  int s = -2;
+  if (id < new_from) {
+    int lo = 0, hi = n_prev;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (prev_ids[mid] < id)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    s = lo < n_prev && prev_ids[lo] == id ? lo : -1;
+  }
   double* X = pts + 3 * (long)i;
   if (s >= 0) {
     if (ok)
@@ -3842,9 +3857,12 @@ __global__ __launch_bounds__(256) void vo_chain_kernel(const double* pc, const d
 }  // namespace
 
 extern "C" int me_vo_ba_chain(me_ctx* c, double* cams, int n_cams, double* pts, int n_pts, const int32_t* cam_src,
-                              const int32_t* pt_src, const me_vo_chain_args* a) {
+                              const int32_t* win_ids, const int32_t* prev_ids, int n_prev, int32_t new_from,
+                              const me_vo_chain_args* a) {
   me_range range_("me_vo_ba_chain");
-  if (!c || !a || n_cams < 1 || n_pts < 0 || !cams || !cam_src || (n_pts && (!pts || !pt_src))) return ME_ERR_INVALID;
+  if (!c || !a || n_cams < 1 || n_pts < 0 || n_prev < 0 || !cams || !cam_src ||
+      (n_pts && (!pts || !win_ids)) || (n_prev && !prev_ids))
+    return ME_ERR_INVALID;
   if (a->mode >= 0 && (a->k1 < 0 || a->k1 >= n_cams - 1 || (a->mode == 1 && (a->k0 < 0 || a->k0 >= n_cams - 1))))
     return me_set_error(c, ME_ERR_INVALID, "me_vo_ba_chain: prediction cameras %d, %d outside the window's first %d",
                         a->k1, a->k0, n_cams - 1);
@@ -3854,8 +3872,8 @@ extern "C" int me_vo_ba_chain(me_ctx* c, double* cams, int n_cams, double* pts, 
   if (!A->P.dev) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: the queued solve is not device-resident");
   ME_HIP(c, hipSetDevice(c->device));
   hipLaunchKernelGGL(vo_chain_kernel, dim3(blocks(std::max(n_pts, 1), 256)), dim3(256), 48 * (size_t)n_cams, c->stream,
-                     A->prob.cams,
-                     A->prob.pts, A->P.b.st, cams, n_cams, pts, n_pts, (const int*)cam_src, (const int*)pt_src, *a);
+                     A->prob.cams, A->prob.pts, A->P.b.st, cams, n_cams, pts, n_pts, (const int*)cam_src,
+                     (const int*)win_ids, (const int*)prev_ids, n_prev, (int)new_from, *a);
   return me_check_launch(c, "me_vo_ba_chain");
 }
 

@@ -380,7 +380,7 @@ class GPUBackend(Backend):
                 self._wstore[k] = self.ctx.malloc(40 * cap)
                 self._wcaps[k] = cap
             self._wcap = cap
-        nb = 48 * nc + 24 * n_pts + 4 * n_pts + 4 * nc + 4 * n_pts
+        nb = 48 * nc + 24 * n_pts + 4 * n_pts + 4 * nc
         for k in (0, 1):
             self._hbuf(f"bw{k}", nb)
             self._dbuf(f"bw{k}", nb)
@@ -756,20 +756,20 @@ class GPUBackend(Backend):
         V = ctypes.c_void_p
         k = self._bw_k
         self._bw_k ^= 1
-        # cams | pts (solved in place) | win_ids | chain: cam_src | pt_src -- one page-locked block, one H2D
+        # cams | pts (solved in place) | win_ids | chain: cam_src -- one page-locked block, one H2D
         o_ids = 48 * nc + 24 * npts
         o_cs = o_ids + 4 * npts
-        o_ps = o_cs + 4 * nc
-        nb = o_ps + 4 * npts
+        nb = o_cs + 4 * nc
         hp = self._hbuf(f"bw{k}", nb)
         self._view(hp, np.float64, 6 * nc)[:] = np.asarray(cams, np.float64).ravel()
         self._view(hp, np.float64, 3 * npts, 48 * nc)[:] = np.asarray(X, np.float64).ravel()
         self._view(hp, np.int32, npts, o_ids)[:] = win_ids
         args = None
+        prev = None
         if chain is not None:
-            assert chain["nc"] == nc and len(chain["pt_src"]) == npts
+            assert chain["nc"] == nc and self._baq and self._baq[-1][0] == "dev"
             self._view(hp, np.int32, nc, o_cs)[:] = chain["cam_src"]
-            self._view(hp, np.int32, npts, o_ps)[:] = chain["pt_src"]
+            prev = self._baq[-1][6]  # (device IDs, count) of the window solved before this one
             args = VOChainArgsC()
             args.pose[:] = [float(x) for x in chain["pose"]]
             args.R[:] = [float(x) for x in np.asarray(chain["R"], np.float64).ravel()]
@@ -797,8 +797,9 @@ class GPUBackend(Backend):
                 self.tlog.append(("enq0", t, time.perf_counter()))
             c.copy_async(d, hp, nb if args is not None else o_cs)
             if args is not None:
-                c.check(c.lib.me_vo_ba_chain(c.h, V(d), nc, V(d + 48 * nc), npts, V(d + o_cs), V(d + o_ps),
-                                             ctypes.byref(args)), "me_vo_ba_chain")
+                c.check(c.lib.me_vo_ba_chain(c.h, V(d), nc, V(d + 48 * nc), npts, V(d + o_cs), V(d + o_ids),
+                                             V(prev[0]), prev[1], chain["new_from"], ctypes.byref(args)),
+                        "me_vo_ba_chain")
             c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
                                                V(d + o_ids), npts, V(di), V(di + 4 * n_obs)),
                     "me_ba_window_indices")
@@ -811,7 +812,9 @@ class GPUBackend(Backend):
         # The launches are queued by a worker thread (the C calls release the
         # GIL): the loop goes on with the next keyframe's front end, which uses
         # the other context; ba_result joins the worker before touching this one.
-        if self.async_enqueue:
+        # A chained window is queued inline: the loop's next call is the wait
+        # for the previous window, which would join the worker at once.
+        if self.async_enqueue and chain is None:
             if self._ba_pool is None:
                 from concurrent.futures import ThreadPoolExecutor
 
@@ -820,8 +823,11 @@ class GPUBackend(Backend):
                 self._ba_fut.result()
             self._ba_fut = self._ba_pool.submit(enqueue)
         else:
+            if self._ba_fut is not None:  # (the previous window's enqueue first: it is the one chained from)
+                fut, self._ba_fut = self._ba_fut, None
+                fut.result()
             enqueue()
-        self._baq.append(("dev", p, opt, args, nc, npts))
+        self._baq.append(("dev", p, opt, args, nc, npts, (d + o_ids, npts)))
         return n_obs
 
     def ba_submit(self, bp, iters):
@@ -857,7 +863,7 @@ class GPUBackend(Backend):
         s = BASummaryC()
         c = self.ctx
         if rec[0] == "dev":
-            _, p, o, args, nc, npts = rec
+            _, p, o, args, nc, npts, _ = rec
             cams = np.empty((nc, 6), np.float64)
             pts = np.empty((npts, 3), np.float64)
             c.check(c.lib.me_ba_wait_out(c.h, ctypes.byref(s), cams.ctypes.data_as(ctypes.c_void_p),
@@ -1196,14 +1202,11 @@ class WindowedStereoVO:
         if k1 < 0 or pt != t - 1:
             return None
         cam_src = np.array([f - pf0 if pf0 <= f <= pt else -1 for f in range(f0, t)] + [-1], np.int32)
-        upts = np.flatnonzero(self.last >= f0)
-        wid = self.ids[upts]
-        pos = np.minimum(np.searchsorted(pwids, wid), max(len(pwids) - 1, 0))
-        hit = (pwids[pos] == wid) if len(pwids) else np.zeros(len(wid), bool)
-        pt_src = np.where(hit, pos, -1).astype(np.int32)
-        pt_src[np.isin(wid, new_ids)] = -2
-        return dict(cam_src=cam_src, pt_src=pt_src, pose=np.asarray(pose, np.float64), R=R_pose, vel=vel, k1=k1,
-                    k0=k0, mode=mode, nc=nc)
+        # the landmarks' sources are found on the device by track ID (window t-1's IDs are ascending; the
+        # tracks new in t hold the largest IDs)
+        new_from = int(new_ids[0]) if len(new_ids) else 2 ** 31 - 1
+        return dict(cam_src=cam_src, new_from=new_from, pose=np.asarray(pose, np.float64), R=R_pose, vel=vel,
+                    k1=k1, k0=k0, mode=mode, nc=nc)
 
     def _ba_submit(self, t, chain=None):
         """The window's BA problem in initialiseObservations order
