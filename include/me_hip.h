@@ -323,10 +323,12 @@ int me_ba_reserve(me_ctx* ctx, int n_cams, int n_pts, int n_obs, int obs_dim, in
    the device from the last queued device-resident solve (window t-1) before
    that solve completes.  cams (n_cams x 6) / pts (n_pts x 3), device memory,
    hold the host's values (the loop state before window t-1's result); camera
-   k / landmark i with cam_src / pt_src >= 0 take that solve's camera / point
-   at the source index when it succeeded (termination != FAILURE); pt_src -2:
-   a landmark new in keyframe t, moved from pose (rotation R, row-major) to
-   the new pose(t) when they differ; camera n_cams - 1 is pose(t):
+   k with cam_src >= 0 takes that solve's camera cam_src, landmark i (track ID
+   win_ids[i]) that solve's point of the same ID in prev_ids (window t-1's
+   ascending IDs, n_prev), when it succeeded (termination != FAILURE); a
+   landmark with ID >= new_from is new in keyframe t, moved from pose
+   (rotation R, row-major) to the new pose(t) when they differ; camera
+   n_cams - 1 is pose(t):
    mode 1: c[k1] + (c[k1] - c[k0]), mode 0: c[k1] + vel, mode -1: kept.  The
    new pose's rotation is a fixed Taylor series in theta^2 (the loop's host
    code repeats the arithmetic bit for bit).  Asynchronous on the ctx stream. */
@@ -337,7 +339,31 @@ typedef struct me_vo_chain_args {
   int k1, k0, mode;
 } me_vo_chain_args;
 int me_vo_ba_chain(me_ctx* ctx, double* cams, int n_cams, double* pts, int n_pts, const int32_t* cam_src,
-                   const int32_t* pt_src, const me_vo_chain_args* a);
+                   const int32_t* win_ids, const int32_t* prev_ids, int n_prev, int32_t new_from,
+                   const me_vo_chain_args* a);
+/* One keyframe's window solve in one call (for a thread that queues window t
+   while another waits for window t-1 with me_ba_wait_out -- the two may run
+   concurrently on one ctx; no other call on the ctx meanwhile): the staged
+   H2D (stage -> dev, stage_bytes, may be 0), me_vo_ba_chain when `chain`
+   (on p->cams / p->pts), me_ba_window_indices (frame / ids of the window's
+   p->n_obs observations, first_frame, win_ids -> p->cam_idx / p->pt_idx),
+   me_ba_solve_async(p, o). */
+typedef struct me_vo_window {
+  const void* stage;
+  void* dev;
+  size_t stage_bytes;
+  int chain;
+  const int32_t* cam_src;
+  const int32_t* win_ids;
+  const int32_t* prev_ids;
+  int n_prev;
+  int32_t new_from;
+  me_vo_chain_args args;
+  const int32_t* frame;
+  const int32_t* ids;
+  int first_frame;
+} me_vo_window;
+int me_vo_window_submit(me_ctx* ctx, const me_vo_window* w, me_ba_problem* p, const me_ba_options* o);
 /* BundleAdjuster<M>::initialiseObservations (BundleAdjuster.h:354-376) for a
    device-resident window: observation i was seen in frame[i] by the track
    ids[i]; cam_idx[i] = frame[i] - first_frame and pt_idx[i] = the position of

@@ -32,12 +32,10 @@ print(f"config {c}: {1e3 * dt / (n - warm):.3f} ms/keyframe", flush=True)
 # BA(t) enqueued vs BA(t-1) completed: a positive lead means the BA stream never waits for the host
 enq = {f: x for k, f, x in be.tlog if k == "enq"}
 enq0 = {f: x for k, f, x in be.tlog if k == "enq0"}
-sol0 = {f: x for k, f, x in be.tlog if k == "solve0"}
 fs = [f for f in enq if f >= warm and f in enq0]
 if fs:
-    print("enqueue: start at %.3f ms into the keyframe, pre-solve part %.3f ms, me_ba_solve_async %.3f ms (means)" % (
-        1e3 * sum(enq0[f] - tin[f] for f in fs) / len(fs), 1e3 * sum(sol0[f] - enq0[f] for f in fs) / len(fs),
-        1e3 * sum(enq[f] - sol0[f] for f in fs) / len(fs)))
+    print("enqueue: start at %.3f ms into the keyframe, me_vo_window_submit %.3f ms (means)" % (
+        1e3 * sum(enq0[f] - tin[f] for f in fs) / len(fs), 1e3 * sum(enq[f] - enq0[f] for f in fs) / len(fs)))
 done = [x for k, f, x in be.tlog if k == "done"]
 ts = sorted(enq)
 for i, f in enumerate(ts[1:], 1):

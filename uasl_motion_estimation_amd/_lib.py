@@ -112,6 +112,14 @@ class VOChainArgsC(ctypes.Structure):
                 ("mode", c_int)]
 
 
+class VOWindowC(ctypes.Structure):
+    """me_vo_window (include/me_hip.h)."""
+    _fields_ = [("stage", c_void_p), ("dev", c_void_p), ("stage_bytes", c_size_t), ("chain", c_int),
+                ("cam_src", c_void_p), ("win_ids", c_void_p), ("prev_ids", c_void_p), ("n_prev", c_int),
+                ("new_from", ctypes.c_int32), ("args", VOChainArgsC), ("frame", c_void_p), ("ids", c_void_p),
+                ("first_frame", c_int)]
+
+
 class KLTParamsC(ctypes.Structure):
     _fields_ = [("win", c_int), ("max_level", c_int), ("max_iters", c_int), ("eps", c_double),
                 ("min_eig", c_double)]
@@ -130,7 +138,7 @@ EXPORTS = [
     "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
     "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_wait_out", "me_ba_reserve", "me_ba_window_indices",
-    "me_vo_ba_chain",
+    "me_vo_ba_chain", "me_vo_window_submit",
     "me_comm_unique_id", "me_comm_create_rccl", "me_comm_create_callback", "me_comm_destroy", "me_comm_info",
     "me_comm_allreduce", "me_ba_solve_comm", "me_ba_shard_worthwhile", "me_ba_shard_exchange_us",
     "me_klt_default_params", "me_klt_track",
@@ -226,6 +234,7 @@ def load_library(path: str = LIB_PATH):
         "me_ba_wait": (c_int, [c_void_p, P(BASummaryC)]),
         "me_ba_wait_out": (c_int, [c_void_p, P(BASummaryC), c_void_p, c_void_p]),
         "me_ba_reserve": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int]),
+        "me_vo_window_submit": (c_int, [c_void_p, P(VOWindowC), P(BAProblemC), P(BAOptionsC)]),
         "me_vo_ba_chain": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                                    ctypes.c_int32, P(VOChainArgsC)]),
         "me_ba_cost": (c_int, [c_void_p, P(BAProblemC), P(c_double)]),

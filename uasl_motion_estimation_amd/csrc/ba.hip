@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <numeric>
 #include <vector>
 #include <hip/hip_ext.h>
@@ -3611,9 +3612,18 @@ struct AsyncSolve {
   me_ba_summary sum{};
 };
 constexpr int kBaQueue = 2;
+// The queue may be used from two host threads at once: one queueing window
+// t (me_ba_solve_async / me_vo_window_submit) while another waits for window
+// t-1 (me_ba_wait_out).  The lock guards the FIFO only; the solve's own
+// queueing and waiting run outside it.  The newest waited solve is retained
+// (`last`) until a newer one is queued: window t may be chained from window
+// t-1 (me_vo_ba_chain) after t-1 was waited.
 struct AsyncQueue {
   AsyncSolve* q[kBaQueue] = {nullptr, nullptr};  // FIFO: q[0] oldest
   int n = 0;
+  AsyncSolve* last = nullptr;  // newest waited solve (chain source)
+  int last_set = 1;            // scratch / staging set of the newest queued solve
+  std::mutex mu;
 };
 
 int ba_complete_one(me_ctx* c, AsyncSolve* A) {
@@ -3632,6 +3642,7 @@ void ba_async_free(me_ctx* c) {
     hipEventDestroy(A->ev);
     delete A;
   }
+  delete Q->last;  // (its event was destroyed when it was waited)
   delete Q;
   c->ba_async = nullptr;
   c->ba_async_free = nullptr;
@@ -3654,6 +3665,12 @@ int ba_drain(me_ctx* c) {
   return ME_OK;
 }
 
+// the solve a new one is chained from: the newest queued, else the newest waited
+AsyncSolve* ba_chain_source(AsyncQueue* Q) {
+  std::lock_guard<std::mutex> lk(Q->mu);
+  return Q->n ? Q->q[Q->n - 1] : Q->last;
+}
+
 }  // namespace
 
 extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
@@ -3661,12 +3678,18 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   AsyncQueue* Q = ba_queue(c);
-  if (Q->n >= kBaQueue)
-    return me_set_error(c, ME_ERR_STATE, "me_ba_solve_async: %d solves already queued on this context (me_ba_wait first)",
-                        kBaQueue);
   auto* A = new AsyncSolve;
+  {
+    std::lock_guard<std::mutex> lk(Q->mu);
+    if (Q->n >= kBaQueue) {
+      delete A;
+      return me_set_error(c, ME_ERR_STATE,
+                          "me_ba_solve_async: %d solves already queued on this context (me_ba_wait first)", kBaQueue);
+    }
+    A->set = 1 - Q->last_set;  // never the set of the solve queued before (queued, or being read back)
+    Q->last_set = A->set;
+  }
   A->prob = *p;
-  A->set = Q->n == 0 ? 0 : 1 - Q->q[0]->set;
   int rc = plan_build(c, p, opt, A->P, A->set, A->set);
   A->P.copy_out = A->P.dev;
   if (rc == ME_OK) {
@@ -3685,7 +3708,13 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
     delete A;
     return rc;
   }
-  Q->q[Q->n++] = A;
+  AsyncSolve* old = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(Q->mu);
+    Q->q[Q->n++] = A;
+    std::swap(old, Q->last);  // a newer solve is queued: the retained chain source goes
+  }
+  delete old;
   return ME_OK;
 }
 
@@ -3693,9 +3722,13 @@ extern "C" int me_ba_wait_out(me_ctx* c, me_ba_summary* s, double* cams, double*
   me_range range_("me_ba_wait");
   if (!c) return ME_ERR_INVALID;
   auto* Q = (AsyncQueue*)c->ba_async;
-  if (!Q || Q->n == 0) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");
+  AsyncSolve* A = nullptr;
+  if (Q) {
+    std::lock_guard<std::mutex> lk(Q->mu);
+    if (Q->n) A = Q->q[0];
+  }
+  if (!A) return me_set_error(c, ME_ERR_STATE, "me_ba_wait: no asynchronous BA solve on this context");
   ME_HIP(c, hipSetDevice(c->device));
-  AsyncSolve* A = Q->q[0];
   ME_TRY(ba_complete_one(c, A));
   const int rc = A->rc;
   if (s && rc == ME_OK) *s = A->sum;
@@ -3706,9 +3739,17 @@ extern "C" int me_ba_wait_out(me_ctx* c, me_ba_summary* s, double* cams, double*
     if (pts && g.np) std::memcpy(pts, A->P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
   }
   hipEventDestroy(A->ev);
-  delete A;
-  for (int i = 1; i < Q->n; ++i) Q->q[i - 1] = Q->q[i];
-  Q->q[--Q->n] = nullptr;
+  A->ev = nullptr;
+  AsyncSolve* gone = A;
+  {
+    std::lock_guard<std::mutex> lk(Q->mu);
+    for (int i = 1; i < Q->n; ++i) Q->q[i - 1] = Q->q[i];
+    Q->q[--Q->n] = nullptr;
+    if (Q->n == 0) {  // the newest: retained as the chain source until a newer one is queued
+      std::swap(gone, Q->last);
+    }
+  }
+  delete gone;
   return rc;
 }
 
@@ -3867,14 +3908,28 @@ extern "C" int me_vo_ba_chain(me_ctx* c, double* cams, int n_cams, double* pts, 
     return me_set_error(c, ME_ERR_INVALID, "me_vo_ba_chain: prediction cameras %d, %d outside the window's first %d",
                         a->k1, a->k0, n_cams - 1);
   auto* Q = (AsyncQueue*)c->ba_async;
-  if (!Q || Q->n == 0) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: no queued BA solve to chain from");
-  AsyncSolve* A = Q->q[Q->n - 1];
-  if (!A->P.dev) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: the queued solve is not device-resident");
+  AsyncSolve* A = Q ? ba_chain_source(Q) : nullptr;
+  if (!A) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: no BA solve to chain from");
+  if (!A->P.dev) return me_set_error(c, ME_ERR_STATE, "me_vo_ba_chain: the previous solve is not device-resident");
   ME_HIP(c, hipSetDevice(c->device));
   hipLaunchKernelGGL(vo_chain_kernel, dim3(blocks(std::max(n_pts, 1), 256)), dim3(256), 48 * (size_t)n_cams, c->stream,
                      A->prob.cams, A->prob.pts, A->P.b.st, cams, n_cams, pts, n_pts, (const int*)cam_src,
                      (const int*)win_ids, (const int*)prev_ids, n_prev, (int)new_from, *a);
   return me_check_launch(c, "me_vo_ba_chain");
+}
+
+extern "C" int me_vo_window_submit(me_ctx* c, const me_vo_window* w, me_ba_problem* p, const me_ba_options* o) {
+  me_range range_("me_vo_window_submit");
+  if (!c || !w || !p || !o) return ME_ERR_INVALID;
+  ME_HIP(c, hipSetDevice(c->device));
+  if (w->stage_bytes) ME_HIP(c, hipMemcpyAsync(w->dev, w->stage, w->stage_bytes, hipMemcpyHostToDevice, c->stream));
+  if (w->chain)
+    ME_TRY(me_vo_ba_chain(c, p->cams, p->n_cams, p->pts, p->n_pts, w->cam_src, w->win_ids, w->prev_ids, w->n_prev,
+                          w->new_from, &w->args));
+  // (the problem's index arrays are the caller's device buffers, filled here)
+  ME_TRY(me_ba_window_indices(c, w->frame, w->ids, p->n_obs, w->first_frame, w->win_ids, p->n_pts,
+                              const_cast<int32_t*>(p->cam_idx), const_cast<int32_t*>(p->pt_idx)));
+  return me_ba_solve_async(c, p, o);
 }
 
 extern "C" void me_ba_default_options(me_ba_options* o) {

@@ -468,6 +468,7 @@ class GPUBackend(Backend):
         if self._scale_pool is not None:
             self._scale_pool.shutdown()
             self._scale_pool = None
+        self._join_enqueue()
         while self._baq:
             self.ba_result()
         if self._ba_pool is not None:
@@ -691,6 +692,7 @@ class GPUBackend(Backend):
         staging alternates by keyframe parity: the copy from the other set,
         two keyframes back, ran before that keyframe's BA, which the loop has
         waited for."""
+        self._join_enqueue()  # (stream order: the previous window's solve is queued before these copies)
         n = len(ids)
         live0 = min((o for o, _ in self._wfrm.values()), default=self._wend)
         live = self._wend - live0
@@ -746,14 +748,14 @@ class GPUBackend(Backend):
         import ctypes
         import time
 
-        from ._lib import ME_DEVICE, BAProblemC, VOChainArgsC
+        from ._lib import ME_DEVICE, BAProblemC, VOWindowC
         from .optimisation import SolverOptions
 
+        self._join_enqueue()  # (the previous window's queueing: this one may chain from it)
         off0 = self._wfrm[f0][0]
         n_obs = self._wend - off0
         npts, nc = len(win_ids), len(cams)
         c = self.ctx
-        V = ctypes.c_void_p
         k = self._bw_k
         self._bw_k ^= 1
         # cams | pts (solved in place) | win_ids | chain: cam_src -- one page-locked block, one H2D
@@ -764,20 +766,23 @@ class GPUBackend(Backend):
         self._view(hp, np.float64, 6 * nc)[:] = np.asarray(cams, np.float64).ravel()
         self._view(hp, np.float64, 3 * npts, 48 * nc)[:] = np.asarray(X, np.float64).ravel()
         self._view(hp, np.int32, npts, o_ids)[:] = win_ids
-        args = None
-        prev = None
+        d = self._dbuf(f"bw{k}", nb)
+        di = self._dbuf(f"bw_idx{k}", 8 * max(n_obs, 1))
+        w = VOWindowC()
+        w.stage, w.dev, w.stage_bytes = hp, d, nb if chain is not None else o_cs
         if chain is not None:
             assert chain["nc"] == nc and self._baq and self._baq[-1][0] == "dev"
             self._view(hp, np.int32, nc, o_cs)[:] = chain["cam_src"]
             prev = self._baq[-1][6]  # (device IDs, count) of the window solved before this one
-            args = VOChainArgsC()
-            args.pose[:] = [float(x) for x in chain["pose"]]
-            args.R[:] = [float(x) for x in np.asarray(chain["R"], np.float64).ravel()]
-            args.vel[:] = [float(x) for x in chain["vel"]]
-            args.k1, args.k0, args.mode = chain["k1"], chain["k0"], chain["mode"]
-        d = self._dbuf(f"bw{k}", nb)
-        di = self._dbuf(f"bw_idx{k}", 8 * max(n_obs, 1))
+            w.chain = 1
+            w.cam_src, w.prev_ids, w.n_prev, w.new_from = d + o_cs, prev[0], prev[1], chain["new_from"]
+            a = w.args
+            a.pose[:] = [float(x) for x in chain["pose"]]
+            a.R[:] = [float(x) for x in np.asarray(chain["R"], np.float64).ravel()]
+            a.vel[:] = [float(x) for x in chain["vel"]]
+            a.k1, a.k0, a.mode = chain["k1"], chain["k0"], chain["mode"]
         o, f, i = self._wview(self._wcur)
+        w.win_ids, w.frame, w.ids, w.first_frame = d + o_ids, f + 4 * off0, i + 4 * off0, f0
         p = BAProblemC()
         p.n_cams, p.n_pts, p.n_obs = nc, npts, n_obs
         p.cams = ctypes.cast(d, ctypes.POINTER(ctypes.c_double))
@@ -792,43 +797,35 @@ class GPUBackend(Backend):
         p.mem, p.obs_dim = ME_DEVICE, 4
         opt = SolverOptions.fixed_iterations(iters).to_c()
 
-        def enqueue():  # H2D, the chained start, the window's indices, the solve (~50 launches of host time)
+        def enqueue():  # H2D, the chained start, the window's indices, the solve: one C call (no GIL)
             if self.tlog is not None:
                 self.tlog.append(("enq0", t, time.perf_counter()))
-            c.copy_async(d, hp, nb if args is not None else o_cs)
-            if args is not None:
-                c.check(c.lib.me_vo_ba_chain(c.h, V(d), nc, V(d + 48 * nc), npts, V(d + o_cs), V(d + o_ids),
-                                             V(prev[0]), prev[1], chain["new_from"], ctypes.byref(args)),
-                        "me_vo_ba_chain")
-            c.check(c.lib.me_ba_window_indices(c.h, V(f + 4 * off0), V(i + 4 * off0), n_obs, f0,
-                                               V(d + o_ids), npts, V(di), V(di + 4 * n_obs)),
-                    "me_ba_window_indices")
-            if self.tlog is not None:
-                self.tlog.append(("solve0", t, time.perf_counter()))
-            c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(opt)), "me_ba_solve_async")
+            c.check(c.lib.me_vo_window_submit(c.h, ctypes.byref(w), ctypes.byref(p), ctypes.byref(opt)),
+                    "me_vo_window_submit")
             if self.tlog is not None:
                 self.tlog.append(("enq", t, time.perf_counter()))
 
-        # The launches are queued by a worker thread (the C calls release the
-        # GIL): the loop goes on with the next keyframe's front end, which uses
-        # the other context; ba_result joins the worker before touching this one.
-        # A chained window is queued inline: the loop's next call is the wait
-        # for the previous window, which would join the worker at once.
-        if self.async_enqueue and chain is None:
+        # Queued by a worker thread (the C call releases the GIL): the loop
+        # goes on -- it waits for the previous window (me_ba_wait_out may run
+        # beside the queueing: the library's solve queue is locked), applies
+        # it and starts the next keyframe.  Stream work of this ctx from the
+        # loop thread (window_add) joins the worker first.
+        fut = None
+        if self.async_enqueue:
             if self._ba_pool is None:
                 from concurrent.futures import ThreadPoolExecutor
 
                 self._ba_pool = ThreadPoolExecutor(max_workers=1)
-            if self._ba_fut is not None:  # (one enqueue at a time on the ctx)
-                self._ba_fut.result()
-            self._ba_fut = self._ba_pool.submit(enqueue)
+            fut = self._ba_fut = self._ba_pool.submit(enqueue)
         else:
-            if self._ba_fut is not None:  # (the previous window's enqueue first: it is the one chained from)
-                fut, self._ba_fut = self._ba_fut, None
-                fut.result()
             enqueue()
-        self._baq.append(("dev", p, opt, args, nc, npts, (d + o_ids, npts)))
+        self._baq.append(("dev", p, opt, w, nc, npts, (d + o_ids, npts), fut))
         return n_obs
+
+    def _join_enqueue(self):
+        if self._ba_fut is not None:  # (and its errors)
+            fut, self._ba_fut = self._ba_fut, None
+            fut.result()
 
     def ba_submit(self, bp, iters):
         """Queue the window's solve on the BA context (me_ba_solve_async: the
@@ -841,9 +838,7 @@ class GPUBackend(Backend):
         o = SolverOptions.fixed_iterations(iters).to_c()
         c = self.ctx
         import ctypes
-        if self._ba_fut is not None:
-            fut, self._ba_fut = self._ba_fut, None
-            fut.result()
+        self._join_enqueue()
         c.check(c.lib.me_ba_solve_async(c.h, ctypes.byref(p), ctypes.byref(o)), "me_ba_solve_async")
         self._baq.append(("host", p, o, cams, pts, keep))
 
@@ -856,14 +851,15 @@ class GPUBackend(Backend):
         from ._lib import BASummaryC
         from .optimisation import _summary
 
-        if self._ba_fut is not None:  # the worker's enqueue (and its errors)
-            fut, self._ba_fut = self._ba_fut, None
-            fut.result()
         rec = self._baq.pop(0)
         s = BASummaryC()
         c = self.ctx
         if rec[0] == "dev":
-            _, p, o, args, nc, npts, _ = rec
+            _, p, o, w, nc, npts, _, fut = rec
+            if fut is not None:  # this window's own queueing (a newer one's may run on beside the wait)
+                fut.result()
+                if fut is self._ba_fut:
+                    self._ba_fut = None
             cams = np.empty((nc, 6), np.float64)
             pts = np.empty((npts, 3), np.float64)
             c.check(c.lib.me_ba_wait_out(c.h, ctypes.byref(s), cams.ctypes.data_as(ctypes.c_void_p),
