@@ -236,39 +236,6 @@ __device__ __forceinline__ void drain_and_barrier() {
 // ---------------------------------------------------------------- kernels
 constexpr int kPtBlock = 64;   // per-point kernels: spread ~N/64 workgroups over the CUs
 
-// One observation's linearisation (Huber-corrected residual and Jacobians ->
-// V_o | g_o at its CSR slot, W_o when its camera is variable); returns the
-// cost term.  (Measured and dropped: the point step linearising speculatively
-// at its candidate into a second obsx / Wo set, which removes the linearize
-// launch of every accepted step -- the step went 15.1 -> 28.7 us for 9.3 us
-// saved, config 3 BA 0.821 -> 0.894 ms.)
-__device__ __forceinline__ double lin_store(const Geo& g, double* obsx, double* Wo, long slot, bool var_cam,
-                                            double* r, double* Jc, double* Jp) {
-  const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
-  double rho0, sc;
-  huber(s, &rho0, &sc);
-  for (int k = 0; k < 4; ++k) r[k] *= sc;
-  for (int k = 0; k < 24; ++k) Jc[k] *= sc;
-  for (int k = 0; k < 12; ++k) Jp[k] *= sc;
-  double* X = obsx + slot * kObsxStride;
-  X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
-  X[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
-  X[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
-  X[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
-  X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
-  X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
-  for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
-  // (the camera normal-equation pieces are formed by cam_assemble from the
-  // same residual and Jacobian: no 216 B per observation through HBM)
-  if (var_cam) {
-    double* W = Wo + 18 * slot;
-    for (int a = 0; a < 6; ++a)
-      for (int c = 0; c < 3; ++c)
-        W[a * 3 + c] = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
-  }
-  return 0.5 * rho0;
-}
-
 // Per observation: corrected residual / Jacobian, cost, and the unscaled
 // per-observation normal-equation pieces W_o = Jc^T Jp (6x3), V_o = Jp^T Jp
 // (6 unique), g_o = Jp^T r, so the per-point stage only sums.
@@ -293,7 +260,30 @@ __global__ __launch_bounds__(BLK) void linearize_kernel(Geo g, Bufs b) {
     const int ci = b.cam_idx[o], pi = b.pt_idx[o];
     double r[4], Jc[24], Jp[12];
     obs_residual<OD>(g, b, o, b.cams[cur] + 6 * ci, b.pts[cur] + 3 * pi, r, Jc, Jp);
-    cost = lin_store(g, b.obsx, b.Wo, b.pos[o], ci - g.nf >= 0, r, Jc, Jp);
+    const double s = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
+    double rho0, sc;
+    huber(s, &rho0, &sc);
+    cost = 0.5 * rho0;
+    for (int k = 0; k < 4; ++k) r[k] *= sc;
+    for (int k = 0; k < 24; ++k) Jc[k] *= sc;
+    for (int k = 0; k < 12; ++k) Jp[k] *= sc;
+    const long slot = b.pos[o];  // CSR-by-point slot: per-point stages read contiguously
+    double* X = b.obsx + slot * kObsxStride;
+    X[0] = Jp[0] * Jp[0] + Jp[3] * Jp[3] + Jp[6] * Jp[6] + Jp[9] * Jp[9];
+    X[1] = Jp[0] * Jp[1] + Jp[3] * Jp[4] + Jp[6] * Jp[7] + Jp[9] * Jp[10];
+    X[2] = Jp[0] * Jp[2] + Jp[3] * Jp[5] + Jp[6] * Jp[8] + Jp[9] * Jp[11];
+    X[3] = Jp[1] * Jp[1] + Jp[4] * Jp[4] + Jp[7] * Jp[7] + Jp[10] * Jp[10];
+    X[4] = Jp[1] * Jp[2] + Jp[4] * Jp[5] + Jp[7] * Jp[8] + Jp[10] * Jp[11];
+    X[5] = Jp[2] * Jp[2] + Jp[5] * Jp[5] + Jp[8] * Jp[8] + Jp[11] * Jp[11];
+    for (int a = 0; a < 3; ++a) X[6 + a] = Jp[a] * r[0] + Jp[3 + a] * r[1] + Jp[6 + a] * r[2] + Jp[9 + a] * r[3];
+    // (the camera normal-equation pieces are formed by cam_assemble from the
+    // same residual and Jacobian: no 216 B per observation through HBM)
+    if (ci - g.nf >= 0) {
+      double* W = b.Wo + 18 * slot;
+      for (int a = 0; a < 6; ++a)
+        for (int c = 0; c < 3; ++c)
+          W[a * 3 + c] = Jc[a] * Jp[c] + Jc[6 + a] * Jp[3 + c] + Jc[12 + a] * Jp[6 + c] + Jc[18 + a] * Jp[9 + c];
+    }
   }
   double v[1] = {cost};
   double out[1];
@@ -2371,6 +2361,10 @@ __device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_d
 
 // (64-thread workgroups measured slower: 17.2 -> 21.6 us at config 3, the
 // last arrival then reduces 4x the partials)
+// (Measured and dropped, round 4 as in rounds 2-3: the step linearising
+// speculatively at its candidate into a second obsx / Wo set, removing the
+// linearize launch of every accepted step -- the step went 15.1 -> 28.7 us
+// for 9.3 us saved; config 3 BA 0.821 -> 0.894 ms per 10 iterations.)
 constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 
 // Model cost change in the normal-equation form (Ceres computes
@@ -3673,8 +3667,10 @@ AsyncSolve* ba_chain_source(AsyncQueue* Q) {
 
 }  // namespace
 
-extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
-  me_range range_("me_ba_solve_async");
+// copy_out: a device-resident problem's solved cams / pts also read back
+// into the staging behind the solve (me_vo_window_submit; me_ba_wait_out
+// then returns them without touching the stream)
+static int solve_async_impl(me_ctx* c, me_ba_problem* p, const me_ba_options* opt, bool copy_out) {
   if (!c || !p || !opt) return ME_ERR_INVALID;
   ME_HIP(c, hipSetDevice(c->device));
   AsyncQueue* Q = ba_queue(c);
@@ -3691,7 +3687,7 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   }
   A->prob = *p;
   int rc = plan_build(c, p, opt, A->P, A->set, A->set);
-  A->P.copy_out = A->P.dev;
+  A->P.copy_out = copy_out && A->P.dev;
   if (rc == ME_OK) {
     for (int it = 0; it <= opt->max_num_iterations && rc == ME_OK; ++it)
       rc = enqueue_iteration(A->P, it == opt->max_num_iterations);
@@ -3718,6 +3714,11 @@ extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_option
   return ME_OK;
 }
 
+extern "C" int me_ba_solve_async(me_ctx* c, me_ba_problem* p, const me_ba_options* opt) {
+  me_range range_("me_ba_solve_async");
+  return solve_async_impl(c, p, opt, false);
+}
+
 extern "C" int me_ba_wait_out(me_ctx* c, me_ba_summary* s, double* cams, double* pts) {
   me_range range_("me_ba_wait");
   if (!c) return ME_ERR_INVALID;
@@ -3732,11 +3733,16 @@ extern "C" int me_ba_wait_out(me_ctx* c, me_ba_summary* s, double* cams, double*
   ME_TRY(ba_complete_one(c, A));
   const int rc = A->rc;
   if (s && rc == ME_OK) *s = A->sum;
-  if (rc == ME_OK && A->P.dev && (cams || pts)) {  // from the staging (read back behind the solve's event)
+  if (rc == ME_OK && A->P.dev && (cams || pts)) {
     constexpr size_t nst = sizeof(State) / 8;
     const Geo& g = A->P.g;
-    if (cams) std::memcpy(cams, A->P.host + nst, 8 * 6 * (size_t)g.nc);
-    if (pts && g.np) std::memcpy(pts, A->P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
+    if (A->P.copy_out) {  // from the staging (read back behind the solve's event)
+      if (cams) std::memcpy(cams, A->P.host + nst, 8 * 6 * (size_t)g.nc);
+      if (pts && g.np) std::memcpy(pts, A->P.host + nst + 6 * (size_t)g.nc, 8 * 3 * (size_t)g.np);
+    } else {  // (blocking copies on the null stream: the solve has completed; the ctx stream is not waited)
+      if (cams) ME_HIP(c, hipMemcpy(cams, A->prob.cams, 8 * 6 * (size_t)g.nc, hipMemcpyDeviceToHost));
+      if (pts && g.np) ME_HIP(c, hipMemcpy(pts, A->prob.pts, 8 * 3 * (size_t)g.np, hipMemcpyDeviceToHost));
+    }
   }
   hipEventDestroy(A->ev);
   A->ev = nullptr;
@@ -3929,7 +3935,7 @@ extern "C" int me_vo_window_submit(me_ctx* c, const me_vo_window* w, me_ba_probl
   // (the problem's index arrays are the caller's device buffers, filled here)
   ME_TRY(me_ba_window_indices(c, w->frame, w->ids, p->n_obs, w->first_frame, w->win_ids, p->n_pts,
                               const_cast<int32_t*>(p->cam_idx), const_cast<int32_t*>(p->pt_idx)));
-  return me_ba_solve_async(c, p, o);
+  return solve_async_impl(c, p, o, true);
 }
 
 extern "C" void me_ba_default_options(me_ba_options* o) {
