@@ -1134,7 +1134,7 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
 // exchange tail instead of finalizing; SA_UNPACK (sharded, after it, when
 // the camera solve does not unpack itself): as SA_SUM from the exchange.
 __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts o, const double* gc_raw, int full,
-                                                            int mode) {
+                                                            int mode, double* img = nullptr) {
   static_assert(kBlock == kFinBlock, "the finalize block runs with the assembly block size");
   if (blockIdx.x == gridDim.x - 1) {
     __shared__ double lds[16];
@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(kBlock) void s_assemble_kernel(Geo g, Bufs b, Opts 
   }
   if (mode != SA_PACK && blockIdx.x == 0 && threadIdx.x == 0 && !(b.st->done || b.st->final_pass))
     b.scal[R_COUNT] = (b.st->fail || (mode == SA_UNPACK && b.xch[xo_fail(g)] != 0.0)) ? 1.0 : 0.0;
-  s_assemble_body<kBlock, false>(g, b, blockIdx.x, full, mode);
+  s_assemble_body<kBlock, false>(g, b, blockIdx.x, full, mode, img, &o);
 }
 
 // One workgroup: S (assembled by s_assemble_kernel, all-reduced in sharded
@@ -1430,6 +1430,10 @@ constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 #define ME_SOLVE_EARLY0 0
 #endif
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
+constexpr int kSkipImg = 4096;                // cam_solve `skip` bit: [S + D; -b^T] already in Abuf (solver layout)
+#ifndef ME_SOLVE_IMG
+#define ME_SOLVE_IMG 1  // non-fused assembly writes the solver's image (0: S | b | diag U, loaded by the solve)
+#endif
 constexpr int kSolveMwMinTs = 16;             // block steps from which the trailing workers are used
 
 template <bool SC1>
@@ -1758,7 +1762,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const double* S0 = b.S;
   const int nn = n * n;
   const bool early0 = kPipe && ME_SOLVE_EARLY0 && fused;
-  if (kLds && fused) {
+  const bool img_ready = (skip & kSkipImg) != 0;  // s_assemble_kernel wrote the image into Abuf (non-fused)
+  if (!kLds && img_ready) {
+    // the working matrix is Abuf itself: nothing to load
+  } else if (kLds && (fused || img_ready)) {
     // the assemblers wrote the solver's image (s_assemble_body img): N x ld
     // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
     // coherent reads (sc1); the barrier below retires them (vmcnt)
@@ -3411,13 +3418,18 @@ int enqueue_linearize(Plan& P) {
 
 // S / b assembly; its last workgroup closes the linearisation (lin_finalize).
 // Sharded: S / b unpacked from the all-reduced exchange.
-int enqueue_assemble(Plan& P) {
+// img: the assembly writes the camera solve's image of [S + D; -b^T] (the
+// solver's padded layout, s_assemble_body) into Abuf, so the solve that
+// follows loads nothing: its element-wise load of S cost wg0 ~70 us at config
+// 5 (tools/solve_ts.py).  Not with full_S (S itself is read back).
+int enqueue_assemble(Plan& P, bool img = false) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
   const int mode = P.comm ? SA_UNPACK : SA_SUM;
   if (g.m > 0)
     hipLaunchKernelGGL(s_assemble_kernel, dim3(blocks((long)g.npairs * 256, kSaElems) + 1), dim3(kBlock), 0,
-                       c->stream, g, P.b, P.o, (const double*)P.gc_raw, P.full_S ? 1 : 0, mode);
+                       c->stream, g, P.b, P.o, (const double*)P.gc_raw, P.full_S ? 1 : 0, mode,
+                       img && !P.full_S ? P.b.Abuf : nullptr);
   else
     hipLaunchKernelGGL(lin_finalize_kernel, dim3(1), dim3(kFinBlock), 0, c->stream, g, P.b, P.o,
                        (const double*)P.gc_raw);
@@ -3460,21 +3472,23 @@ int enqueue_iteration(Plan& P, bool last = false) {
   // they unpack the exchanged system).
   const bool fuse = g.m > 0 && !P.full_S && !last && !P.sequential && nwk == 0 && !P.no_fused_asm;
   const int nasm = fuse ? blocks((long)g.npairs * 256, kSolveBlock / kSaGroups) : 0;
-  if (!fuse) ME_TRY(enqueue_assemble(P));
+  const bool img = !fuse && !last && g.m > 0 && !P.full_S && ME_SOLVE_IMG;
+  if (!fuse) ME_TRY(enqueue_assemble(P, img));
   if (last) return me_check_launch(c, "BA iteration");
   if (g.m == 0) ME_HIP(c, hipMemsetAsync(P.b.scal + R_COUNT, 0, 8, s));
   {
     me_ktimer t(c, ME_KT_BA_SOLVE);
     const double* gc = P.gc_raw;
+    const int sk = P.diag_skip | (img ? kSkipImg : 0);
     if (P.use_lds)
-      hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
-                         0, nasm, gc);
+      hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
+                         nasm, gc);
     else if (nwk > 0)
-      hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o,
-                         P.diag_skip, nwk, 0, gc);
+      hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, nwk,
+                         0, gc);
     else
-      hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, P.diag_skip,
-                         0, nasm, gc);
+      hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
+                         nasm, gc);
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);
