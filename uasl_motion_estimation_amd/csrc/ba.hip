@@ -1673,8 +1673,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     if (threadIdx.x == 0) atomicMin(&g_asm_first, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
     // (sharded: the assemblers unpack the all-reduced exchange instead of summing partials)
-    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM, kLds ? b.Abuf : nullptr,
-                                       &o);
+    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM,
+                                       kLds || ME_SOLVE_IMG ? b.Abuf : nullptr, &o);
     drain_and_barrier();  // every wave's written-through stores have left
 #ifdef ME_SOLVE_TS
     if (threadIdx.x == 0) atomicMax(&g_asm_last, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -1762,10 +1762,16 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const double* S0 = b.S;
   const int nn = n * n;
   const bool early0 = kPipe && ME_SOLVE_EARLY0 && fused;
-  const bool img_ready = (skip & kSkipImg) != 0;  // s_assemble_kernel wrote the image into Abuf (non-fused)
+  // the image of [S + D; -b^T] in Abuf: written by s_assemble_kernel (non-fused), or by this launch's
+  // assemblers (fused; written through)
+  const bool img_ready = (skip & kSkipImg) != 0 || (fused && (kLds || ME_SOLVE_IMG));
   if (!kLds && img_ready) {
-    // the working matrix is Abuf itself: nothing to load
-  } else if (kLds && (fused || img_ready)) {
+    // the working matrix is Abuf itself: nothing to load.  (Fused: the
+    // assemblers' written-through stores bypassed this XCD's L2, which may
+    // still hold lines of Abuf from the previous launch's factorisation: an
+    // agent-scope acquire invalidates them before the first plain load.)
+    if (fused) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  } else if (kLds && img_ready) {
     // the assemblers wrote the solver's image (s_assemble_body img): N x ld
     // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
     // coherent reads (sc1); the barrier below retires them (vmcnt)
