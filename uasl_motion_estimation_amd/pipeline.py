@@ -911,12 +911,15 @@ class WindowedStereoVO:
         self.nx = max(1, int(round(math.sqrt(cfg.n_feats * aw / ah))))
         self.ny = max(1, int(math.ceil(cfg.n_feats / self.nx)))
         self.cw, self.ch = aw / self.nx, ah / self.ny
-        # track table (structure of arrays, index = creation order = ID order)
-        self.ids = np.zeros(0, np.int64)
-        self.X = np.zeros((0, 3))
-        self.active = np.zeros(0, bool)
-        self.first = np.zeros(0, np.int64)   # first frame still held (after pops)
-        self.last = np.zeros(0, np.int64)    # last frame observed
+        # track table (structure of arrays, index = creation order = ID order):
+        # ids, X, active, first (first frame still held, after pops), last
+        # (last frame observed) are views of the first n rows of capacity
+        # buffers, two sets: appends write the tail in place, a pop compacts
+        # into the other set (one copy per keyframe instead of two)
+        self._tab = [None, None]
+        self._tcur, self._tn = 0, 0
+        self._tab_alloc(0, 4096)
+        self._tab_view()
         self.latest_id = 0                   # WBA_Point<pair<Point2f,Point2f>>::latestID
         self.obs = {}                        # t -> (track IDs int64, ascending; (n, 4) float32 {xl, yl, xr, yr})
         self.poses = {}                      # t -> {t, angle-axis} world -> camera
@@ -996,16 +999,36 @@ class WindowedStereoVO:
         R = aa_to_R(pose[3:])
         return (pc - pose[:3][None, :]) @ R  # R^T (pc - t), row form
 
+    _TAB = (("ids", np.int64, ()), ("X", np.float64, (3,)), ("active", bool, ()), ("first", np.int64, ()),
+            ("last", np.int64, ()))
+
+    def _tab_alloc(self, k, cap):
+        self._tab[k] = {nm: np.zeros((cap,) + sh, dt) for nm, dt, sh in self._TAB}
+
+    def _tab_view(self):
+        b, n = self._tab[self._tcur], self._tn
+        self.ids, self.X, self.active = b["ids"][:n], b["X"][:n], b["active"][:n]
+        self.first, self.last = b["first"][:n], b["last"][:n]
+
     def _add_tracks(self, t, uv, xr, pose):
         n = len(uv)
-        ids = np.arange(self.latest_id, self.latest_id + n, dtype=np.int64)
+        n0 = self._tn
+        b = self._tab[self._tcur]
+        if n0 + n > len(b["ids"]):  # grow: the live rows into a larger set
+            cap = 2 * (n0 + n)
+            self._tab_alloc(self._tcur, cap)
+            for nm, _, _ in self._TAB:
+                self._tab[self._tcur][nm][:n0] = b[nm][:n0]
+            b = self._tab[self._tcur]
+        b["ids"][n0:n0 + n] = np.arange(self.latest_id, self.latest_id + n, dtype=np.int64)
         self.latest_id += n
-        self.ids = np.concatenate([self.ids, ids])
-        self.X = np.concatenate([self.X, self._triangulate(uv, xr, pose)])
-        self.active = np.concatenate([self.active, np.ones(n, bool)])
-        self.first = np.concatenate([self.first, np.full(n, t, np.int64)])
-        self.last = np.concatenate([self.last, np.full(n, t, np.int64)])
-        return np.arange(len(self.ids) - n, len(self.ids), dtype=np.int64)
+        b["X"][n0:n0 + n] = self._triangulate(uv, xr, pose)
+        b["active"][n0:n0 + n] = True
+        b["first"][n0:n0 + n] = t
+        b["last"][n0:n0 + n] = t
+        self._tn = n0 + n
+        self._tab_view()
+        return np.arange(n0, n0 + n, dtype=np.int64)
 
     def _wait(self, fn, *a):
         import time
@@ -1050,7 +1073,9 @@ class WindowedStereoVO:
         if self.prev_imgs is not None and self.active.any():
             act = np.flatnonzero(self.active)
             pid, puv = self.obs[self.prev_t]
-            pos = np.searchsorted(pid, self.ids[act])
+            aid = self.ids[act]
+            # (the active tracks are exactly the features of keyframe t-1, in ID order, as a rule)
+            pos = np.arange(len(pid)) if len(aid) == len(pid) and np.array_equal(aid, pid) else np.searchsorted(pid, aid)
             kh = self.be.klt_submit(self.prev_imgs, imgs, np.ascontiguousarray(puv[pos, :2]))
         # 2. pops of frame t-1's completion (active tracks keep their order)
         if self._pending is not None:
@@ -1274,8 +1299,9 @@ class WindowedStereoVO:
                      last=self.last[upts], status=s.get("status"), termination=s.get("termination"))
             os.environ.pop("ME_VO_DUMP_FAILED")
         if s.get("status", 2) == 2:
+            c = np.asarray(c, np.float64)  # (a fresh array per result: its rows are kept as the poses)
             for k, f in enumerate(range(f0, t + 1)):
-                self.poses[f] = np.asarray(c[k], np.float64).copy()
+                self.poses[f] = c[k]
             self.X[j[live]] = np.asarray(p)[live]
         return len(wids), nobs, s
 
@@ -1292,8 +1318,16 @@ class WindowedStereoVO:
             if self.log_events:
                 self._ev.append(("del", self.ids[np.flatnonzero(dead)].copy()))
             keep = ~dead  # (the observation store holds IDs: nothing to re-index)
-            self.ids, self.X, self.active = self.ids[keep], self.X[keep], self.active[keep]
-            self.first, self.last = self.first[keep], self.last[keep]
+            n2 = int(keep.sum())
+            k = 1 - self._tcur
+            cap = len(self._tab[self._tcur]["ids"])
+            if self._tab[k] is None or len(self._tab[k]["ids"]) < cap:
+                self._tab_alloc(k, cap)
+            src, dst = self._tab[self._tcur], self._tab[k]
+            for nm, _, _ in self._TAB:
+                np.compress(keep, src[nm][:self._tn], axis=0, out=dst[nm][:n2])
+            self._tcur, self._tn = k, n2
+            self._tab_view()
 
 
 def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_div: int = 1, first_id: int = 0):
