@@ -52,11 +52,38 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* 
   __syncthreads();
 }
 
-// sum over aligned groups of W lanes (xor butterfly: every lane gets the total)
+// Reductions over aligned groups of W lanes, every lane ending with the same
+// bits: each level combines a lane's value with one from the sibling block
+// (the blocks are uniform after the previous level, and a + b == b + a
+// exactly).  Within a 16-lane row the partners come from DPP (quad permutes,
+// row half-mirror, row mirror: a VALU move each); only the 16- and 32-lane
+// levels go through the LDS crossbar (ds_bpermute).  (Round 3 used an xor
+// butterfly of lane shuffles for every level.)
+#ifndef ME_GROUP_DPP
+#define ME_GROUP_DPP 1
+#endif
+template <int Ctrl>
+__device__ __forceinline__ int dpp_i32(int x) {
+  return __builtin_amdgcn_mov_dpp(x, Ctrl, 0xf, 0xf, false);
+}
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  return __hiloint2double(dpp_i32<Ctrl>(__double2hiint(x)), dpp_i32<Ctrl>(__double2loint(x)));
+}
+constexpr int kDppQuadSwap1 = 0xB1, kDppQuadSwap2 = 0x4E, kDppRowHalfMirror = 0x141, kDppRowMirror = 0x140;
 template <int W>
 __device__ __forceinline__ double group_sum(double x) {
+  if (!ME_GROUP_DPP) {
 #pragma unroll
-  for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+    for (int off = W / 2; off > 0; off >>= 1) x += __shfl_xor(x, off, W);
+    return x;
+  }
+  if (W >= 2) x += dpp_f64<kDppQuadSwap1>(x);
+  if (W >= 4) x += dpp_f64<kDppQuadSwap2>(x);
+  if (W >= 8) x += dpp_f64<kDppRowHalfMirror>(x);
+  if (W >= 16) x += dpp_f64<kDppRowMirror>(x);
+  if (W >= 32) x += __shfl_xor(x, 16, W);
+  if (W >= 64) x += __shfl_xor(x, 32, W);
   return x;
 }
 
@@ -532,14 +559,22 @@ __host__ __device__ inline size_t schur_lds_bytes(int P, int Rz) { return 8 * (s
 
 template <int W>
 __device__ __forceinline__ int group_min(int x) {
-#pragma unroll
-  for (int off = W / 2; off > 0; off >>= 1) x = min(x, __shfl_xor(x, off, W));
+  if (W >= 2) x = min(x, dpp_i32<kDppQuadSwap1>(x));
+  if (W >= 4) x = min(x, dpp_i32<kDppQuadSwap2>(x));
+  if (W >= 8) x = min(x, dpp_i32<kDppRowHalfMirror>(x));
+  if (W >= 16) x = min(x, dpp_i32<kDppRowMirror>(x));
+  if (W >= 32) x = min(x, __shfl_xor(x, 16, W));
+  if (W >= 64) x = min(x, __shfl_xor(x, 32, W));
   return x;
 }
 template <int W>
 __device__ __forceinline__ int group_max(int x) {
-#pragma unroll
-  for (int off = W / 2; off > 0; off >>= 1) x = max(x, __shfl_xor(x, off, W));
+  if (W >= 2) x = max(x, dpp_i32<kDppQuadSwap1>(x));
+  if (W >= 4) x = max(x, dpp_i32<kDppQuadSwap2>(x));
+  if (W >= 8) x = max(x, dpp_i32<kDppRowHalfMirror>(x));
+  if (W >= 16) x = max(x, dpp_i32<kDppRowMirror>(x));
+  if (W >= 32) x = max(x, __shfl_xor(x, 16, W));
+  if (W >= 64) x = max(x, __shfl_xor(x, 32, W));
   return x;
 }
 
