@@ -918,6 +918,7 @@ class WindowedStereoVO:
         # into the other set (one copy per keyframe instead of two)
         self._tab = [None, None]
         self._tcur, self._tn = 0, 0
+        self._gen, self._remap = 0, None  # compactions so far, and the last one's index map
         self._tab_alloc(0, 4096)
         self._tab_view()
         self.latest_id = 0                   # WBA_Point<pair<Point2f,Point2f>>::latestID
@@ -1210,7 +1211,7 @@ class WindowedStereoVO:
         f0 = max(0, t - cfg.window + 1)
         if t - f0 + 1 <= cfg.fixed_frames:
             return None
-        pt, pf0, pwids, _ = self._pending[4]
+        pt, pf0, pwids = self._pending[4][:3]
         nc = t - f0 + 1
         k1 = t - 1 - f0
         if t == 1 or (t - 2) not in self.poses:
@@ -1248,10 +1249,10 @@ class WindowedStereoVO:
             self.be._K, self.be._calib = self.K, (cfg.baseline, cfg.feat_var, cfg.fixed_frames)
             n_obs = self._wait(self.be.ba_submit_window, t, f0, self.ids[upts].astype(np.int32), self.X[upts], cams,
                                cfg.ba_iters, chain)
-            return (t, f0, self.ids[upts].copy(), n_obs)
+            return (t, f0, self.ids[upts].copy(), n_obs, upts, self._gen)
         bp = self.ba_problem(t, f0, upts)
         self._wait(self.be.ba_submit, bp, cfg.ba_iters)
-        return (t, f0, self.ids[upts].copy(), len(bp.obs))
+        return (t, f0, self.ids[upts].copy(), len(bp.obs), upts, self._gen)
 
     def ba_problem(self, t, f0, upts):
         """The window [f0, t]'s BA problem on the host (host-path backends;
@@ -1285,12 +1286,19 @@ class WindowedStereoVO:
     def _ba_finish(self, ba):
         if ba is None:
             return 0, 0, {"iterations": 0, "final_cost": float("nan")}
-        t, f0, wids, nobs = ba
+        t, f0, wids, nobs, upts, gen = ba
         c, p, s = self._wait(self.be.ba_result)
-        # the window's tracks by ID (pops may have compacted the table since the submit; a track
-        # popped out of the table, seen only in the window's first keyframe, needs no landmark)
-        j = np.minimum(np.searchsorted(self.ids, wids), max(len(self.ids) - 1, 0))
-        live = (self.ids[j] == wids) if len(self.ids) else np.zeros(len(wids), bool)
+        # the window's tracks now (a pop may have compacted the table since the submit -- its index map;
+        # a track popped out of the table, seen only in the window's first keyframe, needs no landmark)
+        if gen == self._gen:
+            j, live = upts, np.ones(len(upts), bool)
+        elif gen + 1 == self._gen:
+            j = self._remap[upts]
+            live = j >= 0
+            j = np.maximum(j, 0)
+        else:  # (not reached by the loop: one pop at most between a window's submit and its result)
+            j = np.minimum(np.searchsorted(self.ids, wids), max(len(self.ids) - 1, 0))
+            live = (self.ids[j] == wids) if len(self.ids) else np.zeros(len(wids), bool)
         if s.get("status", 2) != 2 and os.environ.get("ME_VO_DUMP_FAILED"):  # diagnostics: the failed window
             upts = j[live]
             bp = self.ba_problem(t, f0, upts)
@@ -1312,7 +1320,9 @@ class WindowedStereoVO:
             self.be.window_pop(f)
             if self.log_events:
                 self._ev.append(("pop", fid.copy()))
-            self.first[np.searchsorted(self.ids, fid)] = f + 1
+            # (the tracks seen in f are those whose first held frame is f: frames pop oldest first and
+            # a track's features are contiguous -- WBA_Point::pop of each of them)
+            self.first[self.first == f] = f + 1
         dead = (self.last < new_first)
         if dead.any():
             if self.log_events:
@@ -1326,6 +1336,9 @@ class WindowedStereoVO:
             src, dst = self._tab[self._tcur], self._tab[k]
             for nm, _, _ in self._TAB:
                 np.compress(keep, src[nm][:self._tn], axis=0, out=dst[nm][:n2])
+            remap = np.cumsum(keep) - 1  # old table index -> new (-1: deleted)
+            remap[dead] = -1
+            self._remap, self._gen = remap, self._gen + 1
             self._tcur, self._tn = k, n2
             self._tab_view()
 
