@@ -156,24 +156,41 @@ def scale_jacobian(sp, weighting=False, ctx: Context | None = None) -> float:
     return JJ.value
 
 
+class ScaleCall:
+    """One me_scale_optimise call in three parts: the arguments built here,
+    run() -- the C calls only, so a worker thread running it holds the GIL
+    for a few bytecodes (ctypes releases it inside) -- and result()."""
+
+    def __init__(self, sp, params: OptimisationParams | None = None, test=False, ctx: Context | None = None,
+                 img_mem: int = ME_HOST, dev_imgs=None, dev_tracks: dict | None = None):
+        self.ctx = ctx or default_context()
+        self.keep = []
+        self.s = scale_struct(sp, self.keep, img_mem, dev_imgs, dev_tracks)
+        self.p = (params or OptimisationParams()).to_c()
+        self.test = int(test)
+        self.stop, self.it, self.nmi = c_int(), c_int(), c_long()
+        self.trace = np.zeros(2 * 400)
+        self.cnt = (c_long(), c_long(), c_long(), c_long())
+
+    def run(self):
+        c = self.ctx
+        c.check(c.lib.me_scale_optimise(c.h, byref(self.s), byref(self.p), self.test, byref(self.stop),
+                                        byref(self.it), _p(self.trace), 400, byref(self.nmi)), "me_scale_optimise")
+        c.check(c.lib.me_scale_last_counters(c.h, *(byref(x) for x in self.cnt)), "me_scale_last_counters")
+
+    def result(self) -> dict:
+        n = min(self.it.value, 400)
+        nres, nneq, nrej, nexe = (x.value for x in self.cnt)
+        return dict(stop=StopCondition(self.stop.value), scale=self.s.scale, iterations=self.it.value,
+                    trace=self.trace[:2 * n].reshape(-1, 2), track_evals=self.nmi.value, res_evals=nres,
+                    neq_evals=nneq, rejections=nrej, executed_evals=nexe)
+
+
 def scale_optimise(sp, params: OptimisationParams | None = None, test=False, ctx: Context | None = None,
                    img_mem: int = ME_HOST, dev_imgs=None, dev_tracks: dict | None = None) -> dict:
-    ctx = ctx or default_context()
-    params = params or OptimisationParams()
-    keep = []
-    s = scale_struct(sp, keep, img_mem, dev_imgs, dev_tracks)
-    p = params.to_c()
-    stop, it, nmi = c_int(), c_int(), c_long()
-    trace = np.zeros(2 * 400)
-    ctx.check(ctx.lib.me_scale_optimise(ctx.h, byref(s), byref(p), int(test), byref(stop), byref(it), _p(trace), 400,
-                                        byref(nmi)), "me_scale_optimise")
-    n = min(it.value, 400)
-    nres, nneq, nrej, nexe = c_long(), c_long(), c_long(), c_long()
-    ctx.check(ctx.lib.me_scale_last_counters(ctx.h, byref(nres), byref(nneq), byref(nrej), byref(nexe)),
-              "me_scale_last_counters")
-    return dict(stop=StopCondition(stop.value), scale=s.scale, iterations=it.value,
-                trace=trace[:2 * n].reshape(-1, 2), track_evals=nmi.value, res_evals=nres.value,
-                neq_evals=nneq.value, rejections=nrej.value, executed_evals=nexe.value)
+    call = ScaleCall(sp, params, test, ctx, img_mem, dev_imgs, dev_tracks)
+    call.run()
+    return call.result()
 
 
 def scale_state_mi(sp, ctx: Context | None = None):

@@ -663,18 +663,32 @@ class GPUBackend(Backend):
         return self._view(ho, np.float32, n).copy(), self._view(ho, np.uint8, n, 4 * n).astype(bool)
 
     def scale_submit(self, sp, params):
-        """The scale LM on the front-end context, run by a worker thread (the
-        C call releases the GIL): the loop books the keyframe and queues the
-        next BA meanwhile; scale_result joins it."""
+        """The scale LM on the front-end context, run by a worker thread: the
+        arguments are built here, the worker only makes the C calls (which
+        release the GIL), and the loop yields once so the worker starts before
+        the loop's next Python stretch; the loop books the keyframe and queues
+        the next BA meanwhile; scale_result joins it."""
+        import time
+
+        from ._lib import ME_DEVICE
+        from .optimisation import ScaleCall
+
         if self._scale_pool is None:
             from concurrent.futures import ThreadPoolExecutor
 
             self._scale_pool = ThreadPoolExecutor(max_workers=1)
-        self._scale_res = self._scale_pool.submit(self.scale_optimise, sp, params)
+        imgs = sp.imgs_handle
+        call = ScaleCall(sp, params, ctx=self.tctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
+        self._scale_res = (self._scale_pool.submit(call.run), call)
+        time.sleep(0)  # (a GIL hand-over: the worker enters the C call now, not at the loop's next blocking call)
 
     def scale_result(self) -> dict:
         r, self._scale_res = self._scale_res, None
-        return r.result() if r is not None else None
+        if r is None:
+            return None
+        fut, call = r
+        fut.result()
+        return call.result()
 
     # ---- device-resident BA window
     device_window = True
