@@ -33,6 +33,9 @@ using namespace me_dev;
 #ifndef QUAD_U
 #define QUAD_U 4  // quad kernel: walk iterations in flight per lane (table gathers overlapped)
 #endif
+#ifndef MI_PACK
+#define MI_PACK 1  // quad kernel: packed marginal words for N <= 127 (0: byte marginals, float c3 per term)
+#endif
 #ifndef MI_PERM
 #define MI_PERM 37  // histogram update order: pixel p = (k * MI_PERM) mod (PW PH), 1 = row-major
 #endif
@@ -359,17 +362,36 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
 //    reference's float loop, mutual_information.cpp:78-84).
 // Group g's word w lives at lds[16 w + g]: the 16 quads of a wave never
 // share a bank; lanes of one quad do when their words agree mod 4.
-// group words: [0,100) joint, [100,105) right marginal, [105,126) compacted row table (20 + 1 spare),
+// unpacked group words: [0,100) joint, [100,105) right marginal, [105,126) compacted row table (20 + 1 spare),
 // [126,132) its left marginals (bytes), [132,136) lane starts, [136, 136 + N) term slots
-constexpr int kQuadBlock = 64, kQuadGroups = 16, kQuadJoint = 100, kQuadCR = 100, kQuadRows = 105, kQuadRowCL = 126,
-              kQuadStart = 132, kQuadTerms = 136;
+// Packed layout (N <= 127 pixels): the right marginal as one word per column
+// and the row table's left marginals as words, each m -> c3(m) << 13 | m (m - 1) / 2
+// (c3(127) < 2^19, 127 * 126 / 2 < 2^13).  For m >= 1 the words order as m
+// does, so the walk's table index is (max >> 13) + (min & 0x1fff) + cJ - 1 --
+// five operations instead of the float c3 and the triangle product per term.
+// Lane 0 adds its own bins' terms (the first floor(T / 4) of the order) as the
+// walk loads them, so only the other lanes' terms go through slots.
+// group words: [0,100) joint, [100,120) column words, [120,140) row table (no
+// spare: the walk's look-ahead stops at entry 19), [140,160) its left-marginal
+// words, [160,164) lane starts, [164, 164 + N - N / 4) term slots: 255 words
+// for N = 121 (unpacked: 257 at N = 121, 9 workgroups per CU; packed: 10)
+constexpr int kQuadBlock = 64, kQuadGroups = 16;
 
 template <int PW, int PH>
 struct QuadShape {
-  static constexpr int kSlots = (PW > 0 && PH > 0) ? PW * PH : 255;  // >= non-empty bins
-  static constexpr int kWords = kQuadTerms + kSlots;
+  static constexpr bool kPack = MI_PACK && PW > 0 && PH > 0 && PW * PH <= 127;
+  static constexpr int kN = (PW > 0 && PH > 0) ? PW * PH : 255;               // >= non-empty bins
+  static constexpr int kSlots = kPack ? kN - kN / 4 : kN;
+  static constexpr int kCR = 100, kRowTab = kPack ? 120 : 105, kRowCL = kPack ? 140 : 126,
+                       kStart = kPack ? 160 : 132, kTerms = kStart + 4, kClear = kPack ? kStart : kRowCL,
+                       kLastE = kPack ? 19 : 20;  // last row-table entry the walk reads
+  static constexpr int kWords = kTerms + kSlots;
   static constexpr int kRows = PH > 0 ? (PH + 3) / 4 : 4;  // patch rows per lane (PH <= 15)
 };
+
+__device__ __forceinline__ uint32_t mi_pack(uint32_t m) {
+  return ((uint32_t)mi_c3((int)m) << 13) | (mul_u24(m, m - 1u) >> 1);
+}
 
 // Quad reductions over lanes 4g..4g+3 by DPP quad permutes (no LDS round trip).
 template <int CTRL>
@@ -470,7 +492,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
   const int lane = threadIdx.x, g = lane >> 2, q = lane & 3;
   uint32_t* hg = lds + g;  // word w of this quad's pair: hg[16 w]
   // joint words zero (the walk's clears keep them so); row table entries always name a row of this region
-  for (int w = q; w < kQuadRowCL; w += 4) hg[16 * w] = 0u;
+  for (int w = q; w < QS::kClear; w += 4) hg[16 * w] = 0u;
   const __amdgpu_buffer_rsrc_t rtab = __builtin_amdgcn_make_buffer_rsrc((void*)tab, (short)0, tab_bytes, 0x00020000);
   const int ntot = EPI ? (em.n_dev ? min(n, *em.n_dev) : n) * em.nd : n;
   for (int k0 = blockIdx.x * kQuadGroups; k0 < ntot; k0 += gridDim.x * kQuadGroups) {
@@ -533,9 +555,12 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     }
 #pragma unroll
     for (int m = 0; m < 5; ++m) cr4[m] = quad_sum(cr4[m]);
-    if (q == 0) {
+    if (QS::kPack) {  // lane q: columns 4m + q
 #pragma unroll
-      for (int m = 0; m < 5; ++m) hg[16 * (kQuadCR + m)] = cr4[m];
+      for (int m = 0; m < 5; ++m) hg[16 * (QS::kCR + 4 * m + q)] = mi_pack((cr4[m] >> (8 * q)) & 0xffu);
+    } else if (q == 0) {
+#pragma unroll
+      for (int m = 0; m < 5; ++m) hg[16 * (QS::kCR + m)] = cr4[m];
     }
     // Global order = rows ascending, bins ascending within a row.  Per own row:
     // P = bins in earlier rows (its first slot), E = non-empty rows before it
@@ -553,8 +578,9 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     const uint32_t e4 = __builtin_amdgcn_sad_u8(na03, 0u, 0u) + quad_exscan(n4, q);
     // Lane q' takes the bins with slots [b_q', b_q'+1), b_q' = floor(q' T / 4): the
     // owner of the row holding slot b_q' leaves lane q' its start (table entry, bins to skip).
-    uint32_t* rowtab = hg + 16 * kQuadRows;
-    uint8_t* clc = reinterpret_cast<uint8_t*>(hg + 16 * kQuadRowCL);
+    uint32_t* rowtab = hg + 16 * QS::kRowTab;
+    uint32_t* rowcw = hg + 16 * QS::kRowCL;  // (packed layout: left-marginal words)
+    uint8_t* clc = reinterpret_cast<uint8_t*>(rowcw);
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk) {
       const int cnt = kk < 4 ? (int)((c03 >> (8 * kk)) & 0xff) : (int)c4;
@@ -562,37 +588,46 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
       const int E = kk < 4 ? (int)((e03 >> (8 * kk)) & 0xff) : (int)e4;
       if (cnt > 0) {
         rowtab[16 * E] = rb[kk] | ((uint32_t)(q + 4 * kk) << 20);
-        clc[64 * (E >> 2) + (E & 3)] = (uint8_t)(cl >> (8 * kk));
+        if (QS::kPack)
+          rowcw[16 * E] = mi_pack((uint32_t)(cl >> (8 * kk)) & 0xffu);
+        else
+          clc[64 * (E >> 2) + (E & 3)] = (uint8_t)(cl >> (8 * kk));
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const int bq = (qq * total) >> 2;
-          if (P <= bq && bq < P + cnt) hg[16 * (kQuadStart + qq)] = (uint32_t)E | ((uint32_t)(bq - P) << 8);
+          if (P <= bq && bq < P + cnt) hg[16 * (QS::kStart + qq)] = (uint32_t)E | ((uint32_t)(bq - P) << 8);
         }
       }
     }
     wave_sync();  // right marginal, row table and starts visible to the quad
     const int s0 = (q * total) >> 2, nq = (((q + 1) * total) >> 2) - s0;
     const int tmax = QUAD_EXP == 1 ? 0 : wave_max(nq);
-    float* slots = reinterpret_cast<float*>(hg + 16 * kQuadTerms);
-    const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * kQuadCR);
+    float* slots = reinterpret_cast<float*>(hg + 16 * QS::kTerms);
+    const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * QS::kCR);
+    const uint32_t* colw = hg + 16 * QS::kCR;  // (packed layout)
     const uint8_t* jnt = reinterpret_cast<const uint8_t*>(hg);
     int e = 0;
     uint32_t bits = 0, ent = 0, cL = 0, nxt = 0, ncl = 0;
     if (nq > 0) {
-      const uint32_t st = hg[16 * (kQuadStart + q)];
+      const uint32_t st = hg[16 * (QS::kStart + q)];
       e = (int)(st & 0xff);
       ent = rowtab[16 * e];
-      cL = clc[64 * (e >> 2) + (e & 3)];
+      cL = QS::kPack ? rowcw[16 * e] : clc[64 * (e >> 2) + (e & 3)];
       bits = ent & 0xfffffu;
       for (uint32_t sk = st >> 8; sk > 0; --sk) bits &= bits - 1u;
     }
-    nxt = rowtab[16 * (e + 1)];
-    ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+    nxt = rowtab[16 * min(e + 1, QS::kLastE)];
+    ncl = QS::kPack ? rowcw[16 * min(e + 1, QS::kLastE)] : clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
     int rowb = 64 * 5 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
     constexpr int kU = QUAD_U;
     float vp[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
+    // packed: lane 0 sums its terms in order as they arrive (finished lanes load +0.0f)
+    // and the others store theirs from slot 0 on
+    float acc = 0.0f;
+    const bool keep = !QS::kPack || q != 0;
+    const int sb = QS::kPack ? s0 - (total >> 2) : s0;
     for (int t = 0; t < tmax; t += kU) {
       float v[kU];
 #pragma unroll
@@ -601,9 +636,16 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         bits &= bits - 1u;
         const int jo = 64 * (j >> 2) + (j & 3);
         const uint32_t cJ = jnt[rowb + jo];
-        const uint32_t cR = crb[jo];
-        const int a = (int)max(cL, cR), b = (int)min(cL, cR);
-        const int idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + (int)cJ;
+        int idx;
+        if (QS::kPack) {  // cL, cR: packed marginal words
+          const uint32_t cR = colw[16 * j];
+          const uint32_t a = max(cL, cR), b = min(cL, cR);
+          idx = (int)((a >> 13) + (b & 0x1fffu) + cJ);
+        } else {
+          const uint32_t cR = crb[jo];
+          const int a = (int)max(cL, cR), b = (int)min(cL, cR);
+          idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + (int)cJ;
+        }
         const int off = t + u < nq ? 4 * (idx - 1) : 0x7ffffff0;
         if (QUAD_EXP == 4)
           v[u] = (float)off;
@@ -611,24 +653,28 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
           v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
         // next non-empty row of the compacted table (read one ahead)
         const bool z = bits == 0u;
-        e = z ? min(e + 1, 20) : e;
+        e = z ? min(e + 1, QS::kLastE) : e;
         bits = z ? (nxt & 0xfffffu) : bits;
         cL = z ? ncl : cL;
         rowb = z ? 64 * 5 * (int)(nxt >> 20) : rowb;
-        nxt = rowtab[16 * min(e + 1, 20)];
-        ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+        nxt = rowtab[16 * min(e + 1, QS::kLastE)];
+        ncl = QS::kPack ? rowcw[16 * min(e + 1, QS::kLastE)] : clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+      for (int u = 0; u < kU; ++u) {
+        if (QS::kPack) acc += vp[u];
+        if (keep && t - kU + u >= 0 && t - kU + u < nq) slots[16 * (sb + t - kU + u)] = vp[u];
+      }
 #pragma unroll
       for (int u = 0; u < kU; ++u) vp[u] = v[u];
     }
     {
       const int t = (tmax + kU - 1) / kU * kU;
 #pragma unroll
-      for (int u = 0; u < kU; ++u)
-        if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+      for (int u = 0; u < kU; ++u) {
+        if (QS::kPack) acc += vp[u];
+        if (keep && t - kU + u >= 0 && t - kU + u < nq) slots[16 * (sb + t - kU + u)] = vp[u];
+      }
     }
     wave_sync();  // the walk's joint reads precede the clears
     // clear the lane's joint rows for the next pair
@@ -640,16 +686,17 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     }
     wave_sync();  // slots written by the quad
     if (q == 0) {
-      float MI = 0.0f;
+      float MI = acc;
+      const int ns = QS::kPack ? total - (total >> 2) : total;
       int s = 0;
-      for (; s + 8 <= total; s += 8) {
+      for (; s + 8 <= ns; s += 8) {
         float x[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) x[u] = slots[16 * (s + u)];
 #pragma unroll
         for (int u = 0; u < 8; ++u) MI += x[u];
       }
-      for (; s < total; ++s) MI += slots[16 * s];
+      for (; s < ns; ++s) MI += slots[16 * s];
       if (EPI) {
         if (k < ntot) em.sc[k] = live ? (double)MI : -INFINITY;
       } else if (k < n) {
