@@ -1125,7 +1125,10 @@ def main():
         mi_in_frame = {"bound": "hbm", "achieved": round(a_gbs, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                        "frac": round(a_gbs / PEAK_HBM_GBS, 5), "kernel": "scale_res_ctrl_kernel",
                        "track_evaluations_per_frame": round(cfg["n_feats"] * pstats["scale_executed"] / npf, 1),
-                       "us_per_frame": budget["SCALE_RES"]["us_per_frame"]}
+                       "us_per_frame": budget["SCALE_RES"]["us_per_frame"],
+                       # the whole persistent LM launch (control phases and waits included) per track evaluation
+                       "ns_per_track_evaluation": round(1e6 * prof["SCALE_RES"][1] /
+                                                        (cfg["n_feats"] * pstats["scale_executed"]), 2)}
     # the persistent scale LM (one launch per frame) is the whole LM control loop with its
     # phase waits, not one kernel's pass over its data: reported as mi_in_frame, not as the roofline kernel
     persistent_scale = "SCALE_RES" in budget and budget["SCALE_RES"]["launches_per_frame"] <= 1.5
