@@ -619,6 +619,13 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     nxt = rowtab[16 * min(e + 1, QS::kLastE)];
     ncl = QS::kPack ? rowcw[16 * min(e + 1, QS::kLastE)] : clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
     int rowb = 64 * 5 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
+    // packed: the look-ahead entry and the row's joint bytes as byte offsets into the
+    // workgroup's LDS (group base included: no index arithmetic per term)
+    const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(lds);
+    const uint32_t gb = 4u * (uint32_t)g;
+    uint32_t eb = gb + 64u * (uint32_t)(QS::kRowTab + min(e + 1, QS::kLastE));
+    const uint32_t eblast = gb + 64u * (uint32_t)(QS::kRowTab + QS::kLastE);
+    uint32_t rowo = gb + (uint32_t)rowb;
     constexpr int kU = QUAD_U;
     float vp[kU];
 #pragma unroll
@@ -635,7 +642,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         const int j = __builtin_ctz(bits | 0x100000u);  // < 21
         bits &= bits - 1u;
         const int jo = 64 * (j >> 2) + (j & 3);
-        const uint32_t cJ = jnt[rowb + jo];
+        const uint32_t cJ = QS::kPack ? ldsb[rowo + jo] : jnt[rowb + jo];
         int idx;
         if (QS::kPack) {  // cL, cR: packed marginal words
           const uint32_t cR = colw[16 * j];
@@ -653,12 +660,19 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
           v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
         // next non-empty row of the compacted table (read one ahead)
         const bool z = bits == 0u;
-        e = z ? min(e + 1, QS::kLastE) : e;
         bits = z ? (nxt & 0xfffffu) : bits;
         cL = z ? ncl : cL;
-        rowb = z ? 64 * 5 * (int)(nxt >> 20) : rowb;
-        nxt = rowtab[16 * min(e + 1, QS::kLastE)];
-        ncl = QS::kPack ? rowcw[16 * min(e + 1, QS::kLastE)] : clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+        if (QS::kPack) {
+          rowo = z ? gb + 64u * 5u * (nxt >> 20) : rowo;
+          eb = z && eb < eblast ? eb + 64u : eb;
+          nxt = *reinterpret_cast<const uint32_t*>(ldsb + eb);
+          ncl = *reinterpret_cast<const uint32_t*>(ldsb + eb + 64 * (QS::kRowCL - QS::kRowTab));
+        } else {
+          e = z ? min(e + 1, QS::kLastE) : e;
+          rowb = z ? 64 * 5 * (int)(nxt >> 20) : rowb;
+          nxt = rowtab[16 * min(e + 1, QS::kLastE)];
+          ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
