@@ -63,6 +63,12 @@ def parse():
                     help="config-4 landmark-sharded BA line (SURVEY 8e): over RCCL across the ranks when --gpus > 1, "
                          "two contexts on one GPU (host exchange, the crossover point) at N = 1; 0: off")
     ap.add_argument("--sharded-reps", type=int, default=3)
+    ap.add_argument("--comm", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend for N > 1 (gloo: the sharded BA exchanges host-staged through "
+                         "me_comm_create_callback -- rehearses the N-rank branch without RCCL)")
+    ap.add_argument("--rank-device", choices=("local", "zero"), default="local",
+                    help="GPU per rank: LOCAL_RANK (default) or device 0 for every rank (tests: N ranks on one GPU, "
+                         "--comm gloo only)")
     ap.add_argument("--dist", action="store_true",
                     help="initialise the RCCL process group even at one rank (exercises the RCCL exchange path)")
     ap.add_argument("--pipeline-frames", type=int, default=40,
@@ -545,12 +551,14 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": pmc_traffic("MI"), "kernel": kernel,
            "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
     # VALU-issue roofline: the kernel's wave instructions per pair (SQ_INSTS_VALU of the committed
-    # tools/mi_pmc.sh pass) against one wave64 VALU instruction per SIMD per 4 cycles (1024 SIMDs, 2.4 GHz)
+    # tools/mi_pmc.sh pass) against one wave64 VALU instruction per SIMD per 2 cycles (1024 SIMDs,
+    # 2.4 GHz: MI355X_MICROARCH.md "Wave scheduling" / v_fma_f32 row -- 32 lanes per cycle; one wave
+    # alone issues every 4, but the kernel keeps ~8 waves per CU resident)
     cpath = os.path.join(ROOT, "profiles", MI_COUNTERS + ".json")
     if os.path.exists(cpath):
         cnt = json.load(open(cpath))
         if kernel in cnt.get("kernel", ""):
-            peak = 1024 * 2.4e9 / 4 / 1e9
+            peak = 1024 * 2.4e9 / 2 / 1e9
             ach = cnt["valu_insts_per_pair"] * n_pairs / (avg * 1e-3) / 1e9
             out["valu_issue"] = {"bound": "valu-issue", "achieved": round(ach, 1), "peak": round(peak, 1),
                                  "unit": "G wave-instr/s", "frac": round(ach / peak, 4),
@@ -752,23 +760,40 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
         return (time.perf_counter() - t0) / reps, ss
 
     if dist is not None:
+        from uasl_motion_estimation_amd.optimisation import host_staged_allreduce
+
+        gloo = args.comm == "gloo"
         local, (lo, hi) = shard_landmarks(bp, rank, world)
         d = DeviceBAProblem(local, ctx)
-        comm = rccl_comm(ctx)
-        el, ss = timed_comm(d, comm)
-        cams, pts = d.download()
-        xus = exchange_us(ctx, comm, barrier, [17000, 5])
-        comm.close()
+        if gloo:
+            # host-staged exchange: the kernels and the callback's copies ordered on one torch stream
+            stream = torch.cuda.Stream(device=ctx.device)
+            torch.cuda.set_stream(stream)
+            ctx.set_stream(stream.cuda_stream)
+            comm = Comm.callback(ctx, world, rank, host_staged_allreduce())
+        else:
+            comm = rccl_comm(ctx)
+        try:
+            el, ss = timed_comm(d, comm)
+            cams, pts = d.download()
+            xus = exchange_us(ctx, comm, barrier, [17000, 5])
+        finally:
+            comm.close()
+            if gloo:
+                ctx.set_stream(None)
+                torch.cuda.set_stream(torch.cuda.default_stream(ctx.device))
         d.close()
         par = _shard_parity(cams, pts, lo, hi, ss, ref_cams, ref_pts, s1)
         tt = torch.tensor([el, par["cams_max_rel"], par["pts_max_rel"], 0.0 if par["same_iterations"] else 1.0],
-                          device=f"cuda:{local_rank}", dtype=torch.float64)
+                          device="cpu" if gloo else f"cuda:{local_rank}", dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt[0].item())
         par = {"cams_max_rel": float("%.3g" % tt[1].item()), "pts_max_rel": float("%.3g" % tt[2].item()),
                "same_iterations": tt[3].item() == 0.0}
         par["ok"] = _parity_ok(par)
-        out.update({"mode": f"landmark-sharded over native RCCL (me_comm), {world} ranks, one GPU each",
+        out.update({"mode": (f"landmark-sharded over a host-staged gloo exchange (me_comm_create_callback), {world} "
+                             f"ranks" + (" on one GPU" if args.rank_device == "zero" else ", one GPU each")) if gloo
+                    else f"landmark-sharded over native RCCL (me_comm), {world} ranks, one GPU each",
                     "ranks": world, "sharded_ms": round(1e3 * el, 3),
                     "gate_would_shard": shard_worthwhile(len(bp.obs), world), "exchange_us": xus,
                     "sharded_ba_iter_per_s": round(ss["iterations"] / el, 1),
@@ -1020,6 +1045,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rank_device == "zero":  # (tests: every rank on GPU 0; RCCL cannot run two ranks on one GPU)
+        assert args.comm == "gloo" or world == 1, "--rank-device zero needs --comm gloo"
+        local_rank = 0
     pool = pool1 = None
     model, ncpu, avail = host_cpu()
     cpu_workers = args.cpu_workers or min(16, avail)
@@ -1050,7 +1078,7 @@ def main():
         torch.cuda.set_device(local_rank)
         if "MASTER_ADDR" not in os.environ:  # --dist at one rank without a launcher
             os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="29511", RANK="0", WORLD_SIZE="1")
-        dist.init_process_group("nccl", timeout=timedelta(seconds=180))
+        dist.init_process_group(args.comm, timeout=timedelta(seconds=180))
     from uasl_motion_estimation_amd import synthetic as S
     from uasl_motion_estimation_amd._lib import Context, KT
     from uasl_motion_estimation_amd.klt import klt_params
@@ -1165,10 +1193,11 @@ def main():
     frames_total = stats["frames"]
     ba_total = stats["ba_iters"]
     if dist is not None:
-        tt = torch.tensor([elapsed], device=f"cuda:{local_rank}", dtype=torch.float64)
+        tdev = "cpu" if args.comm == "gloo" else f"cuda:{local_rank}"
+        tt = torch.tensor([elapsed], device=tdev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t_max = float(tt.item())
-        cnt = torch.tensor([stats["frames"], stats["ba_iters"]], device=f"cuda:{local_rank}", dtype=torch.float64)
+        cnt = torch.tensor([stats["frames"], stats["ba_iters"]], device=tdev, dtype=torch.float64)
         dist.all_reduce(cnt)
         frames_total, ba_total = int(cnt[0].item()), int(cnt[1].item())
     value = frames_total / t_max

@@ -709,10 +709,20 @@ class MonoVisualOdometry {
     p.inlier_threshold = m_param.inlier_threshold;
     p.ransac = m_param.ransac ? 1 : 0;
     std::vector<int32_t> inl((size_t)std::max(n, 1));
+    std::array<double, 9> E{};
     int ni = 0, ok = 0;
-    m_ctx->check(me_mono_vo_process(m_ctx->get(), f1.data(), f2.data(), n, &p, m_Rt.data(), m_E.data(), inl.data(),
+    m_ctx->check(me_mono_vo_process(m_ctx->get(), f1.data(), f2.data(), n, &p, m_Rt.data(), E.data(), inl.data(),
                                     &ni, &ok),
                  "MonoVisualOdometry::process");
+    // MonoVisualOdometry.cpp:9-52: fewer than 8 matches leaves m_E and the
+    // inlier / outlier lists as they were; an empty E is assigned (empty) and
+    // the lists are kept; otherwise all three are replaced
+    if (n < 8) return ok != 0;
+    bool any = false;
+    for (double v : E) any = any || v != 0.0;
+    m_E = E;
+    m_E_empty = !any;
+    if (!any) return ok != 0;
     m_inliers.assign(inl.begin(), inl.begin() + ni);
     m_outliers.clear();
     for (int i = 0, k = 0; i < n; ++i) {
@@ -722,7 +732,9 @@ class MonoVisualOdometry {
     return ok != 0;
   }
   const std::array<double, 16>& getMotion() const { return m_Rt; }
+  // the reference's m_E as a 3 x 3 array; essentialMatEmpty() is its m_E.empty()
   const std::array<double, 9>& getEssentialMat() const { return m_E; }
+  bool essentialMatEmpty() const { return m_E_empty; }
   const std::vector<int>& getInliersIdx() const { return m_inliers; }
   const std::vector<int>& getOutliersIdx() const { return m_outliers; }
 
@@ -731,6 +743,7 @@ class MonoVisualOdometry {
   amd::Context* m_ctx;
   std::array<double, 16> m_Rt{};
   std::array<double, 9> m_E{};
+  bool m_E_empty = false;  // (the reference ctor sets m_E = eye(4, 4): not empty)
   std::vector<int> m_inliers, m_outliers;
 };
 

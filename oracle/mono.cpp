@@ -25,7 +25,8 @@
 //    maxIters 1000.  LMedS (param ransac = false): fixed iterations
 //    round(log(1 - prob) / log(1 - 0.55^5)) (>= 3, <= 1000), the model of least
 //    median error (k = count / 2), inliers at
-//    2.5 * 1.4826 * (1 + 5 / (count - 5)) * sqrt(median);
+//    sigma = max(2.5 * 1.4826 * (1 + 5 / (count - 5)) * sqrt(median), 0.001)
+//    (the 0.001 floor restated from OpenCV's ptsetreg.cpp; unpinned here);
 //  * recoverPose (distance threshold 500, as the reference passes): E = U D V^T
 //    (det-corrected), R1 = U W V^T, R2 = U W^T V^T, t = U[:, 2]; per pose each
 //    inlier triangulated by the DLT (right singular vector of the 4 x 4 system
@@ -632,7 +633,9 @@ int oracle_mono_vo_process(const float* f1, const float* f2, int n, const oracle
     }
     if (found) {
       double th = 2.5 * 1.4826 * (1 + 5.0 / (count - 5 > 0 ? count - 5 : 1)) * std::sqrt(min_median);
-      th = std::max(th, 1.1920928955078125e-07 * 100);
+      // sigma = MAX(sigma, 0.001): OpenCV LMeDSPointSetRegistrator (calib3d ptsetreg.cpp), restated
+      // (no OpenCV here to check it against: the LMedS mask is parity unpinned, like the RANSAC path)
+      th = std::max(th, 0.001);
       const float t = (float)(th * th);
       good = 0;
       for (int i = 0; i < count; ++i) {

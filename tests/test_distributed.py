@@ -431,3 +431,31 @@ def test_gpu_sharded_handoff_timeout_on_one_rank_fails_every_rank(ctx):
     assert not any(alive), "a rank is stuck in the exchange"
     ME_ERR_STATE = -5
     assert out == [ME_ERR_STATE, ME_ERR_STATE], out
+
+
+@pytest.mark.gpu
+def test_bench_world2_gloo_sharded_branch(tmp_path):
+    """bench.py's N-rank sharded-BA branch (sharded_ba_line, `dist is not None`) at world size 2 --
+    both ranks on GPU 0 over gloo (--comm gloo --rank-device zero: the exchange host-staged through
+    me_comm_create_callback) -- so its first N-rank run is not the driver's 8-GPU one: the bench
+    line completes and the shards' solve equals the single-GPU solve (its parity field)."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"), "--gpus", "2", "--comm",
+           "gloo", "--rank-device", "zero", "--steps", "2", "--warmup", "1", "--frames", "1", "--no-pipeline",
+           "--pipeline-frames", "0", "--mi-pairs", "0", "--vo-matches", "0", "--sharded-reps", "1",
+           "--profile-steps", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    sb = line["sharded_ba"]
+    assert "error" not in sb, sb
+    assert sb["ranks"] == 2 and "gloo" in sb["mode"], sb
+    assert sb["parity_vs_single_gpu"]["ok"], sb["parity_vs_single_gpu"]
+    assert set(sb["exchange_us"]) == {"17000", "5"}

@@ -126,3 +126,70 @@ def test_stereo_stream_stages_frames_on_the_device(tmp_path, ctx):
         assert np.array_equal(gotL, frames[nb][0]) and np.array_equal(gotR, frames[nb][1]) and stamp == 100 * nb
         seen.append(nb)
     assert seen == [2, 3, 4, 5, 6]  # frames.start .. frames.stop
+
+
+AVI_DIR = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "avi")
+
+
+def test_video_capture_reads_committed_avi():
+    """Uncompressed RIFF AVI (file_IO.h:305-343's cv::VideoCapture, VIDEO mode): the committed
+    fixtures (tests/golden/make_avi.py, an independent RIFF writer) decode to their frames bit for bit --
+    8-bit palettised bottom-up rows with padding, JUNK / odd-sized chunks, and 24-bit BGR top-down."""
+    import os
+
+    exp = np.load(os.path.join(AVI_DIR, "frames.npz"))
+    cap = F.VideoCapture(os.path.join(AVI_DIR, "cam0_image.avi"))
+    assert cap.isOpened() and cap.get(F.CAP_PROP_FRAME_COUNT) == 5
+    assert (cap.get(F.CAP_PROP_FRAME_WIDTH), cap.get(F.CAP_PROP_FRAME_HEIGHT)) == (20, 12)
+    for k in range(5):
+        assert cap.get(F.CAP_PROP_POS_FRAMES) == k
+        ok, img = cap.read()
+        assert ok and img.shape == (12, 20, 3)
+        assert np.array_equal(F.bgr2gray(img), exp["cam0"][k])  # gray palette -> BGR -> gray is exact
+    ok, img = cap.read()
+    assert not ok and img is None  # end of stream
+    c = F.VideoCapture(os.path.join(AVI_DIR, "bgr24.avi"))
+    for k in range(3):
+        ok, img = c.read()
+        assert ok and np.array_equal(img, exp["bgr24"][k])
+    # not an AVI / missing file: not opened (cv::VideoCapture::open fails)
+    assert not F.VideoCapture(os.path.join(AVI_DIR, "image_data.csv")).isOpened()
+    assert not F.VideoCapture(os.path.join(AVI_DIR, "missing.avi")).isOpened()
+
+
+def test_video_capture_rejects_compressed_stream(tmp_path):
+    import os
+
+    data = bytearray(open(os.path.join(AVI_DIR, "bgr24.avi"), "rb").read())
+    i = data.find(b"strf")
+    data[i + 8 + 16:i + 8 + 20] = b"MJPG"  # biCompression
+    p = tmp_path / "mjpg.avi"
+    p.write_bytes(bytes(data))
+    assert not F.VideoCapture(str(p)).isOpened()
+
+
+def test_image_reader_video_mode():
+    """ImageReader(Type::VIDEO) (file_IO.h:300-421): the constructor reads until img_nb reaches
+    frames.start (frame numbers from image_data.csv), readStereo seeks each stream by grabbing to
+    CAP_PROP_POS_FRAMES == img_nb and returns the gray frames; past the CSV's end the pair is empty."""
+    import os
+
+    exp = np.load(os.path.join(AVI_DIR, "frames.npz"))
+    cfg = F.Config()
+    cfg.dataset_info.dir = AVI_DIR
+    cfg.dataset_info.type = "stereo"
+    cfg.frame_info.fframe = 2
+    r = F.ImageReader(cfg, os.path.join(AVI_DIR, "image_data.csv"), F.ImageReader.Type.VIDEO)
+    assert r.isValid() and r.get_img_nb() == 2 and r.img_stamp == 1080
+    for nb in (3, 4):
+        L, R = r.readStereo()
+        assert r.get_img_nb() == nb
+        assert np.array_equal(L, exp["cam0"][nb]) and np.array_equal(R, exp["cam1"][nb])
+    L, R = r.readStereo()
+    assert L is None and R is None
+    cfg.dataset_info.type = "mono"
+    cfg.frame_info.fframe = 0
+    cfg.frame_info.skip = 2
+    m = F.ImageReader(cfg, os.path.join(AVI_DIR, "image_data.csv"), F.ImageReader.Type.VIDEO)
+    assert m.get_img_nb() == 1  # first readMono consumed rows 0 and 1 (skip 2)
+    assert np.array_equal(m.readMono(), exp["cam0"][3])

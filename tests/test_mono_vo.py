@@ -113,3 +113,21 @@ def test_gpu_mono_too_few_matches(ctx):
     f1, f2, p, R, t = S.mono_matches(3, 7)
     vo = MonoVisualOdometry(ctx=ctx)
     assert not vo.process((f1, f2)) and np.array_equal(vo.getMotion(), np.eye(4))
+
+
+@pytest.mark.gpu
+def test_gpu_mono_early_exits_keep_state(ctx):
+    """MonoVisualOdometry.cpp:9-52: < 8 matches returns before touching m_E and the
+    inlier / outlier lists; an empty E is assigned (empty) and the lists are kept."""
+    from uasl_motion_estimation_amd.vo import MonoParameters, MonoVisualOdometry
+
+    f1, f2, p, R, t = S.mono_matches(21, 600, noise=0.3)
+    vo = MonoVisualOdometry(MonoParameters(**p), ctx=ctx)
+    assert vo.process((f1, f2))
+    E0, inl0, out0 = vo.getEssentialMat(), vo.getInliersIdx(), vo.getOutliersIdx()
+    a1, a2, *_ = S.mono_matches(3, 7)
+    assert not vo.process((a1, a2)) and np.array_equal(vo.getMotion(), np.eye(4))
+    assert np.array_equal(vo.getEssentialMat(), E0) and vo.getInliersIdx() == inl0 and vo.getOutliersIdx() == out0
+    b1, b2, *_ = S.mono_matches(12, 20, n_invalid=17)  # 3 valid: no essential matrix
+    assert not vo.process((b1, b2)) and np.array_equal(vo.getMotion(), np.eye(4))
+    assert vo.getEssentialMat().size == 0 and vo.getInliersIdx() == inl0 and vo.getOutliersIdx() == out0

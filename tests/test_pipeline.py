@@ -225,3 +225,27 @@ def test_gpu_epipolar_matcher_equals_host_restatement(ctx, oracle, unique):
     assert np.array_equal(got[0][ref[1]].view(np.uint32), ref[0][ref[1]].view(np.uint32))
     assert ref[1].sum() > n // 4  # the comparison covers many accepted matches
     assert not ref[1][:e].any()  # the border features match nothing
+
+
+@pytest.mark.gpu
+def test_pipeline_gpu_shared_context_equals_overlapped(ctx, seq5):
+    """GPUBackend(overlap=False): one context for the front end and the BA (the
+    scale LM and the BA queueing inline, no worker thread calling the same
+    context) takes the overlapped loop's decisions bit for bit."""
+    a_be = PL.GPUBackend(ctx, overlap=False)
+    assert a_be.shared_ctx and not a_be.async_enqueue
+    try:
+        a = _run(5, 16, a_be, window=8, frames=seq5, ba_iters=10)
+    finally:
+        a_be.close()
+    b_be = PL.GPUBackend(ctx)
+    try:
+        b = _run(5, 16, b_be, window=8, frames=seq5, overlap=True, ba_iters=10)
+    finally:
+        b_be.close()
+    assert a.events == b.events and np.array_equal(a.ids, b.ids)
+    for t in a.poses:
+        assert np.array_equal(a.poses[t], b.poses[t]), t
+    assert np.array_equal(a.X, b.X)
+    assert [(r.scale, r.scale_iters, r.ba_iters) for r in a.results] == [(r.scale, r.scale_iters, r.ba_iters)
+                                                                          for r in b.results]

@@ -168,11 +168,14 @@ class VOParamsC(ctypes.Structure):
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libme_hip.so and declare prototypes.  Raises MEError if missing."""
+def load_library(path: str | None = None):
+    """Load libme_hip.so and declare prototypes.  Raises MEError if missing.
+    ME_LIB (environment) names another build of the same library (A/B timing,
+    tools/gpu_ab.sh); the default is the in-tree build."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("ME_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise MEError(-4, f"{path} not built (run __graft_entry__.build())")
     lib = ctypes.CDLL(path)

@@ -724,7 +724,9 @@ extern "C" int me_mono_vo_process(me_ctx* c, const float* f1, const float* f2, i
       }
     if (best_slot >= 0) {
       double th = 2.5 * 1.4826 * (1 + 5.0 / (count - 5 > 0 ? count - 5 : 1)) * std::sqrt(min_median);
-      th = std::max(th, 1.1920928955078125e-07 * 100);
+      // sigma = MAX(sigma, 0.001): OpenCV LMeDSPointSetRegistrator (calib3d ptsetreg.cpp), restated
+      // (no OpenCV here to check it against: the LMedS mask is parity unpinned, like the RANSAC path)
+      th = std::max(th, 0.001);
       mask_t = (float)(th * th);
     }
   }

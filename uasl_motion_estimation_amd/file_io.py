@@ -6,8 +6,12 @@ structures (file_IO.h:30-141), ``IOFile::openFile`` / ``check_header``
 (:100-131), ``ImageFile::readData`` (:133-145) for ``image_data.csv``, and
 the image loaders ``loadImage`` / ``loadImages`` (cam{0,1}_image%0Nd[_appendix].png,
 :296-364) and ``loadImageKitti`` / ``loadImagesKitti`` (L_/R_ %0Nd .png, rows
-0..373, :313-340).  ``StereoImageStream`` stages frames into pinned host
-memory and uploads them asynchronously to HBM for the device pipeline.
+0..373, :313-340), and ``ImageReader`` (file_IO.h:300-421) in both its
+IMAGES and VIDEO modes -- the latter over ``VideoCapture``, an uncompressed
+RIFF-AVI reader (8-bit palettised / 24-bit BGR frames; no codec exists here,
+so compressed streams do not open, as cv::VideoCapture without a backend).
+``StereoImageStream`` stages frames into pinned host memory and uploads them
+asynchronously to HBM for the device pipeline.
 
 Host-side plumbing (like the reference's); no GPU compute.  Image decoding
 uses Pillow.  ``cv::imread(..., IMREAD_GRAYSCALE)`` semantics: 8-bit gray is
@@ -453,3 +457,264 @@ class StereoImageStream:
                 self._dev[s].copy_(h, non_blocking=True)
             H, W = left.shape
             yield nb, stamp, self._dev[s][0].data_ptr(), self._dev[s][1].data_ptr(), W, H
+
+
+# ------------------------------------------------------------------ video (AVI)
+CAP_PROP_POS_FRAMES = 1  # cv::CAP_PROP_POS_FRAMES
+CAP_PROP_FRAME_WIDTH = 3
+CAP_PROP_FRAME_HEIGHT = 4
+CAP_PROP_FRAME_COUNT = 7
+
+
+class VideoCapture:
+    """The subset of cv::VideoCapture that ImageReader's VIDEO mode uses
+    (file_IO.h:314-316, 366-372, 398-401: open / isOpened / get(CAP_PROP_POS_FRAMES)
+    / grab / operator>>), for uncompressed RIFF AVI only: one video stream of
+    BI_RGB frames ('00db' / '00dc' chunks), 8-bit palettised or 24-bit BGR, bottom-up
+    (positive biHeight) or top-down rows, each row padded to 4 bytes.  There is
+    no codec here, so compressed streams (MJPG, H.264, ...) do not open, exactly
+    as cv::VideoCapture::open fails without a backend for them: isOpened() is
+    False.  Frames come back as OpenCV's default CAP_PROP_CONVERT_RGB output:
+    H x W x 3 BGR uint8 (a palettised frame through its palette), rows top-down.
+    The file is memory-mapped: frames are decoded when read, never all at once."""
+
+    def __init__(self, filename: str | None = None):
+        self._mm = None
+        self._frames: list[tuple[int, int]] = []
+        self._pos = 0
+        self._grabbed = -1
+        self.width = self.height = 0
+        if filename:
+            self.open(filename)
+
+    # --- RIFF walk
+    def open(self, filename: str) -> bool:
+        import mmap
+        import struct
+
+        self.release()
+        try:
+            with open(filename, "rb") as fh:
+                mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+        except (OSError, ValueError):
+            return False
+        try:
+            if len(mm) < 12 or mm[0:4] != b"RIFF" or mm[8:12] != b"AVI ":
+                raise ValueError("not a RIFF AVI file")
+            fmt = None
+            vstream = -1
+            nstream = 0
+            frames: list[tuple[int, int]] = []
+
+            def walk(off: int, end: int, depth: int):
+                nonlocal fmt, vstream, nstream
+                while off + 8 <= end:
+                    cid = bytes(mm[off:off + 4])
+                    size = struct.unpack_from("<I", mm, off + 4)[0]
+                    body = off + 8
+                    if body + size > len(mm):
+                        size = len(mm) - body  # truncated file: keep what is there
+                    if cid in (b"RIFF", b"LIST"):
+                        walk(body + 4, body + size, depth + 1)
+                    elif cid == b"strh":
+                        typ = bytes(mm[body:body + 4])
+                        if typ == b"vids" and vstream < 0:
+                            vstream = nstream
+                        nstream += 1
+                    elif cid == b"strf" and vstream == nstream - 1 and fmt is None:
+                        fmt = (body, size)
+                    elif len(cid) == 4 and cid[2:4] in (b"db", b"dc") and cid[0:2].isdigit():
+                        if vstream >= 0 and int(cid[0:2]) == vstream:
+                            frames.append((body, size))
+                    off = body + size + (size & 1)
+
+            walk(12, len(mm), 0)
+            if fmt is None:
+                raise ValueError("no video stream format")
+            body, size = fmt
+            (_bisz, w, h, _planes, bits, comp, _isz, _xp, _yp, clr_used, _clr_imp) = struct.unpack_from(
+                "<IiiHHIIiiII", mm, body)
+            if comp not in (0,) or bits not in (8, 24):
+                raise ValueError(f"unsupported AVI frame format (compression {comp:#x}, {bits} bits)")
+            pal = None
+            if bits == 8:
+                n = clr_used or 256
+                raw = np.frombuffer(mm, np.uint8, count=4 * n, offset=body + _bisz).reshape(n, 4)
+                pal = np.zeros((256, 3), np.uint8)
+                pal[:n] = raw[:, :3]  # RGBQUAD: B, G, R, reserved
+            self._mm = mm
+            self._frames = frames
+            self._bits = bits
+            self._pal = pal
+            self.width, self.height = int(w), abs(int(h))
+            self._bottom_up = h > 0
+            self._stride = ((self.width * bits // 8) + 3) & ~3
+            return True
+        except (ValueError, struct.error):
+            mm.close()
+            return False
+
+    def isOpened(self) -> bool:
+        return self._mm is not None
+
+    def release(self):
+        if self._mm is not None:
+            self._mm.close()
+        self._mm = None
+        self._frames = []
+        self._pos = 0
+        self._grabbed = -1
+
+    def get(self, prop: int) -> float:
+        if self._mm is None:
+            return 0.0
+        if prop == CAP_PROP_POS_FRAMES:
+            return float(self._pos)
+        if prop == CAP_PROP_FRAME_COUNT:
+            return float(len(self._frames))
+        if prop == CAP_PROP_FRAME_WIDTH:
+            return float(self.width)
+        if prop == CAP_PROP_FRAME_HEIGHT:
+            return float(self.height)
+        return 0.0
+
+    def grab(self) -> bool:
+        if self._mm is None or self._pos >= len(self._frames):
+            self._grabbed = -1
+            return False
+        self._grabbed = self._pos
+        self._pos += 1
+        return True
+
+    def retrieve(self):
+        if self._grabbed < 0:
+            return False, None
+        off, size = self._frames[self._grabbed]
+        w, h, s = self.width, self.height, self._stride
+        if size < s * h:  # a dropped / empty frame chunk
+            return False, None
+        rows = np.frombuffer(self._mm, np.uint8, count=s * h, offset=off).reshape(h, s)
+        if self._bottom_up:
+            rows = rows[::-1]
+        if self._bits == 8:
+            img = self._pal[rows[:, :w]]
+        else:
+            img = rows[:, :3 * w].reshape(h, w, 3).copy()
+        return True, np.ascontiguousarray(img)
+
+    def read(self):
+        if not self.grab():
+            return False, None
+        return self.retrieve()
+
+
+def bgr2gray(img: np.ndarray) -> np.ndarray:
+    """cv::cvtColor(COLOR_BGR2GRAY) on 8U: fixed-point (4899 R + 9617 G + 1868 B + 8192) >> 14."""
+    c = img.astype(np.int32)
+    return ((c[..., 2] * 4899 + c[..., 1] * 9617 + c[..., 0] * 1868 + 8192) >> 14).astype(np.uint8)
+
+
+class ImageReader:
+    """ImageReader (file_IO.h:300-421): the next frame of a dataset, from the PNG
+    directory (Type.IMAGES) or from cam{i}_image.avi (Type.VIDEO), frame numbers
+    from image_data.csv (ImageFile) when it exists, else advanced by
+    frame_info.skip.  The constructor reads until img_nb reaches
+    frame_info.fframe, as the reference does; readStereo / readMono return
+    (left, right) / an image, or empty (None) where the reference returns an
+    empty Mat.  A video frame is seeked by grabbing until CAP_PROP_POS_FRAMES
+    reaches img_nb, then read and converted to gray when it has 3 channels."""
+
+    class Type:
+        IMAGES = 0
+        VIDEO = 1
+
+    def __init__(self, cfg: Config, filename: str = "", type_: int = 0, padding: int = 5):
+        self.cfg = cfg
+        self.padding = padding
+        self.fimage = ImageFile(filename)
+        stereo = cfg.dataset_info.type == "stereo"
+        self.cap = [VideoCapture() for _ in range(2 if stereo else 1)]
+        self.type = type_
+        self.img_nb = 0
+        self.img_stamp = 0
+        if not self.fimage.is_open():
+            print(f"[ImageReader] warning: could not find an image file in {cfg.dataset_info.dir}")
+        if self.type == ImageReader.Type.VIDEO:
+            self._open_video()
+        self._seek_first()
+
+    def _open_video(self):
+        for i, c in enumerate(self.cap):
+            c.open(f"{self.cfg.dataset_info.dir}/cam{i}_image.avi")
+
+    def _seek_first(self):
+        # do { readMono(); } while (img_nb < fframe).  The reference spins for
+        # ever once image_data.csv runs out before fframe (readData fails and
+        # img_nb stops moving); here the loop ends there instead.
+        while True:
+            self._last_ok = True
+            self.readMono()
+            if not (self.img_nb < self.cfg.frame_info.fframe) or not self._last_ok:
+                break
+
+    def openReader(self, filename: str = "", type_: int = 0):
+        self.fimage = ImageFile(filename or f"{self.cfg.dataset_info.dir}/image_data.csv")
+        self.type = type_
+        if not self.fimage.is_open():
+            print(f"[ImageReader] warning: could not find an image file in {self.cfg.dataset_info.dir}")
+        elif self.type == ImageReader.Type.VIDEO:
+            self._open_video()
+        self._seek_first()
+
+    def isValid(self) -> bool:
+        valid = bool(self.img_nb)
+        if self.type == ImageReader.Type.VIDEO:
+            for c in self.cap:
+                valid = valid or c.isOpened()  # (the reference's ||, kept)
+        return valid
+
+    def get_img_nb(self) -> int:
+        return self.img_nb
+
+    def _advance(self) -> bool:
+        if self.fimage.is_open():
+            for _ in range(self.cfg.frame_info.skip):
+                ok, nb, stamp = self.fimage.readData()
+                if not ok:
+                    print(f"[Error] could not read image{self.img_nb} in {self.cfg.dataset_info.dir}")
+                    self._last_ok = False
+                    return False
+                self.img_nb, self.img_stamp = nb, stamp
+        else:
+            self.img_nb += self.cfg.frame_info.skip
+        return True
+
+    def _video_frame(self, c: VideoCapture):
+        while c.get(CAP_PROP_POS_FRAMES) < self.img_nb:
+            if not c.grab():
+                break
+        ok, img = c.read()
+        if not ok:
+            return None
+        return bgr2gray(img) if img.ndim == 3 else img
+
+    def readStereo(self):
+        if not self._advance():
+            return None, None
+        if self.type == ImageReader.Type.IMAGES:
+            return loadImages(self.cfg.dataset_info.dir, self.img_nb, self.padding, True, self.cfg.appendix)
+        if len(self.cap) < 2 or not self.cap[0].isOpened() or not self.cap[1].isOpened():
+            print("[ImageReader] Warning: video stream is not opened!")
+            return None, None
+        return self._video_frame(self.cap[0]), self._video_frame(self.cap[1])
+
+    def readMono(self):
+        if not self._advance():
+            return None
+        if self.type == ImageReader.Type.IMAGES:
+            return loadImage(self.cfg.dataset_info.dir, self.cfg.dataset_info.cam_ID, self.img_nb, self.padding,
+                             self.cfg.appendix)
+        if not self.cap[0].isOpened():
+            print("[ImageReader] Warning: video stream is not opened!")
+            return None
+        return self._video_frame(self.cap[0])

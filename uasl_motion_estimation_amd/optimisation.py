@@ -764,12 +764,16 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     the group for gloo, or the given ``allreduce(dev_ptr, n)`` callback.
 
     ``shard``: "auto" applies the landmark-count gate (shard_worthwhile on
-    the window's observation count, the same decision on every rank); below
-    it -- or with shard=False -- every rank solves the whole window on its own
-    GPU (replicated, no collective; the same deterministic solve on every
-    rank) and returns its landmark range of the result.  True always shards.
-    Returns (cams, local pts, (lo, hi), summary); summary["sharded"] says
-    which ran."""
+    the window's observation count, the same decision on every rank) -- but
+    only when the caller passes neither ``comm`` nor ``allreduce``: an
+    explicit exchange means "shard" (a caller's communicator is
+    never silently ignored).  Below the gate -- or with shard=False -- every
+    rank solves the whole window on its own GPU (replicated, no collective;
+    the same deterministic solve on every rank) and returns its landmark range
+    of the result.  True always shards.  Returns (cams, local pts, (lo, hi),
+    summary); summary["sharded"] says which ran.  (Round 4 changed the
+    default from True to "auto"; a caller that wants the old behaviour below
+    the gate passes shard=True.)"""
     import torch
     import torch.distributed as dist
 
@@ -777,7 +781,7 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     local, rng = shard_landmarks(bp, rank, world)
     if shard == "auto":
-        shard = shard_worthwhile(len(bp.obs), world, xch_us)
+        shard = comm is not None or allreduce is not None or shard_worthwhile(len(bp.obs), world, xch_us)
     if not shard:
         cams, pts, summ = ba_solve(bp.copy(), options, ctx)
         summ = dict(summ, sharded=False)

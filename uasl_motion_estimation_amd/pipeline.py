@@ -343,7 +343,11 @@ class GPUBackend(Backend):
         self.mctx = self.ctx if match_on_ba else self.tctx
         self._scale_pool = None  # worker thread of the asynchronous scale LM
         self._ba_pool = self._ba_fut = None  # worker thread queueing the BA launches
-        self.async_enqueue = os.environ.get("ME_VO_ASYNC_ENQUEUE", "1") == "1"
+        # one context for both sides (overlap=False or tctx=ctx): a context takes
+        # one call at a time (me_hip.h), so neither the scale LM nor the BA
+        # queueing runs on a worker thread -- both run inline, in loop order
+        self.shared_ctx = self.tctx is self.ctx
+        self.async_enqueue = os.environ.get("ME_VO_ASYNC_ENQUEUE", "1") == "1" and not self.shared_ctx
         self._imgs = {}
         # device-resident BA window: obs (4 doubles) | frame | track ID per
         # observation, frame by frame; [_wstart, _wend) live in store _wcur
@@ -673,12 +677,20 @@ class GPUBackend(Backend):
         from ._lib import ME_DEVICE
         from .optimisation import ScaleCall
 
+        imgs = sp.imgs_handle
+        call = ScaleCall(sp, params, ctx=self.tctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
+        if self.shared_ctx:  # (no second caller on the context: run it now, in loop order)
+            from concurrent.futures import Future
+
+            self._join_enqueue()
+            fut = Future()
+            fut.set_result(call.run())
+            self._scale_res = (fut, call)
+            return
         if self._scale_pool is None:
             from concurrent.futures import ThreadPoolExecutor
 
             self._scale_pool = ThreadPoolExecutor(max_workers=1)
-        imgs = sp.imgs_handle
-        call = ScaleCall(sp, params, ctx=self.tctx, img_mem=ME_DEVICE, dev_imgs=(imgs[0], imgs[1]))
         self._scale_res = (self._scale_pool.submit(call.run), call)
         time.sleep(0)  # (a GIL hand-over: the worker enters the C call now, not at the loop's next blocking call)
 
@@ -908,7 +920,8 @@ class WindowedStereoVO:
     while the host tracks, matches and books t, and the BA context idles only
     while BA(t - 1) is applied and BA(t) queued.  Every backend takes the same
     decisions; `overlap` only tells the GPU backend to run the front end on its
-    own context (overlap=False: one stream, everything in order).  Call
+    own context (overlap=False: one context and one stream; the scale LM and
+    the BA queueing then run inline on the loop thread, in loop order).  Call
     finish() after the last keyframe."""
 
     def __init__(self, cfg: PipelineConfig, backend: Backend, K=None, first_pose=None, velocity=None,

@@ -206,11 +206,18 @@ class MonoVisualOdometry:
                                          E.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), inl.ctypes.data,
                                          ctypes.byref(ni), ctypes.byref(ok)), "me_mono_vo_process")
         self._Rt = Rt.reshape(4, 4)
-        if n >= 8 and np.any(E):
-            self._E = E.reshape(3, 3)
+        # MonoVisualOdometry.cpp:9-52: fewer than 8 matches leaves m_E and the inlier / outlier lists
+        # as they were; an empty E is assigned (an empty matrix) and the lists kept; otherwise all
+        # three are replaced
+        if n < 8:
+            return bool(ok.value)
+        if not np.any(E):
+            self._E = np.zeros((0, 0))
+            return bool(ok.value)
+        self._E = E.reshape(3, 3)
         self._inliers = [int(i) for i in inl[:ni.value]]
         s = set(self._inliers)
-        self._outliers = [i for i in range(n) if i not in s] if n >= 8 and np.any(E) else self._outliers
+        self._outliers = [i for i in range(n) if i not in s]
         return bool(ok.value)
 
     def getMotion(self) -> np.ndarray:
