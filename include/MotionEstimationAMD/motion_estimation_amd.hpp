@@ -50,6 +50,21 @@ class Context {
     if (rc == ME_ERR_INVALID) throw std::invalid_argument(msg);
     throw std::runtime_error(msg);
   }
+  // CUs of the device, and a restriction of this ctx's stream to a CU set
+  // (me_set_cu_mask; an empty set restores every CU)
+  int cuCount() const {
+    int n = 0;
+    check(me_cu_count(c_.get(), &n), "me_cu_count");
+    return n;
+  }
+  void setCuMask(const std::vector<int>& cus) {
+    std::vector<uint32_t> w;
+    for (int i : cus) {
+      if ((int)w.size() <= i / 32) w.resize(i / 32 + 1, 0u);
+      w[i / 32] |= 1u << (i % 32);
+    }
+    check(me_set_cu_mask(c_.get(), w.empty() ? nullptr : w.data(), (int)w.size()), "me_set_cu_mask");
+  }
   static Context& thread_default() {
     thread_local Context ctx(0);
     return ctx;
@@ -763,5 +778,104 @@ inline void calcOpticalFlowPyrLK(const amd::ImageView& prev, const amd::ImageVie
                          &pts_in[0].x, &pts_out[0].x, status.data(), (int)pts_in.size(), &kp),
             "calcOpticalFlowPyrLK");
 }
+
+// The windowed stereo VO loop (me_vo_loop_*, csrc/vo_loop.hip): the
+// application loop the reference leaves to its caller -- per keyframe KLT,
+// epipolar MI matching, WBA_Point bookkeeping (feature_types.h:121-197),
+// scale LM (Optimiser<ScaleState,...>) and the sliding-window
+// BundleAdjuster<4> -- in native code, the same decisions as
+// uasl_motion_estimation_amd.pipeline.WindowedStereoVO.  Two contexts of one
+// GPU: `ba` runs the window solves, `front` the front end; with
+// frontCus in (0, 16) the two streams get whole XCDs (frontCus / 2 of the 8
+// XCDs to the front end: CU i sits on XCD i mod 8).  `ba` and `front` may be
+// the same context (one stream, no worker threads).
+class WindowedStereoVO {
+ public:
+  struct Config : me_vo_loop_config {
+    Config() { me_vo_loop_default_config(this); }
+  };
+  WindowedStereoVO(amd::Context& ba, amd::Context& front, const Config& cfg, int frontCus = 4)
+      : ba_(ba), front_(front) {
+    if (&ba != &front && frontCus > 0 && frontCus < 16) {
+      const int ncu = ba.cuCount();
+      std::vector<int> f, b;
+      for (int i = 0; i < ncu; ++i) (i % 8 < frontCus / 2 ? f : b).push_back(i);
+      front.setCuMask(f);
+      ba.setCuMask(b);
+      masked_ = true;
+    }
+    me_vo_loop* v = nullptr;
+    ba.check(me_vo_loop_create(ba.get(), front.get(), &cfg, &v), "me_vo_loop_create");
+    v_.reset(v);
+  }
+  ~WindowedStereoVO() {
+    v_.reset();
+    if (masked_) {
+      front_.setCuMask({});
+      ba_.setCuMask({});
+    }
+  }
+  WindowedStereoVO(const WindowedStereoVO&) = delete;
+  WindowedStereoVO& operator=(const WindowedStereoVO&) = delete;
+  // keyframe t (0, 1, 2, ...): host images, copied in
+  void process(int t, const amd::ImageView& left, const amd::ImageView& right) {
+    if (left.empty() || right.empty() || left.step != left.cols || right.step != right.cols)
+      throw std::invalid_argument("WindowedStereoVO::process: dense 8-bit images expected");
+    check(me_vo_loop_process(v_.get(), t, left.data, right.data, ME_HOST), "WindowedStereoVO::process");
+  }
+  // keyframe t from device memory (alive until process(t + 1) returns)
+  void processDevice(int t, const uint8_t* left, const uint8_t* right) {
+    check(me_vo_loop_process(v_.get(), t, left, right, ME_DEVICE), "WindowedStereoVO::processDevice");
+  }
+  void finish() { check(me_vo_loop_finish(v_.get()), "WindowedStereoVO::finish"); }
+  std::vector<me_vo_frame_result> results() const {
+    int n = 0;
+    check(me_vo_loop_results(v_.get(), nullptr, 0, &n), "results");
+    std::vector<me_vo_frame_result> r((size_t)n);
+    check(me_vo_loop_results(v_.get(), r.data(), n, &n), "results");
+    return r;
+  }
+  std::vector<me_vo_event> events() const {
+    long n = 0;
+    check(me_vo_loop_events(v_.get(), nullptr, 0, &n), "events");
+    std::vector<me_vo_event> e((size_t)n);
+    check(me_vo_loop_events(v_.get(), e.data(), n, &n), "events");
+    return e;
+  }
+  std::vector<std::pair<int, std::array<double, 6>>> poses() const {
+    int n = 0;
+    check(me_vo_loop_poses(v_.get(), nullptr, nullptr, 0, &n), "poses");
+    std::vector<int32_t> ts((size_t)n);
+    std::vector<std::array<double, 6>> p((size_t)n);
+    check(me_vo_loop_poses(v_.get(), ts.data(), n ? p[0].data() : nullptr, n, &n), "poses");
+    std::vector<std::pair<int, std::array<double, 6>>> out;
+    for (int i = 0; i < n; ++i) out.emplace_back(ts[i], p[i]);
+    return out;
+  }
+  // live tracks: IDs (WBA_Point::getID) and landmarks (get3DLocation)
+  void tracks(std::vector<int64_t>& ids, std::vector<std::array<double, 3>>& X) const {
+    int n = 0;
+    check(me_vo_loop_tracks(v_.get(), nullptr, nullptr, nullptr, nullptr, nullptr, 0, &n), "tracks");
+    ids.resize((size_t)n);
+    X.resize((size_t)n);
+    check(me_vo_loop_tracks(v_.get(), ids.data(), n ? X[0].data() : nullptr, nullptr, nullptr, nullptr, n, &n),
+          "tracks");
+  }
+
+ private:
+  void check(int rc, const char* what) const {
+    if (rc == ME_OK) return;
+    std::string msg = std::string(what) + ": " + me_vo_loop_last_error(v_.get());
+    if (rc == ME_ERR_INVALID) throw std::invalid_argument(msg);
+    throw std::runtime_error(msg);
+  }
+  struct Del {
+    void operator()(me_vo_loop* v) const { me_vo_loop_destroy(v); }
+  };
+  amd::Context& ba_;
+  amd::Context& front_;
+  bool masked_ = false;
+  std::unique_ptr<me_vo_loop, Del> v_;
+};
 
 }  // namespace me

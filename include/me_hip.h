@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define ME_ABI_VERSION 3
+#define ME_ABI_VERSION 4
 
 enum {
   ME_OK = 0,
@@ -74,6 +74,8 @@ void* me_get_stream(me_ctx* ctx);
    that shares every XCD. */
 int me_set_cu_mask(me_ctx* ctx, const uint32_t* mask, int nwords);
 int me_stream_flags(me_ctx* ctx, unsigned* flags);
+/* Compute units of the ctx device (the CU count a me_set_cu_mask split divides). */
+int me_cu_count(me_ctx* ctx, int* n);
 int me_synchronize(me_ctx* ctx);
 int me_malloc(me_ctx* ctx, void** dptr, size_t bytes);
 int me_free(me_ctx* ctx, void* dptr);
@@ -364,6 +366,74 @@ typedef struct me_vo_window {
   int first_frame;
 } me_vo_window;
 int me_vo_window_submit(me_ctx* ctx, const me_vo_window* w, me_ba_problem* p, const me_ba_options* o);
+/* ---- the windowed stereo VO loop, native (round 5) ----------------------
+ * The application loop around the hot path (pipeline.py WindowedStereoVO
+ * with its GPU backend, every step in C++ behind this ABI): per keyframe t
+ * the KLT of the active tracks, the epipolar MI matching of the tracked and
+ * of the new features (one front-end round trip), the WBA_Point bookkeeping
+ * (include/MotionEstimation/core/feature_types.h:121-197: IDs from the value
+ * constructor, addMatch, pop of features leaving the window, deletion of
+ * empty tracks) over a structure-of-arrays track table, the scale LM
+ * (Optimiser<ScaleState,...>::optimise, optimisation.cpp:29-147) of keyframe
+ * t-1 and the sliding-window BA (BundleAdjuster<4>::optimise over the last
+ * `window` keyframes, initialiseObservations order, BundleAdjuster.h:354-376,
+ * 431-476) queued behind the previous window's solve (me_vo_window_submit).
+ * The loop is lagged exactly as pipeline.py's: BA(t-1) enters the state after
+ * keyframe t is matched and booked.  Two contexts of one device: `ba` runs the
+ * window solves, `front` the KLT, the matchers and the scale LM (they may be
+ * the same ctx: then nothing runs on a worker thread).  Results are the
+ * Python loop's bit for bit (tests/test_vo_loop.py).  One loop per pair of
+ * contexts; no other call on either ctx while a loop call runs. */
+typedef struct {
+  int width, height, n_feats, window;
+  int ba_iters, scale_iters, fixed_frames, d_min, d_max;
+  double baseline, feat_var;
+  double K[9];                /* row-major intrinsics (both cameras) */
+  double first_pose[6];       /* {t, angle-axis} world -> camera of keyframe 0 */
+  double velocity[6];         /* motion prior of keyframe 1 (has_velocity) */
+  int has_velocity;
+  int log_events;             /* keep the WBA_Point event log (me_vo_loop_events) */
+  int async_enqueue;          /* window solves queued from a worker thread (ignored when ba == front) */
+} me_vo_loop_config;
+typedef struct {              /* pipeline.FrameResult */
+  int t, n_tracked, n_new, n_active, n_window_pts, n_window_obs;
+  double scale;
+  int scale_stop, scale_iters, ba_iters;
+  double ba_cost;
+  double pose[6];
+} me_vo_frame_result;
+typedef struct {              /* one WBA_Point call: kind 0 new (value ctor), 1 addMatch, 2 pop, 3 deleted */
+  int kind, t;
+  int64_t id;
+  float feat[4];              /* {xl, yl, xr, yr} (new / add) */
+} me_vo_event;
+typedef struct me_vo_loop me_vo_loop;
+void me_vo_loop_default_config(me_vo_loop_config* c);
+int me_vo_loop_create(me_ctx* ba, me_ctx* front, const me_vo_loop_config* cfg, me_vo_loop** out);
+void me_vo_loop_destroy(me_vo_loop* v);
+const char* me_vo_loop_last_error(const me_vo_loop* v);
+/* Keyframe t (t = 0, 1, 2, ... in order): left / right 8-bit images of
+   width x height (stride = width).  mem = ME_DEVICE: device memory on the
+   ctx device, read during this call and the next one (keep it alive until
+   me_vo_loop_process(t + 1) returns); ME_HOST: copied in. */
+int me_vo_loop_process(me_vo_loop* v, int t, const uint8_t* left, const uint8_t* right, me_mem mem);
+/* Completes the last keyframe (its pops, scale LM and BA). */
+int me_vo_loop_finish(me_vo_loop* v);
+/* Results of the completed keyframes (*n = their number; min(cap, *n) copied). */
+int me_vo_loop_results(me_vo_loop* v, me_vo_frame_result* out, int cap, int* n);
+int me_vo_loop_events(me_vo_loop* v, me_vo_event* out, long cap, long* n);
+/* Live track table (creation = ID order): IDs, landmarks (3 per track), active flag, first held / last frame. */
+int me_vo_loop_tracks(me_vo_loop* v, int64_t* ids, double* X, uint8_t* active, int64_t* first, int64_t* last, int cap,
+                      int* n);
+int me_vo_loop_poses(me_vo_loop* v, int32_t* ts, double* poses, int cap, int* n);
+/* Observations of keyframe t still held (ascending track IDs, {xl, yl, xr, yr}); *n = -1 when none. */
+int me_vo_loop_frame_obs(me_vo_loop* v, int t, int64_t* ids, float* feats, int cap, int* n);
+int me_vo_loop_frames(me_vo_loop* v, int32_t* ts, int cap, int* n);
+/* [0] host seconds outside waits, [1] seconds blocked on device results, [2] tracks created (latestID),
+   [3..8] seconds blocked in: KLT + matching, first-keyframe matching, scale LM submit, window submit,
+   BA result, scale LM result. */
+int me_vo_loop_stats(me_vo_loop* v, double* out, int n);
+
 /* BundleAdjuster<M>::initialiseObservations (BundleAdjuster.h:354-376) for a
    device-resident window: observation i was seen in frame[i] by the track
    ids[i]; cam_idx[i] = frame[i] - first_frame and pt_idx[i] = the position of

@@ -22,7 +22,7 @@ def test_library_builds_and_loads():
     from uasl_motion_estimation_amd import _lib
 
     lib = _lib.load_library()
-    assert lib.me_abi_version() == 3
+    assert lib.me_abi_version() == 4
 
 
 def test_exports_every_header_symbol():

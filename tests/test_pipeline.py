@@ -106,6 +106,41 @@ def seq5():
     return PL.synthetic_sequence(5, N_SLIDE)
 
 
+_ORACLE_RUNS = {}
+
+
+def _oracle_run(seq5, window, n):
+    """The sequential oracle loop on config 5's keyframes (cached per module: the Python GPU loop and
+    the native loop are both checked against it)."""
+    from pipeline_oracle import OracleBackend
+
+    key = (window, n)
+    if key not in _ORACLE_RUNS:
+        _ORACLE_RUNS[key] = _run(5, n, OracleBackend(), window=window, frames=seq5, ba_iters=10)
+    return _ORACLE_RUNS[key]
+
+
+def _check_against_oracle(g, o, window, n):
+    if window == 50:  # the window slid: its oldest keyframe is n - 50, and pops happened
+        assert min(g.obs) == n - window and any(ev[0] == "pop" for ev in g.events)
+    assert g.events == o.events  # track IDs, frames and feature positions, bit for bit
+    assert np.array_equal(g.ids, o.ids)
+    gr, orr = g.results, o.results
+    assert len(gr) == len(orr) == n
+    for rg, ro in zip(gr, orr):
+        assert (rg.n_tracked, rg.n_new, rg.n_window_pts, rg.n_window_obs, rg.ba_iters) == \
+            (ro.n_tracked, ro.n_new, ro.n_window_pts, ro.n_window_obs, ro.ba_iters), (rg, ro)
+        assert (rg.scale_stop, rg.scale_iters) == (ro.scale_stop, ro.scale_iters), (rg, ro)
+        np.testing.assert_allclose(rg.scale, ro.scale, rtol=1e-6)
+    gp, op = g.poses, o.poses
+    for t in gp:
+        np.testing.assert_allclose(gp[t], op[t], rtol=1e-6, atol=1e-9)
+    # landmarks: all but the ill-conditioned few (near-zero parallax far points,
+    # where summation-order differences are amplified) within 1e-6
+    rel = np.abs(g.X - o.X) / (np.abs(o.X) + 1e-9)
+    assert (rel > 1e-6).mean() < 1e-3 and np.median(rel) < 1e-9, (rel.max(), (rel > 1e-6).sum())
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("window,n", [(50, N_SLIDE), (8, 24)])
 def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window, n):
@@ -113,29 +148,134 @@ def test_pipeline_gpu_matches_oracle(ctx, oracle, seq5, window, n):
     keyframes -- the window fills and slides (pops of the oldest keyframe,
     feature_types.h:142) -- and a W = 8 window over 24 keyframes (many pops
     and track deletions)."""
-    from pipeline_oracle import OracleBackend
-
     be = PL.GPUBackend(ctx)  # front end on its own context, the loop pipelined
     try:
         g = _run(5, n, be, window=window, frames=seq5, overlap=True, ba_iters=10)
     finally:
         be.close()
-    o = _run(5, n, OracleBackend(), window=window, frames=seq5, ba_iters=10)
-    if window == 50:  # the window slid: its oldest keyframe is n - 50, and pops happened
-        assert min(g.obs) == n - window and any(ev[0] == "pop" for ev in g.events)
-    assert g.events == o.events  # track IDs, frames and feature positions, bit for bit
-    assert np.array_equal(g.ids, o.ids)
-    for rg, ro in zip(g.results, o.results):
-        assert (rg.n_tracked, rg.n_new, rg.n_window_pts, rg.n_window_obs, rg.ba_iters) == \
-            (ro.n_tracked, ro.n_new, ro.n_window_pts, ro.n_window_obs, ro.ba_iters), (rg, ro)
-        assert (rg.scale_stop, rg.scale_iters) == (ro.scale_stop, ro.scale_iters), (rg, ro)
-        np.testing.assert_allclose(rg.scale, ro.scale, rtol=1e-6)
-    for t in g.poses:
-        np.testing.assert_allclose(g.poses[t], o.poses[t], rtol=1e-6, atol=1e-9)
-    # landmarks: all but the ill-conditioned few (near-zero parallax far points,
-    # where summation-order differences are amplified) within 1e-6
-    rel = np.abs(g.X - o.X) / (np.abs(o.X) + 1e-9)
-    assert (rel > 1e-6).mean() < 1e-3 and np.median(rel) < 1e-9, (rel.max(), (rel > 1e-6).sum())
+    _check_against_oracle(g, _oracle_run(seq5, window, n), window, n)
+
+
+def _native(ctx, n, window, frames, log=True, **kw):
+    fr, K, p0, v, truth = frames
+    cfg = PL.PipelineConfig.from_config(5, ba_iters=10)
+    cfg.window = window
+    vo = PL.NativeStereoVO(cfg, ctx, K, p0, v, log_events=log, **kw)
+    for t in range(n):
+        vo.process(t, fr[t].left, fr[t].right)
+    vo.finish()
+    return vo
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window,n", [(50, N_SLIDE), (8, 24)])
+def test_native_loop_matches_oracle(ctx, oracle, seq5, window, n):
+    """The loop in native code (me_vo_loop_*, csrc/vo_loop.hip) against the
+    sequential oracle loop: WBA_Point events bit for bit, results, poses and
+    landmarks to 1e-6 -- the same bar as the Python GPU loop."""
+    g = _native(ctx, n, window, seq5)
+    try:
+        _check_against_oracle(g, _oracle_run(seq5, window, n), window, n)
+    finally:
+        g.close()
+
+
+class _DevFrame:
+    def __init__(self, left, right):
+        self.left, self.right = left, right
+
+
+@pytest.mark.gpu
+def test_native_loop_shared_context_and_device_images(ctx, seq5):
+    """overlap=False (one context: the scale LM and the window queueing inline)
+    and device-resident images (ME_DEVICE) take the overlapped host-image run's
+    decisions and values bit for bit."""
+    import torch
+
+    a = _native(ctx, 16, 8, seq5)
+    b = _native(ctx, 16, 8, seq5, overlap=False)
+    fr = seq5[0]
+    dev = [_DevFrame(torch.from_numpy(fr[t].left).cuda(), torch.from_numpy(fr[t].right).cuda()) for t in range(16)]
+    torch.cuda.synchronize()
+    c = _native(ctx, 16, 8, (dev,) + tuple(seq5[1:]))
+    try:
+        ea = a.event_records()
+        for o in (b, c):
+            assert np.array_equal(ea, o.event_records())
+            assert np.array_equal(a.ids, o.ids) and np.array_equal(a.X, o.X)
+            pa, po = a.poses, o.poses
+            assert all(np.array_equal(pa[t], po[t]) for t in pa)
+            assert [(r.scale, r.ba_cost) for r in a.results] == [(r.scale, r.ba_cost) for r in o.results]
+    finally:
+        for o in (a, b, c):
+            o.close()
+
+
+def _write_cli_input(path, frames, n, window):
+    fr, K, p0, v, truth = frames
+    cfg = PL.PipelineConfig.from_config(5, ba_iters=10)
+    iv = np.array([cfg.width, cfg.height, cfg.n_feats, window, cfg.ba_iters, cfg.scale_iters, cfg.fixed_frames,
+                   cfg.d_min, cfg.d_max, n, 1], np.int32)
+    dv = np.concatenate([[cfg.baseline, cfg.feat_var], np.asarray(K, np.float64).ravel(), p0, v]).astype(np.float64)
+    with open(path, "wb") as fh:
+        fh.write(iv.tobytes())
+        fh.write(dv.tobytes())
+        for t in range(n):
+            fh.write(np.ascontiguousarray(fr[t].left, np.uint8).tobytes())
+            fh.write(np.ascontiguousarray(fr[t].right, np.uint8).tobytes())
+
+
+@pytest.mark.gpu
+def test_cpp_host_drives_the_loop(ctx, seq5, tmp_path):
+    """A compiled C++ caller (tests/cpp/vo_loop_cli.cpp over me::WindowedStereoVO
+    in include/MotionEstimationAMD/motion_estimation_amd.hpp, no Python in the
+    process) runs the loop: its results, WBA_Point events, poses and track
+    table equal the Python-driven native loop's bit for bit."""
+    import os
+    import subprocess
+
+    from uasl_motion_estimation_amd._lib import VO_EVENT_DTYPE
+
+    n, window = 16, 8
+    cli = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "vo_loop_cli")
+    assert os.path.exists(cli), "tests/cpp/vo_loop_cli not built (__graft_entry__.build())"
+    _write_cli_input(tmp_path / "in.bin", seq5, n, window)
+    r = subprocess.run([cli, str(tmp_path / "in.bin"), str(tmp_path / "out.bin")], capture_output=True, text=True,
+                       timeout=100)
+    assert r.returncode == 0, r.stderr
+    buf = (tmp_path / "out.bin").read_bytes()
+    pos = 0
+
+    def take(dtype, count):
+        nonlocal pos
+        a = np.frombuffer(buf, dtype, count, pos)
+        pos += a.nbytes
+        return a
+
+    nres = int(take(np.int64, 1)[0])
+    rdt = np.dtype([("t", "i4"), ("n_tracked", "i4"), ("n_new", "i4"), ("n_active", "i4"), ("nwp", "i4"),
+                    ("nwo", "i4"), ("scale", "f8"), ("stop", "i4"), ("sit", "i4"), ("bit", "i4"), ("cost", "f8"),
+                    ("pose", "f8", 6)], align=True)
+    res = take(rdt, nres)
+    ev = take(VO_EVENT_DTYPE, int(take(np.int64, 1)[0]))
+    pdt = np.dtype([("t", "i4"), ("pad", "i4"), ("pose", "f8", 6)])
+    ps = take(pdt, int(take(np.int64, 1)[0]))
+    nt = int(take(np.int64, 1)[0])
+    ids = take(np.int64, nt)
+    X = take(np.float64, 3 * nt).reshape(nt, 3)
+    assert pos == len(buf)
+    py = _native(ctx, n, window, seq5)
+    try:
+        assert np.array_equal(ev, py.event_records())
+        assert np.array_equal(ids, py.ids) and np.array_equal(X, py.X)
+        pp = py.poses
+        assert [int(t) for t in ps["t"]] == sorted(pp) and all(np.array_equal(p["pose"], pp[int(p["t"])]) for p in ps)
+        pr = py.results
+        assert nres == n == len(pr)
+        assert all((int(a["t"]), int(a["n_tracked"]), int(a["n_new"]), float(a["scale"]), float(a["cost"]))
+                   == (b.t, b.n_tracked, b.n_new, b.scale, b.ba_cost) for a, b in zip(res, pr))
+    finally:
+        py.close()
 
 
 @pytest.mark.gpu

@@ -120,6 +120,26 @@ class VOWindowC(ctypes.Structure):
                 ("first_frame", c_int)]
 
 
+class VOLoopConfigC(ctypes.Structure):
+    """me_vo_loop_config (include/me_hip.h)."""
+    _fields_ = [("width", c_int), ("height", c_int), ("n_feats", c_int), ("window", c_int), ("ba_iters", c_int),
+                ("scale_iters", c_int), ("fixed_frames", c_int), ("d_min", c_int), ("d_max", c_int),
+                ("baseline", c_double), ("feat_var", c_double), ("K", c_double * 9), ("first_pose", c_double * 6),
+                ("velocity", c_double * 6), ("has_velocity", c_int), ("log_events", c_int),
+                ("async_enqueue", c_int)]
+
+
+class VOFrameResultC(ctypes.Structure):
+    """me_vo_frame_result (include/me_hip.h)."""
+    _fields_ = [("t", c_int), ("n_tracked", c_int), ("n_new", c_int), ("n_active", c_int), ("n_window_pts", c_int),
+                ("n_window_obs", c_int), ("scale", c_double), ("scale_stop", c_int), ("scale_iters", c_int),
+                ("ba_iters", c_int), ("ba_cost", c_double), ("pose", c_double * 6)]
+
+
+# me_vo_event as a numpy record (32 bytes: int kind, int t, int64 id, float feat[4])
+VO_EVENT_DTYPE = np.dtype([("kind", np.int32), ("t", np.int32), ("id", np.int64), ("feat", np.float32, 4)])
+
+
 class KLTParamsC(ctypes.Structure):
     _fields_ = [("win", c_int), ("max_level", c_int), ("max_iters", c_int), ("eps", c_double),
                 ("min_eig", c_double)]
@@ -130,7 +150,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 # every symbol include/me_hip.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "me_abi_version", "me_range_push", "me_range_pop", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
-    "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
+    "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_cu_count", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_memcpy_async", "me_host_alloc", "me_host_free",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
@@ -145,6 +165,9 @@ EXPORTS = [
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
     "me_mono_default_params", "me_mono_vo_process",
+    "me_vo_loop_default_config", "me_vo_loop_create", "me_vo_loop_destroy", "me_vo_loop_last_error",
+    "me_vo_loop_process", "me_vo_loop_finish", "me_vo_loop_results", "me_vo_loop_events", "me_vo_loop_tracks",
+    "me_vo_loop_poses", "me_vo_loop_frame_obs", "me_vo_loop_frames", "me_vo_loop_stats",
 ]
 
 class MonoParamsC(ctypes.Structure):
@@ -257,6 +280,20 @@ def load_library(path: str | None = None):
         "me_ba_solve_comm": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), c_void_p, P(BASummaryC)]),
         "me_ba_shard_worthwhile": (c_int, [c_long, c_int, c_double]),
         "me_ba_shard_exchange_us": (c_double, [c_int]),
+        "me_cu_count": (c_int, [c_void_p, P(c_int)]),
+        "me_vo_loop_default_config": (None, [P(VOLoopConfigC)]),
+        "me_vo_loop_create": (c_int, [c_void_p, c_void_p, P(VOLoopConfigC), P(c_void_p)]),
+        "me_vo_loop_destroy": (None, [c_void_p]),
+        "me_vo_loop_last_error": (ctypes.c_char_p, [c_void_p]),
+        "me_vo_loop_process": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int]),
+        "me_vo_loop_finish": (c_int, [c_void_p]),
+        "me_vo_loop_results": (c_int, [c_void_p, P(VOFrameResultC), c_int, P(c_int)]),
+        "me_vo_loop_events": (c_int, [c_void_p, c_void_p, c_long, P(c_long)]),
+        "me_vo_loop_tracks": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, P(c_int)]),
+        "me_vo_loop_poses": (c_int, [c_void_p, c_void_p, c_void_p, c_int, P(c_int)]),
+        "me_vo_loop_frame_obs": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, P(c_int)]),
+        "me_vo_loop_frames": (c_int, [c_void_p, c_void_p, c_int, P(c_int)]),
+        "me_vo_loop_stats": (c_int, [c_void_p, P(c_double), c_int]),
         "me_klt_default_params": (None, [P(KLTParamsC)]),
         "me_klt_track": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                  c_void_p, c_int, P(KLTParamsC)]),

@@ -198,6 +198,12 @@ int me_set_cu_mask(me_ctx* c, const uint32_t* mask, int nwords) {
   return ME_OK;
 }
 
+int me_cu_count(me_ctx* c, int* n) {
+  if (!c || !n) return ME_ERR_INVALID;
+  *n = c->num_cu;
+  return ME_OK;
+}
+
 int me_stream_flags(me_ctx* c, unsigned* flags) {
   if (!c || !flags) return ME_ERR_INVALID;
   ME_HIP(c, hipStreamGetFlags(c->stream, flags));

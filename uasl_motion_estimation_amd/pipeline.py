@@ -1384,3 +1384,219 @@ def synthetic_sequence(c: int, n_frames: int, seed: int | None = None, render_di
     for fr in frames:
         poses.append(np.concatenate([fr.t, S.R_to_aa_robust(fr.R)]))
     return frames, K, poses[0], poses[1] - poses[0], poses
+
+
+class NativeStereoVO:
+    """The windowed stereo VO loop of WindowedStereoVO with the GPU backend,
+    every step in native code behind the C ABI (me_vo_loop_*, csrc/vo_loop.hip):
+    the Python layer only hands images in and reads results out.  Same
+    decisions, events, results and poses as WindowedStereoVO(GPUBackend)
+    (tests/test_vo_loop.py).  Two contexts of the device as GPUBackend sets
+    them up: `ctx` runs the window solves, `tctx` (front_cus of every 16 CUs,
+    whole XCDs) the KLT, the matchers and the scale LM; overlap=False runs
+    everything on `ctx` (no worker threads).  Images: numpy (copied in) or
+    device tensors exposing data_ptr() (kept referenced for two keyframes)."""
+
+    def __init__(self, cfg: PipelineConfig, ctx=None, K=None, first_pose=None, velocity=None, log_events=False,
+                 overlap: bool = True, front_cus: int = 4, tctx=None, async_enqueue: bool = True):
+        import ctypes
+
+        from ._lib import Context, VOLoopConfigC, cu_split, default_context
+
+        self.cfg = cfg
+        self.ctx = ctx or default_context()
+        self._own_t = tctx is None and overlap
+        self.tctx = tctx or (Context(self.ctx.device) if overlap else self.ctx)
+        self._masked = False
+        front_cus = int(os.environ.get("ME_VO_FRONT_CUS", front_cus))
+        if self.tctx is not self.ctx and 0 < front_cus < 16:
+            import torch
+
+            ncu = torch.cuda.get_device_properties(self.ctx.device).multi_processor_count
+            front, back = cu_split(ncu, front_cus)
+            self.tctx.set_cu_mask(front)
+            self.ctx.set_cu_mask(back)
+            self._masked = True
+        self.lib = self.ctx.lib
+        self.K = np.asarray(S.intrinsics(cfg.width, cfg.height) if K is None else K, np.float64)
+        c = VOLoopConfigC()
+        self.lib.me_vo_loop_default_config(ctypes.byref(c))
+        c.width, c.height, c.n_feats, c.window = cfg.width, cfg.height, cfg.n_feats, cfg.window
+        c.ba_iters, c.scale_iters, c.fixed_frames, c.d_min, c.d_max = (cfg.ba_iters, cfg.scale_iters,
+                                                                      cfg.fixed_frames, cfg.d_min, cfg.d_max)
+        c.baseline, c.feat_var = float(cfg.baseline), float(cfg.feat_var)
+        c.K[:] = [float(x) for x in self.K.ravel()]
+        c.first_pose[:] = [float(x) for x in (np.zeros(6) if first_pose is None else np.asarray(first_pose))]
+        c.has_velocity = int(velocity is not None)
+        if velocity is not None:
+            c.velocity[:] = [float(x) for x in np.asarray(velocity)]
+        c.log_events = int(log_events)
+        c.async_enqueue = int(async_enqueue)
+        h = ctypes.c_void_p()
+        self.ctx.check(self.lib.me_vo_loop_create(self.ctx.h, self.tctx.h, ctypes.byref(c), ctypes.byref(h)),
+                       "me_vo_loop_create")
+        self.h = h
+        self.log_events = log_events
+        self._keep = {}  # device images of the last two keyframes (the loop reads them until process(t + 1))
+
+    def _check(self, rc, what):
+        if rc != 0:
+            from ._lib import MEError
+
+            msg = self.lib.me_vo_loop_last_error(self.h)
+            raise MEError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def process(self, t: int, left, right):
+        import ctypes
+
+        from ._lib import ME_DEVICE, ME_HOST
+
+        if hasattr(left, "data_ptr"):
+            self._keep[t] = (left, right)
+            self._keep.pop(t - 2, None)
+            rc = self.lib.me_vo_loop_process(self.h, t, ctypes.c_void_p(left.data_ptr()),
+                                             ctypes.c_void_p(right.data_ptr()), ME_DEVICE)
+        else:
+            L = np.ascontiguousarray(left, np.uint8)
+            R = np.ascontiguousarray(right, np.uint8)
+            rc = self.lib.me_vo_loop_process(self.h, t, L.ctypes.data, R.ctypes.data, ME_HOST)
+        self._check(rc, "me_vo_loop_process")
+
+    def finish(self):
+        self._check(self.lib.me_vo_loop_finish(self.h), "me_vo_loop_finish")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.me_vo_loop_destroy(self.h)
+            self.h = None
+        self._keep = {}
+        if self._masked:
+            self.ctx.set_cu_mask(None)
+            self.tctx.set_cu_mask(None)
+            self._masked = False
+        if self._own_t:
+            self.tctx.close()
+            self._own_t = False
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- results (the attributes WindowedStereoVO exposes)
+    @property
+    def results(self):
+        import ctypes
+
+        from ._lib import VOFrameResultC
+
+        n = ctypes.c_int()
+        self._check(self.lib.me_vo_loop_results(self.h, None, 0, ctypes.byref(n)), "results")
+        arr = (VOFrameResultC * max(n.value, 1))()
+        self._check(self.lib.me_vo_loop_results(self.h, arr, n.value, ctypes.byref(n)), "results")
+        return [FrameResult(r.t, r.n_tracked, r.n_new, r.n_active, r.n_window_pts, r.n_window_obs, r.scale,
+                            r.scale_stop, r.scale_iters, r.ba_iters, r.ba_cost, np.array(r.pose[:], np.float64))
+                for r in arr[:n.value]]
+
+    def event_records(self) -> np.ndarray:
+        """The WBA_Point event log as a numpy record array (kind 0 new, 1 add, 2 pop, 3 del)."""
+        import ctypes
+
+        from ._lib import VO_EVENT_DTYPE
+
+        n = ctypes.c_long()
+        self._check(self.lib.me_vo_loop_events(self.h, None, 0, ctypes.byref(n)), "events")
+        a = np.zeros(n.value, VO_EVENT_DTYPE)
+        if n.value:
+            self._check(self.lib.me_vo_loop_events(self.h, a.ctypes.data, n.value, ctypes.byref(n)), "events")
+        return a
+
+    @property
+    def events(self):
+        """WindowedStereoVO.events: ("new"|"add", id, t, (xl, yl, xr, yr)), ("pop", id), ("del", id)."""
+        out = []
+        kinds = ("new", "add", "pop", "del")
+        for e in self.event_records():
+            k = int(e["kind"])
+            if k < 2:
+                out.append((kinds[k], int(e["id"]), int(e["t"]), tuple(float(v) for v in e["feat"])))
+            else:
+                out.append((kinds[k], int(e["id"])))
+        return out
+
+    def _tracks(self):
+        import ctypes
+
+        n = ctypes.c_int()
+        self._check(self.lib.me_vo_loop_tracks(self.h, None, None, None, None, None, 0, ctypes.byref(n)), "tracks")
+        m = n.value
+        ids, X = np.zeros(m, np.int64), np.zeros((m, 3))
+        act, first, last = np.zeros(m, np.uint8), np.zeros(m, np.int64), np.zeros(m, np.int64)
+        self._check(self.lib.me_vo_loop_tracks(self.h, ids.ctypes.data, X.ctypes.data, act.ctypes.data,
+                                               first.ctypes.data, last.ctypes.data, m, ctypes.byref(n)), "tracks")
+        return ids, X, act.astype(bool), first, last
+
+    @property
+    def ids(self):
+        return self._tracks()[0]
+
+    @property
+    def X(self):
+        return self._tracks()[1]
+
+    @property
+    def active(self):
+        return self._tracks()[2]
+
+    @property
+    def poses(self) -> dict:
+        import ctypes
+
+        n = ctypes.c_int()
+        self._check(self.lib.me_vo_loop_poses(self.h, None, None, 0, ctypes.byref(n)), "poses")
+        ts, ps = np.zeros(n.value, np.int32), np.zeros((n.value, 6))
+        self._check(self.lib.me_vo_loop_poses(self.h, ts.ctypes.data, ps.ctypes.data, n.value, ctypes.byref(n)),
+                    "poses")
+        return {int(t): ps[i] for i, t in enumerate(ts)}
+
+    @property
+    def obs(self) -> dict:
+        """Keyframe -> (track IDs, (n, 4) float32 features) of the observations still held."""
+        import ctypes
+
+        n = ctypes.c_int()
+        self._check(self.lib.me_vo_loop_frames(self.h, None, 0, ctypes.byref(n)), "frames")
+        ts = np.zeros(n.value, np.int32)
+        self._check(self.lib.me_vo_loop_frames(self.h, ts.ctypes.data, n.value, ctypes.byref(n)), "frames")
+        out = {}
+        for t in ts:
+            m = ctypes.c_int()
+            self._check(self.lib.me_vo_loop_frame_obs(self.h, int(t), None, None, 0, ctypes.byref(m)), "obs")
+            ids, fe = np.zeros(m.value, np.int64), np.zeros((m.value, 4), np.float32)
+            self._check(self.lib.me_vo_loop_frame_obs(self.h, int(t), ids.ctypes.data, fe.ctypes.data, m.value,
+                                                      ctypes.byref(m)), "obs")
+            out[int(t)] = (ids, fe)
+        return out
+
+    def _stats(self):
+        import ctypes
+
+        s = (ctypes.c_double * 9)()
+        self._check(self.lib.me_vo_loop_stats(self.h, s, 9), "stats")
+        return list(s)
+
+    @property
+    def latest_id(self) -> int:
+        return int(self._stats()[2])
+
+    @property
+    def stage_s(self) -> dict:
+        s = self._stats()
+        return {"host": s[0], "wait": s[1]}
+
+    @property
+    def wait_by_stage(self) -> dict:
+        s = self._stats()
+        names = ("klt_match_new", "match", "scale_submit", "ba_submit_window", "ba_result", "scale_result")
+        return {nm: v for nm, v in zip(names, s[3:])}
