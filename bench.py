@@ -63,6 +63,8 @@ def parse():
                     help="config-4 landmark-sharded BA line (SURVEY 8e): over RCCL across the ranks when --gpus > 1, "
                          "two contexts on one GPU (host exchange, the crossover point) at N = 1; 0: off")
     ap.add_argument("--sharded-reps", type=int, default=3)
+    ap.add_argument("--vo-loop", choices=("native", "python"), default="native",
+                    help="the VO loop lines' host loop: native (me_vo_loop_*, C++) or the Python WindowedStereoVO")
     ap.add_argument("--comm", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend for N > 1 (gloo: the sharded BA exchanges host-staged through "
                          "me_comm_create_callback -- rehearses the N-rank branch without RCCL)")
@@ -872,6 +874,27 @@ def sharded_ba_line(args, ctx, dist, world, rank, local_rank, barrier):
     return out
 
 
+def _frame_event_records(vo):
+    """The keyframe (new / addMatch) events of a loop's WBA_Point log as me_vo_event records, in log order."""
+    from uasl_motion_estimation_amd._lib import VO_EVENT_DTYPE
+
+    if hasattr(vo, "event_records"):
+        e = vo.event_records()
+        return e[e["kind"] < 2]
+    recs = [r for r in vo._ev if r[0] == "frame"]
+    n = sum(len(r[1]) for r in recs)
+    out = np.zeros(n, VO_EVENT_DTYPE)
+    k = 0
+    for _, ids, t, feats, is_new in recs:
+        m = len(ids)
+        out["kind"][k:k + m] = np.where(is_new, 0, 1)
+        out["t"][k:k + m] = t
+        out["id"][k:k + m] = ids
+        out["feat"][k:k + m] = feats
+        k += m
+    return out
+
+
 def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_prefix: int = 0):
     """The windowed stereo VO loop itself (uasl_motion_estimation_amd/
     pipeline.py) on one synthetic stream of config c: per keyframe KLT, the
@@ -897,38 +920,66 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_pr
     gen = time.perf_counter() - t0
     cfg = PL.PipelineConfig.from_config(c)
 
+    native = args.vo_loop == "native"
+
     def run(timed_families=False, log=False):
-        be = PL.GPUBackend(ctx)
-        for t in range(n):
-            be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
-        ctx.synchronize()
-        vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=log, overlap=True)
+        from types import SimpleNamespace
+
+        import torch
+
+        if native:  # the loop in C++ (me_vo_loop_*); the images device-resident before timing
+            dev = [(torch.from_numpy(fr[t].left).to(f"cuda:{ctx.device}"),
+                    torch.from_numpy(fr[t].right).to(f"cuda:{ctx.device}")) for t in range(n)]
+            torch.cuda.synchronize()
+            vo = PL.NativeStereoVO(cfg, ctx, K, p0, v, log_events=log, overlap=True)
+            tctx, be = vo.tctx, None
+
+            def proc(t):
+                vo.process(t, *dev[t])
+        else:
+            be = PL.GPUBackend(ctx)
+            for t in range(n):
+                be.frame_images(t, fr[t].left, fr[t].right)  # resident before timing
+            ctx.synchronize()
+            vo = PL.WindowedStereoVO(cfg, be, K, p0, v, log_events=log, overlap=True)
+            tctx = be.tctx
+
+            def proc(t):
+                vo.process(t, fr[t].left, fr[t].right)
         for t in range(warm):
-            vo.process(t, fr[t].left, fr[t].right)
+            proc(t)
         # (no finish() here: the loop applies BA(t-1) after keyframe t's matching, so the timed span
         # starts in steady state, with the last warm-up keyframe's BA in flight)
-        for cc in (ctx, be.tctx):
+        for cc in (ctx, tctx):
             cc.timing_reset()
             cc.timing(timed_families)
         h0, w0 = vo.stage_s["host"], vo.stage_s["wait"]
         ws0 = dict(vo.wait_by_stage)
         t1 = time.perf_counter()
         for t in range(warm, n):
-            vo.process(t, fr[t].left, fr[t].right)
+            proc(t)
         vo.finish()
         el = time.perf_counter() - t1
         fam = {}
         if timed_families:
             for name in ("MI", "SCALE_RES", "SCALE_NEQ", "BA_LINEARIZE", "BA_SCHUR", "BA_SOLVE", "BA_STEP", "KLT",
                          "PYR"):
-                ms = sum(cc.timing_read(name)[1] for cc in (ctx, be.tctx))
+                ms = sum(cc.timing_read(name)[1] for cc in (ctx, tctx))
                 if ms > 0:
                     fam[name] = round(1e3 * ms / (n - warm), 1)
-            for cc in (ctx, be.tctx):
+            for cc in (ctx, tctx):
                 cc.timing(False)
-        be.close()
-        ws = {k: round(1e3 * (v - ws0.get(k, 0.0)) / (n - warm), 3) for k, v in vo.wait_by_stage.items()}
-        return vo, el, (vo.stage_s["host"] - h0), (vo.stage_s["wait"] - w0), fam, ws
+        stage, wbs = vo.stage_s, vo.wait_by_stage
+        ws = {k: round(1e3 * (v_ - ws0.get(k, 0.0)) / (n - warm), 3) for k, v_ in wbs.items()}
+        # a snapshot of what the line reads (the native loop's state goes with close())
+        snap = SimpleNamespace(results=vo.results, poses=vo.poses, ids=vo.ids, latest_id=vo.latest_id,
+                               events=vo.events if log else None,
+                               frame_events=_frame_event_records(vo) if log else None)
+        if native:
+            vo.close()
+        else:
+            be.close()
+        return snap, el, (stage["host"] - h0), (stage["wait"] - w0), fam, ws
 
     # the timed run keeps no event log (a test artefact); the family-timed run logs the events
     # the parity leg compares (the same decisions: events are only recorded, never read back)
@@ -939,6 +990,7 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_pr
     out = {"workload": f"config {c}: {cfg.width}x{cfg.height} stereo, {cfg.n_feats} features, {cfg.window}-keyframe "
                        f"sliding window, {n} keyframes (KLT + epipolar MI matching + tracks + scale LM + "
                        f"{cfg.ba_iters}-iteration BA per keyframe), pipelined on two contexts",
+           "host_loop": "native (me_vo_loop_*, C++)" if native else "python (WindowedStereoVO)",
            "frames_per_s": round(m / el, 2), "ms_per_frame": round(1e3 * el / m, 3), "frames_timed": m,
            "host_ms_per_frame": round(1e3 * host_s / m, 3), "wait_ms_per_frame": round(1e3 * wait_s / m, 3),
            "wait_ms_per_frame_by_call": ws,
@@ -975,11 +1027,11 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_pr
         for t in range(P):
             ov.process(t, fr[t].left, fr[t].right)
         ov.finish()
-        frames_g = [e for e in vo_ev._ev if e[0] == "frame" and e[2] < P]
-        frames_o = [e for e in ov._ev if e[0] == "frame"]
-        ev_ok = len(frames_g) == len(frames_o) and all(
-            np.array_equal(a[1], b[1]) and a[2] == b[2] and np.array_equal(a[3].view(np.uint32), b[3].view(np.uint32))
-            and np.array_equal(a[4], b[4]) for a, b in zip(frames_g, frames_o))
+        fg = vo_ev.frame_events
+        fg = fg[fg["t"] < P]
+        fo = _frame_event_records(ov)
+        ev_ok = len(fg) == len(fo) and all(np.array_equal(fg[k], fo[k]) for k in ("kind", "t", "id")) and \
+            np.array_equal(fg["feat"].view(np.uint32), fo["feat"].view(np.uint32))
         rg, ro = vo_ev.results[:P], ov.results[:P]
         same = all((a.n_tracked, a.n_new, a.n_window_pts, a.n_window_obs, a.ba_iters, a.scale_stop, a.scale_iters)
                    == (b.n_tracked, b.n_new, b.n_window_pts, b.n_window_obs, b.ba_iters, b.scale_stop, b.scale_iters)

@@ -911,6 +911,15 @@ __device__ __noinline__ void lm_neq_tracks(const ScaleArgs* ga, double scale, co
   if (t < a.nL + a.nR)
     neq_track(a, td, t, h, uniform_ptr(res), uniform_ptr(jj), uniform_ptr(je), uniform_ptr(err));
 }
+#ifdef ME_SCALE_TS  // timing experiment only (tools/scale_ts.py): phase split of the persistent LM, 100 MHz ticks
+// workgroup (0, 0)'s view: [0] phases, [1] launches, [2] launch wall, [3] track work A/D, [4] B, [5] C,
+// [6] waits for the phase's control (after its own work), [7] phases of type A/D, [8] B, [9] C;
+// the controlling workgroup: [10] reduce + control (from its arrival), [11] controls
+__device__ unsigned long long g_scale_ts[16];
+#define SC_T() ((long long)__builtin_amdgcn_s_memrealtime())
+#define SC_ADD(k, v) atomicAdd(&g_scale_ts[(k)], (unsigned long long)(v))
+#define SC_WG0 (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+#endif
 __device__ __forceinline__ void lm_publish(unsigned* epoch, unsigned v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   __hip_atomic_store(epoch, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -931,7 +940,14 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
     return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const unsigned long long*>(q),
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   };
+#ifdef ME_SCALE_TS
+  long long ts_launch = 0, ts_ph = 0, ts_work = 0;
+  if (SC_WG0) ts_launch = SC_T();
+#endif
   for (int ph = 0; ph < max_phases; ++ph) {
+#ifdef ME_SCALE_TS
+    if (SC_WG0) ts_ph = SC_T();
+#endif
     if (threadIdx.x == 0) {
       s_phase = ld_i(&lm->phase);
       s_cur = ld_i(&lm->cur);
@@ -942,13 +958,42 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
     }
     __syncthreads();
     const int phase = s_phase;
+#ifdef ME_SCALE_TS
+    if (phase == PH_DONE) {
+      if (SC_WG0) {
+        SC_ADD(1, 1);
+        SC_ADD(2, SC_T() - ts_launch);
+      }
+      return;
+    }
+#else
     if (phase == PH_DONE) return;
+#endif
     const int cur = s_cur;
+#ifdef ME_SCALE_TS
+    long long ts_ctrl = 0;
+    auto sc_work_done = [&](int k) {
+      if (SC_WG0) {
+        ts_work = SC_T();
+        SC_ADD(k, ts_work - ts_ph);
+        SC_ADD(k + 4, 1);
+        SC_ADD(0, 1);
+      }
+    };
+    auto sc_ctrl_begin = [&]() { if (threadIdx.x == 0) ts_ctrl = SC_T(); };
+    auto sc_ctrl_end = [&]() { if (threadIdx.x == 0) { SC_ADD(10, SC_T() - ts_ctrl); SC_ADD(11, 1); } };
+#else
+    auto sc_work_done = [](int) {};
+    auto sc_ctrl_begin = []() {};
+    auto sc_ctrl_end = []() {};
+#endif
     if (phase == PH_B) {
       if (blockIdx.y == 0) {
         const double* res = resb + (long)cur * rows_pad;
         if (!p.test) lm_neq_tracks(gaN, s_scale, gtd, res, jj, je, err);
+        sc_work_done(4);
         if (last_block_arrives(cnt + 1, nwg)) {
+          sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           double sx = 0, sy = 0;
           if (!p.test) block_reduce2<kScBlock>(jj, je, p.n, 0, &sx, &sy);
@@ -957,13 +1002,16 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
             scale_ctrl_run(lm, sp, p, PH_B, sx, sy, *err);
             lm_publish(epoch, (unsigned)ph + 1);
           }
+          sc_ctrl_end();
         }
       }
     } else if (phase == PH_A || phase == PH_D) {
       if (blockIdx.y == 0) {
         double* res = res_buf(resb, rows_pad, cur);
         lm_res_tracks(gaR, s_scale, gtd, res, err);
+        sc_work_done(3);
         if (last_block_arrives(cnt + 1, nwg)) {
+          sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           double sx, sy;
           block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
@@ -972,6 +1020,7 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
             scale_ctrl_run(lm, sp, p, phase, sx, 0.0, *err);
             lm_publish(epoch, (unsigned)ph + 1);
           }
+          sc_ctrl_end();
         }
       }
     } else {  // PH_C: the batch's candidates
@@ -980,6 +1029,7 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
         double* res = res_buf(resb, rows_pad, (cur + 1 + j) % kResBufs);
         lm_res_tracks(gaR, s_ts[j], gtd, res, err);
         if (last_block_arrives(cnt + 1 + j, nwg)) {
+          sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           double sx, sy;
           block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
@@ -995,8 +1045,10 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
               lm_publish(epoch, (unsigned)ph + 1);
             }
           }
+          sc_ctrl_end();
         }
       }
+      sc_work_done(5);
     }
     // wait for the phase's control (bounded), then read the next phase
     if (threadIdx.x == 0) {
@@ -1007,6 +1059,9 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
       }
       s_quit = k == kPhaseSpin;
       if (s_quit) atomicOr(err, kErrSpin);
+#ifdef ME_SCALE_TS
+      if (SC_WG0) SC_ADD(6, SC_T() - ts_work);
+#endif
     }
     __syncthreads();
     if (s_quit) return;
@@ -1743,3 +1798,15 @@ extern "C" int me_scale_state_mi(me_ctx* c, const me_scale_state* s, double* mi_
   if (n_patches) *n_patches = (int)o[1];
   return ME_OK;
 }
+
+#ifdef ME_SCALE_TS
+extern "C" int me_scale_ts(long long* out, int reset) {
+  hipDeviceSynchronize();
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scale_ts), sizeof(g_scale_ts));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_scale_ts), z, sizeof(z));
+  }
+  return 0;
+}
+#endif

@@ -44,7 +44,7 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
 #define ME_DIAG_EXP 0  // timing experiments only (tools/ubench_diag.hip), results invalid: 1 no Newton step, 2 no MFMA, 4 no rsq, 8 no substitutions
 #endif
 #ifndef ME_DIAG_GATHER
-#define ME_DIAG_GATHER 1  // 1: permlane swaps + readlane, 0: wave-private LDS scratch
+#define ME_DIAG_GATHER 1  // 1: permlane swaps + readlane, 2: permlane swaps + DPP row broadcasts, 0: wave-private LDS scratch
 #endif
 __device__ __forceinline__ double lane_read(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
@@ -64,12 +64,45 @@ __device__ __forceinline__ void col_gather4(double x, double o[4]) {
   o[2] = __hiloint2double((int)ah[1], (int)al[1]);
   o[3] = __hiloint2double((int)bh[1], (int)bl[1]);
 }
+// Rounds whose pivots are all padding or the right-hand-side row (p0 >= nreal:
+// the last diagonal block of a system whose n + 1 rows end inside it) are
+// skipped: nothing reads their L entries (no trailing block follows, the
+// backward solve starts at block (n - 1) / 16), and their X rows are written
+// as zeros -- the backward solve multiplies them by the zero entries of u
+// past n.  Config 3 (n = 108): the last block's fourth round; config 5
+// (n = 288): the whole last block.
+#ifndef ME_DIAG_SKIP_PAD
+#define ME_DIAG_SKIP_PAD 1
+#endif
+template <int S>
+__device__ __forceinline__ double row_bcast(double x) {  // lane S of every 16-lane row, to the whole row (DPP)
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x150 + S, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x150 + S, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
 template <int R>
 __device__ __forceinline__ void diag_round_mfma(double4_t& A4, double4_t& Y4, int q, int c, int nreal, bool& ok,
                                                 double* Lblk, int lld, double* X, double* gx) {
   constexpr int p0 = 4 * R;
+  if (ME_DIAG_SKIP_PAD && p0 >= nreal) {  // (wave-uniform)
+    X[(p0 + q) * 16 + c] = 0.0;
+    return;
+  }
   double acol[4], ycol[4], Lq[4][4];
-  if (ME_DIAG_GATHER) {
+  if (ME_DIAG_GATHER == 2) {
+    // the pivot block from the column gather: lane (q, p0 + v) holds acol[u] =
+    // A[p0 + u][p0 + v] in every row, broadcast along the row by DPP (VGPR
+    // results, no readlane / SGPR round trip)
+    col_gather4(A4[R], acol);
+    col_gather4(Y4[R], ycol);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      Lq[u][0] = row_bcast<p0 + 0>(acol[u]);
+      if (u >= 1) Lq[u][1] = row_bcast<p0 + 1>(acol[u]);
+      if (u >= 2) Lq[u][2] = row_bcast<p0 + 2>(acol[u]);
+      if (u >= 3) Lq[u][3] = row_bcast<p0 + 3>(acol[u]);
+    }
+  } else if (ME_DIAG_GATHER) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
