@@ -205,7 +205,8 @@ def test_native_loop_shared_context_and_device_images(ctx, seq5):
             assert np.array_equal(a.ids, o.ids) and np.array_equal(a.X, o.X)
             pa, po = a.poses, o.poses
             assert all(np.array_equal(pa[t], po[t]) for t in pa)
-            assert [(r.scale, r.ba_cost) for r in a.results] == [(r.scale, r.ba_cost) for r in o.results]
+            ra = np.array([(r.scale, r.ba_cost) for r in a.results])
+            assert np.array_equal(ra, np.array([(r.scale, r.ba_cost) for r in o.results]), equal_nan=True)
     finally:
         for o in (a, b, c):
             o.close()
@@ -272,8 +273,10 @@ def test_cpp_host_drives_the_loop(ctx, seq5, tmp_path):
         assert [int(t) for t in ps["t"]] == sorted(pp) and all(np.array_equal(p["pose"], pp[int(p["t"])]) for p in ps)
         pr = py.results
         assert nres == n == len(pr)
-        assert all((int(a["t"]), int(a["n_tracked"]), int(a["n_new"]), float(a["scale"]), float(a["cost"]))
-                   == (b.t, b.n_tracked, b.n_new, b.scale, b.ba_cost) for a, b in zip(res, pr))
+        assert [(int(a["t"]), int(a["n_tracked"]), int(a["n_new"])) for a in res] == [(b.t, b.n_tracked, b.n_new)
+                                                                                        for b in pr]
+        assert np.array_equal(np.array([(a["scale"], a["cost"]) for a in res]),
+                              np.array([(b.scale, b.ba_cost) for b in pr]), equal_nan=True)  # (no-BA keyframes: NaN cost)
     finally:
         py.close()
 

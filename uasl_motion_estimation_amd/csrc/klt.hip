@@ -115,6 +115,16 @@ constexpr int kMaxWinPx = 7;  // pixels per lane: ceil(21*21/64)
 // levels narrower or shorter than the region read global memory directly.
 // Same pixel values either way, so results are unchanged bit for bit.
 constexpr int kRegion = 32;
+// Template staging (ME_KLT_TSTAGE): per level the (win + 1)^2 template
+// footprint of I, DX and DY is copied into the wave's LDS with row-contiguous
+// loads (ceil(22 * 22 / 64) = 8 elements of each array per lane: 24 narrow
+// loads instead of the 84 scattered ones of the per-pixel 2 x 2 gathers), and
+// the bilinear taps are read from LDS.  Same values in the same order: same
+// bits.
+#ifndef ME_KLT_TSTAGE
+#define ME_KLT_TSTAGE 0
+#endif
+constexpr int kTplMax = 22;  // (win + 1) for win <= 21
 
 // wave-local ordering of this wave's LDS region (no cross-wave sharing)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -144,6 +154,10 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
                                                   uint8_t* __restrict__ status, int n, int win, int max_iters,
                                                   double eps2, double min_eig) {
   __shared__ __attribute__((aligned(16))) uint8_t regions[4][kRegion * kRegion];
+#if ME_KLT_TSTAGE
+  __shared__ uint8_t tplI[4][kTplMax * kTplMax];
+  __shared__ int16_t tplX[4][kTplMax * kTplMax], tplY[4][kTplMax * kTplMax];
+#endif
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= n) return;  // wave-uniform
@@ -190,6 +204,49 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const int16_t* DX = P.dx[L];
     const int16_t* DY = P.dy[L];
     int i4[kMaxWinPx][4], x4[kMaxWinPx][4], y4[kMaxWinPx][4];
+#if ME_KLT_TSTAGE
+    if (win + 1 <= kTplMax) {
+      const int tw = win + 1, tn = tw * tw, wv = threadIdx.x >> 6;
+      uint8_t* TI = tplI[wv];
+      int16_t* TX = tplX[wv];
+      int16_t* TY = tplY[wv];
+      int vi[8], vx[8], vy[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = min(lane + 64 * k, tn - 1), r = e / tw, cc = e - r * tw;
+        vi[k] = I[(long)(iy0 + r) * SI + ix0 + cc];
+        vx[k] = DX[(long)(iy0 + r) * W + ix0 + cc];
+        vy[k] = DY[(long)(iy0 + r) * W + ix0 + cc];
+      }
+      wave_lds_sync();  // the previous level's reads of the template are done
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = lane + 64 * k;
+        if (e < tn) {
+          TI[e] = (uint8_t)vi[k];
+          TX[e] = (int16_t)vx[k];
+          TY[e] = (int16_t)vy[k];
+        }
+      }
+      wave_lds_sync();
+#pragma unroll
+      for (int q = 0; q < kMaxWinPx; ++q) {
+        const int o = wy[q] * tw + wx[q];
+        i4[q][0] = TI[o];
+        i4[q][1] = TI[o + 1];
+        i4[q][2] = TI[o + tw];
+        i4[q][3] = TI[o + tw + 1];
+        x4[q][0] = TX[o];
+        x4[q][1] = TX[o + 1];
+        x4[q][2] = TX[o + tw];
+        x4[q][3] = TX[o + tw + 1];
+        y4[q][0] = TY[o];
+        y4[q][1] = TY[o + 1];
+        y4[q][2] = TY[o + tw];
+        y4[q][3] = TY[o + tw + 1];
+      }
+    } else
+#endif
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
       const long o = (long)(iy0 + wy[q]) * W + ix0 + wx[q], oi = (long)(iy0 + wy[q]) * SI + ix0 + wx[q];

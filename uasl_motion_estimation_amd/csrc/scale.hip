@@ -872,7 +872,11 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, T
 // parameters (written by the prep launch), re-read in every phase with
 // scalar loads; inlined into the phase loop, its invariants (the kernel
 // arguments) are hoisted across the loop and the kernel needs >400 registers.
-constexpr int kCandY = 2;
+constexpr int kCandY = 2;  // candidate rows of the persistent grid (at least; up to kCandYMax when they fit)
+#ifndef ME_SCALE_CANDY_MAX
+#define ME_SCALE_CANDY_MAX 2
+#endif
+constexpr int kCandYMax = ME_SCALE_CANDY_MAX;
 constexpr int kEpochWord = 40;  // P.bar[kEpochWord]: phases completed (zeroed by the prep launch with the counters)
 constexpr long kPhaseSpin = 1L << 22;
 constexpr int kErrSpin = 8;
@@ -1574,13 +1578,17 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     if (c->cu_active > 0) cus = std::min(cus, c->cu_active);  // own stream restricted by me_set_cu_mask
     c->scale_lm_cap = per_cu * cus;
   }
-  const bool persist = !blocks_env && 2L * nb * kCandY <= c->scale_lm_cap;
+  // candidate rows: as many as fit co-resident within half the device (a
+  // batch of n candidates takes ceil(n / rows) passes over the tracks)
+  int cand_y = kCandY;
+  while (cand_y < kCandYMax && 2L * nb * (2 * cand_y) <= c->scale_lm_cap) cand_y *= 2;
+  const bool persist = !blocks_env && 2L * nb * cand_y <= c->scale_lm_cap;
   if (persist) {
     lp.mirror_done_only = 1;
     {
       me_ktimer t(c, ME_KT_SCALE_RES);
       const int max_phases = 256 * (p.max_nb_iter + 2);
-      hipLaunchKernelGGL(scale_lm_kernel, dim3(nb, kCandY), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
+      hipLaunchKernelGGL(scale_lm_kernel, dim3(nb, cand_y), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
                          P.res, P.rows_pad, P.jj, P.je, P.err, P.lm, P.spec, lp, P.bar, P.bar + kEpochWord,
                          max_phases);
     }
