@@ -25,6 +25,7 @@ buf = (ctypes.c_longlong * 24)()
 names = {1: "lin_finalize", 2: "asm_wait", 11: "ts_asm_probe", 12: "load_issue", 13: "load_diag_barrier",
          3: "load_rest", 4: "factor", 5: "backward", 6: "tail", 8: "asm_last_exit", 9: "asm_first_entry",
          19: "f_diag0", 16: "f_w0_panel", 17: "f_w0_diag", 18: "f_barrier_wait"}
+names5 = {**names, 16: "m2_w0_diag", 17: "m2_count_wait", 18: "m2_panel", 19: "m2_drain_publish"}
 for c in (3, 5):
     cfg = S.CONFIGS[c]
     bp = S.ba_problem(S.SEED0 * 7 + c, cfg["n_feats"], cfg["window"], cfg["width"], cfg["height"])
@@ -35,7 +36,7 @@ for c in (3, 5):
         ba_solve(bp.copy(), SolverOptions.fixed_iterations(10), ctx=ctx)
     fn(buf, 1)
     calls = max(buf[15], 1)
-    us = {nm: round(buf[i] / calls / 100.0, 2) for i, nm in names.items()}
+    us = {nm: round(buf[i] / calls / 100.0, 2) for i, nm in (names5 if c == 5 else names).items()}
     tot = sum(buf[i] for i in (1, 2, 3, 4, 5, 6, 11, 12, 13, 16, 17, 18, 19)) / calls / 100.0
     clk = buf[10] / calls / (tot * 1e-6) / 1e9 if tot > 0 else 0.0
     print(f"config {c}: calls {calls} us/launch {us} wg0 total {tot:.2f} us, core clock {clk:.2f} GHz", flush=True)

@@ -822,9 +822,6 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
         }
       };
       auto contract = [&](int ks, const double* a, const double* bb) {
-#ifdef ME_SCHUR_NO_MFMA  // timing experiment only: operands read, no contraction
-        return;
-#endif
 #pragma unroll
         for (int u = 0; u < NT; ++u)
           if ((hm[u] >> ks) & 1ull) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], bb[u], acc[u], 0, 0, 0);
@@ -1261,158 +1258,12 @@ __device__ unsigned long long g_asm_first = ~0ull, g_asm_last = 0ull;
 #endif
 
 // dynamic LDS: X (Ts x 256) | z/y (N) | row exchange (256) | A (N x ld, when it fits)
-#ifndef ME_CHOL_PB
-#define ME_CHOL_PB 4
-#endif
-constexpr int kXchDoubles = 48 * ME_CHOL_PB;  // per buffer: pivot rows A (16 PB) | pivot rows Y (16 PB) | column group (16 PB)
+constexpr int kXchDoubles = 192;  // per buffer: the one-wave diagonal factor's LDS scratch (ME_DIAG_GATHER 0)
 constexpr int kDiagLd = 17;  // staged diagonal block (global-memory form): 16 x 17 doubles
 __host__ __device__ inline size_t solve_small_doubles(int Ts) {
   return 256 * (size_t)Ts + 16 * (size_t)Ts + 2 * (size_t)kXchDoubles + 16 * kDiagLd;
 }
 __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 * Ts) * solve_ld(Ts); }
-
-template <int S>
-__device__ __forceinline__ double quad_bcast(double x) {
-  constexpr int ctrl = S | (S << 2) | (S << 4) | (S << 6);
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), ctrl, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), ctrl, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-}
-
-// Diagonal block of the blocked Cholesky, spread over the four SIMDs: wave w
-// (< 4) owns rows 4w..4w+3, lane = 16 (i - 4w) + c holds A[i][c] and Y[i][c]
-// (Y -> X = L^-1).  Four rounds of 4 pivots; per round one LDS exchange
-// (pivot rows of wave R + column group R of every row) behind one barrier,
-// the 4x4 pivot block factored and inverted redundantly by every lane
-// (uniform values), then 4-term updates.  1/sqrt by v_rsq_f64 + two Newton
-// steps.  Measured on gfx950: dependent FP64 FMA ~8.5 cycles, rsq ~19,
-// LDS round trip ~105, barrier ~80 -- so the round is bound by the pivot
-// chain, and splitting the updates over 4 SIMDs removes the single-wave
-// issue bottleneck of the previous one-wave version.
-// PB = pivots per round (PB x PB pivot block, factored and inverted
-// redundantly by every lane); round R eliminates columns PB R .. PB R + PB - 1.
-// The per-round cost is a fixed ~690 cycles (barrier + LDS exchange + read
-// latency) plus the uniform PB x PB work, which every lane issues.  Measured
-// on config 3 (7 diagonal blocks): PB = 4 -> 45.4k cycles of diagonal work per
-// solve, PB = 2 (8 rounds per block) -> 56.1k; PB = 4 stays.
-#ifdef ME_ROUND_STAMPS  // timing experiment only (tools/abl): per-round phase times of the diagonal factor
-__device__ unsigned long long g_round_stamps[8];
-#define RSTAMP(k, dep)                                                                                 \
-  do {                                                                                                 \
-    if (threadIdx.x == 0) {                                                                            \
-      asm volatile("" ::"v"(dep));                                                                     \
-      unsigned long long tt_;                                                                          \
-      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt_)::"memory");                     \
-      if ((k) > 0) atomicAdd(&g_round_stamps[(k)-1], tt_ - rs_prev_);                                 \
-      rs_prev_ = tt_;                                                                                  \
-    }                                                                                                  \
-  } while (0)
-#else
-#define RSTAMP(k, dep) \
-  do {                 \
-  } while (0)
-#endif
-template <int PB, int R>
-__device__ __forceinline__ void cholw_round(double& a, double& y, bool act, int i, int c, int nreal, bool& ok,
-                                            double* Ablk, int ld, double* X, double* xch) {
-  double* xb = xch + kXchDoubles * (R & 1);
-  constexpr int p0 = PB * R;
-#ifdef ME_ROUND_STAMPS
-  unsigned long long rs_prev_ = 0;
-#endif
-  RSTAMP(0, a);
-  if (act) {
-    if (i >= p0 && i < p0 + PB) {
-      xb[16 * (i - p0) + c] = a;            // A[p0+u][c]
-      xb[16 * PB + 16 * (i - p0) + c] = y;  // Y[p0+u][c]
-    }
-    if (c >= p0 && c < p0 + PB) xb[32 * PB + PB * i + (c - p0)] = a;  // A[i][p0+u]
-  }
-  __syncthreads();
-  if (!act) return;
-  RSTAMP(1, a);
-  // Uniform PB x PB Cholesky of the pivot block (every lane, redundantly),
-  // interleaved with the forward substitutions that need its columns as
-  // they appear: this lane's row of the panel, L[i][p0+t]; the row the update
-  // pairs it with, L[c][p0+t]; and the pivot rows of X = L^-1, X[p0+t][c].
-  // No inverse of the pivot block is formed, and the rank-PB update is summed
-  // as the columns arrive, so after the last pivot only one substitution step
-  // and one update term remain on the round's dependency chain.
-  double Lq[PB][PB], ar[PB], xa[PB], xy[PB];
-#pragma unroll
-  for (int u = 0; u < PB; ++u) {
-    ar[u] = xb[32 * PB + PB * i + u];  // A[i][p0+u]
-    xa[u] = xb[16 * u + c];            // A[p0+u][c] = A[c][p0+u]
-    xy[u] = xb[16 * PB + 16 * u + c];  // Y[p0+u][c]
-#pragma unroll
-    for (int v = u; v < PB; ++v) Lq[v][u] = xb[16 * v + p0 + u];  // A[p0+v][p0+u] (lower)
-  }
-  double Lr[PB], Lc[PB], Xg[PB];
-  double av = a, yv = y;
-#pragma unroll
-  for (int t = 0; t < PB; ++t) {
-    double piv = Lq[t][t];
-#pragma unroll
-    for (int u = 0; u < t; ++u) piv = fma(-Lq[t][u], Lq[t][u], piv);
-    const bool pad = p0 + t >= nreal;  // padding / right-hand-side row: never a failure
-    ok = ok && (pad || piv > 0);
-    piv = (pad && !(piv > 0)) ? 1.0 : piv;
-    const double r = rsqrt_nr(piv);
-    Lq[t][t] = piv * r;
-#pragma unroll
-    for (int v = t + 1; v < PB; ++v) {
-      double x = Lq[v][t];
-#pragma unroll
-      for (int u = 0; u < t; ++u) x = fma(-Lq[v][u], Lq[t][u], x);
-      Lq[v][t] = x * r;
-    }
-    double sr = ar[t], sc = xa[t], sx = xy[t];
-#pragma unroll
-    for (int u = 0; u < t; ++u) {
-      sr = fma(-Lr[u], Lq[t][u], sr);
-      sc = fma(-Lc[u], Lq[t][u], sc);
-      sx = fma(-Lq[t][u], Xg[u], sx);
-    }
-    Lr[t] = sr * r;  // L[i][p0+t]
-    Lc[t] = sc * r;  // L[c][p0+t]
-    Xg[t] = sx * r;  // X[p0+t][c]
-    av = fma(-Lr[t], Lc[t], av);
-    yv = fma(-Lr[t], Xg[t], yv);
-  }
-  RSTAMP(2, Lq[PB - 1][PB - 1]);
-  RSTAMP(3, Lr[PB - 1] + Lc[PB - 1] + Xg[PB - 1]);
-  if (c >= p0 && c < p0 + PB && c <= i) {
-    double v = Lr[0];
-#pragma unroll
-    for (int t = 1; t < PB; ++t)
-      if (c - p0 == t) v = Lr[t];
-    if (c == i) {
-#pragma unroll
-      for (int t = 0; t < PB; ++t)
-        if (c - p0 == t) v = Lq[t][t];
-    }
-    Ablk[i * ld + c] = v;
-  }
-  if (i >= p0 && i < p0 + PB) {
-    double v = Xg[0];
-#pragma unroll
-    for (int t = 1; t < PB; ++t)
-      if (i - p0 == t) v = Xg[t];
-    X[i * 16 + c] = v;
-  }
-  if (i >= p0 + PB) {
-    a = av;
-    y = yv;
-  }
-  RSTAMP(4, a + y);
-}
-
-template <int PB, int R>
-__device__ __forceinline__ void chol_rounds(double& a, double& y, bool act, int i, int c, int nreal, bool& ok,
-                                            double* Ablk, int ld, double* X, double* xch) {
-  cholw_round<PB, R>(a, y, act, i, c, nreal, ok, Ablk, ld, X, xch);
-  if constexpr (R + 1 < 16 / PB) chol_rounds<PB, R + 1>(a, y, act, i, c, nreal, ok, Ablk, ld, X, xch);
-}
 
 // Global-memory form (windows whose [S; -b^T] does not fit the LDS, config 4
 // and 5): block 0 factors the diagonal blocks and panels as below, and the
@@ -1432,38 +1283,6 @@ constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 // to the counter (agent-scope atomic), the consumer polls with an sc1 load and
 // reads A only with sc1 loads after its barrier -- no release fence (an L2
 // write-back) and no acquire (an L1 invalidate) per hand-off.
-#ifndef ME_SOLVE_LOOKAHEAD
-#define ME_SOLVE_LOOKAHEAD 1
-#endif
-#ifndef ME_SOLVE_PIPE
-#define ME_SOLVE_PIPE 1
-#endif
-#ifndef ME_SOLVE_BWD1
-// LDS form without ME_SOLVE_INVE: backward solve on wave 0, u in registers
-// (0: all waves, two barriers per block).  Measured: 4.7 vs 3.8 us; off.
-#define ME_SOLVE_BWD1 0
-#endif
-#ifndef ME_SOLVE_INVE
-// LDS form: the worker waves accumulate E = L^-T in the (otherwise unused)
-// upper block triangle during the factorisation, so the backward solve is
-// one product y = E z (see the kPipe loop).  Measured (config 3 stamps):
-// backward 3.78 -> 1.45 us, but wave 0's panels 4.22 -> 5.59 and the step
-// barriers 1.60 -> 2.87 us (the workers' extra tiles), +1.2 us for E's last
-// column: 37.0 vs 35.5 us per solve; off.
-#define ME_SOLVE_INVE 0
-#endif
-#ifndef ME_SOLVE_PANEL_REG
-// wave 0's panel tile kept in registers for the diagonal update (0: through
-// LDS).  Measured (config 3 stamps): panel 4.23 -> 4.97 us, diagonal 12.50 ->
-// 11.81 us per solve -- no gain; off.
-#define ME_SOLVE_PANEL_REG 0
-#endif
-#ifndef ME_SOLVE_EARLY0
-// fused LDS form: wave 0 copies rows 0-15 itself and factors block 0 while
-// the rest arrives.  Measured: no gain (one wave's 17 KiB copy takes as long
-// as the whole 133 KiB over eight waves, 2.5 us); off.
-#define ME_SOLVE_EARLY0 0
-#endif
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
 constexpr int kSkipImg = 4096;                // cam_solve `skip` bit: [S + D; -b^T] already in Abuf (solver layout)
 #ifndef ME_SOLVE_IMG
@@ -1562,6 +1381,7 @@ __device__ __forceinline__ void trailing_tile(double* A, int ld, int J, int I, i
 // l holds A_IK[(l >> 4) + 4 s][l & 15] in element s: the layout the one-wave
 // diagonal factorisation takes its block in) instead of stored.
 // (Diagonal tile, K = I: both MFMA operands come from the same panel tile.)
+template <bool SC1 = false>
 __device__ __forceinline__ double4_t trailing_diag_acc(const double* A, int ld, int J, int I, int lane) {
   const int j0 = 16 * J, i0 = 16 * I;
   double av[4], bv[4];
@@ -1569,9 +1389,9 @@ __device__ __forceinline__ double4_t trailing_diag_acc(const double* A, int ld, 
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int cc = j0 + 4 * s + (lane >> 4);
-    bv[s] = A[(long)(i0 + (lane & 15)) * ld + cc];
+    bv[s] = a_ld<SC1>(&A[(long)(i0 + (lane & 15)) * ld + cc]);
     av[s] = -bv[s];
-    acc[s] = A[(long)(i0 + (lane >> 4) + 4 * s) * ld + i0 + (lane & 15)];
+    acc[s] = a_ld<SC1>(&A[(long)(i0 + (lane >> 4) + 4 * s) * ld + i0 + (lane & 15)]);
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s], bv[s], acc, 0, 0, 0);
@@ -1599,9 +1419,12 @@ __device__ __forceinline__ void spin_timeout(const Bufs& b) {
 // owned by one wave of one worker for the whole solve (linear index
 // (I-1) I / 2 + K - 1, dealt round-robin over the workers' waves), so its
 // successive updates are ordered by that wave's program order.  Per block step
-// J (after block 0 publishes the panel of J): the tiles of column J + 1 first
-// -- block 0 factors that column next -- then the worker signals, then its
-// other tiles, which overlap block 0's diagonal block and panel of J + 1.
+// J (after block 0 publishes the panel of J): the tiles of column J + 1 below
+// the diagonal and the diagonal tile (J + 2, J + 2) first -- block 0 needs
+// them for the panel of J + 1 and the diagonal block J + 2 -- then the worker
+// signals, then its other tiles.  The diagonal tile (J + 1, J + 1) is left to
+// block 0, which applies step J to it in registers and factors it while the
+// workers update column J + 1.
 __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
   __shared__ unsigned sep;
   const State* st = b.st;
@@ -1633,7 +1456,11 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
           ++I;
         }
         const int K = r + 1;
-        if (pass == 0 ? K == J + 1 : K > J + 1) trailing_tile<true>(b.Abuf, ld, J, I, K, lane);
+        // pass 0: column J + 1 below the diagonal tile, and the diagonal tile
+        // (J + 2, J + 2); pass 1: the rest.  Tile (J + 1, J + 1) is block 0's
+        // (it applies step J to it in registers before factoring it).
+        const bool col = K == J + 1 && I > J + 1, nd = I == J + 2 && K == J + 2;
+        if (pass == 0 ? (col || nd) : (K > J + 1 && !nd)) trailing_tile<true>(b.Abuf, ld, J, I, K, lane);
       }
       if (pass == 0) {
         drain_and_barrier();
@@ -1690,14 +1517,14 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // the panel fused with the column-(J+1) update in one phase (transposed
   // panel tiles as MFMA operands, no barrier between; 43.8 us) and a one-wave
   // backward solve without workgroup barriers (unchanged).
-  constexpr bool kLook = ME_DIAG_MFMA && ME_SOLVE_LOOKAHEAD && kMode != 2;
+  // Also measured and dropped (git history keeps the code):
+  // the panel tile kept in registers for the diagonal update, E = L^-T
+  // accumulated by the workers, a one-wave backward solve, block 0 factored
+  // beside the LDS copy, a four-wave diagonal factor.
+  constexpr bool kLook = kMode != 2;
   // LDS-resident system: wave 0 alone on the critical path (see below)
-  constexpr bool kPipe = kLook && kLds && ME_SOLVE_PIPE;
-  constexpr bool kInvE = kPipe && ME_SOLVE_INVE;
+  constexpr bool kPipe = kLds;
   __shared__ unsigned pflag, pdone;
-  // Measured and dropped (config 3): panel fused with the column-(J+1) update
-  // in one phase (transposed panel tiles as MFMA operands, no barrier between;
-  // 43.8 vs 42.0 us) and a one-wave backward solve without barriers (no change)
   if (kMode == 2 && blockIdx.x > 0) {
     cam_solve_worker(g, b, nworkers);
     return;
@@ -1796,7 +1623,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int CC = (N + 63) >> 6, RT = (N + nw - 1) / nw, NQ = RT * CC;
   const double* S0 = b.S;
   const int nn = n * n;
-  const bool early0 = kPipe && ME_SOLVE_EARLY0 && fused;
   // the image of [S + D; -b^T] in Abuf: written by s_assemble_kernel (non-fused), or by this launch's
   // assemblers (fused; written through)
   const bool img_ready = (skip & kSkipImg) != 0 || (fused && (kLds || ME_SOLVE_IMG));
@@ -1810,14 +1636,9 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     // the assemblers wrote the solver's image (s_assemble_body img): N x ld
     // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
     // coherent reads (sc1); the barrier below retires them (vmcnt)
-    // (early0: wave 0 takes the chunks of rows 0-15 -- diagonal block 0 --
-    // and the other waves the rest, round-robin)
     const int nbytes = N * ld * 8, nchunk = (nbytes + 1023) >> 10;
-    const int c0 = early0 ? (16 * ld * 8 + 1023) >> 10 : 0;
-    const int kb = early0 ? (wave == 0 ? 0 : c0 + wave - 1) : wave;
-    const int ke = early0 && wave == 0 ? c0 : nchunk, ks = early0 ? (wave == 0 ? 1 : nw - 1) : nw;
     if (!done)
-      for (int k = kb; k < ke; k += ks) {
+      for (int k = wave; k < nchunk; k += nw) {
         const int off = (k << 10) + 16 * lane;
         if (off < nbytes)
           __builtin_amdgcn_global_load_lds((const void*)((const char*)b.Abuf + off),
@@ -1874,10 +1695,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     pflag = 0u;
     pdone = 0u;
   }
-  if (early0 && wave == 0) {  // block 0 from wave 0's own copies, beside the other waves' copies
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    if (!diag_factor_wave(A, ld, X, xch, n, 0, diag_load_wave(A, ld, 0, lane), lane)) sfail = 1;
-  }
   if ((skip & 256) && tid == 0) st->stamps[15] += 1;
   SOLVE_START(0);
   __syncthreads();
@@ -1919,37 +1736,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4) A[(long)(i0 + (lane >> 4) + 4 * q4) * ld + j0 + (lane & 15)] = acc[q4];
     };
-#if ME_SOLVE_PANEL_REG
-    // Wave 0's panel tile of step J, transposed: P = L_{J+1,J}^T = X_J A_{J+1,J}^T
-    // (the operands of panel_tile swapped: the same products and K order, so
-    // the same bits).  In the accumulator layout (lane l, register s holds
-    // P[(l >> 4) + 4 s][l & 15]) P is already both MFMA operands of K-step s
-    // of the diagonal update A_{J+1,J+1} - P^T P: no LDS round trip between
-    // the panel and the factorisation on the critical path.  L_{J+1,J} is
-    // stored (transposed) for the other waves.
-    auto panel_diag = [&](int J) -> double4_t {
-      const int j0 = 16 * J, i0 = 16 * (J + 1);
-      const double* XJ = X + 256 * J;
-      double av[4], bv[4];
-      double4_t D;
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) {
-        av[s4] = XJ[(lane & 15) * 16 + 4 * s4 + (lane >> 4)];
-        bv[s4] = A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)];
-        D[s4] = A[(long)(i0 + (lane >> 4) + 4 * s4) * ld + i0 + (lane & 15)];
-      }
-      double4_t P = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) P = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], P, 0, 0, 0);
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) A[(long)(i0 + (lane & 15)) * ld + j0 + (lane >> 4) + 4 * q4] = P[q4];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) pflag = (unsigned)(J + 1);
-#pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) D = __builtin_amdgcn_mfma_f64_16x16x4f64(-P[s4], P[s4], D, 0, 0, 0);
-      return D;
-    };
-#endif
     auto lds_wait = [&](volatile unsigned* f, unsigned want) {
       long k = 0;
       for (; k < kSolveSpin && *f < want; ++k) __builtin_amdgcn_s_sleep(1);
@@ -1959,11 +1745,9 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
-    if (!early0) {
-      if (wave == 0) diag_factor(0, diag_load_wave(A, ld, 0, lane));
-      STS(19);
-      __syncthreads();
-    }
+    if (wave == 0) diag_factor(0, diag_load_wave(A, ld, 0, lane));
+    STS(19);
+    __syncthreads();
     for (int J = 0; J + 1 < Ts; ++J) {
       if (sfail) break;
       STS(18);
@@ -1971,83 +1755,117 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         // step J on the diagonal tile, handed to the factorisation in registers
         // (its updated values are read by no one else: the factorisation
         // overwrites the lower triangle with L, the upper one is never read)
-#if ME_SOLVE_PANEL_REG
-        const double4_t D = panel_diag(J);
-        STS(16);
-        diag_factor(J + 1, D);
-#else
         panel_tile(J, J + 1);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) pflag = (unsigned)(J + 1);
         solve_wave_sync();  // the panel tile just stored is an operand
         STS(16);
         diag_factor(J + 1, trailing_diag_acc(A, ld, J, J + 1, lane));
-#endif
         STS(17);
       } else if (worker) {
         for (int I = J + 2 + widx; I < Ts; I += nwk) panel_tile(J, I);
-        if (kInvE)  // E panel tiles E_IJ = B_IJ X_J^T, I < J (B: E's rows before step J)
-          for (int I = (widx + nwk - (Ts - J - 2) % nwk) % nwk; I < J; I += nwk) panel_tile(J, I);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         if (lane == 0) atomicAdd(&pdone, 1u);
         lds_wait(&pflag, (unsigned)(J + 1));
         for (int I = J + 2 + widx; I < Ts; I += nwk) trailing_tile<false>(A, ld, J, I, J + 1, lane);
         lds_wait(&pdone, (unsigned)(nwk * (J + 1)));
         trailing_split<false>(A, ld, Ts, J, false, widx, nwk, lane);  // tiles (I, K), J + 2 <= K <= I
-        if (kInvE) {
-          // E's trailing tiles of step J: E_IK -= E_IJ L_KJ^T, I <= J < K
-          // (I = J: E_JJ = X_J^T, and E_JK starts from 0), continuing the
-          // round-robin of the tiles above
-          const int rem = Ts - J - 1, ntr = rem * (rem - 1) / 2, cnt = (J + 1) * rem;
-          for (int p = (widx + nwk - ntr % nwk) % nwk; p < cnt; p += nwk) {
-            const int I = p / rem, K = J + 1 + p % rem;
-            if (I < J) {
-              trailing_tile<false>(A, ld, J, I, K, lane);
-            } else {
-              const int j0 = 16 * J, k0 = 16 * K;
-              const double* XJ = X + 256 * J;
-              double av[4], bv[4];
-              double4_t acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-              for (int s4 = 0; s4 < 4; ++s4) {
-                av[s4] = -XJ[(4 * s4 + (lane >> 4)) * 16 + (lane & 15)];
-                bv[s4] = A[(long)(k0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)];
-              }
-#pragma unroll
-              for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
-#pragma unroll
-              for (int q4 = 0; q4 < 4; ++q4) A[(long)(j0 + (lane >> 4) + 4 * q4) * ld + k0 + (lane & 15)] = acc[q4];
-            }
-          }
-        }
       }
       __syncthreads();
     }
-    if (kInvE && !sfail) {  // E's last block column, once X_{Ts-1} is formed
-      for (int I = wave; I < Ts - 1; I += nw) panel_tile(Ts - 1, I);
+  } else if (kMode == 2 && nworkers > 0) {
+    // Global-memory form with trailing workers (config 5), pipelined like the
+    // LDS form: per block step J, wave 0 applies step J - 1 to the diagonal
+    // tile (J, J) in registers (the workers left it out) and factors it, while
+    // thread 64 waits for the workers' column-J count (their first pass of step
+    // J - 1: column J below the diagonal and the diagonal tile (J + 1, J + 1)).
+    // Then every wave forms the panel of J, and block 0 publishes step J and
+    // goes on to the next diagonal tile without waiting for the workers: their
+    // round trip overlaps the next diagonal block.  Same operations on the same
+    // operands as the phased loop below: identical results.  (Measured and
+    // dropped: wave 0 forming its panel tile transposed in registers and going
+    // on without the panel barrier, the other waves publishing through an LDS
+    // counter, and LDS-only barriers -- 144 vs 134 us per config-5 solve: the
+    // workers' round trip, not wave 0, sets the step.)
+    const int c = lane & 15, q = lane >> 4;
+    double* Lblk = xch + 2 * kXchDoubles;
+    for (int J = 0; J < Ts; ++J) {
+      const int j0 = 16 * J;
+      double* Ablk = A + (long)j0 * ld + j0;
+      if (wave == 0) {
+        double4_t A4, Y4;
+        if (J > 0) {
+          A4 = trailing_diag_acc<true>(A, ld, J - 1, J, lane);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) A4[r] = a_ld<true>(&Ablk[(q + 4 * r) * ld + c]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Y4[r] = (q + 4 * r == c) ? 1.0 : 0.0;
+        bool ok = true;
+        double* XJw = X + 256 * J;
+        diag_round_mfma<0>(A4, Y4, q, c, n - j0, ok, Lblk, kDiagLd, XJw, xch);
+        diag_round_mfma<1>(A4, Y4, q, c, n - j0, ok, Lblk, kDiagLd, XJw, xch);
+        diag_round_mfma<2>(A4, Y4, q, c, n - j0, ok, Lblk, kDiagLd, XJw, xch);
+        diag_round_mfma<3>(A4, Y4, q, c, n - j0, ok, Lblk, kDiagLd, XJw, xch);
+        solve_wave_sync();
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c <= q + 4 * r) a_st<true>(&Ablk[(q + 4 * r) * ld + c], Lblk[(q + 4 * r) * kDiagLd + c]);
+        if (!ok) sfail = 1;  // benign race: every writer stores 1
+        STS(16);
+      } else if (tid == 64 && J > 0 && J + 1 < Ts) {
+        const unsigned want = (unsigned)nworkers * (unsigned)J;
+        long k = 0;
+        for (; k < kSolveSpin; ++k) {
+          if (__hip_atomic_load(b.ssync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (k == kSolveSpin) {  // a worker not co-resident (narrow CU mask, busy CUs): the solve ends in error
+          sfail = 1;
+          st->spin_err = 1;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
       __syncthreads();
+      STS(17);
+      if (sfail || J + 1 == Ts) break;
+      // panel of J on the matrix cores: L_IJ = A_IJ X_J^T
+      const double* XJ = X + 256 * J;
+      for (int I = J + 1 + wave; I < Ts; I += nw) {
+        const int i0 = 16 * I;
+        double av[4], bv[4];
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          av[s4] = a_ld<true>(&A[(long)(i0 + (lane & 15)) * ld + j0 + 4 * s4 + (lane >> 4)]);
+          bv[s4] = XJ[(lane & 15) * 16 + 4 * s4 + (lane >> 4)];
+        }
+        double4_t acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[s4], bv[s4], acc, 0, 0, 0);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) a_st<true>(&A[(long)(i0 + (lane >> 4) + 4 * q4) * ld + j0 + (lane & 15)], acc[q4]);
+      }
+      STS(18);
+      drain_and_barrier();  // the panel's (and diagonal copy-back's) sc1 stores have left
+      if (tid == 0) __hip_atomic_store(b.ssync, (unsigned)(J + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      STS(19);
     }
   } else
   for (int J = 0; J < Ts; ++J) {
     const int j0 = 16 * J;
     SOLVE_START(1);
-    // (a) diagonal block + its inverse (waves 0-3; every wave joins the barriers)
+    // (a) diagonal block + its inverse (wave 0; every wave joins the barrier)
     {
-      const bool act = !ME_DIAG_MFMA && wave < 4;  // four-wave form
-      const int i = 4 * wave + (lane >> 4), c = lane & 15;
+      const int c = lane & 15;
       double* Ablk = A + (long)j0 * ld + j0;
       // global-memory form: the rounds write the block's L into LDS (a round's
       // barrier would otherwise wait for its global stores), copied back after
       double* Lblk = kLds ? Ablk : xch + 2 * kXchDoubles;
       const int lld = kLds ? ld : kDiagLd;
-      double a = 0.0, y = 0.0;
-      if (act) {
-        a = a_ld<kSc1>(&Ablk[i * ld + c]);
-        y = (c == i) ? 1.0 : 0.0;
-      }
       bool ok = true;
       double* XJw = X + 256 * J;
-      if (ME_DIAG_MFMA) {
+      {
         // lookahead: the trailing tiles of step J - 1 outside column J run on
         // waves 1-3 and 5-7 while wave 0 factors this block (wave 4 shares
         // wave 0's SIMD and stays out of its way)
@@ -2074,14 +1892,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
           }
           if (!ok) sfail = 1;  // benign race: every writer stores 1
         }
-      } else {
-        if (!(skip & 1)) {
-          chol_rounds<ME_CHOL_PB, 0>(a, y, act, i, c, n - j0, ok, Lblk, lld, XJw, xch);
-        } else {  // timing diagnostics (ME_SOLVE_SKIP & 1): the rounds' barriers only
-          for (int r = 0; r < 16 / ME_CHOL_PB; ++r) __syncthreads();
-        }
-        if (!kLds && act && c <= i) a_st<kSc1>(&Ablk[i * ld + c], Lblk[i * kDiagLd + c]);
-        if (act && !ok) sfail = 1;  // benign race: every writer stores 1
       }
     }
     __syncthreads();
@@ -2110,26 +1920,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     SOLVE_STAMP(2);
     SOLVE_START(3);
     // (c) trailing update on the matrix cores: A_IK -= L_IJ L_KJ^T, J < K <= I
-    if (kMode == 2 && nworkers > 0) {
-      if (J + 1 < Ts) {  // hand the step to the workers and wait for all of them
-        drain_and_barrier();  // the panel's (and diagonal copy-back's) sc1 stores have left
-        if (tid == 0) {
-          __hip_atomic_store(b.ssync, (unsigned)(J + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const unsigned want = (unsigned)nworkers * (unsigned)(J + 1);
-          long k = 0;
-          for (; k < kSolveSpin; ++k) {
-            if (__hip_atomic_load(b.ssync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
-            __builtin_amdgcn_s_sleep(1);
-          }
-          if (k == kSolveSpin) {  // a worker not co-resident (narrow CU mask, busy CUs): the solve ends in error
-            sfail = 1;
-            st->spin_err = 1;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
-        __syncthreads();
-      }
-    } else {
+    {
       if (!(skip & 4)) {
         if (kLook)
           trailing_split<kSc1>(A, ld, Ts, J, true, wave, nw, lane);  // column J + 1 now, the rest with the next block
@@ -2150,91 +1941,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     return;
   }
   SOLVE_START(5);
-  // backward solve L^T y = z (z = row n of L), block by block.
-  // LDS form (ME_SOLVE_BWD1; Ts <= 8 there, so N <= 128): wave 0 alone, no
-  // workgroup barrier, u in registers -- lane l holds u[l] and u[l + 64].
-  // Per block J: r_J is broadcast from its 16 lanes (readlane), each lane
-  // forms y_J[l & 15] = (X_J^T r_J)[l & 15], y_J is broadcast back, and every
-  // lane subtracts L_{J,K}^T y_J from its own entries below j0 (L rows of
-  // block J, requested before the chain needs them).  (A left-looking form on
-  // wave 0, LDS-resident u: 6.07 vs 3.82 us.)  Otherwise wave 0 forms y_J =
-  // X_J^T z_J and every wave updates the entries above the block (two
+  // backward solve L^T y = z (z = row n of L), block by block: wave 0 forms
+  // y_J = X_J^T z_J and every wave updates the entries above the block (two
   // barriers per block).
-  if (kInvE) {
-    // y = E z, E = L^-T (upper block triangle of A; diagonal blocks X_J^T),
-    // z = row n of A: four lanes per row, strided over the columns
-    const int i = tid >> 2, gq = tid & 3;
-    double a0 = 0.0, a1 = 0.0;
-    if (i < n && !(skip & 8)) {
-      const int i0 = i & ~15;
-      const double* XJ = X + 16 * i0;  // X_J, J = i >> 4 (256 doubles per block)
-      const double* zr = A + (long)n * ld;
-      int j = i + gq;
-      for (; j < i0 + 16 && j < n; j += 4) a0 = fma(XJ[(j - i0) * 16 + (i - i0)], zr[j], a0);
-      for (; j + 4 < n; j += 8) {
-        a0 = fma(A[(long)i * ld + j], zr[j], a0);
-        a1 = fma(A[(long)i * ld + j + 4], zr[j + 4], a1);
-      }
-      if (j < n) a0 = fma(A[(long)i * ld + j], zr[j], a0);
-    }
-    double acc = a0 + a1;
-    acc += __shfl_xor(acc, 1, 64);
-    acc += __shfl_xor(acc, 2, 64);
-    if (gq == 0 && i < N) u[i] = i < n ? acc : 0.0;
-    for (int c = (nt >> 2) + tid; c < N; c += nt) u[c] = 0.0;  // (N > nt / 4: not in the LDS form)
-    __syncthreads();
-  } else if (kLds && ME_SOLVE_BWD1) {
-    if (wave == 0) {
-      const int t = lane & 15;
-      double u0 = lane < n ? A[(long)n * ld + lane] : 0.0;
-      double u1 = lane + 64 < n ? A[(long)n * ld + lane + 64] : 0.0;
-      for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
-        const int j0 = 16 * J, base = j0 & 63;
-        const double* XJ = X + 256 * J;
-        double xm[16], l0[16], l1[16];
-#pragma unroll
-        for (int m = 0; m < 16; ++m) xm[m] = XJ[m * 16 + t];
-        if (j0 > 0) {
-#pragma unroll
-          for (int m = 0; m < 16; ++m) l0[m] = A[(long)(j0 + m) * ld + lane];
-        }
-        if (j0 > 64) {
-#pragma unroll
-          for (int m = 0; m < 16; ++m) l1[m] = A[(long)(j0 + m) * ld + lane + 64];
-        }
-        const double rj = j0 >= 64 ? u1 : u0;
-        double s4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int m = 0; m < 16; ++m) s4[m & 3] = fma(xm[m], lane_read(rj, base + m), s4[m & 3]);
-        double s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-        s = j0 + t < n ? s : 0.0;
-        if (lane >= base && lane < base + 16) {
-          if (j0 >= 64)
-            u1 = s;
-          else
-            u0 = s;
-        }
-        if (j0 > 0) {
-          double y[16];
-#pragma unroll
-          for (int m = 0; m < 16; ++m) y[m] = lane_read(s, m);
-          double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int m = 0; m < 16; ++m) a4[m & 3] = fma(l0[m], y[m], a4[m & 3]);
-          if (lane < j0) u0 -= (a4[0] + a4[1]) + (a4[2] + a4[3]);
-          if (j0 > 64) {
-            double b4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int m = 0; m < 16; ++m) b4[m & 3] = fma(l1[m], y[m], b4[m & 3]);
-            if (lane + 64 < j0) u1 -= (b4[0] + b4[1]) + (b4[2] + b4[3]);
-          }
-        }
-      }
-      if (lane < N) u[lane] = u0;
-      if (lane + 64 < N) u[lane + 64] = u1;
-    }
-    __syncthreads();
-  } else {
+  {
   for (int c = tid; c < N; c += nt) u[c] = c < n ? a_ld<kSc1>(&A[(long)n * ld + c]) : 0.0;
   __syncthreads();
   for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
@@ -4012,16 +3722,6 @@ extern "C" int me_ba_solve(me_ctx* c, me_ba_problem* p, const me_ba_options* o, 
   return solve_impl(c, p, o, nullptr, s);
 }
 
-#ifdef ME_ROUND_STAMPS
-extern "C" int me_round_stamps(unsigned long long* out, int reset) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_round_stamps), sizeof(g_round_stamps));
-  if (reset) {
-    unsigned long long z[8] = {0};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_round_stamps), z, sizeof(z));
-  }
-  return 0;
-}
-#endif
 
 #ifdef ME_SOLVE_TS
 extern "C" int me_solve_ts(long long* out, int reset) {

@@ -20,8 +20,7 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
   if (ME_RSQ_NR > 1) r = r * fma(-0.5 * p * r, r, 1.5);
   return r;
 }
-// Diagonal block on ONE wave with the rank-4 updates on the matrix cores
-// (ME_DIAG_MFMA, default).  The block [A | Y] (Y -> X = L^-1) sits in two
+// Diagonal block on ONE wave with the rank-4 updates on the matrix cores.  The block [A | Y] (Y -> X = L^-1) sits in two
 // v_mfma_f64_16x16x4f64 accumulators: lane l = 16 q + c holds A[q + 4i][c] and
 // Y[q + 4i][c] in register i.  Round R (pivots p0 = 4R .. p0 + 3):
 //  * register R holds the round's pivot rows: A[p0 + q][c] (= A[c][p0 + q],
@@ -37,14 +36,12 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
 //    above), whose operand in lane l is L[c][p0 + q] for both A and B.
 // No workgroup barrier and no LDS round trip inside the block: per round the
 // uniform pivot chain, the substitutions and two MFMAs.
-#ifndef ME_DIAG_MFMA
-#define ME_DIAG_MFMA 1
-#endif
 #ifndef ME_DIAG_EXP
 #define ME_DIAG_EXP 0  // timing experiments only (tools/ubench_diag.hip), results invalid: 1 no Newton step, 2 no MFMA, 4 no rsq, 8 no substitutions
 #endif
 #ifndef ME_DIAG_GATHER
-#define ME_DIAG_GATHER 1  // 1: permlane swaps + readlane, 2: permlane swaps + DPP row broadcasts, 0: wave-private LDS scratch
+#define ME_DIAG_GATHER 1  // 1: permlane swaps + readlane, 0: wave-private LDS scratch (3.34k vs 3.49k ticks per block in
+                          // isolation, tools/ubench_diag.hip; DPP row broadcasts instead of readlane: 3.64k, dropped)
 #endif
 __device__ __forceinline__ double lane_read(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
@@ -74,12 +71,6 @@ __device__ __forceinline__ void col_gather4(double x, double o[4]) {
 #ifndef ME_DIAG_SKIP_PAD
 #define ME_DIAG_SKIP_PAD 1
 #endif
-template <int S>
-__device__ __forceinline__ double row_bcast(double x) {  // lane S of every 16-lane row, to the whole row (DPP)
-  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x150 + S, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x150 + S, 0xf, 0xf, false);
-  return __hiloint2double(hi, lo);
-}
 template <int R>
 __device__ __forceinline__ void diag_round_mfma(double4_t& A4, double4_t& Y4, int q, int c, int nreal, bool& ok,
                                                 double* Lblk, int lld, double* X, double* gx) {
@@ -89,20 +80,7 @@ __device__ __forceinline__ void diag_round_mfma(double4_t& A4, double4_t& Y4, in
     return;
   }
   double acol[4], ycol[4], Lq[4][4];
-  if (ME_DIAG_GATHER == 2) {
-    // the pivot block from the column gather: lane (q, p0 + v) holds acol[u] =
-    // A[p0 + u][p0 + v] in every row, broadcast along the row by DPP (VGPR
-    // results, no readlane / SGPR round trip)
-    col_gather4(A4[R], acol);
-    col_gather4(Y4[R], ycol);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      Lq[u][0] = row_bcast<p0 + 0>(acol[u]);
-      if (u >= 1) Lq[u][1] = row_bcast<p0 + 1>(acol[u]);
-      if (u >= 2) Lq[u][2] = row_bcast<p0 + 2>(acol[u]);
-      if (u >= 3) Lq[u][3] = row_bcast<p0 + 3>(acol[u]);
-    }
-  } else if (ME_DIAG_GATHER) {
+  if (ME_DIAG_GATHER) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
