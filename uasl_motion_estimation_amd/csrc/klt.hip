@@ -108,23 +108,19 @@ __device__ __forceinline__ double wave_sum_exact(int v) {
 __device__ __forceinline__ int descale32(int v, int n) { return (v + (1 << (n - 1))) >> n; }
 
 constexpr int kMaxWinPx = 7;  // pixels per lane: ceil(21*21/64)
-// Next-image region staged in LDS per wave: 32x32 bytes around the current
+// Next-image region staged in LDS per wave: 32x32 pixels around the current
 // window (the (win+1)^2 bilinear footprint plus a margin), so the LK
 // iterations read LDS instead of making an L2 round trip each.  When the
 // window walks out of the region it is restaged around the new position;
 // levels narrower or shorter than the region read global memory directly.
-// Same pixel values either way, so results are unchanged bit for bit.
+// The region holds one 32-bit word per pixel with its whole bilinear
+// footprint -- bytes J(x, y), J(x+1, y), J(x, y+1), J(x+1, y+1) -- so a tap
+// set is one aligned ds_read_b32 (the byte form's taps were pairs of bytes
+// at odd addresses, merged into unaligned ds_read_u16: SQ_LDS_UNALIGNED_STALL
+// matched the LDS-active cycles and the LDS waits were 20 % of the wave's
+// time, profiles/r05_klt_sq_counters_before.txt; after: r05_klt_sq_counters_after.txt).  Same pixel values either way, so
+// results are unchanged bit for bit.
 constexpr int kRegion = 32;
-// Template staging (ME_KLT_TSTAGE): per level the (win + 1)^2 template
-// footprint of I, DX and DY is copied into the wave's LDS with row-contiguous
-// loads (ceil(22 * 22 / 64) = 8 elements of each array per lane: 24 narrow
-// loads instead of the 84 scattered ones of the per-pixel 2 x 2 gathers), and
-// the bilinear taps are read from LDS.  Same values in the same order: same
-// bits.
-#ifndef ME_KLT_TSTAGE
-#define ME_KLT_TSTAGE 0
-#endif
-constexpr int kTplMax = 22;  // (win + 1) for win <= 21
 
 // wave-local ordering of this wave's LDS region (no cross-wave sharing)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -133,17 +129,29 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// lane = (row lane>>1, half lane&1): 16 bytes of row ry0 + (lane>>1)
-__device__ __forceinline__ void stage_region(uint8_t* reg, const uint8_t* __restrict__ J, int SI, int rx0, int ry0,
+// lane = (row y = lane>>1, half lane&1): the 16 footprint words of row
+// ry0 + y, columns 16 (lane & 1) .. + 15.  Footprints reaching past the
+// region's last row or column (x or y = 31, never a tap of a window inside
+// the region) are built from clamped addresses: defined, never read.
+__device__ __forceinline__ void stage_region(uint32_t* reg, const uint8_t* __restrict__ J, int SI, int rx0, int ry0,
                                              int lane) {
-  const uint8_t* src = J + (long)(ry0 + (lane >> 1)) * SI + rx0 + 16 * (lane & 1);
-  uint32_t w[4];
+  const int y = lane >> 1, x0 = 16 * (lane & 1);
+  const uint8_t* r0 = J + (long)(ry0 + y) * SI + rx0;
+  const uint8_t* r1 = J + (long)(ry0 + min(y + 1, kRegion - 1)) * SI + rx0;
+  uint32_t b0[17], b1[17];
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    w[k] = (uint32_t)src[4 * k] | ((uint32_t)src[4 * k + 1] << 8) | ((uint32_t)src[4 * k + 2] << 16) |
-           ((uint32_t)src[4 * k + 3] << 24);
+  for (int k = 0; k < 17; ++k) {
+    const int x = min(x0 + k, kRegion - 1);
+    b0[k] = r0[x];
+    b1[k] = r1[x];
+  }
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = b0[k] | (b0[k + 1] << 8) | (b1[k] << 16) | (b1[k + 1] << 24);
   wave_lds_sync();  // earlier reads of the previous region are done
-  *(uint4*)(reg + 16 * lane) = make_uint4(w[0], w[1], w[2], w[3]);
+  uint4* dst = reinterpret_cast<uint4*>(reg + y * kRegion + x0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
   wave_lds_sync();
 }
 
@@ -153,15 +161,11 @@ __device__ __forceinline__ void stage_region(uint8_t* reg, const uint8_t* __rest
 __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict__ pin, float* __restrict__ pout,
                                                   uint8_t* __restrict__ status, int n, int win, int max_iters,
                                                   double eps2, double min_eig) {
-  __shared__ __attribute__((aligned(16))) uint8_t regions[4][kRegion * kRegion];
-#if ME_KLT_TSTAGE
-  __shared__ uint8_t tplI[4][kTplMax * kTplMax];
-  __shared__ int16_t tplX[4][kTplMax * kTplMax], tplY[4][kTplMax * kTplMax];
-#endif
+  __shared__ __attribute__((aligned(16))) uint32_t regions[4][kRegion * kRegion];
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= n) return;  // wave-uniform
-  uint8_t* reg = regions[threadIdx.x >> 6];
+  uint32_t* reg = regions[threadIdx.x >> 6];
   const int half = (win - 1) / 2, npx = win * win;
   const double FLT_SCALE = 1.0 / (1 << 20);
   uint8_t st = 1;
@@ -204,49 +208,6 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const int16_t* DX = P.dx[L];
     const int16_t* DY = P.dy[L];
     int i4[kMaxWinPx][4], x4[kMaxWinPx][4], y4[kMaxWinPx][4];
-#if ME_KLT_TSTAGE
-    if (win + 1 <= kTplMax) {
-      const int tw = win + 1, tn = tw * tw, wv = threadIdx.x >> 6;
-      uint8_t* TI = tplI[wv];
-      int16_t* TX = tplX[wv];
-      int16_t* TY = tplY[wv];
-      int vi[8], vx[8], vy[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = min(lane + 64 * k, tn - 1), r = e / tw, cc = e - r * tw;
-        vi[k] = I[(long)(iy0 + r) * SI + ix0 + cc];
-        vx[k] = DX[(long)(iy0 + r) * W + ix0 + cc];
-        vy[k] = DY[(long)(iy0 + r) * W + ix0 + cc];
-      }
-      wave_lds_sync();  // the previous level's reads of the template are done
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = lane + 64 * k;
-        if (e < tn) {
-          TI[e] = (uint8_t)vi[k];
-          TX[e] = (int16_t)vx[k];
-          TY[e] = (int16_t)vy[k];
-        }
-      }
-      wave_lds_sync();
-#pragma unroll
-      for (int q = 0; q < kMaxWinPx; ++q) {
-        const int o = wy[q] * tw + wx[q];
-        i4[q][0] = TI[o];
-        i4[q][1] = TI[o + 1];
-        i4[q][2] = TI[o + tw];
-        i4[q][3] = TI[o + tw + 1];
-        x4[q][0] = TX[o];
-        x4[q][1] = TX[o + 1];
-        x4[q][2] = TX[o + tw];
-        x4[q][3] = TX[o + tw + 1];
-        y4[q][0] = TY[o];
-        y4[q][1] = TY[o + 1];
-        y4[q][2] = TY[o + tw];
-        y4[q][3] = TY[o + tw + 1];
-      }
-    } else
-#endif
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
       const long o = (long)(iy0 + wy[q]) * W + ix0 + wx[q], oi = (long)(iy0 + wy[q]) * SI + ix0 + wx[q];
@@ -309,14 +270,14 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
           ry0 = min(max(jy0 - (kRegion - win - 1) / 2, 0), H - kRegion);
           stage_region(reg, J, SI, rx0, ry0, lane);
         }
-        const uint8_t* R0 = reg + (jy0 - ry0) * kRegion + (jx0 - rx0);
+        const uint32_t* R0 = reg + (jy0 - ry0) * kRegion + (jx0 - rx0);
 #pragma unroll
         for (int q = 0; q < kMaxWinPx; ++q) {
-          const uint8_t* r = R0 + wy[q] * kRegion + wx[q];
-          j4[q][0] = r[0];
-          j4[q][1] = r[1];
-          j4[q][2] = r[kRegion];
-          j4[q][3] = r[kRegion + 1];
+          const uint32_t f = R0[wy[q] * kRegion + wx[q]];
+          j4[q][0] = f & 0xff;
+          j4[q][1] = (f >> 8) & 0xff;
+          j4[q][2] = (f >> 16) & 0xff;
+          j4[q][3] = f >> 24;
         }
       } else {
 #pragma unroll
