@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
   uint8_t st = 1;
   float nx = 0, ny = 0;
   int iv[kMaxWinPx], ixv[kMaxWinPx], iyv[kMaxWinPx];
-  int wy[kMaxWinPx], wx[kMaxWinPx];  // window coordinates of this lane's pixels
+  int wy[kMaxWinPx], wx[kMaxWinPx], roff[kMaxWinPx];  // window coordinates of this lane's pixels, region offsets
   bool wok[kMaxWinPx];
 #pragma unroll
   for (int q = 0; q < kMaxWinPx; ++q) {
@@ -180,6 +180,7 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const int kk = wok[q] ? k : 0;
     wy[q] = kk / win;
     wx[q] = kk - wy[q] * win;
+    roff[q] = wy[q] * kRegion + wx[q];
   }
   const float px0 = pin[2 * f], py0 = pin[2 * f + 1];
   for (int L = P.nl - 1; L >= 0; --L) {
@@ -262,7 +263,14 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       const int jw01 = (int)rintf(c * (1.f - d) * 16384.f);
       const int jw10 = (int)rintf((1.f - c) * d * 16384.f);
       const int jw11 = 16384 - jw00 - jw01 - jw10;
-      int j4[kMaxWinPx][4];
+      // the bilinear sum of a footprint word f (bytes J00 J01 J10 J11) as two
+      // packed u8 dot products: w = 128 (w >> 7) + (w & 127), both halves fit
+      // a byte (w <= 16384), the sums are exact in 32 bits
+      const uint32_t whp = (uint32_t)(jw00 >> 7) | ((uint32_t)(jw01 >> 7) << 8) | ((uint32_t)(jw10 >> 7) << 16) |
+                           ((uint32_t)(jw11 >> 7) << 24);
+      const uint32_t wlp = (uint32_t)(jw00 & 127) | ((uint32_t)(jw01 & 127) << 8) | ((uint32_t)(jw10 & 127) << 16) |
+                           ((uint32_t)(jw11 & 127) << 24);
+      uint32_t f4[kMaxWinPx];
       if (staged) {
         if (jx0 < rx0 || jy0 < ry0 || jx0 + win >= rx0 + kRegion || jy0 + win >= ry0 + kRegion) {
           // centre the region on the window, clamped inside the level
@@ -272,27 +280,18 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
         }
         const uint32_t* R0 = reg + (jy0 - ry0) * kRegion + (jx0 - rx0);
 #pragma unroll
-        for (int q = 0; q < kMaxWinPx; ++q) {
-          const uint32_t f = R0[wy[q] * kRegion + wx[q]];
-          j4[q][0] = f & 0xff;
-          j4[q][1] = (f >> 8) & 0xff;
-          j4[q][2] = (f >> 16) & 0xff;
-          j4[q][3] = f >> 24;
-        }
+        for (int q = 0; q < kMaxWinPx; ++q) f4[q] = R0[roff[q]];
       } else {
 #pragma unroll
         for (int q = 0; q < kMaxWinPx; ++q) {
           const uint8_t* r = J + (long)(jy0 + wy[q]) * SI + jx0 + wx[q];
-          j4[q][0] = r[0];
-          j4[q][1] = r[1];
-          j4[q][2] = r[SI];
-          j4[q][3] = r[SI + 1];
+          f4[q] = (uint32_t)r[0] | ((uint32_t)r[1] << 8) | ((uint32_t)r[SI] << 16) | ((uint32_t)r[SI + 1] << 24);
         }
       }
       int b1l = 0, b2l = 0;
 #pragma unroll
       for (int q = 0; q < kMaxWinPx; ++q) {
-        const int v = j4[q][0] * jw00 + j4[q][1] * jw01 + j4[q][2] * jw10 + j4[q][3] * jw11;
+        const int v = (int)((__builtin_amdgcn_udot4(f4[q], whp, 0u, false) << 7) + __builtin_amdgcn_udot4(f4[q], wlp, 0u, false));
         const int diff = descale32(v, 9) - iv[q];
         b1l += diff * ixv[q];  // ixv = iyv = 0 on masked pixels
         b2l += diff * iyv[q];
