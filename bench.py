@@ -437,7 +437,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MI_COUNTERS = "r04_f_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
+MI_COUNTERS = "r05_b_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
@@ -1100,6 +1100,12 @@ def main():
     if args.rank_device == "zero":  # (tests: every rank on GPU 0; RCCL cannot run two ranks on one GPU)
         assert args.comm == "gloo" or world == 1, "--rank-device zero needs --comm gloo"
         local_rank = 0
+        if world > 1:
+            # the persistent scale-LM grid needs its workgroups co-resident, which
+            # several processes sharing one GPU cannot promise each other: the
+            # per-phase launches instead (read by the library once, at its first
+            # scale solve)
+            os.environ.setdefault("ME_SCALE_BLOCKS", "1")
     pool = pool1 = None
     model, ncpu, avail = host_cpu()
     cpu_workers = args.cpu_workers or min(16, avail)

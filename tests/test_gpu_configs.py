@@ -295,3 +295,23 @@ def test_cu_masked_frontend_backend_overlap(oracle, sp_cfg3):
     finally:
         front.close()
         back.close()
+
+
+def test_klt_many_features_rare_weights(ctx, oracle):
+    """40 000 features at random sub-pixel positions of a config-3 pair (about
+    a million LK iterations): the bilinear weight jw11 = 16384 - the other three
+    comes out -1 in about 1e-5 of them, where the packed-byte dot product of the
+    staged footprint words cannot hold it (klt.hip takes the per-tap sum there).
+    Bit-exact against the restatement."""
+    from uasl_motion_estimation_amd.klt import calcOpticalFlowPyrLK
+
+    c = S.CONFIGS[3]
+    seed = S.SEED0 + 3
+    scene, K, stream = S.stereo_stream(seed, c["width"], c["height"], 2)
+    rng = np.random.default_rng(20261018)
+    n = 40000
+    pts = np.stack([rng.uniform(30, c["width"] - 30, n), rng.uniform(30, c["height"] - 30, n)], 1).astype(np.float32)
+    got, gst = calcOpticalFlowPyrLK(stream[0].left, stream[1].left, pts, ctx=ctx)
+    ref, rst = oracle.klt(stream[0].left, stream[1].left, pts)
+    assert np.array_equal(gst, rst)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))

@@ -47,4 +47,6 @@ print(f"front_cus {front or 16}/16: launches {buf[1]}, phases/launch {buf[0] / L
       f"(A/D {buf[7] / L:.1f}, B {buf[8] / L:.1f}, C {buf[9] / L:.1f}); executed track evaluations/launch {evals}")
 print(f"  wall {us(2)} us/launch: wg0 track work A/D {us(3)} B {us(4)} C {us(5)}; wg0 waits for control {us(6)}; "
       f"control (reduce + decide, controlling wg) {us(10)} over {buf[11] / L:.1f} reductions")
+print(f"  A/D controls (per control): acquire {buf[12] / max(buf[7], 1) / 100.0:.2f}, reduce {buf[13] / max(buf[7], 1) / 100.0:.2f}, "
+      f"control {buf[14] / max(buf[7], 1) / 100.0:.2f}, publish {buf[15] / max(buf[7], 1) / 100.0:.2f} us")
 print(f"  ns per executed track evaluation: {1e3 * buf[2] / L / 100.0 / max(evals, 1):.2f}")

@@ -985,10 +985,20 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
       }
     };
     auto sc_ctrl_begin = [&]() { if (threadIdx.x == 0) ts_ctrl = SC_T(); };
+    // A/B/D controls: [12] acquire, [13] reduce, [14] control, [15] publish (from the arrival)
+    long long ts_sub = 0;
+    auto sc_sub = [&](int k) {
+      if (threadIdx.x == 0) {
+        const long long t_ = SC_T();
+        SC_ADD(k, t_ - (k == 12 ? ts_ctrl : ts_sub));
+        ts_sub = t_;
+      }
+    };
     auto sc_ctrl_end = [&]() { if (threadIdx.x == 0) { SC_ADD(10, SC_T() - ts_ctrl); SC_ADD(11, 1); } };
 #else
     auto sc_work_done = [](int) {};
     auto sc_ctrl_begin = []() {};
+    auto sc_sub = [](int) {};
     auto sc_ctrl_end = []() {};
 #endif
     if (phase == PH_B) {
@@ -1017,12 +1027,16 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
         if (last_block_arrives(cnt + 1, nwg)) {
           sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          sc_sub(12);
           double sx, sy;
           block_reduce2<kScBlock>(res, nullptr, p.rows, 1, &sx, &sy);
+          sc_sub(13);
           if (threadIdx.x == 0) {
             __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             scale_ctrl_run(lm, sp, p, phase, sx, 0.0, *err);
+            sc_sub(14);
             lm_publish(epoch, (unsigned)ph + 1);
+            sc_sub(15);
           }
           sc_ctrl_end();
         }
