@@ -265,11 +265,15 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       const int jw11 = 16384 - jw00 - jw01 - jw10;
       // the bilinear sum of a footprint word f (bytes J00 J01 J10 J11) as two
       // packed u8 dot products: w = 128 (w >> 7) + (w & 127), both halves fit
-      // a byte (w <= 16384), the sums are exact in 32 bits
+      // a byte (0 <= w <= 16384), the sums are exact in 32 bits.  jw11 =
+      // 16384 - the other three comes out -1 in ~1e-5 of the iterations (the
+      // three roundings): the dot products then take 0 for it and J11 is
+      // subtracted afterwards (a wave-uniform branch; the same integer)
+      const int w11 = max(jw11, 0);
       const uint32_t whp = (uint32_t)(jw00 >> 7) | ((uint32_t)(jw01 >> 7) << 8) | ((uint32_t)(jw10 >> 7) << 16) |
-                           ((uint32_t)(jw11 >> 7) << 24);
+                           ((uint32_t)(w11 >> 7) << 24);
       const uint32_t wlp = (uint32_t)(jw00 & 127) | ((uint32_t)(jw01 & 127) << 8) | ((uint32_t)(jw10 & 127) << 16) |
-                           ((uint32_t)(jw11 & 127) << 24);
+                           ((uint32_t)(w11 & 127) << 24);
       uint32_t f4[kMaxWinPx];
       if (staged) {
         if (jx0 < rx0 || jy0 < ry0 || jx0 + win >= rx0 + kRegion || jy0 + win >= ry0 + kRegion) {
@@ -288,11 +292,18 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
           f4[q] = (uint32_t)r[0] | ((uint32_t)r[1] << 8) | ((uint32_t)r[SI] << 16) | ((uint32_t)r[SI + 1] << 24);
         }
       }
+      int vq[kMaxWinPx];
+#pragma unroll
+      for (int q = 0; q < kMaxWinPx; ++q)
+        vq[q] = (int)((__builtin_amdgcn_udot4(f4[q], whp, 0u, false) << 7) + __builtin_amdgcn_udot4(f4[q], wlp, 0u, false));
+      if (jw11 < 0) {  // (wave-uniform, rare) jw11 = -1
+#pragma unroll
+        for (int q = 0; q < kMaxWinPx; ++q) vq[q] -= (int)(f4[q] >> 24);
+      }
       int b1l = 0, b2l = 0;
 #pragma unroll
       for (int q = 0; q < kMaxWinPx; ++q) {
-        const int v = (int)((__builtin_amdgcn_udot4(f4[q], whp, 0u, false) << 7) + __builtin_amdgcn_udot4(f4[q], wlp, 0u, false));
-        const int diff = descale32(v, 9) - iv[q];
+        const int diff = descale32(vq[q], 9) - iv[q];
         b1l += diff * ixv[q];  // ixv = iyv = 0 on masked pixels
         b2l += diff * iyv[q];
       }
