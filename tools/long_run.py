@@ -6,7 +6,9 @@ first --parity-frames keyframes also run, sequentially, on the oracle backend
 (tests/pipeline_oracle.py, the checker): events bit-exact, poses 1e-6.
 Reports frames/s (loop only and with rendering), per-segment rates, drift
 against the ground-truth trajectory and the window sizes.
-Usage: tools/long_run.py [--frames 10000] [--config 5] [--out FILE]"""
+--loop native (default) runs the C++ loop (me_vo_loop_*, NativeStereoVO); its
+parity prefix is a separate native run of the first keyframes with the event
+log on.  Usage: tools/long_run.py [--frames 10000] [--config 5] [--loop native|python] [--out FILE]"""
 import argparse
 import json
 import os
@@ -28,6 +30,7 @@ def main():
     ap.add_argument("--segment", type=int, default=1000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--trace", type=int, default=0, help="print tracking / drift stats every N keyframes")
+    ap.add_argument("--loop", choices=("native", "python"), default="native")
     args = ap.parse_args()
     import torch
 
@@ -43,9 +46,14 @@ def main():
     centres = [-R.T @ t for (R, t) in arc]
     K = S.intrinsics(cfg.width, cfg.height)
     ctx = default_context()
-    be = PL.GPUBackend(ctx)
-    vo = PL.WindowedStereoVO(cfg, be, K, truth[0], truth[1] - truth[0], log_events=args.parity_frames > 0,
-                             overlap=True)
+    native = args.loop == "native"
+    if native:
+        be = None
+        vo = PL.NativeStereoVO(cfg, ctx, K, truth[0], truth[1] - truth[0], log_events=False, overlap=True)
+    else:
+        be = PL.GPUBackend(ctx)
+        vo = PL.WindowedStereoVO(cfg, be, K, truth[0], truth[1] - truth[0], log_events=args.parity_frames > 0,
+                                 overlap=True)
     host_frames = []  # the parity prefix's images on the host (for the oracle backend)
     t_loop = t_render = 0.0
     seg_t0, seg_f0, segs = time.perf_counter(), 0, []
@@ -61,14 +69,17 @@ def main():
             t = c0 + k
             if t < args.parity_frames:
                 host_frames.append((L.cpu().numpy(), R.cpu().numpy()))
-            be.frame_images_device(t, L, R)
-            pending[t] = (L, R)
-            vo.process(t, None, None)
-            if t == args.parity_frames:
-                vo.log_events = False  # (the event log of the prefix only: frames < P and their pops)
-            for old in [f for f in pending if f < t - 1]:
-                be.release(old)
-                del pending[old]
+            if native:
+                vo.process(t, L.contiguous(), R.contiguous())  # (the loop keeps the last two keyframes' images)
+            else:
+                be.frame_images_device(t, L, R)
+                pending[t] = (L, R)
+                vo.process(t, None, None)
+                if t == args.parity_frames:
+                    vo.log_events = False  # (the event log of the prefix only: frames < P and their pops)
+                for old in [f for f in pending if f < t - 1]:
+                    be.release(old)
+                    del pending[old]
             if args.trace and t % args.trace == 0 and vo.results:
                 r = vo.results[-1]
                 e = np.abs(PL.camera_centre(vo.poses[r.t]) - centres[r.t]).max()
@@ -82,15 +93,19 @@ def main():
         t_loop += time.perf_counter() - t1
     vo.finish()
     wall = time.perf_counter() - t_all
-    be.close()
-    err = np.array([np.abs(PL.camera_centre(vo.poses[t]) - centres[t]).max() for t in range(n)])
-    res = vo.results
+    poses, res, host_s, latest = vo.poses, vo.results, vo.stage_s["host"], vo.latest_id
+    if native:
+        vo.close()
+    else:
+        be.close()
+    err = np.array([np.abs(PL.camera_centre(poses[t]) - centres[t]).max() for t in range(n)])
     out = {"workload": f"config {c}: {cfg.width}x{cfg.height} stereo, {cfg.n_feats} features, {cfg.window}-keyframe "
                        f"sliding window, {n} keyframes on the ring-corridor arc, 10-iteration BA per keyframe, "
                        f"pipelined loop on one MI355X (front end 4/16 CUs, BA 12/16)",
+           "host_loop": "native (me_vo_loop_*, C++)" if native else "python (WindowedStereoVO)",
            "keyframes": n, "frames_per_s": round(n / t_loop, 2), "frames_per_s_with_render": round(n / wall, 2),
            "render_s": round(t_render, 1), "loop_s": round(t_loop, 1),
-           "host_ms_per_frame": round(1e3 * vo.stage_s["host"] / n, 3),
+           "host_ms_per_frame": round(1e3 * host_s / n, 3),
            "segments": segs,
            "drift_m": {"last": round(float(err[-1]), 4), "max": round(float(err.max()), 4),
                        "per_1000_frames_max": [round(float(err[i:i + 1000].max()), 4) for i in range(0, n, 1000)],
@@ -100,7 +115,7 @@ def main():
            "window_landmarks": {"mean": round(float(np.mean([r.n_window_pts for r in res[cfg.window:]] or [0])), 1),
                                 "max": int(max([r.n_window_pts for r in res] or [0]))},
            "window_observations_max": int(max([r.n_window_obs for r in res] or [0])),
-           "tracks_created": int(vo.latest_id)}
+           "tracks_created": int(latest)}
     if args.parity_frames > 0:
         from pipeline_oracle import OracleBackend  # the checker
 
@@ -111,9 +126,17 @@ def main():
             ov.process(t, *host_frames[t])
         ov.finish()
         ct = time.perf_counter() - t1
-        gev = vo.events
+        if native:  # the prefix again on a native loop with the event log on
+            vp = PL.NativeStereoVO(cfg, ctx, K, truth[0], truth[1] - truth[0], log_events=True, overlap=True)
+            for t in range(P):
+                vp.process(t, *host_frames[t])
+            vp.finish()
+            gev, gres = vp.events, vp.results
+            vp.close()
+        else:
+            gev, gres = vo.events, res
         # each frame's pose as its own BA left it (later windows refine it again on the GPU run only)
-        pose_rel = max(float(np.max(np.abs(vo.results[t].pose - ov.results[t].pose) / (np.abs(ov.results[t].pose) + 1e-3)))
+        pose_rel = max(float(np.max(np.abs(gres[t].pose - ov.results[t].pose) / (np.abs(ov.results[t].pose) + 1e-3)))
                        for t in range(P))
         out["parity_prefix"] = {"keyframes": P, "events_bit_exact": gev[:len(ov.events)] == ov.events,
                                 "events_compared": len(ov.events),
@@ -124,8 +147,8 @@ def main():
     out["drift_outlier_frames"] = [int(x) for x in bad[:20]]
     if len(bad):
         out["drift_outliers"] = [{"t": int(t), "err": round(float(err[t]), 3),
-                                  "ba_iters": vo.results[t].ba_iters, "ba_cost": vo.results[t].ba_cost,
-                                  "tracked": vo.results[t].n_tracked} for t in bad[:5]]
+                                  "ba_iters": res[t].ba_iters, "ba_cost": res[t].ba_cost,
+                                  "tracked": res[t].n_tracked} for t in bad[:5]]
     line = json.dumps(out)
     print(line)
     if args.out:
