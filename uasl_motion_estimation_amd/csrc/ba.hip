@@ -1497,6 +1497,25 @@ __device__ __forceinline__ double4_t diag_load_wave(const double* A, int ld, int
   return A4;
 }
 
+// y = sum_m X[m][t] u_m over the 16 lanes of this lane's 16-lane row (lane m
+// of the row holds u_m; lane t reads column t of X): DPP row broadcasts, in m
+// order.
+// (four partial sums over m mod 4, then (y0 + y1) + (y2 + y3): a 4-deep chain)
+template <int M>
+__device__ __forceinline__ void row_dot16_acc(double u, const double* X, int t, double (&y)[4]) {
+  if constexpr (M < 16) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(u), 0x150 + M, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(u), 0x150 + M, 0xf, 0xf, false);
+    y[M & 3] = fma(X[M * 16 + t], __hiloint2double(hi, lo), y[M & 3]);
+    row_dot16_acc<M + 1>(u, X, t, y);
+  }
+}
+__device__ __forceinline__ double row_dot16(double u, const double* X, int t) {
+  double y[4] = {0.0, 0.0, 0.0, 0.0};
+  row_dot16_acc<0>(u, X, t, y);
+  return (y[0] + y[1]) + (y[2] + y[3]);
+}
+
 // kMode: 0 = [S; -b^T] in LDS, one workgroup; 1 = in global memory, one workgroup;
 // 2 = in global memory, trailing updates on `nworkers` more workgroups (sc1 hand-offs)
 template <int kMode>
@@ -1941,13 +1960,83 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     return;
   }
   SOLVE_START(5);
-  // backward solve L^T y = z (z = row n of L), block by block: wave 0 forms
-  // y_J = X_J^T z_J and every wave updates the entries above the block (two
-  // barriers per block).
-  {
+  // backward solve L^T y = z (z = row n of L), block by block.
+  // One column per thread (N <= 512): lane cc keeps u[cc] in a register and
+  // walks the blocks K from the last down to its own; wave w owns blocks
+  // 4w .. 4w + 3 (its 16-lane rows).  Per block K the owning row finalises
+  // y_K = X_K^T u_K (its lanes' u by DPP row broadcasts), publishes y_K in
+  // LDS and bumps an LDS flag; every lane of a lower block then subtracts
+  // L_K^T y_K from its u (the previous form's sums in the same order).  No
+  // workgroup barrier on the chain: a wave waits only for the blocks of other
+  // waves, and the lanes' L entries of the next block are requested one block
+  // ahead (global forms: a memory round trip per block otherwise).
+  const int Jlast = (skip & 8) ? -1 : (n - 1) >> 4;
+  // Global forms only: in the LDS form the two-barrier loop below is faster
+  // (config 3: 3.7 vs 5.3 us); at W = 50 this one is (17.4 vs 19.9 us).
+  if (!kLds && N <= nt) {
+    if (tid == 0) pflag = 0u;
+    __syncthreads();
+    const int cc = tid, myJ = cc >> 4, t = cc & 15;
+    double acc = (cc < n && myJ <= Jlast) ? a_ld<kSc1>(&A[(long)n * ld + cc]) : 0.0;
+    // the L entries of the next block in flight
+    constexpr int kPf = 1;  // (3 blocks ahead measured slower: 20.3 vs 17.4 us at W = 50)
+    double lpf[kPf][16];
+    auto fetchL = [&](int K, double* dst) {
+      if (K >= 0 && myJ < K) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) dst[m] = a_ld<kSc1>(&A[(long)(16 * K + m) * ld + cc]);
+      }
+    };
+#pragma unroll
+    for (int d = 0; d < kPf; ++d) fetchL(Jlast - d, lpf[d]);
+    for (int K = Jlast; K >= 4 * wave; --K) {  // (wave-uniform)
+      double lk[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) lk[m] = lpf[0][m];
+#pragma unroll
+      for (int d = 0; d + 1 < kPf; ++d)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) lpf[d][m] = lpf[d + 1][m];
+      fetchL(K - kPf, lpf[kPf - 1]);
+      const unsigned want = (unsigned)(Jlast - K + 1);
+      if ((K >> 2) == wave) {
+        if (myJ == K) {
+          double y = row_dot16(acc, X + 256 * K, t);
+          y = 16 * K + t < n ? y : 0.0;
+          u[16 * K + t] = y;
+          acc = y;
+        }
+        solve_wave_sync();  // y_K in LDS for this wave's lanes
+        if (lane == 0) *(volatile unsigned*)&pflag = want;
+      } else {
+        long k = 0;
+        for (; k < kSolveSpin && *(volatile unsigned*)&pflag < want; ++k) __builtin_amdgcn_s_sleep(1);
+        if (k == kSolveSpin) {
+          sfail = 1;
+          st->spin_err = 1;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      }
+      if (myJ < K) {
+        double yk[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) yk[m] = u[16 * K + m];
+        double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+        for (int m = 0; m < 16; m += 2) {
+          a0 = fma(lk[m], yk[m], a0);
+          a1 = fma(lk[m + 1], yk[m + 1], a1);
+        }
+        acc -= a0 + a1;
+      }
+    }
+    __syncthreads();
+  } else {
+  // (LDS form, and N > 512: wave 0 forms y_J = X_J^T z_J and every wave
+  // updates the entries above the block, two barriers per block)
   for (int c = tid; c < N; c += nt) u[c] = c < n ? a_ld<kSc1>(&A[(long)n * ld + c]) : 0.0;
   __syncthreads();
-  for (int J = (skip & 8) ? -1 : (n - 1) >> 4; J >= 0; --J) {
+  for (int J = Jlast; J >= 0; --J) {
     const int j0 = 16 * J;
     if (wave == 0) {
       const double* XJ = X + 256 * J;
