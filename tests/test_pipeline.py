@@ -304,6 +304,59 @@ def test_pipeline_gpu_chained_equals_unchained(ctx, seq5):
     assert np.array_equal([r.ba_cost for r in a.results], [r.ba_cost for r in b.results], equal_nan=True)
 
 
+@pytest.mark.gpu
+def test_pipeline_gpu_chained_equals_unchained_after_failed_ba(ctx, seq5):
+    """the chained start after a FAILED BA(t - 1) -- the device
+    chain (vo_chain_kernel) keeps the host's poses and landmarks when the
+    previous solve ended with termination 2, the host loop skips the write
+    back for status 3.  Every second window solve fails (test hook
+    me_debug_solve_flags(2048): each of its camera solves fails, every LM
+    step is invalid, the solve ends after max_num_consecutive_invalid_steps
+    with the parameters untouched); events, poses and landmarks bit for bit
+    between the chained and the unchained loop, and the native loop takes
+    the same decisions."""
+    import ctypes
+
+    hook = ctx.lib.me_debug_solve_flags
+    hook.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    runs = []
+    for chain in (True, False):
+        be = PL.GPUBackend(ctx)
+        be.chain_window = chain
+        assert hook(ctx.h, 2048) == 0
+        try:
+            runs.append(_run(5, 16, be, window=8, frames=seq5, overlap=True, ba_iters=10))
+        finally:
+            hook(ctx.h, 0)
+            be.close()
+    a, b = runs
+    assert a.events == b.events and np.array_equal(a.ids, b.ids)
+    assert np.array_equal(a.X, b.X)
+    assert all(np.array_equal(a.poses[t], b.poses[t]) for t in a.poses)
+    assert [r.ba_iters for r in a.results] == [r.ba_iters for r in b.results]
+    assert np.array_equal([r.ba_cost for r in a.results], [r.ba_cost for r in b.results], equal_nan=True)
+    # the hook did fail windows: a failed solve leaves the predicted poses, so the
+    # run leaves the unhooked run's poses
+    be = PL.GPUBackend(ctx)
+    try:
+        ref = _run(5, 16, be, window=8, frames=seq5, overlap=True, ba_iters=10)
+    finally:
+        be.close()
+    assert not all(np.array_equal(a.poses[t], ref.poses[t]) for t in a.poses)
+    assert hook(ctx.h, 2048) == 0
+    try:
+        n = _native(ctx, 16, 8, seq5)
+    finally:
+        hook(ctx.h, 0)
+    try:
+        assert n.events == a.events and np.array_equal(n.ids, a.ids)
+        assert [r.ba_iters for r in n.results] == [r.ba_iters for r in a.results]
+        for t in a.poses:
+            np.testing.assert_allclose(n.poses[t], a.poses[t], rtol=1e-9, atol=1e-12)
+    finally:
+        n.close()
+
+
 def test_rot_series_equals_rodrigues():
     """The loop's pose(t) re-prediction rotation (pipeline.rot_series: a
     Taylor series in theta^2, the device chain's arithmetic) against the

@@ -1617,7 +1617,8 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // flags, radius and the whole lower block triangle of [S; -b^T] are
   // requested together: one round of global latency instead of a chain
   const int done = st->done;
-  const int fail_in = st->fail || st->spin_err || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0);
+  const int fail_in = st->fail || st->spin_err || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0) ||
+                      (skip & 1024);  // (1024: test hook, a forced solve failure)
   const double radius = st->radius;
   // the candidate-camera inputs (current cameras, Jacobi scales) are requested
   // now; they are consumed after the factorisation, which hides their latency
@@ -2899,7 +2900,12 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   P.c = c;
   if (const char* sk = getenv("ME_SOLVE_SKIP")) P.diag_skip = atoi(sk);
-  P.diag_skip |= c->dbg_solve_flags;
+  int dbg = c->dbg_solve_flags;
+  if (dbg & 2048) {  // (test hook: every second solve on this ctx has every camera solve fail)
+    if (c->dbg_solve_count++ & 1) dbg |= 1024;
+    dbg &= ~2048;
+  }
+  P.diag_skip |= dbg;
   if (const char* sw = getenv("ME_SOLVE_WORKERS")) P.solve_workers = atoi(sw);  // A/B timing (0: one workgroup)
   if (const char* sq = getenv("ME_BA_SEQUENTIAL")) P.sequential = atoi(sq) != 0;
   if (const char* fa = getenv("ME_BA_NOFUSEASM")) P.no_fused_asm = atoi(fa) != 0;
@@ -4016,10 +4022,15 @@ extern "C" int me_ba_window_indices(me_ctx* c, const int32_t* frame, const int32
 
 // Test hook (not part of the drop-in ABI): flags OR-ed into this ctx's camera
 // solve diagnostics; 512 forces the fused-assembly wait to time out
-// (tests/test_distributed.py: a hand-off timeout on one rank of a sharded solve).
+// (tests/test_distributed.py: a hand-off timeout on one rank of a sharded solve),
+// 1024 fails every camera solve (each LM step invalid: the solve ends with
+// termination 2 after max_num_consecutive_invalid_steps), 2048 does that to
+// every second solve queued on the ctx (tests/test_pipeline.py: the chained
+// window start after a failed BA).
 extern "C" int me_debug_solve_flags(me_ctx* c, int flags) {
   if (!c) return ME_ERR_INVALID;
   c->dbg_solve_flags = flags;
+  c->dbg_solve_count = 0;
   return ME_OK;
 }
 
