@@ -7,10 +7,12 @@
 //    image by 2-D kernels; levels resident in HBM;
 //  * one wavefront per feature: the 21x21 window is spread over 64 lanes
 //    (7 pixels each), template values / gradients stay in VGPRs across the
-//    LK iterations, the 2x2 normal matrix and the mismatch vector are int64
-//    sums reduced with wave shuffles (exact, so order-independent and
-//    bit-identical to the serial restatement);
-//  * the 2x2 solve runs redundantly in every lane (wave-uniform control).
+//    LK iterations, the 2x2 normal matrix and the mismatch vector are exact
+//    wave sums (int32 DPP stages while the partial sums fit, then FP64 on
+//    integers: order-independent and bit-identical to the serial restatement);
+//  * the 2x2 solve runs redundantly in every lane; the window position, its
+//    bilinear weights and the region tests are wave-uniform and kept in
+//    scalar registers (the weight packing runs on the scalar unit).
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -94,13 +96,64 @@ __device__ __forceinline__ double readlane_f64(double x, int l) {
   const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
   return __hiloint2double(hi, lo);
 }
+// lanes outside row_mask read 0 (update_dpp's old value)
+template <int Ctrl, int RowMask>
+__device__ __forceinline__ double dpp_f64_masked(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), Ctrl, RowMask, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), Ctrl, RowMask, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int Ctrl>
+__device__ __forceinline__ int dpp_i32k(int x) {
+  return __builtin_amdgcn_mov_dpp(x, Ctrl, 0xf, 0xf, true);  // (bound_ctrl: lets the mov fold into the add)
+}
+// Exact wave sum of int32 lane values whose sums over any (1 << INT_STAGES)
+// lanes still fit int32: the first INT_STAGES butterfly stages add in 32-bit
+// integers (one DPP-sourced add each), the rest in FP64 (integers below 2^53:
+// exact, so the order does not matter), the four row sums gathered in lane 63
+// by row broadcasts (row_bcast15 / row_bcast31) and read once.
+template <int INT_STAGES>
 __device__ __forceinline__ double wave_sum_exact(int v) {
-  double x = (double)v;
-  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
-  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
-  x += dpp_f64<0x141>(x);  // row_half_mirror
-  x += dpp_f64<0x140>(x);  // row_mirror
-  return (readlane_f64(x, 0) + readlane_f64(x, 16)) + (readlane_f64(x, 32) + readlane_f64(x, 48));
+  uint32_t u = (uint32_t)v;  // (wrapping adds: no overflow for the bounded inputs, none for the compiler either)
+  if (INT_STAGES >= 1) u += (uint32_t)dpp_i32k<0xB1>((int)u);   // quad_perm [1,0,3,2]
+  if (INT_STAGES >= 2) u += (uint32_t)dpp_i32k<0x4E>((int)u);   // quad_perm [2,3,0,1]
+  if (INT_STAGES >= 3) u += (uint32_t)dpp_i32k<0x141>((int)u);  // row_half_mirror
+  if (INT_STAGES >= 4) u += (uint32_t)dpp_i32k<0x140>((int)u);  // row_mirror
+  double x = (double)(int)u;
+  if (INT_STAGES < 1) x += dpp_f64<0xB1>(x);
+  if (INT_STAGES < 2) x += dpp_f64<0x4E>(x);
+  if (INT_STAGES < 3) x += dpp_f64<0x141>(x);
+  if (INT_STAGES < 4) x += dpp_f64<0x140>(x);  // every lane of a row: the row's sum
+  x += dpp_f64_masked<0x142, 0xA>(x);          // rows 1, 3 += rows 0, 2 (row_bcast15)
+  x += dpp_f64_masked<0x143, 0xC>(x);          // rows 2, 3 += row 1 (row_bcast31): lane 63 holds the total
+  return readlane_f64(x, 63);
+}
+// two sums, stage by stage (the second fills the first's DPP wait states)
+template <int INT_STAGES>
+__device__ __forceinline__ void wave_sum2_exact(int v1, int v2, double& s1, double& s2) {
+  uint32_t u1 = (uint32_t)v1, u2 = (uint32_t)v2;
+  if (INT_STAGES >= 1) {
+    u1 += (uint32_t)dpp_i32k<0xB1>((int)u1);
+    u2 += (uint32_t)dpp_i32k<0xB1>((int)u2);
+  }
+  if (INT_STAGES >= 2) {
+    u1 += (uint32_t)dpp_i32k<0x4E>((int)u1);
+    u2 += (uint32_t)dpp_i32k<0x4E>((int)u2);
+  }
+  if (INT_STAGES >= 3) {
+    u1 += (uint32_t)dpp_i32k<0x141>((int)u1);
+    u2 += (uint32_t)dpp_i32k<0x141>((int)u2);
+  }
+  static_assert(INT_STAGES == 3, "the row_mirror stage below is the FP64 one");
+  double x1 = (double)(int)u1, x2 = (double)(int)u2;
+  x1 += dpp_f64<0x140>(x1);
+  x2 += dpp_f64<0x140>(x2);
+  x1 += dpp_f64_masked<0x142, 0xA>(x1);
+  x2 += dpp_f64_masked<0x142, 0xA>(x2);
+  x1 += dpp_f64_masked<0x143, 0xC>(x1);
+  x2 += dpp_f64_masked<0x143, 0xC>(x2);
+  s1 = readlane_f64(x1, 63);
+  s2 = readlane_f64(x2, 63);
 }
 // 32-bit form: every per-pixel product below fits in int32 (|I w| <= 255 * 16384,
 // |DX w| <= 4080 * 16384, |diff * grad| <= 8160 * 4080, 7 pixels per lane), so
@@ -163,15 +216,16 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
                                                   double eps2, double min_eig) {
   __shared__ __attribute__((aligned(16))) uint32_t regions[4][kRegion * kRegion];
   const int lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // (scalar: the feature, its region and
+  const int f = blockIdx.x * 4 + wv;                                 // its window origin live in scalar registers)
   if (f >= n) return;  // wave-uniform
-  uint32_t* reg = regions[threadIdx.x >> 6];
+  uint32_t* reg = regions[wv];
   const int half = (win - 1) / 2, npx = win * win;
   const double FLT_SCALE = 1.0 / (1 << 20);
   uint8_t st = 1;
   float nx = 0, ny = 0;
   int iv[kMaxWinPx], ixv[kMaxWinPx], iyv[kMaxWinPx];
-  int wy[kMaxWinPx], wx[kMaxWinPx], roff[kMaxWinPx];  // window coordinates of this lane's pixels, region offsets
+  int wy[kMaxWinPx], wx[kMaxWinPx], roff[kMaxWinPx];  // window coordinates of this lane's pixels, region byte offsets
   bool wok[kMaxWinPx];
 #pragma unroll
   for (int q = 0; q < kMaxWinPx; ++q) {
@@ -180,7 +234,8 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const int kk = wok[q] ? k : 0;
     wy[q] = kk / win;
     wx[q] = kk - wy[q] * win;
-    roff[q] = wy[q] * kRegion + wx[q];
+    roff[q] = 4 * (wy[q] * kRegion + wx[q]);  // (bytes)
+    asm volatile("" : "+v"(roff[q]));  // kept in a register: one add per tap address in the LK loop
   }
   const float px0 = pin[2 * f], py0 = pin[2 * f + 1];
   for (int L = P.nl - 1; L >= 0; --L) {
@@ -195,7 +250,9 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       ny = ny * 2.0f;
     }
     const float pxw = px - (float)half, pyw = py - (float)half;
-    const int ix0 = (int)floorf(pxw), iy0 = (int)floorf(pyw);
+    int iv0[2] = {(int)floorf(pxw), (int)floorf(pyw)};
+    asm volatile("" : "+v"(iv0[0]), "+v"(iv0[1]));
+    const int ix0 = __builtin_amdgcn_readfirstlane(iv0[0]), iy0 = __builtin_amdgcn_readfirstlane(iv0[1]);
     if (ix0 < 0 || iy0 < 0 || ix0 + win >= W || iy0 + win >= H) {
       if (L == 0) st = 0;
       continue;
@@ -205,25 +262,29 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const int iw01 = (int)rintf(a * (1.f - b) * 16384.f);
     const int iw10 = (int)rintf((1.f - a) * b * 16384.f);
     const int iw11 = 16384 - iw00 - iw01 - iw10;
-    const uint8_t* I = P.I[L];
-    const int16_t* DX = P.dx[L];
-    const int16_t* DY = P.dy[L];
+    // window origin as scalar base pointers, the lane's pixels as 32-bit
+    // offsets from them (scalar-base loads: no 64-bit address per tap)
+    const uint8_t* I = P.I[L] + (long)iy0 * SI + ix0;
+    const char* DX = reinterpret_cast<const char*>(P.dx[L] + (long)iy0 * W + ix0);
+    const char* DY = reinterpret_cast<const char*>(P.dy[L] + (long)iy0 * W + ix0);
+    auto ld16 = [](const char* base, uint32_t byte_off) { return (int)*reinterpret_cast<const int16_t*>(base + byte_off); };
     int i4[kMaxWinPx][4], x4[kMaxWinPx][4], y4[kMaxWinPx][4];
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
-      const long o = (long)(iy0 + wy[q]) * W + ix0 + wx[q], oi = (long)(iy0 + wy[q]) * SI + ix0 + wx[q];
+      const uint32_t o = 2u * (uint32_t)(wy[q] * W + wx[q]), oi = (uint32_t)(wy[q] * SI + wx[q]);  // (bytes)
+      const uint32_t oW = o + 2u * (uint32_t)W, oS = oi + (uint32_t)SI;
       i4[q][0] = I[oi];
       i4[q][1] = I[oi + 1];
-      i4[q][2] = I[oi + SI];
-      i4[q][3] = I[oi + SI + 1];
-      x4[q][0] = DX[o];
-      x4[q][1] = DX[o + 1];
-      x4[q][2] = DX[o + W];
-      x4[q][3] = DX[o + W + 1];
-      y4[q][0] = DY[o];
-      y4[q][1] = DY[o + 1];
-      y4[q][2] = DY[o + W];
-      y4[q][3] = DY[o + W + 1];
+      i4[q][2] = I[oS];
+      i4[q][3] = I[oS + 1];
+      x4[q][0] = ld16(DX, o);
+      x4[q][1] = ld16(DX, o + 2);
+      x4[q][2] = ld16(DX, oW);
+      x4[q][3] = ld16(DX, oW + 2);
+      y4[q][0] = ld16(DY, o);
+      y4[q][1] = ld16(DY, o + 2);
+      y4[q][2] = ld16(DY, oW);
+      y4[q][3] = ld16(DY, oW + 2);
     }
     int a11l = 0, a12l = 0, a22l = 0;
 #pragma unroll
@@ -238,8 +299,10 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
       a12l += ixv[q] * iyv[q];
       a22l += iyv[q] * iyv[q];
     }
-    const double a11 = wave_sum_exact(a11l) * FLT_SCALE, a12 = wave_sum_exact(a12l) * FLT_SCALE,
-                 a22 = wave_sum_exact(a22l) * FLT_SCALE;
+    // (|ix|, |iy| <= 4080, 7 pixels per lane: a 16-lane sum of the products
+    // is at most 1.87e9, inside int32 -- four integer stages)
+    const double a11 = wave_sum_exact<4>(a11l) * FLT_SCALE, a12 = wave_sum_exact<4>(a12l) * FLT_SCALE,
+                 a22 = wave_sum_exact<4>(a22l) * FLT_SCALE;
     const double D = a11 * a22 - a12 * a12;
     const double minEig = (a22 + a11 - sqrt((a11 - a22) * (a11 - a22) + 4.0 * a12 * a12)) / (2.0 * win * win);
     if (minEig < min_eig || D < 1.1920928955078125e-07) {
@@ -253,15 +316,23 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const bool staged = W >= kRegion && H >= kRegion && win + 1 <= kRegion;
     int rx0 = -(1 << 30), ry0 = -(1 << 30);  // no region yet
     for (int j = 0; j < max_iters; ++j) {
-      const int jx0 = (int)floorf(nxw), jy0 = (int)floorf(nyw);
+      // (the position, its weights and the region test are wave-uniform -- every
+      // lane runs the same arithmetic on the same values: scalar registers)
+      const int jx0 = __builtin_amdgcn_readfirstlane((int)floorf(nxw));
+      const int jy0 = __builtin_amdgcn_readfirstlane((int)floorf(nyw));
       if (jx0 < 0 || jy0 < 0 || jx0 + win >= W || jy0 + win >= H) {
         if (L == 0) st = 0;
         break;
       }
       const float c = nxw - (float)jx0, d = nyw - (float)jy0;
-      const int jw00 = (int)rintf((1.f - c) * (1.f - d) * 16384.f);
-      const int jw01 = (int)rintf(c * (1.f - d) * 16384.f);
-      const int jw10 = (int)rintf((1.f - c) * d * 16384.f);
+      // (converted in a vector register, then read once into a scalar one: the
+      // weight packing below runs on the scalar unit)
+      int jv[3] = {(int)rintf((1.f - c) * (1.f - d) * 16384.f), (int)rintf(c * (1.f - d) * 16384.f),
+                   (int)rintf((1.f - c) * d * 16384.f)};
+      asm volatile("" : "+v"(jv[0]), "+v"(jv[1]), "+v"(jv[2]));
+      const int jw00 = __builtin_amdgcn_readfirstlane(jv[0]);
+      const int jw01 = __builtin_amdgcn_readfirstlane(jv[1]);
+      const int jw10 = __builtin_amdgcn_readfirstlane(jv[2]);
       const int jw11 = 16384 - jw00 - jw01 - jw10;
       // the bilinear sum of a footprint word f (bytes J00 J01 J10 J11) as two
       // packed u8 dot products: w = 128 (w >> 7) + (w & 127), both halves fit
@@ -282,9 +353,9 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
           ry0 = min(max(jy0 - (kRegion - win - 1) / 2, 0), H - kRegion);
           stage_region(reg, J, SI, rx0, ry0, lane);
         }
-        const uint32_t* R0 = reg + (jy0 - ry0) * kRegion + (jx0 - rx0);
+        const char* R0 = reinterpret_cast<const char*>(reg + (jy0 - ry0) * kRegion + (jx0 - rx0));
 #pragma unroll
-        for (int q = 0; q < kMaxWinPx; ++q) f4[q] = R0[roff[q]];
+        for (int q = 0; q < kMaxWinPx; ++q) f4[q] = *reinterpret_cast<const uint32_t*>(R0 + roff[q]);
       } else {
 #pragma unroll
         for (int q = 0; q < kMaxWinPx; ++q) {
@@ -307,7 +378,11 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
         b1l += diff * ixv[q];  // ixv = iyv = 0 on masked pixels
         b2l += diff * iyv[q];
       }
-      const double b1d = wave_sum_exact(b1l) * FLT_SCALE, b2d = wave_sum_exact(b2l) * FLT_SCALE;
+      // (|diff| <= 8160, |ix| <= 4080: an 8-lane sum is at most 1.87e9 -- three integer stages)
+      double b1d, b2d;
+      wave_sum2_exact<3>(b1l, b2l, b1d, b2d);
+      b1d *= FLT_SCALE;
+      b2d *= FLT_SCALE;
       const float ddx = (float)((a12 * b2d - a22 * b1d) * Dinv);
       const float ddy = (float)((a12 * b1d - a11 * b2d) * Dinv);
       nxw += ddx;
