@@ -2233,10 +2233,12 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   double mc = 0, cc = 0, s2 = 0, xn2 = 0;
   if (j < g.np && !st->fail) {  // uniform within a 16-lane group
     // Every load of the point and of this lane's first CSR slot is requested
-    // in two dependent rounds (point data + offsets | slot: camera, obs
+    // in three dependent rounds (point data + offsets | slot: camera, obs
     // index, W | camera step / scales, observation, candidate camera) before
     // any arithmetic; further slots (points with more than 16 observations)
-    // load in the loops.
+    // load in the loops.  The slot's camera is p_cam + nf (plan_segsort_kernel
+    // writes p_cam[q] = cam_idx[p_obs[q]] - nf), so the candidate camera does
+    // not wait for a cam_idx read.
     const int cur = st->cur;
     const double* Wo = b.Wo;
     double psv[3], gpv[3], Lv[9], xv[3], Vv[9];
@@ -2265,7 +2267,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     if (has0) {
       if (ci0 >= 0)
         for (int a = 0; a < 6; ++a) ys0[a] = b.csc[6 * ci0 + a] * b.yc[6 * ci0 + a];
-      cam0 = b.cam_idx[o0];
+      cam0 = ci0 + g.nf;
       for (int k = 0; k < OD; ++k) f0[k] = b.obs[(long)OD * o0 + k];
       if (OD == 2) right0 = b.cam_id[o0] != 0;
     }
@@ -2331,7 +2333,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
         right = right0;
       } else {
         const int o = b.p_obs[q];
-        const int cam = b.cam_idx[o];
+        const int cam = b.p_cam[q] + g.nf;
         for (int a = 0; a < 6; ++a) cv[a] = cams_c[6 * cam + a];
         for (int k = 0; k < OD; ++k) f[k] = b.obs[(long)OD * o + k];
         if (OD == 2) right = b.cam_id[o] != 0;
@@ -2936,7 +2938,15 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   // slower with 8)
   // (and once 16-landmark sub-chunks outnumber 256 workgroups: the config-3
   // VO window, ~4 400 landmarks, BA_SCHUR 430 -> 340 us per keyframe)
-  if ((g.npairs > 40 || g.np > 256 * kSchurPts) && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap)
+  // Few tiles and landmarks (config 3: 28 pairs, 2 000 landmarks): 32-landmark
+  // sub-chunks whose run is split into two tile groups of 2 tiles per wave --
+  // the same 48 MFMAs per wave as 16 landmarks x 4 tiles, half the runs, so
+  // half the partial tiles written here and summed by the assembly
+  // (pt_schur 15.8 -> 14.9 us, cam_solve 31.8 -> 31.4 us per iteration,
+  // rocprofv3 A/B); a run's Y block is formed twice (once per group).
+  const bool split_wide = g.npairs <= 40 && g.np <= 256 * kSchurPts &&
+                          schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap;
+  if ((g.npairs > 40 || g.np > 256 * kSchurPts || split_wide) && schur_lds_bytes(kSchurPtsWide, g.Rpad) <= kSchurLdsCap)
     g.spts = kSchurPtsWide;
   else
     g.spts = g.npairs > 100 ? kSchurPtsSmall : kSchurPts;
@@ -2954,6 +2964,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   // (measured, tools/ab_schur.py: 4 tiles per wave at config 4 -- 5 spill -- but 5 for
   // the 50-keyframe window, where fewer tile groups per run recompute fewer Y blocks)
   g.stpw = 8 * std::min((g.npairs + 7) / 8, g.npairs > 100 ? kSchurNtMax : std::min(kSchurNtMax, 4));
+  if (split_wide && g.spts == kSchurPtsWide) g.stpw = std::min(g.stpw, 16);
+  if (const char* e = getenv("ME_SCHUR_STPW")) {  // A/B timing only: tiles per group (8 x tiles per wave)
+    const int v = atoi(e);
+    if (v >= 16 && v <= 8 * kSchurNtMax && v % 8 == 0) g.stpw = v;
+  }
   g.sgrp = (g.npairs + g.stpw - 1) / g.stpw;
   g.ksplit = g.nruns * g.sgrp;  // Schur workgroups (a run's surplus tile groups exit at once)
   // band order pays once the tile set is large (config 4: 66 pairs, config 5: 190); for
@@ -3142,7 +3157,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
 #define ME_SCHUR_K(N)                                                                                   \
   (const void*)pt_schur_kernel<N, 512, kSchurPts>, (const void*)pt_schur_kernel<N, 512, kSchurPtsWide>, \
       (const void*)pt_schur_kernel<N, 512, kSchurPtsSmall>
-    for (const void* k : {ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5)})
+    for (const void* k : {ME_SCHUR_K(2), ME_SCHUR_K(3), ME_SCHUR_K(4), ME_SCHUR_K(5)})
 #undef ME_SCHUR_K
       ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSchurLdsCap));
     c->ba_lds_attr = 1;
@@ -3242,7 +3257,8 @@ int enqueue_linearize(Plan& P) {
                             P.o, ca);                                                                        \
   } while (0)
     static_assert(kSchurNtMax >= 3 && kSchurNtMax <= 5, "instantiated tile counts");
-    if (pw8 <= 3) ME_SCHUR(3);
+    if (pw8 <= 2) ME_SCHUR(2);
+    else if (pw8 <= 3) ME_SCHUR(3);
     else if (pw8 <= 4) ME_SCHUR(4);
     else ME_SCHUR(5);
 #undef ME_SCHUR
