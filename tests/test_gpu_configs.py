@@ -204,14 +204,14 @@ def test_ba_config4_8000x30(ctx, oracle):
     c = S.CONFIGS[4]
     bp = S.ba_problem(S.SEED0 + 4, c["n_feats"], c["window"], c["width"], c["height"])
     assert len(bp.pts) == 8000 and len(bp.cams) == 30
-    _ba_fixed(ctx, oracle, bp, 4)
+    _ba_fixed(ctx, oracle, bp, 10)  # (the bench's 10 iterations, unsharded -- VERDICT r4)
 
 
 def test_ba_config5_2000x50(ctx, oracle):
     c = S.CONFIGS[5]
     bp = S.ba_problem(S.SEED0 + 5, c["n_feats"], c["window"], c["width"], c["height"])
     assert len(bp.pts) == 2000 and len(bp.cams) == 50
-    _ba_fixed(ctx, oracle, bp, 4)
+    _ba_fixed(ctx, oracle, bp, 10)
 
 
 # ------------------------------------------------------------------ config-sized KLT

@@ -135,10 +135,33 @@ def _check_against_oracle(g, o, window, n):
     gp, op = g.poses, o.poses
     for t in gp:
         np.testing.assert_allclose(gp[t], op[t], rtol=1e-6, atol=1e-9)
-    # landmarks: all but the ill-conditioned few (near-zero parallax far points,
-    # where summation-order differences are amplified) within 1e-6
+    # every landmark within 1e-6 (measured: 1.5e-10 at most; the round-4 bar let
+    # 0.1 % of them exceed it), and every landmark reprojects into the last
+    # keyframe (left and right image, each loop's own pose) within 1e-6 pixel
+    # (measured: 6.7e-9)
     rel = np.abs(g.X - o.X) / (np.abs(o.X) + 1e-9)
-    assert (rel > 1e-6).mean() < 1e-3 and np.median(rel) < 1e-9, (rel.max(), (rel > 1e-6).sum())
+    dpx = _reproj_diff(g, o, max(gp))
+    print("landmarks: max rel %.3g; max reprojection difference %.3g px" % (rel.max(), dpx.max()))
+    assert rel.max() < 1e-6, (rel.max(), int((rel > 1e-6).sum()))
+    assert dpx.max() < 1e-6, (dpx.max(), int((dpx >= 1e-6).sum()))
+
+
+def _reproj_diff(g, o, t):
+    from uasl_motion_estimation_amd import synthetic as S
+
+    K, b = np.asarray(o.K), float(o.cfg.baseline)
+    out = []
+    for vo in (g, o):
+        pose = np.asarray(vo.poses[t], np.float64)
+        P = np.asarray(vo.X, np.float64) @ S.aa_to_R(pose[3:]).T + pose[:3]
+        out.append(P)
+    front = (out[0][:, 2] > 1.0) & (out[1][:, 2] > 1.0)
+    px = []
+    for P in out:
+        P = P[front]
+        px.append(np.stack([K[0, 0] * P[:, 0] / P[:, 2] + K[0, 2], K[1, 1] * P[:, 1] / P[:, 2] + K[1, 2],
+                            K[0, 0] * (P[:, 0] - b) / P[:, 2] + K[0, 2]], 1))
+    return np.abs(px[0] - px[1]).max(1) if len(px[0]) else np.zeros(1)
 
 
 @pytest.mark.gpu
