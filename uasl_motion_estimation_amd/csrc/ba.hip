@@ -623,7 +623,15 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   if (blockIdx.x == 0 && threadIdx.x == 0) st->final_pass = final_pass;
   const int P = g.spts, Rz = g.Rpad, rows = 3 * P, nks = rows / 4;
   // this workgroup's run and tile group; the run's tile set is [bA, bB] plus the z tile T - 1
-  const int run = blockIdx.x / g.sgrp, tgrp = blockIdx.x - run * g.sgrp;
+  // Workgroups are dealt round-robin over the 8 XCDs: a run's tile groups sit
+  // at blocks b, b + 8, ... so they share an XCD's L2 -- the second group's
+  // reads of the run's slots (W, obsx) hit the lines the first one fetched.
+  const int sup = blockIdx.x / (8 * g.sgrp), r8 = blockIdx.x - sup * 8 * g.sgrp;
+  const int run = 8 * sup + (r8 & 7), tgrp = r8 >> 3;
+  if (run >= g.nruns) {  // (uniform) padding of the last block of 8 runs
+    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = 0.0;
+    return;
+  }
   const int bA = g.sorted ? b.rband[2 * run] : 0, bB = g.sorted ? b.rband[2 * run + 1] : g.T - 1;
   const int nb = bB - bA + 1, ns = nb + (bB < g.T - 1 ? 1 : 0), ntile = ns * (ns + 1) / 2;
   if (tgrp * g.stpw >= ntile) {  // (uniform) the run's tiles are all taken by lower groups
@@ -2970,7 +2978,9 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     if (v >= 16 && v <= 8 * kSchurNtMax && v % 8 == 0) g.stpw = v;
   }
   g.sgrp = (g.npairs + g.stpw - 1) / g.stpw;
-  g.ksplit = g.nruns * g.sgrp;  // Schur workgroups (a run's surplus tile groups exit at once)
+  // Schur workgroups: runs in blocks of 8 (one per XCD) x sgrp tile groups (a
+  // run's surplus tile groups and the padding runs exit at once)
+  g.ksplit = (g.sgrp > 1 ? (int)rup((long)g.nruns, 8) : g.nruns) * g.sgrp;
   // band order pays once the tile set is large (config 4: 66 pairs, config 5: 190); for
   // config 3 (28 pairs) the two plan launches cost more than the partial traffic saves
   g.sorted = g.npairs > 40 ? 1 : 0;
