@@ -437,7 +437,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MI_COUNTERS = "r05_c_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
+MI_COUNTERS = "r05_e_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
