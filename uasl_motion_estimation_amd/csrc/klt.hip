@@ -267,24 +267,37 @@ __global__ __launch_bounds__(256) void klt_kernel(Pyr P, const float* __restrict
     const uint8_t* I = P.I[L] + (long)iy0 * SI + ix0;
     const char* DX = reinterpret_cast<const char*>(P.dx[L] + (long)iy0 * W + ix0);
     const char* DY = reinterpret_cast<const char*>(P.dy[L] + (long)iy0 * W + ix0);
-    auto ld16 = [](const char* base, uint32_t byte_off) { return (int)*reinterpret_cast<const int16_t*>(base + byte_off); };
+    // horizontal tap pairs as one (unaligned) load each: I(x), I(x+1) as 16
+    // bits, DX / DY(x), (x+1) as 32 bits, split in registers
+    auto ld_u16 = [](const uint8_t* base, uint32_t off) {
+      uint16_t v;
+      __builtin_memcpy(&v, base + off, 2);
+      return (uint32_t)v;
+    };
+    auto ld_u32 = [](const char* base, uint32_t off) {
+      uint32_t v;
+      __builtin_memcpy(&v, base + off, 4);
+      return v;
+    };
     int i4[kMaxWinPx][4], x4[kMaxWinPx][4], y4[kMaxWinPx][4];
 #pragma unroll
     for (int q = 0; q < kMaxWinPx; ++q) {
       const uint32_t o = 2u * (uint32_t)(wy[q] * W + wx[q]), oi = (uint32_t)(wy[q] * SI + wx[q]);  // (bytes)
       const uint32_t oW = o + 2u * (uint32_t)W, oS = oi + (uint32_t)SI;
-      i4[q][0] = I[oi];
-      i4[q][1] = I[oi + 1];
-      i4[q][2] = I[oS];
-      i4[q][3] = I[oS + 1];
-      x4[q][0] = ld16(DX, o);
-      x4[q][1] = ld16(DX, o + 2);
-      x4[q][2] = ld16(DX, oW);
-      x4[q][3] = ld16(DX, oW + 2);
-      y4[q][0] = ld16(DY, o);
-      y4[q][1] = ld16(DY, o + 2);
-      y4[q][2] = ld16(DY, oW);
-      y4[q][3] = ld16(DY, oW + 2);
+      const uint32_t i01 = ld_u16(I, oi), i23 = ld_u16(I, oS);
+      const uint32_t x01 = ld_u32(DX, o), x23 = ld_u32(DX, oW), y01 = ld_u32(DY, o), y23 = ld_u32(DY, oW);
+      i4[q][0] = (int)(i01 & 255u);
+      i4[q][1] = (int)(i01 >> 8);
+      i4[q][2] = (int)(i23 & 255u);
+      i4[q][3] = (int)(i23 >> 8);
+      x4[q][0] = (int)(int16_t)(x01 & 0xffffu);
+      x4[q][1] = (int)x01 >> 16;
+      x4[q][2] = (int)(int16_t)(x23 & 0xffffu);
+      x4[q][3] = (int)x23 >> 16;
+      y4[q][0] = (int)(int16_t)(y01 & 0xffffu);
+      y4[q][1] = (int)y01 >> 16;
+      y4[q][2] = (int)(int16_t)(y23 & 0xffffu);
+      y4[q][3] = (int)y23 >> 16;
     }
     int a11l = 0, a12l = 0, a22l = 0;
 #pragma unroll
