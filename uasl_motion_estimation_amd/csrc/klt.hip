@@ -189,18 +189,27 @@ __device__ __forceinline__ void wave_lds_sync() {
 __device__ __forceinline__ void stage_region(uint32_t* reg, const uint8_t* __restrict__ J, int SI, int rx0, int ry0,
                                              int lane) {
   const int y = lane >> 1, x0 = 16 * (lane & 1);
-  const uint8_t* r0 = J + (long)(ry0 + y) * SI + rx0;
-  const uint8_t* r1 = J + (long)(ry0 + min(y + 1, kRegion - 1)) * SI + rx0;
-  uint32_t b0[17], b1[17];
+  const uint8_t* r0 = J + (long)(ry0 + y) * SI + rx0 + x0;
+  const uint8_t* r1 = J + (long)(ry0 + min(y + 1, kRegion - 1)) * SI + rx0 + x0;
+  // the row segment's 16 bytes as four (unaligned) dwords, the 17th byte
+  // (clamped to the region) on its own; each footprint word picks bytes
+  // k, k + 1 of both rows (alignbyte + perm)
+  uint32_t d0[5], d1[5];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    const int x = min(x0 + k, kRegion - 1);
-    b0[k] = r0[x];
-    b1[k] = r1[x];
+  for (int i = 0; i < 4; ++i) {
+    __builtin_memcpy(&d0[i], r0 + 4 * i, 4);
+    __builtin_memcpy(&d1[i], r1 + 4 * i, 4);
   }
+  const int x16 = min(x0 + 16, kRegion - 1) - x0;
+  d0[4] = r0[x16];
+  d1[4] = r1[x16];
   uint32_t w[16];
 #pragma unroll
-  for (int k = 0; k < 16; ++k) w[k] = b0[k] | (b0[k + 1] << 8) | (b1[k] << 16) | (b1[k + 1] << 24);
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t a0 = __builtin_amdgcn_alignbyte(d0[k / 4 + 1], d0[k / 4], k % 4);  // row y: bytes k .. k + 3
+    const uint32_t a1 = __builtin_amdgcn_alignbyte(d1[k / 4 + 1], d1[k / 4], k % 4);  // row y + 1
+    w[k] = __builtin_amdgcn_perm(a1, a0, 0x05040100u);  // J(k), J(k+1), J'(k), J'(k+1)
+  }
   wave_lds_sync();  // earlier reads of the previous region are done
   uint4* dst = reinterpret_cast<uint4*>(reg + y * kRegion + x0);
 #pragma unroll
