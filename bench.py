@@ -1100,12 +1100,6 @@ def main():
     if args.rank_device == "zero":  # (tests: every rank on GPU 0; RCCL cannot run two ranks on one GPU)
         assert args.comm == "gloo" or world == 1, "--rank-device zero needs --comm gloo"
         local_rank = 0
-        if world > 1:
-            # the persistent scale-LM grid needs its workgroups co-resident, which
-            # several processes sharing one GPU cannot promise each other: the
-            # per-phase launches instead (read by the library once, at its first
-            # scale solve)
-            os.environ.setdefault("ME_SCALE_BLOCKS", "1")
     pool = pool1 = None
     model, ncpu, avail = host_cpu()
     cpu_workers = args.cpu_workers or min(16, avail)

@@ -229,6 +229,14 @@ int me_scale_optimise(me_ctx* ctx, me_scale_state* s, const me_optim_params* p, 
    result is already known (same state) still counts.  executed = residual
    evaluations the device actually ran (speculative candidates included). */
 int me_scale_last_counters(me_ctx* ctx, long* res_evals, long* neq_evals, long* rejections, long* executed);
+/* Launch form me_scale_optimise picks for nb track blocks (16 tracks each)
+   when `cap` workgroups of the persistent LM kernel fit on the ctx's CUs:
+   1 = the one persistent launch (nb x 2 workgroups, at most half of cap),
+   0 = one launch per LM phase.  The persistent grid does not need to be
+   co-resident (a workgroup roster deals the work over the workgroups that
+   run), so this is a throughput choice; no environment
+   variable changes it.  Host only: no device, no ctx. */
+int me_scale_persistent(int nb, int cap);
 /* double ScaleState::compute_residuals(std::vector<std::pair<cv::Mat,cv::Mat>>&)
    (include/MotionEstimation/optimisation/optimisation.h:86, src/optimisation/optimisation.cpp:230-278):
    one mutual information over the stacked 2w x 2w patch pairs of the left

@@ -315,3 +315,64 @@ def test_klt_many_features_rare_weights(ctx, oracle):
     ref, rst = oracle.klt(stream[0].left, stream[1].left, pts)
     assert np.array_equal(gst, rst)
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+
+
+# ------------------------------------------------------------------ co-residency roster (csrc/roster.hpp)
+@pytest.fixture
+def roster_now(ctx):
+    """Test hook me_debug_solve_flags(8192): every roster on this ctx closes at
+    once, so the persistent scale LM and the camera solve's workers run on
+    whichever workgroups had joined by then (usually a few: the rest leave
+    at once and their units are dealt over the joined ones; with none, block
+    0 works alone), and the camera solve's block 0 claims every fused
+    assembly unit not yet claimed without waiting (roster.hpp CLAIM)."""
+    import ctypes
+
+    hook = ctx.lib.me_debug_solve_flags
+    hook.argtypes = [ctypes.c_void_p, ctypes.c_int]
+
+    def set_(on):
+        assert hook(ctx.h, 8192 if on else 0) == 0
+
+    yield set_
+    set_(False)
+
+
+def test_roster_scale_lm_identical_at_any_participant_count(ctx, oracle, sp_cfg3, roster_now):
+    """the persistent scale LM no longer assumes its grid
+    co-resident.  With the roster closed at once the phases run on fewer
+    workgroups: the same stop, counts, scale and trace bit for bit, and the
+    oracle's."""
+    from uasl_motion_estimation_amd.optimisation import scale_optimise
+
+    sp = sp_cfg3[0]
+    out = []
+    for on in (False, True):
+        roster_now(on)
+        out.append(scale_optimise(sp, OptimisationParams(), ctx=ctx))
+    a, b = out
+    for k in ("stop", "iterations", "res_evals", "neq_evals", "rejections", "track_evals"):
+        assert a[k] == b[k], k
+    assert np.float64(a["scale"]).tobytes() == np.float64(b["scale"]).tobytes()
+    assert np.array_equal(np.asarray(a["trace"]), np.asarray(b["trace"]))
+    _scale_check(ctx, oracle, sp, OptimisationParams())  # (hook still on)
+
+
+@pytest.mark.parametrize("cfg,iters", [(3, 10), (5, 4)])
+def test_roster_camera_solve_identical_at_any_participant_count(ctx, roster_now, cfg, iters):
+    """The camera solve's fused assembly units (config 3, LDS form: claimed
+    by block 0 as well as by the assemblers) and trailing tiles (config 5,
+    global-memory form with workers, dealt over whichever workers joined the
+    roster): bit-identical cameras, points and summary."""
+    from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
+
+    c = S.CONFIGS[cfg]
+    bp = S.ba_problem(S.SEED0 + cfg, c["n_feats"], c["window"], c["width"], c["height"])
+    out = []
+    for on in (False, True):
+        roster_now(on)
+        out.append(ba_solve(bp.copy(), SolverOptions.fixed_iterations(iters), ctx=ctx))
+    (c0, p0, s0), (c1, p1, s1) = out
+    assert np.array_equal(c0, c1) and np.array_equal(p0, p1)
+    assert (s0["iterations"], s0["successful_steps"], s0["final_cost"]) == \
+        (s1["iterations"], s1["successful_steps"], s1["final_cost"])

@@ -149,3 +149,41 @@ def test_cu_split_is_a_disjoint_cover(front, mode):
     if mode == "xcd" and front % 2 == 0:
         xf, xb = {i % 8 for i in f}, {i % 8 for i in b}
         assert not xf & xb and len(xf) == front // 2
+
+
+# --------------------------------------------------- co-residency roster (csrc/roster.hpp)
+def test_roster_protocol_host_threads():
+    """The roster the cross-workgroup kernels join (scale_lm_kernel, the camera
+    solve's workers and fused assemblers), run by tests/cpp/roster_test over
+    std atomics with threads as workgroups, some dispatched after the close:
+    every unit of every phase runs exactly once, late workgroups run nothing,
+    nobody waits for a workgroup that did not join, and with no participant
+    the decider does every unit itself."""
+    exe = os.path.join(ROOT, "tests", "cpp", "roster_test")
+    assert os.path.exists(exe), "build() compiles tests/cpp/roster_test"
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert "roster_test: ok" in p.stdout
+
+
+def test_scale_lm_launch_form_selection():
+    """me_scale_persistent (host only): the one persistent scale-LM launch
+    while its nb x 2 workgroups take at most half of the co-resident capacity,
+    else the per-phase launches; no capacity (occupancy query failed) always
+    takes the per-phase launches.  No environment variable enters the choice
+    (bench.py no longer sets ME_SCALE_BLOCKS)."""
+    lib = _lib.load_library()
+    assert lib.me_scale_persistent(125, 2048) == 1  # config 3: 2 000 tracks, 16 per block
+    assert lib.me_scale_persistent(256, 1024) == 1  # exactly half
+    assert lib.me_scale_persistent(257, 1024) == 0
+    assert lib.me_scale_persistent(1000, 2048) == 0  # config 4 size: per-phase launches
+    assert lib.me_scale_persistent(1, 0) == 0
+    assert lib.me_scale_persistent(1, -1) == 0
+    os.environ["ME_SCALE_BLOCKS"] = "1"  # ignored by the library
+    try:
+        assert lib.me_scale_persistent(125, 2048) == 1
+    finally:
+        del os.environ["ME_SCALE_BLOCKS"]
+    src = open(os.path.join(ROOT, "uasl_motion_estimation_amd", "csrc", "scale.hip")).read()
+    assert "ME_SCALE_BLOCKS" not in src and "getenv(\"ME_SCALE" not in src
+    assert "ME_SCALE_BLOCKS" not in open(os.path.join(ROOT, "bench.py")).read()

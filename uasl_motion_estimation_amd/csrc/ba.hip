@@ -14,6 +14,7 @@
 #include <hip/hip_ext.h>
 #include "me_internal.hpp"
 #include "ba_kernels.hpp"
+#include "roster.hpp"
 #include "solve_diag.hpp"
 #include "me_device.hpp"
 
@@ -1023,11 +1024,20 @@ enum { SA_SUM = 0, SA_PACK = 1, SA_UNPACK = 2 };
 // block symmetric, identity padding), written through -- so the solve copies
 // it into LDS with a few LDS-DMA instructions instead of an element-wise load
 // (whose one-time code dominated the launch, tools/solve_ts.py).
+//
+// claim (fused assembly): the unit is first claimed for launch generation
+// `gen` (atomic max on its claim word, issued before the loads, its result
+// read only before the stores); a unit another workgroup claimed first is
+// left to it -- no stores, and the function returns false.
 template <int NTH, bool SC1>
-__device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, int mode = SA_SUM,
-                                double* img = nullptr, const Opts* o = nullptr) {
+__device__ bool s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, int mode = SA_SUM,
+                                double* img = nullptr, const Opts* o = nullptr, unsigned* claim = nullptr,
+                                unsigned gen = 0) {
   constexpr int EL = NTH / kSaGroups;
   __shared__ double part[kSaGroups][EL];
+  __shared__ int s_claimed;
+  unsigned claim_old = 0;
+  if (claim && threadIdx.x == 0) claim_old = me_roster_dev::fetch_max(claim, gen);  // (roster.hpp CLAIM, split)
   const State* st = b.st;
   const bool live = !(st->done || st->final_pass);  // final pass: no step follows, S is not needed
   const int n = g.n6;
@@ -1094,7 +1104,9 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
     }
   }
   part[grp][e] = acc;
+  if (claim && threadIdx.x == 0) s_claimed = claim_old < gen;
   __syncthreads();
+  if (claim && !s_claimed) return false;
   if (img != nullptr) {
     // every element of the tile pair when live (padding included): the image
     // is complete without any other writer
@@ -1128,7 +1140,7 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
       }
       a_st<SC1>(&img[diag ? (long)gr * ld + gc : (long)gc * ld + gr], v);
     }
-    return;
+    return true;
   }
   if (grp == 0 && use) {
     double sum = 0.0;
@@ -1168,6 +1180,7 @@ __device__ void s_assemble_body(const Geo& g, const Bufs& b, int blk, int full, 
   } else if (mode == SA_PACK && grp == 0 && idx < g.npairs * 256) {
     b.xch[idx] = 0.0;  // padding (and a finished solve): defined values in the exchange
   }
+  return true;
 }
 
 // mode SA_PACK (sharded, before the exchange): the last workgroup writes the
@@ -1275,15 +1288,18 @@ __host__ __device__ inline size_t solve_a_doubles(int Ts) { return (size_t)(16 *
 
 // Global-memory form (windows whose [S; -b^T] does not fit the LDS, config 4
 // and 5): block 0 factors the diagonal blocks and panels as below, and the
-// trailing update of each block step is spread over `nworkers` further
-// workgroups of the same launch.  Hand-offs through b.ssync (zeroed by
+// trailing update of each block step is spread over the further workgroups
+// of the same launch that joined its roster (roster.hpp: block 0 never waits
+// for a workgroup that was not dispatched; with none, it updates the tiles
+// itself).  Hand-offs through b.ssync (zeroed by
 // s_assemble before every solve): block 0 publishes step J (epoch J + 1)
 // once the panel of J is stored (every thread: agent-scope release fence,
 // barrier, release store); a worker waits for the epoch (acquire, barrier),
 // updates its tiles of step J and counts itself done (fence, barrier,
 // release add); block 0 waits for all workers before the next diagonal
-// block.  Every spin is bounded: a missing partner ends the solve as a
-// failed step, never a hang.
+// block.  Every spin is also bounded (a safety net: every partner waited on
+// is resident): a missing partner ends the solve as a failed step, never a
+// hang.
 constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 // Hand-off form (MI355X_MICROARCH.md, inter-workgroup visibility, Valid forms
 // row 1): every store of A is write-through (sc1), every storing wave drains
@@ -1293,6 +1309,7 @@ constexpr unsigned kSolveTerm = 0x40000000u;  // epoch: stop (block 0 failed)
 // write-back) and no acquire (an L1 invalidate) per hand-off.
 constexpr long kSolveSpin = 1L << 21;         // bounded waits (~0.5 s with s_sleep)
 constexpr int kSkipImg = 4096;                // cam_solve `skip` bit: [S + D; -b^T] already in Abuf (solver layout)
+constexpr int kSkipRosterNow = 8192;          // cam_solve `skip` bit (test hook): the roster closes at once
 #ifndef ME_SOLVE_IMG
 #define ME_SOLVE_IMG 1  // non-fused assembly writes the solver's image (0: S | b | diag U, loaded by the solve)
 #endif
@@ -1433,13 +1450,40 @@ __device__ __forceinline__ void spin_timeout(const Bufs& b) {
 // signals, then its other tiles.  The diagonal tile (J + 1, J + 1) is left to
 // block 0, which applies step J to it in registers and factors it while the
 // workers update column J + 1.
+//
+// The workers join the solve's roster (roster.hpp) first; block 0 closes it
+// and the tiles are dealt over the P workers that joined (worker p, wave w:
+// slot p nw + w), so block 0 never waits for a worker that was not
+// dispatched.  Which wave updates a tile does not change its operations:
+// the results are the same for any P.
 __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
   __shared__ unsigned sep;
+  __shared__ int s_pid, s_np;
   const State* st = b.st;
-  if (st->done || st->fail || b.scal[R_COUNT] != 0.0) return;  // block 0 returns for the same reasons
+  if (st->done) return;  // block 0 returns for the same reason (before its close)
+  if (threadIdx.x == 0) {
+    // (no last-joiner close: the workers depend on block 0, which may not be
+    // dispatched yet; without its count within kAbandonTicks they close the
+    // roster empty and leave, and block 0 works alone)
+    int pid = me_roster::join<me_roster_dev>(b.roster, 0u), np = 0;
+    if (pid >= 0) {
+      np = me_roster::count_or_abandon<me_roster_dev>(b.roster);
+      if (np < 0) {  // a first closer that never published (not reachable: it is running)
+        b.st->spin_err = 1;
+        pid = -1;
+      } else if (pid >= np) {
+        pid = -1;  // the roster was abandoned (np = 0): block 0 updates every tile
+      }
+    }
+    s_pid = pid;
+    s_np = np;
+  }
+  __syncthreads();
+  if (s_pid < 0) return;  // dispatched after the close: the joined workers own every tile
+  if (st->fail || b.scal[R_COUNT] != 0.0) return;  // block 0 skips the factorisation for the same reasons
   const int Ts = g.Ts, ld = solve_ld(Ts);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const int slot0 = (blockIdx.x - 1) * nw + wave, nslots = nworkers * nw;
+  const int slot0 = s_pid * nw + wave, nslots = s_np * nw;
   const int ntiles = (Ts - 1) * Ts / 2;
   for (int J = 0; J + 1 < Ts; ++J) {
     if (tid == 0) {
@@ -1534,7 +1578,7 @@ template <int kMode>
 // waits for the count (bounded), re-arms it and reads S with sc1 loads.  One
 // launch per LM iteration fewer than s_assemble_kernel + cam_solve_kernel.
 __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, Opts o, int skip, int nworkers, int nasm,
-                                                                const double* gc_raw) {
+                                                                const double* gc_raw, unsigned asm_gen) {
   extern __shared__ double smem[];
   __shared__ double red[64];
   __shared__ int sfail;
@@ -1561,14 +1605,21 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 #ifdef ME_SOLVE_TS
     if (threadIdx.x == 0) atomicMin(&g_asm_first, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
+    // Unit u = blockIdx.x - 1, claimed first (s_assemble_body `claim`): block
+    // 0 takes the units nobody claimed once it has waited kCloseTicks for them
+    // (an assembler held back behind other work, another process's kernels or
+    // a CU mask), so it never waits for a workgroup that was not dispatched;
+    // a late assembler finds its unit claimed and stores nothing.
+    const int u = blockIdx.x - 1;
     // (sharded: the assemblers unpack the all-reduced exchange instead of summing partials)
-    s_assemble_body<kSolveBlock, true>(g, b, blockIdx.x - 1, 0, b.xch ? SA_UNPACK : SA_SUM,
-                                       kLds || ME_SOLVE_IMG ? b.Abuf : nullptr, &o);
+    const bool mine = s_assemble_body<kSolveBlock, true>(g, b, u, 0, b.xch ? SA_UNPACK : SA_SUM,
+                                                         kLds || ME_SOLVE_IMG ? b.Abuf : nullptr, &o,
+                                                         b.asm_claim + u, asm_gen);
     drain_and_barrier();  // every wave's written-through stores have left
 #ifdef ME_SOLVE_TS
     if (threadIdx.x == 0) atomicMax(&g_asm_last, (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mine && threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   State* st = b.st;
@@ -1586,6 +1637,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     for (int k = 0; k < 6; ++k) urow[k] = Ur[k];
     gcr = b.gcs[threadIdx.x];
   }
+  __shared__ int s_steal;
   if (fused) {
     lin_finalize_body(g, b, o, gc_raw, red);
     STS(1);
@@ -1593,15 +1645,47 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       const int live = !st->done;
       // (what s_assemble's first block writes in the unfused form; read by decide)
       b.scal[R_COUNT] = (st->fail || (b.xch && b.xch[xo_fail(g)] != 0.0)) ? 1.0 : 0.0;
-      long k = (skip & 512) ? kSolveSpin : 0;  // (512: test hook, a forced timeout on this ctx)
+      // the assemblers' units: wait kCloseTicks for them, then claim and do
+      // every unit still unclaimed here (normally none)
+      s_steal = 0;
       if (live) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        const long long lim = (skip & kSkipRosterNow) ? 0 : me_roster::kCloseTicks;
+        while (__hip_atomic_load(asm_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nasm) {
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 >= lim) {
+            s_steal = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+    }
+    __syncthreads();
+    if (s_steal) {
+      for (int u = 0; u < nasm; ++u) {
+        if (__hip_atomic_load(b.asm_claim + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= asm_gen) continue;
+        const bool mine = s_assemble_body<kSolveBlock, true>(g, b, u, 0, b.xch ? SA_UNPACK : SA_SUM,
+                                                             kLds || ME_SOLVE_IMG ? b.Abuf : nullptr, &o,
+                                                             b.asm_claim + u, asm_gen);
+        drain_and_barrier();
+        if (mine && threadIdx.x == 0) __hip_atomic_fetch_add(asm_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (threadIdx.x == 0) {
+      const int live = !st->done;
+      long k = (skip & 512) ? kSolveSpin : 0;  // (512: test hook, a forced timeout on this ctx)
+      if (live && (s_steal || k)) {  // (all counted in the first wait: nothing left to wait for)
         for (; k < kSolveSpin; ++k) {
           if (__hip_atomic_load(asm_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (unsigned)nasm) break;
           __builtin_amdgcn_s_sleep(1);
         }
+      }
+      if (live) {
         if (k == kSolveSpin) {
-          // a missing assembler: the solve ends in error (a late one may still
-          // arrive, so the counter is not re-armed: the next plan clears it)
+          // a unit never counted (not reachable: every claimed unit's owner is
+          // running; kept as a safety net and for the test hook): the solve ends
+          // in error (a late count may still come, so the counter is not
+          // re-armed: the next plan clears it)
           spin_timeout(b);
         } else {
           __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
@@ -1718,10 +1802,17 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     }
   }
   if (done) return;
+  // trailing-update workers: close their roster (roster.hpp; at once when the
+  // solve fails here anyway) -- the tiles are dealt over those that joined,
+  // none of them: block 0 updates them itself (the phased loop)
+  __shared__ int s_nwk;
   if (tid == 0) {
     sfail = fail_in;
     pflag = 0u;
     pdone = 0u;
+    if (kMode == 2 && nworkers > 0)
+      s_nwk = (int)me_roster::close<me_roster_dev>(b.roster, (unsigned)nworkers,
+                                                   fail_in || (skip & kSkipRosterNow) ? 0 : me_roster::kCloseTicks);
   }
   if ((skip & 256) && tid == 0) st->stamps[15] += 1;
   SOLVE_START(0);
@@ -1801,7 +1892,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       __syncthreads();
     }
-  } else if (kMode == 2 && nworkers > 0) {
+  } else if (kMode == 2 && nworkers > 0 && s_nwk > 0) {
     // Global-memory form with trailing workers (config 5), pipelined like the
     // LDS form: per block step J, wave 0 applies step J - 1 to the diagonal
     // tile (J, J) in registers (the workers left it out) and factors it, while
@@ -1843,7 +1934,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         if (!ok) sfail = 1;  // benign race: every writer stores 1
         STS(16);
       } else if (tid == 64 && J > 0 && J + 1 < Ts) {
-        const unsigned want = (unsigned)nworkers * (unsigned)J;
+        const unsigned want = (unsigned)s_nwk * (unsigned)J;
         long k = 0;
         for (; k < kSolveSpin; ++k) {
           if (__hip_atomic_load(b.ssync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= want) break;
@@ -2235,6 +2326,9 @@ template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
   const State* st = b.st;
+  // the camera solve's roster, re-armed for the next iteration's solve (every
+  // workgroup of the solve launch, late joiners included, has finished)
+  if (blockIdx.x == 0 && threadIdx.x < 2) b.roster[threadIdx.x] = 0u;
   if (st->done) return;
   const int gl = threadIdx.x & (kStepG - 1);
   const int j = blockIdx.x * kStepPts + (threadIdx.x / kStepG);
@@ -2856,6 +2950,7 @@ __global__ __launch_bounds__(kBlock) void output_kernel(Geo g, Bufs b, double* c
 struct Plan {
   me_ctx* c = nullptr;
   Geo g;
+  unsigned asm_gen = 0;  // fused-assembly launches since the plan cleared the claim words
   Bufs b;
   Opts o;
   double* colnorm = nullptr;
@@ -3074,7 +3169,8 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(8 * (size_t)g.n6, &P.gc_raw);
   add(8 * 21 * (size_t)std::max(g.m, 1), &P.Uraw);
   add(8 * 27 * (size_t)std::max(g.m, 1) * g.ck, &P.cpart);
-  add(4 * (size_t)(g.m + 1 + 3), &b.cnt);  // counters: per camera (cam_assemble) | pt_step | solve sync (2) | fused assembly
+  add(4 * (size_t)(g.m + 1 + 3 + 2), &b.cnt);  // counters: per camera (cam_assemble) | pt_step | solve sync (2) | fused assembly | roster (2)
+  add(4 * (size_t)blocks((long)g.npairs * 256, kSolveBlock / kSaGroups), &b.asm_claim);  // (cleared with cnt)
   const size_t work_bytes = 4 * (2 * (size_t)g.np + (size_t)g.nblk_obs * g.nc + 4);
   add(work_bytes, &b.work);
   const size_t out_doubles = sizeof(State) / 8 + 6 * (size_t)g.nc + 3 * (size_t)g.np;
@@ -3094,6 +3190,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
     ptr += it.first;
   }
   b.ssync = b.cnt + g.m + 1;
+  b.roster = b.cnt + g.m + 4;
   b.bvec = b.S + (size_t)g.n6 * g.n6;
   b.diagU = b.bvec + g.n6;
   void* hp;
@@ -3137,6 +3234,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   }
   // cnt | work are adjacent in the arena: one fill clears both
   ME_HIP(c, hipMemsetAsync(b.cnt, 0, (size_t)((char*)b.work - (char*)b.cnt) + work_bytes, s));
+  P.asm_gen = 0;  // (the claim words were just cleared)
   const double* cams_in = dev ? p->cams : b.cams[0];
   const double* pts_in = dev ? p->pts : b.pts[0];
   const long nthr = std::max({(long)g.nblk_obs * kBlock, (long)g.np, 6L * g.nc, 3L * g.np});
@@ -3172,11 +3270,11 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
       ME_HIP(c, hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSchurLdsCap));
     c->ba_lds_attr = 1;
   }
-  // the multi-workgroup camera solve needs block 0 and every worker resident
-  // at once: the workers it may use are capped by the co-resident count on
-  // the ctx's CUs; a hand-off that still times out is an error
-  // (queried for every global-memory solve: an explicit worker count is
-  // clamped by it too)
+  // the multi-workgroup camera solve deals its tiles over the workers that
+  // joined its roster (roster.hpp), so residency is never assumed; the
+  // workers launched are still capped by what fits on the ctx's CUs (more
+  // could only join late and leave), and an explicit worker count is clamped
+  // by it too
   if (!P.use_lds) {
     int per_cu = 0;
     ME_HIP(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cam_solve_kernel<2>, kSolveBlock, P.solve_lds));
@@ -3352,15 +3450,16 @@ int enqueue_iteration(Plan& P, bool last = false) {
     me_ktimer t(c, ME_KT_BA_SOLVE);
     const double* gc = P.gc_raw;
     const int sk = P.diag_skip | (img ? kSkipImg : 0);
+    const unsigned gen = nasm > 0 ? ++P.asm_gen : 0u;  // fused assembly: this launch's claim generation
     if (P.use_lds)
       hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
-                         nasm, gc);
+                         nasm, gc, gen);
     else if (nwk > 0)
       hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, nwk,
-                         0, gc);
+                         0, gc, gen);
     else
       hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
-                         nasm, gc);
+                         nasm, gc, gen);
   }
   {
     me_ktimer t(c, ME_KT_BA_STEP);

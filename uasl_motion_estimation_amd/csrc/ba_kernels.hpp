@@ -130,6 +130,8 @@ struct Bufs {
   int* work;          // plan build: cnt_p[np] | fill_p[np] | blk_cam[nblk_obs*nc] | flags[4] (zeroed)
   unsigned* cnt;      // last-arrival counters: m (cam_assemble, per camera) + 1 (pt_step); re-armed by the last
   unsigned* ssync;    // camera solve, global-memory form: {step epoch, worker step count} (zeroed by s_assemble)
+  unsigned* roster;   // camera solve: the trailing workers' roster (roster.hpp; 2 words, re-zeroed by pt_step)
+  unsigned* asm_claim;  // fused assembly: per unit, the generation of the launch whose workgroup claimed it
   double* out;        // State | cams[cur] | pts[cur] for the single read-back
   double* xch;        // sharded only (else null): the packed per-iteration exchange, see xo_* below
 };

