@@ -252,6 +252,7 @@ def load_library(path: str | None = None):
         "me_scale_optimise": (c_int, [c_void_p, P(ScaleStateC), P(OptimParamsC), c_int, P(c_int), P(c_int),
                                       P(c_double), c_int, P(c_long)]),
         "me_scale_last_counters": (c_int, [c_void_p, P(c_long), P(c_long), P(c_long), P(c_long)]),
+        "me_scale_persistent": (c_int, [c_int, c_int]),
         "me_scale_state_mi": (c_int, [c_void_p, P(ScaleStateC), P(c_double), P(c_int)]),
         "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
         "me_ba_default_options": (None, [P(BAOptionsC)]),
