@@ -3455,8 +3455,18 @@ int enqueue_iteration(Plan& P, bool last = false) {
       hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
                          nasm, gc, gen);
     else if (nwk > 0)
+#ifdef ME_COOP_LAUNCH  // measurement build only (tools/coop_ab.sh): the worker grid as a cooperative launch
+    {
+      int skv = sk, nwv = nwk, z = 0;
+      unsigned gv = gen;
+      void* args[] = {(void*)&g, (void*)&P.b, (void*)&P.o, &skv, &nwv, &z, (void*)&gc, &gv};
+      ME_HIP(c, hipLaunchCooperativeKernel((const void*)cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), args,
+                                           (unsigned)P.solve_lds, s));
+    }
+#else
       hipLaunchKernelGGL(cam_solve_kernel<2>, dim3(1 + nwk), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, nwk,
                          0, gc, gen);
+#endif
     else
       hipLaunchKernelGGL(cam_solve_kernel<1>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
                          nasm, gc, gen);

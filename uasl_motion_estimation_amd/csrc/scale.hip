@@ -1638,9 +1638,23 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     {
       me_ktimer t(c, ME_KT_SCALE_RES);
       const int max_phases = 256 * (p.max_nb_iter + 2);
+#ifdef ME_COOP_LAUNCH  // measurement build only (tools/coop_ab.sh): the same grid as a cooperative launch
+      {
+        const ScaleArgs* a0 = P.dargs;
+        const ScaleArgs* a1 = P.dargs + 1;
+        const TrackDev* td = P.dtd;
+        double* rs = P.res;
+        int rp = P.rows_pad;
+        unsigned *cnt = P.bar, *ep = P.bar + kEpochWord, *ro = P.bar + kRosterWord;
+        int mp = max_phases, nbv = nb;
+        void* args[] = {&a0, &a1, &td, &rs, &rp, &P.jj, &P.je, &P.err, &P.lm, &P.spec, &lp, &cnt, &ep, &ro, &nbv, &mp};
+        ME_HIP(c, hipLaunchCooperativeKernel((const void*)scale_lm_kernel, dim3(nb * kCandY), dim3(kScBlock), args, 0, st));
+      }
+#else
       hipLaunchKernelGGL(scale_lm_kernel, dim3(nb * kCandY), dim3(kScBlock), 0, st, P.dargs, P.dargs + 1, P.dtd,
                          P.res, P.rows_pad, P.jj, P.je, P.err, P.lm, P.spec, lp, P.bar, P.bar + kEpochWord,
                          P.bar + kRosterWord, nb, max_phases);
+#endif
     }
     if (int rc = me_check_launch(c, "scale_lm_kernel")) return drain(rc);
     ME_HIP(c, hipEventRecord(c->poll_ev[0], st));
