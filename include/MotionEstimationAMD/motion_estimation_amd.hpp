@@ -795,7 +795,7 @@ class WindowedStereoVO {
     Config() { me_vo_loop_default_config(this); }
   };
   WindowedStereoVO(amd::Context& ba, amd::Context& front, const Config& cfg, int frontCus = 4)
-      : ba_(ba), front_(front) {
+      : ba_(ba), front_(front), width_(cfg.width), height_(cfg.height) {
     if (&ba != &front && frontCus > 0 && frontCus < 16) {
       const int ncu = ba.cuCount();
       std::vector<int> f, b;
@@ -805,7 +805,15 @@ class WindowedStereoVO {
       masked_ = true;
     }
     me_vo_loop* v = nullptr;
-    ba.check(me_vo_loop_create(ba.get(), front.get(), &cfg, &v), "me_vo_loop_create");
+    try {
+      ba.check(me_vo_loop_create(ba.get(), front.get(), &cfg, &v), "me_vo_loop_create");
+    } catch (...) {  // no destructor runs: give the caller's contexts their CUs back
+      if (masked_) {
+        front.setCuMask({});
+        ba.setCuMask({});
+      }
+      throw;
+    }
     v_.reset(v);
   }
   ~WindowedStereoVO() {
@@ -817,14 +825,19 @@ class WindowedStereoVO {
   }
   WindowedStereoVO(const WindowedStereoVO&) = delete;
   WindowedStereoVO& operator=(const WindowedStereoVO&) = delete;
-  // keyframe t (0, 1, 2, ...): host images, copied in
+  // keyframe t (0, 1, 2, ...): host images of the configured size, copied in
   void process(int t, const amd::ImageView& left, const amd::ImageView& right) {
     if (left.empty() || right.empty() || left.step != left.cols || right.step != right.cols)
       throw std::invalid_argument("WindowedStereoVO::process: dense 8-bit images expected");
+    if (left.rows != height_ || left.cols != width_ || right.rows != height_ || right.cols != width_)
+      throw std::invalid_argument("WindowedStereoVO::process: images of the configured width x height expected");
     check(me_vo_loop_process(v_.get(), t, left.data, right.data, ME_HOST), "WindowedStereoVO::process");
   }
-  // keyframe t from device memory (alive until process(t + 1) returns)
+  // keyframe t from device memory: dense width x height bytes each, written
+  // before the call in stream order with the loop (or synchronised by the
+  // caller), alive until process(t + 1) returns
   void processDevice(int t, const uint8_t* left, const uint8_t* right) {
+    if (!left || !right) throw std::invalid_argument("WindowedStereoVO::processDevice: null image");
     check(me_vo_loop_process(v_.get(), t, left, right, ME_DEVICE), "WindowedStereoVO::processDevice");
   }
   void finish() { check(me_vo_loop_finish(v_.get()), "WindowedStereoVO::finish"); }
@@ -874,6 +887,7 @@ class WindowedStereoVO {
   };
   amd::Context& ba_;
   amd::Context& front_;
+  int width_, height_;
   bool masked_ = false;
   std::unique_ptr<me_vo_loop, Del> v_;
 };

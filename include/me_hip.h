@@ -390,7 +390,7 @@ int me_vo_window_submit(me_ctx* ctx, const me_vo_window* w, me_ba_problem* p, co
  * keyframe t is matched and booked.  Two contexts of one device: `ba` runs the
  * window solves, `front` the KLT, the matchers and the scale LM (they may be
  * the same ctx: then nothing runs on a worker thread).  Results are the
- * Python loop's bit for bit (tests/test_vo_loop.py).  One loop per pair of
+ * Python loop's bit for bit (tests/test_pipeline.py (test_native_loop_*, test_cpp_host_drives_the_loop)).  One loop per pair of
  * contexts; no other call on either ctx while a loop call runs. */
 typedef struct {
   int width, height, n_feats, window;

@@ -2,7 +2,7 @@
 // through me::WindowedStereoVO (include/MotionEstimationAMD/
 // motion_estimation_amd.hpp over the C ABI): the loop the reference's
 // application would run, with no Python in the process.  Used by
-// tests/test_vo_loop.py.
+// tests/test_pipeline.py (test_native_loop_*, test_cpp_host_drives_the_loop).
 //   vo_loop_cli <in.bin> <out.bin> [front_cus]
 // in.bin : int32 {width, height, n_feats, window, ba_iters, scale_iters, fixed_frames, d_min, d_max, n_frames,
 //          has_velocity}, float64 {baseline, feat_var, K[9], first_pose[6], velocity[6]},

@@ -218,8 +218,9 @@ def test_native_loop_shared_context_and_device_images(ctx, seq5):
     a = _native(ctx, 16, 8, seq5)
     b = _native(ctx, 16, 8, seq5, overlap=False)
     fr = seq5[0]
+    # (no torch.cuda.synchronize(): process() orders the loop's streams after
+    # the producing torch stream itself)
     dev = [_DevFrame(torch.from_numpy(fr[t].left).cuda(), torch.from_numpy(fr[t].right).cuda()) for t in range(16)]
-    torch.cuda.synchronize()
     c = _native(ctx, 16, 8, (dev,) + tuple(seq5[1:]))
     try:
         ea = a.event_records()
@@ -233,6 +234,35 @@ def test_native_loop_shared_context_and_device_images(ctx, seq5):
     finally:
         for o in (a, b, c):
             o.close()
+
+
+@pytest.mark.gpu
+def test_native_loop_rejects_images_that_do_not_match_the_config(ctx, seq5):
+    """the native loop copies width x height bytes from the
+    caller's pointer, so NativeStereoVO.process checks dtype, shape,
+    contiguity and device first and raises; the loop is untouched by a
+    rejected call and the next correct keyframe goes through."""
+    import torch
+
+    fr, K, p0, v, truth = seq5
+    cfg = PL.PipelineConfig.from_config(5, ba_iters=10)
+    cfg.window = 8
+    vo = PL.NativeStereoVO(cfg, ctx, K, p0, v)
+    try:
+        L, R = fr[0].left, fr[0].right
+        bad = [(L[:-1], R), (L, R[:, :-1]), (L.astype(np.float32), R), (L, R.T)]
+        for a, b in bad:
+            with pytest.raises(ValueError):
+                vo.process(0, a, b)
+        dL, dR = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
+        strided = torch.zeros((L.shape[0], 2 * L.shape[1]), dtype=torch.uint8, device=dL.device)[:, ::2]
+        for a, b in [(dL[:-1], dR), (dL.float(), dR), (dL.t(), dR), (dL, dR.cpu()), (strided, dR)]:
+            with pytest.raises(ValueError):
+                vo.process(0, a, b)
+        vo.process(0, L, R)
+        vo.process(1, dL, dR)
+    finally:
+        vo.close()
 
 
 def _write_cli_input(path, frames, n, window):

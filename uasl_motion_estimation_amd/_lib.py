@@ -155,7 +155,7 @@ EXPORTS = [
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
-    "me_scale_optimise", "me_scale_last_counters", "me_scale_state_mi", "me_scale_inliers",
+    "me_scale_optimise", "me_scale_last_counters", "me_scale_persistent", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
     "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_wait_out", "me_ba_reserve", "me_ba_window_indices",
     "me_vo_ba_chain", "me_vo_window_submit",

@@ -40,8 +40,8 @@ struct me_ctx {
   int rand_f = 3, rand_r = 0;
   bool rand_init = false;
   long long dbg[16] = {0};  // diagnostics (last BA solve phase stamps)
-  int dbg_solve_flags = 0;
-  unsigned dbg_solve_count = 0;  // (solves queued since the hook was set; reset by it)   // test hook (me_debug_solve_flags): OR-ed into the camera solve's diagnostic flags
+  int dbg_solve_flags = 0;        // test hook (me_debug_solve_flags): OR-ed into the camera solve's diagnostic flags
+  unsigned dbg_solve_count = 0;  // solves queued since the hook was set (reset by it)
   // asynchronous BA solve in flight (me_ba_solve_async / me_ba_wait, ba.hip):
   // its own pinned staging, so later calls on the ctx cannot overwrite it
   void* ba_async = nullptr;

@@ -475,10 +475,6 @@ __device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restric
   }
 }
 
-__device__ __forceinline__ uint32_t lds_u8(const uint32_t* word, int byte) {
-  return (uint32_t)reinterpret_cast<const uint8_t*>(word)[byte];
-}
-
 template <int PW, int PH, bool EPI = false>
 __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                              const uint8_t* __restrict__ imgR, int strideR,

@@ -57,7 +57,11 @@ class Worker {
   }
   long submit(std::function<int()> f) {
     if (!th_.joinable()) th_ = std::thread([this] { run(); });
-    std::lock_guard<std::mutex> lk(m_);
+    std::unique_lock<std::mutex> lk(m_);
+    // one job at a time: a job still pending or running is finished first
+    // (its result code stays for the next wait), so queued_ never runs ahead
+    // of a job that would be overwritten
+    cv_.wait(lk, [&] { return done_ >= queued_; });
     job_ = std::move(f);
     has_ = true;
     ++queued_;
@@ -252,6 +256,7 @@ struct me_vo_loop {
   std::vector<double> sc_trace = std::vector<double>(800);
   bool scale_queued = false;
   long scale_seq = 0;
+  bool failed = false;  // a process() call returned an error: later calls are refused
   Worker scale_worker, ba_worker;
   // ---- results / events / stats
   std::vector<me_vo_frame_result> results;
@@ -295,9 +300,26 @@ struct me_vo_loop {
     if (rc_ != ME_OK) return fail(rc_, (what)); \
   } while (0)
 
+  // Joins the worker threads before a buffer grows: the growth path
+  // synchronises, frees and allocates on both contexts, which a worker may be
+  // using (a ctx takes one call at a time).  reserve() sizes every
+  // buffer for the configuration, so this is not expected after it.
+  int quiesce() {
+    if (scale_queued) {
+      scale_queued = false;
+      VL_TRY(scale_worker.wait(scale_seq), "me_scale_optimise");
+    }
+    if (enq_seq) {
+      const long q = enq_seq;
+      enq_seq = 0;
+      VL_TRY(ba_worker.wait(q), "window submit");
+    }
+    return ME_OK;
+  }
   int dbuf(const char* name, size_t nbytes, void** out) {
     Buf& b = dev[name];
     if (b.p == nullptr || b.n < nbytes) {
+      VL_TRY(quiesce(), "grow");
       if (b.p) {
         VL_TRY(me_synchronize(tctx), "sync");
         VL_TRY(me_synchronize(ctx), "sync");
@@ -314,6 +336,7 @@ struct me_vo_loop {
   int hbuf(const char* name, size_t nbytes, void** out) {
     Buf& b = pin[name];
     if (b.p == nullptr || b.n < nbytes) {
+      VL_TRY(quiesce(), "grow");
       if (b.p) {
         VL_TRY(me_synchronize(tctx), "sync");
         VL_TRY(me_synchronize(ctx), "sync");
@@ -575,6 +598,10 @@ struct me_vo_loop {
 
   // ---- scale LM (Optimiser<ScaleState,...>::optimise over the tracks seen in t, images of t)
   int scale_submit(int t, const std::vector<int64_t>& tids) {
+    if (scale_queued) {  // a scale job left queued by an earlier error return: it reads sc_s / sc_X
+      scale_queued = false;
+      VL_TRY(scale_worker.wait(scale_seq), "me_scale_optimise");
+    }
     const size_t n = tids.size();
     const Pose& pose = poses[t];
     const Mat3 R = aa_to_R(&pose[3]);
@@ -1242,8 +1269,14 @@ int me_vo_loop_process(me_vo_loop* v, int t, const uint8_t* left, const uint8_t*
     v->err = "me_vo_loop_process: keyframes must come in order 0, 1, 2, ...";
     return ME_ERR_STATE;
   }
+  if (v->failed) {
+    v->err = "me_vo_loop_process: an earlier call failed (" + v->err + "); the loop state is undefined";
+    return ME_ERR_STATE;
+  }
   me_range range_("me_vo_loop_process");
-  return v->process(t, left, right, mem);
+  const int rc = v->process(t, left, right, mem);
+  if (rc != ME_OK) v->failed = true;  // the loop may have stopped half-way through a keyframe
+  return rc;
 }
 
 int me_vo_loop_finish(me_vo_loop* v) {

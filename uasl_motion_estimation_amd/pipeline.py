@@ -1391,7 +1391,7 @@ class NativeStereoVO:
     every step in native code behind the C ABI (me_vo_loop_*, csrc/vo_loop.hip):
     the Python layer only hands images in and reads results out.  Same
     decisions, events, results and poses as WindowedStereoVO(GPUBackend)
-    (tests/test_vo_loop.py).  Two contexts of the device as GPUBackend sets
+    (tests/test_pipeline.py, test_native_loop_*).  Two contexts of the device as GPUBackend sets
     them up: `ctx` runs the window solves, `tctx` (front_cus of every 16 CUs,
     whole XCDs) the KLT, the matchers and the scale LM; overlap=False runs
     everything on `ctx` (no worker threads).  Images: numpy (copied in) or
@@ -1451,14 +1451,34 @@ class NativeStereoVO:
 
         from ._lib import ME_DEVICE, ME_HOST
 
+        shape = (self.cfg.height, self.cfg.width)
         if hasattr(left, "data_ptr"):
+            import torch
+
+            for name, im in (("left", left), ("right", right)):
+                if not (isinstance(im, torch.Tensor) and im.dtype == torch.uint8 and tuple(im.shape) == shape
+                        and im.is_contiguous() and im.is_cuda and im.device.index == self.ctx.device):
+                    raise ValueError(f"NativeStereoVO.process: {name} must be a contiguous uint8 tensor of shape "
+                                     f"{shape} on cuda:{self.ctx.device}, got "
+                                     f"{getattr(im, 'dtype', None)} {tuple(getattr(im, 'shape', ()))} "
+                                     f"on {getattr(im, 'device', None)}")
+            # the loop reads the images on its own streams: order them after
+            # the torch stream that produced them (no host wait)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(left.device))
+            for sp in {self.ctx.stream_ptr(), self.tctx.stream_ptr()}:
+                torch.cuda.ExternalStream(sp, device=left.device).wait_event(ev)
             self._keep[t] = (left, right)
             self._keep.pop(t - 2, None)
             rc = self.lib.me_vo_loop_process(self.h, t, ctypes.c_void_p(left.data_ptr()),
                                              ctypes.c_void_p(right.data_ptr()), ME_DEVICE)
         else:
-            L = np.ascontiguousarray(left, np.uint8)
-            R = np.ascontiguousarray(right, np.uint8)
+            L, R = np.asarray(left), np.asarray(right)
+            for name, im in (("left", L), ("right", R)):
+                if im.dtype != np.uint8 or im.shape != shape:
+                    raise ValueError(f"NativeStereoVO.process: {name} must be a uint8 array of shape {shape}, "
+                                     f"got {im.dtype} {im.shape}")
+            L, R = np.ascontiguousarray(L), np.ascontiguousarray(R)
             rc = self.lib.me_vo_loop_process(self.h, t, L.ctypes.data, R.ctypes.data, ME_HOST)
         self._check(rc, "me_vo_loop_process")
 
