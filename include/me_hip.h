@@ -103,6 +103,12 @@ int me_timing_reset(me_ctx* ctx);
    the default): a live measurement of the average launch duration whose
    event records perturb the stream k times less. */
 int me_timing_sample(me_ctx* ctx, int every);
+/* Measured HBM bandwidth of this device (GB/s, read + write bytes / time):
+   a 16-byte-per-lane streaming copy of `bytes` bytes, `reps` timed launches
+   on the ctx stream (after one untimed) -- the measured denominator beside
+   the 8 TB/s datasheet peak in bench.py's roofline objects.  Allocates and
+   frees 2 x bytes of device memory; synchronises the ctx stream. */
+int me_hbm_copy_gbs(me_ctx* ctx, size_t bytes, int reps, double* gbs);
 
 /* ---- A1/A2: mutual information ---------------------------------------
  * Replaces float me::computeMutualInformation(const cv::Mat&, const cv::Mat&)
@@ -483,7 +489,13 @@ int me_ba_covariance(me_ctx* ctx, const me_ba_problem* p, double* cov /* n_cams*
  *  - me_comm_create_callback: a caller all-reduce (allreduce(dev_ptr, n, user)
  *    sums n doubles in place over the ranks, n < 0: max over |n|; it must be
  *    ordered on the ctx stream, e.g. host-staged gloo, or threads driving
- *    several contexts of one GPU).
+ *    several contexts of one GPU).  Collective like the RCCL form: every
+ *    rank creates its communicator concurrently.
+ * Both creators calibrate the communicator (me_comm_calibrate): a few
+ * all-reduces at the two exchange sizes of a sharded LM iteration, timed on
+ * this rank, then the max over the ranks (one more exchange), so every rank
+ * holds the same per-exchange costs and the landmark-count gate takes the
+ * same decision everywhere (me_ba_shard_worthwhile_comm).
  * Per LM iteration the sharded solve exchanges twice: one sum of the packed
  * reduced camera system [S upper block triangle | b | diag(U) | camera
  * gradient | cost | failure count | per-rank gradient max-norm slots] after
@@ -502,6 +514,20 @@ void me_comm_destroy(me_comm* comm);
 int me_comm_info(const me_comm* comm, int* world, int* rank, int* native);
 /* In-place all-reduce of n doubles of device memory on the ctx stream. */
 int me_comm_allreduce(me_comm* comm, double* dev_buf, long n, int op);
+/* Re-measures the communicator's exchange costs (collective: every rank
+   calls it): `reps` timed all-reduces (after 3 untimed) of ME_COMM_CAL_SYSTEM
+   doubles -- the packed reduced camera system of a 30-keyframe window -- and
+   of 5 doubles (the step scalars), wall time per call including the stream
+   synchronisation, max over the ranks.  The creators run it with reps = 10. */
+#define ME_COMM_CAL_SYSTEM 17000
+int me_comm_calibrate(me_comm* comm, int reps);
+/* The calibrated costs (microseconds per exchange) of the system and the
+   scalar exchange; 0 before any calibration. */
+int me_comm_exchange_us(const me_comm* comm, double* system_us, double* scalars_us);
+/* The gate below with this communicator's world and calibrated costs
+   (xch_us = the mean of the two, so 2 * xch_us is one LM iteration's
+   exchanges); uncalibrated: the built-in estimate.  Host only. */
+int me_ba_shard_worthwhile_comm(const me_comm* comm, long n_obs);
 int me_ba_solve_comm(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, me_comm* comm, me_ba_summary* s);
 /* The same with a bare callback and no rank information (ABI v2 form): the
    gradient max-norm then travels in a separate max all-reduce. */
@@ -516,7 +542,8 @@ int me_ba_solve_sharded(me_ctx* ctx, me_ba_problem* p, const me_ba_options* o, m
    bench.py's sharded_ba.crossover_model); returns 1 when
    t(n_obs) - t(ceil(n_obs / world)) > 2 * xch_us, else 0 (world <= 1: 0).
    xch_us <= 0 takes the built-in per-exchange estimate for `world`
-   (me_ba_shard_exchange_us).  Host only: no device, no ctx. */
+   (me_ba_shard_exchange_us, a fallback only: a communicator measures its
+   own, me_comm_exchange_us).  Host only: no device, no ctx. */
 #define ME_SHARD_OBS_NS 1.0
 #define ME_SHARD_FLOOR_US 40.0
 int me_ba_shard_worthwhile(long n_obs, int world, double xch_us);

@@ -323,12 +323,63 @@ def test_gpu_comm_allreduce_native_and_callback(ctx):
         assert np.array_equal(x, y)  # one rank: identity
         seen = []
         cb = Comm.callback(ctx, 3, 1, lambda ptr, n: seen.append((ptr, n)))
+        # creation calibrates: (3 untimed + 10 timed) sums of each exchange size, then one max of the two costs
+        sizes = [n for _, n in seen]
+        assert sizes == [17000] * 13 + [5] * 13 + [-2], sizes
+        assert cb.exchange_us()["system"] > 0 and cb.exchange_us()["scalars"] > 0
+        seen.clear()
         cb.allreduce(d, 7)
         cb.allreduce(d, 5, "max")
         assert seen == [(d, 7), (d, -5)] and cb.info() == {"world": 3, "rank": 1, "native": False}
         cb.close()
     finally:
         ctx.free(d)
+
+
+@pytest.mark.gpu
+def test_gpu_comm_calibration_feeds_the_gate():
+    """two ranks (two contexts of one GPU, threads, a
+    host-staged exchange) create their communicators concurrently; each
+    measures its exchanges at creation and takes the max over the ranks, so
+    both hold the same costs, and me_ba_shard_worthwhile_comm decides with
+    them (equal to the host gate at their mean) -- the same on both ranks."""
+    import threading
+
+    from uasl_motion_estimation_amd._lib import Context
+    from uasl_motion_estimation_amd.optimisation import Comm, ThreadAllReduce, shard_worthwhile
+
+    world = 2
+    ar = ThreadAllReduce(world)
+    ctxs = [Context(0) for _ in range(world)]
+    comms, errs = [None] * world, []
+
+    def mk(r):
+        try:
+            comms[r] = Comm.callback(ctxs[r], world, r, ar.callback(r, ctxs[r]))
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+            ar.barrier.abort()
+
+    th = [threading.Thread(target=mk, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    try:
+        assert not errs, errs
+        cal = [c.exchange_us() for c in comms]
+        assert cal[0] == cal[1] and cal[0]["system"] > 0 and cal[0]["scalars"] > 0
+        x = 0.5 * (cal[0]["system"] + cal[0]["scalars"])
+        for n in (19012, 100010, 134053, 10 ** 6, 10 ** 8):
+            want = shard_worthwhile(n, world, x)
+            assert comms[0].shard_worthwhile(n) == comms[1].shard_worthwhile(n) == want, n
+        assert comms[0].shard_worthwhile(10 ** 8)  # a window big enough always pays
+    finally:
+        for c in comms:
+            if c is not None:
+                c.close()
+        for c in ctxs:
+            c.close()
 
 
 @pytest.mark.gpu
@@ -459,3 +510,10 @@ def test_bench_world2_gloo_sharded_branch(tmp_path):
     assert sb["ranks"] == 2 and "gloo" in sb["mode"], sb
     assert sb["parity_vs_single_gpu"]["ok"], sb["parity_vs_single_gpu"]
     assert set(sb["exchange_us"]) == {"17000", "5"}
+    # the gate reads the communicator's own calibration
+    gi = sb["gate_inputs"]
+    cal = gi["calibrated_exchange_us"]
+    assert cal["system"] > 0 and cal["scalars"] > 0
+    assert gi["per_exchange_us"] == round(0.5 * (cal["system"] + cal["scalars"]), 2)
+    from uasl_motion_estimation_amd.optimisation import shard_worthwhile
+    assert sb["gate_would_shard"] == shard_worthwhile(100010, 2, 0.5 * (cal["system"] + cal["scalars"]))

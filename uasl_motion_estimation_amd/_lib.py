@@ -151,7 +151,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, POINTER(c_double), c_int, c_void_p)
 EXPORTS = [
     "me_abi_version", "me_range_push", "me_range_pop", "me_device_count", "me_create", "me_destroy", "me_last_error", "me_set_stream",
     "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_cu_count", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
-    "me_memcpy_async", "me_host_alloc", "me_host_free",
+    "me_memcpy_async", "me_host_alloc", "me_host_free", "me_hbm_copy_gbs",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
     "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
@@ -160,7 +160,7 @@ EXPORTS = [
     "me_ba_solve_sharded", "me_ba_covariance", "me_ba_solve_async", "me_ba_wait", "me_ba_wait_out", "me_ba_reserve", "me_ba_window_indices",
     "me_vo_ba_chain", "me_vo_window_submit",
     "me_comm_unique_id", "me_comm_create_rccl", "me_comm_create_callback", "me_comm_destroy", "me_comm_info",
-    "me_comm_allreduce", "me_ba_solve_comm", "me_ba_shard_worthwhile", "me_ba_shard_exchange_us",
+    "me_comm_allreduce", "me_comm_calibrate", "me_comm_exchange_us", "me_ba_shard_worthwhile_comm", "me_ba_solve_comm", "me_ba_shard_worthwhile", "me_ba_shard_exchange_us",
     "me_klt_default_params", "me_klt_track",
     "me_nms_scanline3x3",
     "me_vo_default_params", "me_vo_srand", "me_vo_rand", "me_vo_process",
@@ -228,6 +228,7 @@ def load_library(path: str | None = None):
         "me_timing_sample": (c_int, [c_void_p, c_int]),
         "me_timing_read": (c_int, [c_void_p, c_int, P(c_long), P(c_double)]),
         "me_timing_reset": (c_int, [c_void_p]),
+        "me_hbm_copy_gbs": (c_int, [c_void_p, c_size_t, c_int, P(c_double)]),
         "me_mi_scores": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
                                  c_void_p, c_int, c_int, c_int, c_void_p]),
         "me_mutual_information": (c_int, [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_int, c_int,
@@ -278,6 +279,9 @@ def load_library(path: str | None = None):
         "me_comm_destroy": (None, [c_void_p]),
         "me_comm_info": (c_int, [c_void_p, P(c_int), P(c_int), P(c_int)]),
         "me_comm_allreduce": (c_int, [c_void_p, c_void_p, c_long, c_int]),
+        "me_comm_calibrate": (c_int, [c_void_p, c_int]),
+        "me_comm_exchange_us": (c_int, [c_void_p, P(c_double), P(c_double)]),
+        "me_ba_shard_worthwhile_comm": (c_int, [c_void_p, c_long]),
         "me_ba_solve_comm": (c_int, [c_void_p, P(BAProblemC), P(BAOptionsC), c_void_p, P(BASummaryC)]),
         "me_ba_shard_worthwhile": (c_int, [c_long, c_int, c_double]),
         "me_ba_shard_exchange_us": (c_double, [c_int]),

@@ -64,6 +64,7 @@ struct me_comm {
   void* nccl = nullptr;            // ncclComm_t (native RCCL over xGMI)
   me_allreduce_fn ar = nullptr;    // else: caller all-reduce (host-staged)
   void* user = nullptr;
+  double xch_us[2] = {0.0, 0.0};   // calibrated us per exchange: packed system, step scalars (max over ranks)
 };
 // All-reduce of n doubles in place on the ctx stream (op ME_COMM_SUM / ME_COMM_MAX).
 int me_comm_allreduce_impl(me_comm* m, double* buf, long n, int op);

@@ -461,6 +461,24 @@ class Comm:
         self.ctx.check(self.ctx.lib.me_comm_info(self.h, byref(w), byref(r), byref(nat)), "me_comm_info")
         return dict(world=w.value, rank=r.value, native=bool(nat.value))
 
+    def exchange_us(self) -> dict:
+        """The communicator's calibrated exchange costs (me_comm_exchange_us:
+        measured at creation, max over the ranks), microseconds per all-reduce
+        of the packed camera system and of the step scalars."""
+        a, b = c_double(), c_double()
+        self.ctx.check(self.ctx.lib.me_comm_exchange_us(self.h, byref(a), byref(b)), "me_comm_exchange_us")
+        return {"system": a.value, "scalars": b.value}
+
+    def calibrate(self, reps: int = 10) -> dict:
+        """Re-measure the exchange costs (collective: every rank calls it)."""
+        self.ctx.check(self.ctx.lib.me_comm_calibrate(self.h, int(reps)), "me_comm_calibrate")
+        return self.exchange_us()
+
+    def shard_worthwhile(self, n_obs: int) -> bool:
+        """The landmark-count gate at this communicator's world and calibrated
+        costs (me_ba_shard_worthwhile_comm): the same answer on every rank."""
+        return bool(self.ctx.lib.me_ba_shard_worthwhile_comm(self.h, int(n_obs)))
+
     def allreduce(self, dev_ptr: int, n: int, op: str = "sum"):
         self.ctx.check(self.ctx.lib.me_comm_allreduce(self.h, ctypes.c_void_p(dev_ptr), int(n),
                                                       0 if op == "sum" else 1), "me_comm_allreduce")
@@ -741,6 +759,27 @@ def rccl_comm(ctx: Context, group=None, key: str = "me_rccl_uid") -> "Comm":
     return Comm.rccl(ctx, world, rank, uid)
 
 
+_GROUP_COMMS = {}
+
+
+def group_comm(ctx: Context, group=None) -> "Comm":
+    """The library communicator of a torch.distributed group on this ctx,
+    created (collectively, calibrated) on first use and kept: native RCCL for
+    the nccl backend, a host-staged callback for gloo."""
+    import torch.distributed as dist
+
+    key = (id(ctx), id(group))
+    comm = _GROUP_COMMS.get(key)
+    if comm is None or comm.ctx is not ctx:
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        if dist.get_backend(group) == "gloo":
+            comm = Comm.callback(ctx, world, rank, host_staged_allreduce(group))
+        else:
+            comm = rccl_comm(ctx, group)
+        _GROUP_COMMS[key] = comm
+    return comm
+
+
 def shard_worthwhile(n_obs: int, world: int, xch_us: float = 0.0) -> bool:
     """The landmark-count gate of the sharded solve (me_ba_shard_worthwhile,
     include/me_hip.h): True when splitting n_obs observations over `world`
@@ -763,9 +802,12 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     for the nccl backend (``comm``, or one created here), host-staged through
     the group for gloo, or the given ``allreduce(dev_ptr, n)`` callback.
 
-    ``shard``: "auto" applies the landmark-count gate (shard_worthwhile on
-    the window's observation count, the same decision on every rank) -- but
-    only when the caller passes neither ``comm`` nor ``allreduce``: an
+    ``shard``: "auto" applies the landmark-count gate (Comm.shard_worthwhile
+    on the window's observation count, priced at the exchange costs the
+    group's communicator measured when it was created -- the max over the
+    ranks, so the same decision on every rank; the communicator is created
+    once per group and kept, ``xch_us`` > 0 overrides the measurement) --
+    but only when the caller passes neither ``comm`` nor ``allreduce``: an
     explicit exchange means "shard" (a caller's communicator is
     never silently ignored).  Below the gate -- or with shard=False -- every
     rank solves the whole window on its own GPU (replicated, no collective;
@@ -780,13 +822,21 @@ def ba_solve_distributed(bp, options: SolverOptions | None = None, ctx: Context 
     ctx = ctx or default_context()
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     local, rng = shard_landmarks(bp, rank, world)
+    own = False
     if shard == "auto":
-        shard = comm is not None or allreduce is not None or shard_worthwhile(len(bp.obs), world, xch_us)
+        if comm is not None or allreduce is not None:
+            shard = True
+        elif xch_us > 0.0:
+            shard = shard_worthwhile(len(bp.obs), world, xch_us)
+        elif world <= 1:
+            shard = False
+        else:  # the group's calibrated communicator prices the exchanges
+            comm = group_comm(ctx, group)
+            shard = comm.shard_worthwhile(len(bp.obs))
     if not shard:
         cams, pts, summ = ba_solve(bp.copy(), options, ctx)
         summ = dict(summ, sharded=False)
         return cams, pts[rng[0]:rng[1]], rng, summ
-    own = False
     if comm is None:
         if allreduce is None and dist.get_backend(group) != "gloo":
             comm, own = rccl_comm(ctx, group), True
