@@ -56,9 +56,11 @@ def parse():
     ap.add_argument("--front-cus", type=int, default=8,
                     help="frontend overlap: the tracker context's stream runs on CUs i with i %% 16 < F and the "
                          "back-end stream on the others (me_set_cu_mask; whole XCDs per side, _lib.cu_split); 0: shared CUs")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="extra measurement: S independent VO streams per GPU (one context, HIP stream and host "
-                         "thread each), reported as multi_stream; the headline value stays one stream per GPU")
+    ap.add_argument("--streams", default="2,4",
+                    help="extra measurement: S independent replica streams per GPU (one context, HIP stream and "
+                         "host thread each, every stream's frames sequential), for each S of this comma list, "
+                         "reported as multi_stream; the headline value stays one pipelined stream per GPU "
+                         "(config 5's 8-GPU throughput story is replicas: this is its one-GPU part); '1': off")
     ap.add_argument("--sharded-ba", type=int, default=1,
                     help="config-4 landmark-sharded BA line (SURVEY 8e): over RCCL across the ranks when --gpus > 1, "
                          "two contexts on one GPU (host exchange, the crossover point) at N = 1; 0: off")
@@ -682,9 +684,10 @@ def crossover_model(ctx, opts, reps, xch_lb_us=None):
 
 def hbm_copy_gbs(ctx, nbytes: int = 1 << 30, reps: int = 20):
     """Measured HBM bandwidth of this GPU (read + write bytes / time): the
-    library's 16-byte-per-lane streaming copy of a 1 GiB buffer
-    (me_hbm_copy_gbs, the MI355X guide's float4-copy pattern, ~6.3 TB/s
-    there) -- the measured denominator beside the 8 TB/s datasheet peak
+    library's 16-byte-per-lane nontemporal streaming copy of a 1 GiB buffer
+    (me_hbm_copy_gbs, the best of tools/ubench_copy.hip's sweep, ~6.0 TB/s;
+    the MI355X guide quotes 6.29 TB/s for a float4 copy) -- the measured
+    denominator beside the 8 TB/s datasheet peak
     (SURVEY §8d).  (Round 5 used a torch uint8 copy_, 4.8-4.9 TB/s, which
     inflated every frac_vs_measured_copy by ~1.3x)"""
     g = ctypes.c_double()
@@ -1064,16 +1067,17 @@ def pipeline_line(args, ctx, cpu: bool, c: int, n: int, warm: int = 6, parity_pr
     return out
 
 
-def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
+def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier, S_):
     """S independent stereo streams on this GPU, each sequential (its own
     context = HIP stream + scratch, its own host thread; ctypes releases the
     GIL inside the library): whole-GPU throughput of small latency-bound
-    frames.  Returns frames/s over all streams and the per-stream rate."""
+    frames.  Returns frames/s over all streams and the per-stream rate.
+    Several persistent scale-LM grids and camera solves run at once here: the
+    cross-workgroup launches rely on no co-residency (csrc/roster.hpp)."""
     import threading
 
     from uasl_motion_estimation_amd._lib import Context
 
-    S_ = args.streams
     ctxs = [Context(local_rank) for _ in range(S_)]
     fr = []
     for k, c in enumerate(ctxs):
@@ -1108,7 +1112,8 @@ def multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier):
         raise errs[0]
     nfr = sum(st["frames"] for st in stats)
     return {"streams": S_, "frames": nfr, "value": round(nfr / el, 2), "unit": "frames/s",
-            "per_stream": round(nfr / el / S_, 2), "ba_iter_per_s": round(sum(st["ba_iters"] for st in stats) / el, 1)}
+            "per_stream": round(nfr / el / S_, 2), "ba_iter_per_s": round(sum(st["ba_iters"] for st in stats) / el, 1),
+            "frame": "sequential per stream (KLT, scale LM, BA on one context: no front-end / BA overlap)"}
 
 
 def main():
@@ -1307,7 +1312,8 @@ def main():
         if r_ is not None:
             r_["peak_measured_copy"] = copy_gbs
             r_["frac_vs_measured_copy"] = round(r_["achieved"] / copy_gbs, 5)
-    multi = multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier) if args.streams > 1 else None
+    multi = [multi_stream(args, cfg, seed, local_rank, kp, ba_opts, barrier, S_)
+             for S_ in sorted({int(x) for x in str(args.streams).split(",") if x.strip()}) if S_ > 1] or None
     pipe_line = pipe_c5 = None
     if args.pipeline_frames > 0 and rank == 0:
         cpu_leg = world == 1 and not args.no_cpu_baseline

@@ -1446,6 +1446,35 @@ class NativeStereoVO:
             msg = self.lib.me_vo_loop_last_error(self.h)
             raise MEError(rc, f"{what}: {msg.decode() if msg else ''}")
 
+    def _order_after_torch(self, device):
+        """The loop reads device images on its own streams: order those after
+        the torch stream that produced them, without a host wait.  A
+        CU-masked ctx stream is a blocking stream and already orders after
+        work on the legacy null stream; recording an event on the null
+        stream would also wait for every blocking stream's work -- the BA in
+        flight -- and serialise the pipeline, so from the null stream only
+        non-blocking loop streams get an event wait."""
+        import ctypes
+
+        import torch
+
+        cur = torch.cuda.current_stream(device)
+        waiters = []
+        for c in {self.ctx, self.tctx}:
+            sp = c.stream_ptr()
+            if cur.cuda_stream == 0:
+                fl = ctypes.c_uint()
+                c.check(c.lib.me_stream_flags(c.h, ctypes.byref(fl)), "me_stream_flags")
+                if fl.value == 0:  # blocking: ordered after the null stream already
+                    continue
+            if sp != cur.cuda_stream:
+                waiters.append(sp)
+        if waiters:
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            for sp in waiters:
+                torch.cuda.ExternalStream(sp, device=device).wait_event(ev)
+
     def process(self, t: int, left, right):
         import ctypes
 
@@ -1462,12 +1491,7 @@ class NativeStereoVO:
                                      f"{shape} on cuda:{self.ctx.device}, got "
                                      f"{getattr(im, 'dtype', None)} {tuple(getattr(im, 'shape', ()))} "
                                      f"on {getattr(im, 'device', None)}")
-            # the loop reads the images on its own streams: order them after
-            # the torch stream that produced them (no host wait)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(left.device))
-            for sp in {self.ctx.stream_ptr(), self.tctx.stream_ptr()}:
-                torch.cuda.ExternalStream(sp, device=left.device).wait_event(ev)
+            self._order_after_torch(left.device)
             self._keep[t] = (left, right)
             self._keep.pop(t - 2, None)
             rc = self.lib.me_vo_loop_process(self.h, t, ctypes.c_void_p(left.data_ptr()),
