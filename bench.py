@@ -439,7 +439,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MI_COUNTERS = "r05_e_mi_sq_counters"  # tools/mi_pmc.sh + tools/mi_counters.py of the current batch MI kernel
+MI_COUNTERS = "r05_e_mi_sq_counters"  # SQ counters of the current batch MI kernel (tools/gpu.sh sq)
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
@@ -478,7 +478,7 @@ FAMILY_KERNELS = {
 }
 
 
-# PMC traffic = 2 x FETCH_SIZE + WRITE_SIZE (tools/pmc_summary.py).  The MI355X
+# PMC traffic = 2 x FETCH_SIZE + WRITE_SIZE (tools/summarise.py pmc).  The MI355X
 # guide calibrates the x2 on FETCH_SIZE only for 16-byte-per-lane streaming
 # reads (and WRITE_SIZE for 16-byte streaming stores); none of these kernels
 # is such a stream (pt_schur_kernel: 8-byte double gathers of W / obs rows and
@@ -491,7 +491,7 @@ TRAFFIC_CALIBRATION = ("uncalibrated: 2 x FETCH_SIZE + WRITE_SIZE, the guide's c
 
 def pmc_traffic(family: str):
     """HBM bytes per family launch from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from separate
+    (profiles/*_pmc_traffic.json, written by tools/summarise.py pmc from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench); None if absent."""
     import glob
     import re
@@ -510,7 +510,7 @@ def pmc_traffic(family: str):
 def rocprof_avg_ms(family: str):
     """Average duration (ms) of the family's kernel in the newest committed
     headline-frame rocprofv3 summary (profiles/*_kernel_stats.txt written by
-    tools/prof_cycle.sh: the bench's config-3 frame without event timing), and
+    tools/gpu.sh prof: the bench's config-3 frame without event timing), and
     that file's name; (None, None) if absent.  The live HIP-event average
     brackets each sampled launch with two event packets on the BA stream, so
     it also carries the dependent-launch gap and the events' own cost."""
@@ -567,18 +567,19 @@ def mi_batch_roofline(ctx, frames, n_pairs: int, reps: int = 10):
            "traffic_calibration": TRAFFIC_CALIBRATION, "kernel": kernel,
            "pairs": n_pairs, "avg_launch_ms": round(avg, 5), "pairs_per_s": round(n_pairs / (avg * 1e-3), 1)}
     # VALU-issue roofline: the kernel's wave instructions per pair (SQ_INSTS_VALU of the committed
-    # tools/mi_pmc.sh pass) against one wave64 VALU instruction per SIMD per 2 cycles (1024 SIMDs,
+    # tools/gpu.sh sq pass) against one wave64 VALU instruction per SIMD per 2 cycles (1024 SIMDs,
     # 2.4 GHz: MI355X_MICROARCH.md "Wave scheduling" / v_fma_f32 row -- 32 lanes per cycle; one wave
     # alone issues every 4, but the kernel keeps ~8 waves per CU resident)
     cpath = os.path.join(ROOT, "profiles", MI_COUNTERS + ".json")
     if os.path.exists(cpath):
         cnt = json.load(open(cpath))
-        if kernel in cnt.get("kernel", ""):
+        vpp = cnt.get("valu_insts_per_pair", cnt.get("insts_valu_per_pair"))  # (round-5 / tools/summarise.py keys)
+        if kernel in cnt.get("kernel", "") and vpp:
             peak = 1024 * 2.4e9 / 2 / 1e9
-            ach = cnt["valu_insts_per_pair"] * n_pairs / (avg * 1e-3) / 1e9
+            ach = vpp * n_pairs / (avg * 1e-3) / 1e9
             out["valu_issue"] = {"bound": "valu-issue", "achieved": round(ach, 1), "peak": round(peak, 1),
                                  "unit": "G wave-instr/s", "frac": round(ach / peak, 4),
-                                 "valu_insts_per_pair": round(cnt["valu_insts_per_pair"], 2),
+                                 "valu_insts_per_pair": round(vpp, 2),
                                  "resident_waves_per_cu": round(cnt["resident_waves_per_cu"], 2),
                                  "counters": "profiles/" + MI_COUNTERS + ".txt"}
     return out
@@ -685,7 +686,7 @@ def crossover_model(ctx, opts, reps, xch_lb_us=None):
 def hbm_copy_gbs(ctx, nbytes: int = 1 << 30, reps: int = 20):
     """Measured HBM bandwidth of this GPU (read + write bytes / time): the
     library's 16-byte-per-lane nontemporal streaming copy of a 1 GiB buffer
-    (me_hbm_copy_gbs, the best of tools/ubench_copy.hip's sweep, ~6.0 TB/s;
+    (me_hbm_copy_gbs, the best of tools/ubench/copy.hip's sweep, ~6.0 TB/s;
     the MI355X guide quotes 6.29 TB/s for a float4 copy) -- the measured
     denominator beside the 8 TB/s datasheet peak
     (SURVEY §8d).  (Round 5 used a torch uint8 copy_, 4.8-4.9 TB/s, which

@@ -194,7 +194,7 @@ _lib = None
 def load_library(path: str | None = None):
     """Load libme_hip.so and declare prototypes.  Raises MEError if missing.
     ME_LIB (environment) names another build of the same library (A/B timing,
-    tools/gpu_ab.sh); the default is the in-tree build."""
+    tools/gpu.sh ab); the default is the in-tree build."""
     global _lib
     if _lib is not None:
         return _lib

@@ -579,7 +579,7 @@ __device__ __forceinline__ int group_max(int x) {
   return x;
 }
 
-#ifdef ME_SCHUR_STAMPS  // timing experiment only (tools/abl): workgroup 0's phase times in st->stamps[6..11]
+#ifdef ME_SCHUR_STAMPS  // timing experiment only (tools/drivers.py schur_stamps): workgroup 0's phase times in st->stamps[6..11]
 #define SCHUR_T(i)                                                                     \
   do {                                                                                 \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                         \
@@ -1023,7 +1023,7 @@ enum { SA_SUM = 0, SA_PACK = 1, SA_UNPACK = 2 };
 // LM diagonal clamp(diag U) / radius added, row n = -b^T, the last diagonal
 // block symmetric, identity padding), written through -- so the solve copies
 // it into LDS with a few LDS-DMA instructions instead of an element-wise load
-// (whose one-time code dominated the launch, tools/solve_ts.py).
+// (whose one-time code dominated the launch, tools/drivers.py solve_ts).
 //
 // claim (fused assembly): the unit is first claimed for launch generation
 // `gen` (atomic max on its claim word, issued before the loads, its result
@@ -1229,7 +1229,7 @@ constexpr int kLoadBatch = 32;
     if ((skip & 256) && tid == 0) st->stamps[(i)] -= (long long)__builtin_amdgcn_s_memtime(); \
   } while (0)
 
-#ifdef ME_SOLVE_TS  // timing experiment only (tools/solve_ts.py): wall-clock phases of cam_solve, 100 MHz ticks
+#ifdef ME_SOLVE_TS  // timing experiment only (tools/drivers.py solve_ts): wall-clock phases of cam_solve, 100 MHz ticks
 // [1] lin_finalize, [2] assembly wait, [3] load, [4] factorisation, [5] backward
 // solve, [6] candidate / cost tail, [8] last assembler exit - wg 0 entry,
 // [9] first assembler entry - wg 0 entry, [10] s_memtime ticks of [1..6], [15] calls
@@ -1726,7 +1726,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // before the first use, so a batch costs one round of global latency.
   // (Per-element branches with the use inside them made the compiler wait on
   // every load: the load phase took 15.2 of the 45 us launch at config 3 and
-  // 100 of 265 us at config 5, tools/solve_ts.py.)  S | b | diag(U) are one
+  // 100 of 265 us at config 5, tools/drivers.py solve_ts.)  S | b | diag(U) are one
   // allocation (plan), so every element is an index off b.S.  The LM diagonal
   // (Ceres: clamp(diag(U)) / radius) goes through LDS (u, free until the
   // backward solve), loaded beside the first batch.  Loads are coherent (sc1):
@@ -3064,7 +3064,7 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   g.rsub = (int)std::max(1L, ((long)g.nsub + 255) / 256);
   g.rlen = g.spts * g.rsub;
   g.nruns = (int)std::max(1L, ((long)g.np + g.rlen - 1) / g.rlen);
-  // (measured, tools/ab_schur.py: 4 tiles per wave at config 4 -- 5 spill -- but 5 for
+  // (measured, tools/drivers.py ba_wall: 4 tiles per wave at config 4 -- 5 spill -- but 5 for
   // the 50-keyframe window, where fewer tile groups per run recompute fewer Y blocks)
   g.stpw = 8 * std::min((g.npairs + 7) / 8, g.npairs > 100 ? kSchurNtMax : std::min(kSchurNtMax, 4));
   if (split_wide && g.spts == kSchurPtsWide) g.stpw = std::min(g.stpw, 16);
@@ -3391,7 +3391,7 @@ int enqueue_linearize(Plan& P) {
 // img: the assembly writes the camera solve's image of [S + D; -b^T] (the
 // solver's padded layout, s_assemble_body) into Abuf, so the solve that
 // follows loads nothing: its element-wise load of S cost wg0 ~70 us at config
-// 5 (tools/solve_ts.py).  Not with full_S (S itself is read back).
+// 5 (tools/drivers.py solve_ts).  Not with full_S (S itself is read back).
 int enqueue_assemble(Plan& P, bool img = false) {
   me_ctx* c = P.c;
   const Geo& g = P.g;
@@ -3455,7 +3455,7 @@ int enqueue_iteration(Plan& P, bool last = false) {
       hipLaunchKernelGGL(cam_solve_kernel<0>, dim3(1 + nasm), dim3(kSolveBlock), P.solve_lds, s, g, P.b, P.o, sk, 0,
                          nasm, gc, gen);
     else if (nwk > 0)
-#ifdef ME_COOP_LAUNCH  // measurement build only (tools/coop_ab.sh): the worker grid as a cooperative launch
+#ifdef ME_COOP_LAUNCH  // measurement build only (tools/gpu.sh coop): the worker grid as a cooperative launch
     {
       int skv = sk, nwv = nwk, z = 0;
       unsigned gv = gen;

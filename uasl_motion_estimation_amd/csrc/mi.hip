@@ -16,7 +16,7 @@
 
 using namespace me_dev;
 
-// development timing experiments only (tools/mi_exp.sh builds variants out of tree):
+// development timing experiments only (tools/build_variant.sh builds variants out of tree):
 // 1 no term walk, 2 walk without the table gather, 3 no histogram updates
 #ifndef MI_EXP
 #define MI_EXP 0

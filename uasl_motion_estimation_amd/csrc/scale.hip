@@ -817,7 +817,7 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
   const int t = blockIdx.x * kTracksPerBlock + grp;
-#if ME_SCALE_EXP != 1  // timing experiments only (tools/exp): 1 = no track work
+#if ME_SCALE_EXP != 1  // timing experiments only (tools/build_variant.sh): 1 = no track work
   if (t < a.nL + a.nR) residual_track(a, td, t, h, res, err);
 #endif
   if (!last_block_arrives(cnt + 1 + j, gridDim.x)) return;
@@ -924,7 +924,7 @@ __device__ __noinline__ void lm_neq_tracks(const ScaleArgs* ga, double scale, co
   if (t < a.nL + a.nR)
     neq_track(a, td, t, h, uniform_ptr(res), uniform_ptr(jj), uniform_ptr(je), uniform_ptr(err));
 }
-#ifdef ME_SCALE_TS  // timing experiment only (tools/scale_ts.py): phase split of the persistent LM, 100 MHz ticks
+#ifdef ME_SCALE_TS  // timing experiment only (tools/drivers.py scale_ts): phase split of the persistent LM, 100 MHz ticks
 // workgroup (0, 0)'s view: [0] phases, [1] launches, [2] launch wall, [3] track work A/D, [4] B, [5] C,
 // [6] waits for the phase's control (after its own work), [7] phases of type A/D, [8] B, [9] C;
 // the controlling workgroup: [10] reduce + control (from its arrival), [11] controls
@@ -1638,7 +1638,7 @@ extern "C" int me_scale_optimise(me_ctx* c, me_scale_state* s, const me_optim_pa
     {
       me_ktimer t(c, ME_KT_SCALE_RES);
       const int max_phases = 256 * (p.max_nb_iter + 2);
-#ifdef ME_COOP_LAUNCH  // measurement build only (tools/coop_ab.sh): the same grid as a cooperative launch
+#ifdef ME_COOP_LAUNCH  // measurement build only (tools/gpu.sh coop): the same grid as a cooperative launch
       {
         const ScaleArgs* a0 = P.dargs;
         const ScaleArgs* a1 = P.dargs + 1;

@@ -1,5 +1,5 @@
 // solve_diag.hpp -- the camera solve's diagonal-block factorisation (ba.hip),
-// kept in a header so tools/ubench_diag.hip times the same code in isolation.
+// kept in a header so tools/ubench/diag.hip times the same code in isolation.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -37,11 +37,11 @@ __device__ __forceinline__ double rsqrt_nr(double p) {
 // No workgroup barrier and no LDS round trip inside the block: per round the
 // uniform pivot chain, the substitutions and two MFMAs.
 #ifndef ME_DIAG_EXP
-#define ME_DIAG_EXP 0  // timing experiments only (tools/ubench_diag.hip), results invalid: 1 no Newton step, 2 no MFMA, 4 no rsq, 8 no substitutions
+#define ME_DIAG_EXP 0  // timing experiments only (tools/ubench/diag.hip), results invalid: 1 no Newton step, 2 no MFMA, 4 no rsq, 8 no substitutions
 #endif
 #ifndef ME_DIAG_GATHER
 #define ME_DIAG_GATHER 1  // 1: permlane swaps + readlane, 0: wave-private LDS scratch (3.34k vs 3.49k ticks per block in
-                          // isolation, tools/ubench_diag.hip; DPP row broadcasts instead of readlane: 3.64k, dropped)
+                          // isolation, tools/ubench/diag.hip; DPP row broadcasts instead of readlane: 3.64k, dropped)
 #endif
 __device__ __forceinline__ double lane_read(double x, int l) {
   return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),

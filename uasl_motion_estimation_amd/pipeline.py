@@ -364,7 +364,7 @@ class GPUBackend(Backend):
         self._bw_k = 0  # staging / device buffer set of the next window solve
         # window t's BA start formed on the device behind window t - 1's solve (me_vo_ba_chain)
         self.chain_window = os.environ.get("ME_VO_CHAIN", "1") == "1"
-        self.tlog = None  # diagnostics (tools/pipe_run.py): (event, frame, perf_counter) of BA enqueues / completions
+        self.tlog = None  # diagnostics: (event, frame, perf_counter) of BA enqueues / completions
         self._scale_res = None
 
     def reserve(self, cfg):
