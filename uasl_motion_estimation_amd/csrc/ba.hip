@@ -1738,6 +1738,16 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   // the image of [S + D; -b^T] in Abuf: written by s_assemble_kernel (non-fused), or by this launch's
   // assemblers (fused; written through)
   const bool img_ready = (skip & kSkipImg) != 0 || (fused && (kLds || ME_SOLVE_IMG));
+  // LDS-DMA chunks of the image: all, or (pipelined form) the ones holding block row 0 first
+  const int dma_bytes = N * ld * 8, dma_chunks = (dma_bytes + 1023) >> 10;
+  const int dma_first = kPipe ? min(dma_chunks, (16 * ld * 8 + 1023) >> 10) : dma_chunks;
+  auto dma_chunk = [&](int k) {
+    const int off = (k << 10) + 16 * lane;
+    if (off < dma_bytes)
+      __builtin_amdgcn_global_load_lds((const void*)((const char*)b.Abuf + off),
+                                       (__attribute__((address_space(3))) void*)((char*)A + (k << 10)), 16, 0,
+                                       16 /* sc1 */);
+  };
   if (!kLds && img_ready) {
     // the working matrix is Abuf itself: nothing to load.  (Fused: the
     // assemblers' written-through stores bypassed this XCD's L2, which may
@@ -1747,16 +1757,11 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   } else if (kLds && img_ready) {
     // the assemblers wrote the solver's image (s_assemble_body img): N x ld
     // doubles, copied by LDS-DMA, 1 KiB per wave-instruction (lane-linear),
-    // coherent reads (sc1); the barrier below retires them (vmcnt)
-    const int nbytes = N * ld * 8, nchunk = (nbytes + 1023) >> 10;
+    // coherent reads (sc1); the barrier below retires them (vmcnt).  Only the
+    // chunks of block row 0 here: the pipelined factorisation (kPipe) has
+    // waves 1.. copy the rest while wave 0 factors diagonal block 0.
     if (!done)
-      for (int k = wave; k < nchunk; k += nw) {
-        const int off = (k << 10) + 16 * lane;
-        if (off < nbytes)
-          __builtin_amdgcn_global_load_lds((const void*)((const char*)b.Abuf + off),
-                                           (__attribute__((address_space(3))) void*)((char*)A + (k << 10)), 16, 0,
-                                           16 /* sc1 */);
-      }
+      for (int k = wave; k < dma_first; k += nw) dma_chunk(k);
   } else
   for (int q0 = 0; q0 < NQ; q0 += kLoadBatch) {
     double xv[kLoadBatch];
@@ -1864,7 +1869,14 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
-    if (wave == 0) diag_factor(0, diag_load_wave(A, ld, 0, lane));
+    if (wave == 0) {
+      diag_factor(0, diag_load_wave(A, ld, 0, lane));
+    } else if (img_ready && nw > 1) {
+      // the rest of the image, beside wave 0's block 0 (its rows are in LDS:
+      // the barrier above retired their chunks); retired before the barrier
+      for (int k = dma_first + wave - 1; k < dma_chunks; k += nw - 1) dma_chunk(k);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     STS(19);
     __syncthreads();
     for (int J = 0; J + 1 < Ts; ++J) {
