@@ -16,29 +16,11 @@
 
 using namespace me_dev;
 
-// development timing experiments only (tools/build_variant.sh builds variants out of tree):
-// 1 no term walk, 2 walk without the table gather, 3 no histogram updates
-#ifndef MI_EXP
-#define MI_EXP 0
-#endif
-#ifndef MI_MREG
-#define MI_MREG 0  // marginal counts: 1 registers (byte select), 0 LDS words
-#endif
-#ifndef MI_UCLR
-#define MI_UCLR 1  // joint-word clear in the walk: 1 unconditional store, 0 predicated
-#endif
-#ifndef QUAD_EXP
-#define QUAD_EXP 0  // quad kernel timing variants (tools/build_variant.sh): 1 no walk, 2 no histogram updates, 4 no gathers
-#endif
-#ifndef QUAD_U
-#define QUAD_U 4  // quad kernel: walk iterations in flight per lane (table gathers overlapped)
-#endif
-#ifndef MI_PACK
-#define MI_PACK 1  // quad kernel: packed marginal words for N <= 127 (0: byte marginals, float c3 per term)
-#endif
-#ifndef MI_PERM
-#define MI_PERM 37  // histogram update order: pixel p = (k * MI_PERM) mod (PW PH), 1 = row-major
-#endif
+// quad kernel: walk iterations in flight per lane (table gathers overlapped;
+// 2 / 4 / 6 / 8 measured 267.8 / 266.4 / 268.3 / 272.0 us per 1 M pairs)
+constexpr int kQuadU = 4;
+// lane kernel: histogram update order, pixel p = (k * kMiPerm) mod (PW PH)
+constexpr int kMiPerm = 37;
 
 namespace {
 
@@ -80,7 +62,7 @@ __global__ void mi_table_kernel(int N, float invN, float* __restrict__ tab) {
 //    math, terms from the per-N table, summed left to right as they arrive
 //    (bit-identical to the reference's float loop).
 constexpr int kLaneBlock = 64;
-constexpr int kLaneBm = 100, kLaneMarg = 114, kLaneWords = MI_MREG ? 114 : 124;  // joint | bitmap | 0 | marginals
+constexpr int kLaneBm = 100, kLaneMarg = 114, kLaneWords = 124;  // joint | bitmap | 0 | marginals
 constexpr int kLaneUnroll = 4;
 
 __device__ __forceinline__ int wave_max(int v) {
@@ -117,8 +99,7 @@ __device__ __forceinline__ void lane_hist_row(uint32_t* h, const uint32_t pl[3],
     if (PW > 0 ? x < PW : x < pw) {
       const int bl = bin20((pl[x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[x >> 2] >> (8 * (x & 3))) & 0xff);
       const int code = bl * 20 + br;
-      if (MI_EXP != 3) atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
-      else if (code == 1023) h[0] = 1u;
+      atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
     }
   }
 }
@@ -138,11 +119,10 @@ __device__ __forceinline__ void lane_hist_pair(uint32_t* h, const uint8_t* __res
     // joint bin, and back-to-back atomics on one LDS word serialise
 #pragma unroll
     for (int k = 0; k < PW * PH; ++k) {
-      const int p = (k * MI_PERM) % (PW * PH), r = p / PW, x = p % PW;
+      const int p = (k * kMiPerm) % (PW * PH), r = p / PW, x = p % PW;
       const int bl = bin20((pl[r][x >> 2] >> (8 * (x & 3))) & 0xff), br = bin20((pr[r][x >> 2] >> (8 * (x & 3))) & 0xff);
       const int code = bl * 20 + br;
-      if (MI_EXP != 3) atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
-      else if (code == 1023) h[0] = 1u;
+      atomicAdd(&h[64 * (code >> 2)], 1u << ((code & 3) * 8));
     }
   } else {
     for (int r = 0; r < ph; ++r) {
@@ -246,12 +226,10 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
     }
     uint32_t nz = 0;  // non-empty bitmap words
     int nnz = 0;
-    if (!MI_MREG) {
 #pragma unroll
-      for (int q = 0; q < 5; ++q) {
-        h[64 * (kLaneMarg + q)] = cl4[q];
-        h[64 * (kLaneMarg + 5 + q)] = cr4[q];
-      }
+    for (int q = 0; q < 5; ++q) {
+      h[64 * (kLaneMarg + q)] = cl4[q];
+      h[64 * (kLaneMarg + 5 + q)] = cr4[q];
     }
 #pragma unroll
     for (int w = 0; w < 13; ++w) {
@@ -259,7 +237,7 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
       nz |= (bm[w] != 0u ? 1u : 0u) << w;
       nnz += __builtin_popcount(bm[w]);
     }
-    const int tmax = MI_EXP == 1 ? 0 : wave_max(nnz);
+    const int tmax = wave_max(nnz);
     // Branch-free walk.  State: current word wd and its remaining bits, the
     // words still to visit (nz), and the next non-empty word nw with its bits
     // read one step ahead (nxt); word 13 is a permanent zero sentinel.  A
@@ -299,29 +277,17 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
         // otherwise the word is stored back unchanged (no branch)
         const int ncode = (wd << 5) | __builtin_ctz(bits | 0x80000000u);
         const bool clr = t + u < nnz && ((ncode >> 2) != cw || t + u + 1 >= nnz);
-        if (MI_UCLR)
-          h[64 * cw] = clr ? 0u : hw;
-        else if (clr)
-          h[64 * cw] = 0u;
+        h[64 * cw] = clr ? 0u : hw;
         const int qi = i >> 2, qj = j >> 2;  // i <= 22 for a finished lane's garbage code
-        uint32_t wl, wr;
-        if (MI_MREG) {
-          wl = qi == 0 ? cl4[0] : qi == 1 ? cl4[1] : qi == 2 ? cl4[2] : qi == 3 ? cl4[3] : cl4[4];
-          wr = qj == 0 ? cr4[0] : qj == 1 ? cr4[1] : qj == 2 ? cr4[2] : qj == 3 ? cr4[3] : cr4[4];
-        } else {
-          wl = h[64 * (kLaneMarg + qi)];
-          wr = h[64 * (kLaneMarg + 5 + qj)];
-        }
+        const uint32_t wl = h[64 * (kLaneMarg + qi)];
+        const uint32_t wr = h[64 * (kLaneMarg + 5 + qj)];
         const int cL = (wl >> ((i & 3) * 8)) & 0xff;
         const int cR = (wr >> ((j & 3) * 8)) & 0xff;
         const int a = max(cL, cR), b = min(cL, cR);
         const int idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + cJ;
         // out-of-range buffer offsets read 0: a finished lane adds +0.0f, no branch
         const int off = t + u < nnz ? 4 * (idx - 1) : 0x7ffffff0;
-        if (MI_EXP == 2)
-          v[u] = (float)(off >> 2);
-        else
-          v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
+        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
       }
 #pragma unroll
       for (int u = 0; u < kLaneUnroll; ++u) MI += vp[u];  // previous iteration: +0.0f when finished (MI is never -0)
@@ -379,7 +345,7 @@ constexpr int kQuadBlock = 64, kQuadGroups = 16;
 
 template <int PW, int PH>
 struct QuadShape {
-  static constexpr bool kPack = MI_PACK && PW > 0 && PH > 0 && PW * PH <= 127;
+  static constexpr bool kPack = PW > 0 && PH > 0 && PW * PH <= 127;
   static constexpr int kN = (PW > 0 && PH > 0) ? PW * PH : 255;               // >= non-empty bins
   static constexpr int kSlots = kPack ? kN - kN / 4 : kN;
   static constexpr int kCR = 100, kRowTab = kPack ? 120 : 105, kRowCL = kPack ? 140 : 126,
@@ -429,22 +395,7 @@ __device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restric
     }
 #pragma unroll
     for (int rr = 0; rr < QS::kRows; ++rr) {
-      if (QUAD_EXP == 6 && q + 4 * rr < PH) {  // run-length merged updates along the row
-        int code[PW > 0 ? PW : 1];
-#pragma unroll
-        for (int x = 0; x < PW; ++x)
-          code[x] = bin20((pl[rr][x >> 2] >> (8 * (x & 3))) & 0xff) * 20 + bin20((pr[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
-        uint32_t run = 1;
-#pragma unroll
-        for (int x = 0; x < PW; ++x) {
-          if (x + 1 < PW && code[x + 1] == code[x]) {
-            ++run;
-          } else {
-            atomicAdd(&hg[16 * (code[x] >> 2)], run << ((code[x] & 3) * 8));
-            run = 1;
-          }
-        }
-      } else if (q + 4 * rr < PH) {
+      if (q + 4 * rr < PH) {
 #pragma unroll
         for (int k = 0; k < PW; ++k) {
           // scattered (a multiplier coprime to PW): neighbouring pixels often share a joint word
@@ -452,9 +403,7 @@ __device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restric
           const int bl = bin20((pl[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
           const int br = bin20((pr[rr][x >> 2] >> (8 * (x & 3))) & 0xff);
           const int code = bl * 20 + br;
-          if (QUAD_EXP == 5) hg[16 * (code >> 2)] = 1u << ((code & 3) * 8);  // timing only: plain stores
-          else if (QUAD_EXP != 2) atomicAdd(&hg[16 * (code >> 2)], 1u << ((code & 3) * 8));
-          else if (code == 1023) hg[0] = 1u;
+          atomicAdd(&hg[16 * (code >> 2)], 1u << ((code & 3) * 8));
         }
       }
     }
@@ -597,7 +546,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     }
     wave_sync();  // right marginal, row table and starts visible to the quad
     const int s0 = (q * total) >> 2, nq = (((q + 1) * total) >> 2) - s0;
-    const int tmax = QUAD_EXP == 1 ? 0 : wave_max(nq);
+    const int tmax = wave_max(nq);
     float* slots = reinterpret_cast<float*>(hg + 16 * QS::kTerms);
     const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * QS::kCR);
     const uint32_t* colw = hg + 16 * QS::kCR;  // (packed layout)
@@ -622,7 +571,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     uint32_t eb = gb + 64u * (uint32_t)(QS::kRowTab + min(e + 1, QS::kLastE));
     const uint32_t eblast = gb + 64u * (uint32_t)(QS::kRowTab + QS::kLastE);
     uint32_t rowo = gb + (uint32_t)rowb;
-    constexpr int kU = QUAD_U;
+    constexpr int kU = kQuadU;
     float vp[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
@@ -650,10 +599,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
           idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + (int)cJ;
         }
         const int off = t + u < nq ? 4 * (idx - 1) : 0x7ffffff0;
-        if (QUAD_EXP == 4)
-          v[u] = (float)off;
-        else
-          v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
+        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
         // next non-empty row of the compacted table (read one ahead)
         const bool z = bits == 0u;
         bits = z ? (nxt & 0xfffffu) : bits;

@@ -26,9 +26,6 @@ using namespace me_dev;
 namespace {
 
 constexpr int kScBlock = 256;
-#ifndef ME_SCALE_EXP
-#define ME_SCALE_EXP 0
-#endif
 
 struct ScaleArgs {
   double K1[9], K2[9], q1[4], t1[3], q2[4], t2[3];
@@ -316,18 +313,10 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
   float mi;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, lx, ly, P);
-#if ME_SCALE_EXP == 2  // timing experiment: projection only, no MI
-    mi = (float)lx;
-#else
     mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN, a.tab);
-#endif
   } else {
     if (a.weighting) wv = sobel_weight(a.imgR, a.stride, a.cols, a.rows, rx, ry, P);
-#if ME_SCALE_EXP == 2
-    mi = (float)rx;
-#else
     mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN, a.tab);
-#endif
   }
   if (h.gl == 0) wt_store(&res[row], (double)mi * wv);
 }
@@ -817,9 +806,7 @@ __global__ __launch_bounds__(kScBlock) void scale_res_ctrl_kernel(ScaleArgs a, T
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
   const int t = blockIdx.x * kTracksPerBlock + grp;
-#if ME_SCALE_EXP != 1  // timing experiments only (tools/build_variant.sh): 1 = no track work
   if (t < a.nL + a.nR) residual_track(a, td, t, h, res, err);
-#endif
   if (!last_block_arrives(cnt + 1 + j, gridDim.x)) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   double sx, sy;
