@@ -335,22 +335,23 @@ __global__ __launch_bounds__(kLaneBlock) void mi_lane_kernel(const uint8_t* __re
 // (c3(127) < 2^19, 127 * 126 / 2 < 2^13).  For m >= 1 the words order as m
 // does, so the walk's table index is (max >> 13) + (min & 0x1fff) + cJ - 1 --
 // five operations instead of the float c3 and the triangle product per term.
-// Lane 0 adds its own bins' terms (the first floor(T / 4) of the order) as the
-// walk loads them, so only the other lanes' terms go through slots.
-// group words: [0,100) joint, [100,120) column words, [120,140) row table (no
-// spare: the walk's look-ahead stops at entry 19), [140,160) its left-marginal
-// words, [160,164) lane starts, [164, 164 + N - N / 4) term slots: 255 words
-// for N = 121 (unpacked: 257 at N = 121, 9 workgroups per CU; packed: 10)
+// Packed shapes keep the terms in registers and sum them in order by DPP quad
+// broadcasts; the group words are [0,100) joint, [100,120) column words,
+// [120,140) row table (no spare: the walk's look-ahead stops at entry 19),
+// [140,160) its left-marginal words, [160,164) lane starts: 164 words per pair,
+// 10.5 KB per workgroup.  Unpacked shapes (N > 127) add N term slots.
 constexpr int kQuadBlock = 64, kQuadGroups = 16;
 
 template <int PW, int PH>
 struct QuadShape {
   static constexpr bool kPack = PW > 0 && PH > 0 && PW * PH <= 127;
   static constexpr int kN = (PW > 0 && PH > 0) ? PW * PH : 255;               // >= non-empty bins
-  static constexpr int kSlots = kPack ? kN - kN / 4 : kN;
-  static constexpr int kCR = 100, kRowTab = kPack ? 120 : 105, kRowCL = kPack ? 140 : 126,
-                       kStart = kPack ? 160 : 132, kTerms = kStart + 4, kClear = kPack ? kStart : kRowCL,
-                       kLastE = kPack ? 19 : 20;  // last row-table entry the walk reads
+  static constexpr int kSlots = kPack ? 0 : kN;  // packed: terms in registers
+  static constexpr int kMaxT = kPack ? ((kN + 3) / 4 + kQuadU - 1) / kQuadU * kQuadU : 0;  // >= a lane's run
+  // packed: 22 row-table entries (up to 20 rows + 2 sentinels), no bound on the walk's look-ahead
+  static constexpr int kCR = 100, kRowTab = kPack ? 120 : 105, kRowCL = kPack ? 142 : 126,
+                       kStart = kPack ? 164 : 132, kTerms = kStart + 4, kClear = kPack ? kStart : kRowCL,
+                       kLastE = kPack ? 21 : 20;  // last row-table entry the walk reads
   static constexpr int kWords = kTerms + kSlots;
   static constexpr int kRows = PH > 0 ? (PH + 3) / 4 : 4;  // patch rows per lane (PH <= 15)
 };
@@ -424,7 +425,94 @@ __device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restric
   }
 }
 
-template <int PW, int PH, bool EPI = false>
+// Binned images for large batches (every pixel is read by ~n pw ph / (W H)
+// patches: at 1 M 11x11 pairs on 720p, 130 times).  One pass writes a u16
+// word per pixel whose sum over a left / right pixel pair IS the joint update:
+//   left  320 bl                              (= 64 x the row's first word, 5 bl)
+//   right 64 (br >> 2) | 8 (br & 3)           (word within the row, byte shift)
+// so s = L + R has the LDS byte offset of word 5 bl + br / 4 in bits 6.. and
+// the byte's shift in bits 0..4 (bit 5 clear): ds_add at (s & ~63) | 4 g of
+// 1 << s -- three VALU per pixel instead of nine (two byte multiplies, two
+// shifts, the code, its word, its shift), and one 32-bit add sums two pixels
+// (each half <= 6 080 + 280 < 2^16: no carry crosses).
+__device__ __forceinline__ uint32_t mi_bin_word(uint32_t b, bool right) {
+  return right ? ((b >> 2) << 6) | ((b & 3) << 3) : 320u * b;
+}
+
+// Both images in one launch (blockIdx.z: left / right), four pixels per lane.
+__global__ void mi_bin_kernel(const uint8_t* __restrict__ imgL, int strideL, const uint8_t* __restrict__ imgR,
+                              int strideR, int width, int height, int ostride, uint32_t* __restrict__ outL,
+                              uint32_t* __restrict__ outR) {
+  const bool right = blockIdx.z != 0;
+  const uint8_t* row = (right ? imgR : imgL) + (long)blockIdx.y * (right ? strideR : strideL);
+  uint32_t* orow = (right ? outR : outL) + (long)blockIdx.y * (ostride >> 1);
+  const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (x >= ostride) return;
+  uint32_t px = 0;
+  if (x + 3 < width && ((uintptr_t)(row + x) & 3) == 0) {
+    px = *reinterpret_cast<const uint32_t*>(row + x);
+  } else {
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+      if (x + h < width) px |= (uint32_t)row[x + h] << (8 * h);
+  }
+  uint32_t w[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    w[h] = mi_bin_word((uint32_t)bin20((int)((px >> (16 * h)) & 0xff)), right) |
+           (mi_bin_word((uint32_t)bin20((int)((px >> (16 * h + 8)) & 0xff)), right) << 16);
+  orow[x >> 1] = w[0];
+  if (x + 2 < ostride) orow[(x >> 1) + 1] = w[1];
+}
+
+// One patch's histogram from the binned images (u16 rows of ostride words,
+// every row start 4-byte aligned; the scratch holds 64 bytes past the last
+// row): lane q takes rows q, q + 4, ...  Each row is 6 aligned dwords from the
+// pixel's dword down, realigned by its 0 / 2-byte offset.
+template <int PW, int PH>
+__device__ __forceinline__ void quad_hist_bin(uint8_t* ldsb, const uint16_t* __restrict__ bL,
+                                              const uint16_t* __restrict__ bR, int ostride, long oL, long oR, int q,
+                                              uint32_t gb) {
+  static_assert(PW >= 2 && PW <= 11 && PH > 0, "binned rows: 6 dwords");
+  constexpr int kRows = (PH + 3) / 4, kD = (PW + 1) / 2;
+  uint32_t dl[kRows][6], dr[kRows][6], al[kRows], ar[kRows];
+#pragma unroll
+  for (int rr = 0; rr < kRows; ++rr) {
+    const int r = q + 4 * rr;
+    if (r < PH) {
+      const char* pl = reinterpret_cast<const char*>(bL + oL + (long)r * ostride);
+      const char* pr = reinterpret_cast<const char*>(bR + oR + (long)r * ostride);
+      al[rr] = (uint32_t)(uintptr_t)pl & 3u;
+      ar[rr] = (uint32_t)(uintptr_t)pr & 3u;
+      // (pointer arithmetic, not an integer round trip: the loads stay global_load)
+      const uint32_t* ql = reinterpret_cast<const uint32_t*>(pl - al[rr]);
+      const uint32_t* qr = reinterpret_cast<const uint32_t*>(pr - ar[rr]);
+#pragma unroll
+      for (int d = 0; d < 6; ++d) {
+        dl[rr][d] = ql[d];
+        dr[rr][d] = qr[d];
+      }
+    }
+  }
+#pragma unroll
+  for (int rr = 0; rr < kRows; ++rr) {
+    if (q + 4 * rr < PH) {
+#pragma unroll
+      for (int d = 0; d < kD; ++d) {
+        const uint32_t l = __builtin_amdgcn_alignbyte(dl[rr][d + 1 < 6 ? d + 1 : d], dl[rr][d], al[rr]);
+        const uint32_t r = __builtin_amdgcn_alignbyte(dr[rr][d + 1 < 6 ? d + 1 : d], dr[rr][d], ar[rr]);
+        const uint32_t s = l + r;  // two pixels' joint updates
+        atomicAdd(reinterpret_cast<uint32_t*>(ldsb + ((s & 0xffc0u) | gb)), 1u << (s & 31u));
+        if (2 * d + 1 < PW) {
+          const uint32_t t = s >> 16;
+          atomicAdd(reinterpret_cast<uint32_t*>(ldsb + ((t & 0xffc0u) | gb)), 1u << (t & 31u));
+        }
+      }
+    }
+  }
+}
+
+template <int PW, int PH, bool EPI = false, bool BIN = false>
 __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                              const uint8_t* __restrict__ imgR, int strideR,
                                                              long bytesL, long bytesR,
@@ -465,7 +553,11 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
       oR = (long)cr.y * strideR + cr.x;
     }
     wave_sync();  // the previous pair's clears and slot reads precede this pair's updates
-    if (live) {
+    if constexpr (BIN) {
+      if (live)
+        quad_hist_bin<PW, PH>(reinterpret_cast<uint8_t*>(lds), reinterpret_cast<const uint16_t*>(imgL),
+                              reinterpret_cast<const uint16_t*>(imgR), strideL, oL, oR, q, 4u * (uint32_t)g);
+    } else if (live) {
       const int rows = PH > 0 ? PH : ph;
       const bool fast = oL >= 3 && oR >= 3 && oL + (long)(rows - 1) * strideL + 16 <= bytesL &&
                         oR + (long)(rows - 1) * strideR + 16 <= bytesR;
@@ -518,7 +610,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     const uint32_t p4 = __builtin_amdgcn_sad_u8(a03, 0u, 0u) + quad_exscan(c4, q);
     const int total = (int)(__builtin_amdgcn_sad_u8(a03, 0u, 0u) + a4);
     const uint32_t n03 = ((c03 + 0x7f7f7f7fu) & 0x80808080u) >> 7, n4 = c4 ? 1u : 0u;
-    const uint32_t na03 = quad_sum(n03);
+    const uint32_t na03 = quad_sum(n03), na4 = quad_sum(n4);
     const uint32_t e03 = na03 * 0x01010100u + quad_exscan(n03, q);
     const uint32_t e4 = __builtin_amdgcn_sad_u8(na03, 0u, 0u) + quad_exscan(n4, q);
     // Lane q' takes the bins with slots [b_q', b_q'+1), b_q' = floor(q' T / 4): the
@@ -532,7 +624,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
       const int P = kk < 4 ? (int)((p03 >> (8 * kk)) & 0xff) : (int)p4;
       const int E = kk < 4 ? (int)((e03 >> (8 * kk)) & 0xff) : (int)e4;
       if (cnt > 0) {
-        rowtab[16 * E] = rb[kk] | ((uint32_t)(q + 4 * kk) << 20);
+        rowtab[16 * E] = rb[kk] | ((uint32_t)(5 * (q + 4 * kk)) << 20);  // (the row's first joint word)
         if (QS::kPack)
           rowcw[16 * E] = mi_pack((uint32_t)(cl >> (8 * kk)) & 0xffu);
         else
@@ -544,10 +636,17 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         }
       }
     }
+    if (QS::kPack && q == 0) {
+      // two sentinel rows of 20 bins after the last: a lane's run of <= kMaxT
+      // steps never exhausts both, so its look-ahead needs no bound (their
+      // terms lie beyond the run: masked loads)
+      const uint32_t nrows = __builtin_amdgcn_sad_u8(na03, 0u, 0u) + na4;
+      rowtab[16 * nrows] = 0xfffffu;
+      rowtab[16 * (nrows + 1)] = 0xfffffu;
+    }
     wave_sync();  // right marginal, row table and starts visible to the quad
     const int s0 = (q * total) >> 2, nq = (((q + 1) * total) >> 2) - s0;
     const int tmax = wave_max(nq);
-    float* slots = reinterpret_cast<float*>(hg + 16 * QS::kTerms);
     const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * QS::kCR);
     const uint32_t* colw = hg + 16 * QS::kCR;  // (packed layout)
     const uint8_t* jnt = reinterpret_cast<const uint8_t*>(hg);
@@ -563,25 +662,16 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     }
     nxt = rowtab[16 * min(e + 1, QS::kLastE)];
     ncl = QS::kPack ? rowcw[16 * min(e + 1, QS::kLastE)] : clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
-    int rowb = 64 * 5 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
+    int rowb = 64 * (int)(ent >> 20);  // byte offset of the row's first joint word (group-relative)
     // packed: the look-ahead entry and the row's joint bytes as byte offsets into the
     // workgroup's LDS (group base included: no index arithmetic per term)
     const uint8_t* ldsb = reinterpret_cast<const uint8_t*>(lds);
     const uint32_t gb = 4u * (uint32_t)g;
     uint32_t eb = gb + 64u * (uint32_t)(QS::kRowTab + min(e + 1, QS::kLastE));
-    const uint32_t eblast = gb + 64u * (uint32_t)(QS::kRowTab + QS::kLastE);
     uint32_t rowo = gb + (uint32_t)rowb;
     constexpr int kU = kQuadU;
-    float vp[kU];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
-    // packed: lane 0 sums its terms in order as they arrive (finished lanes load +0.0f)
-    // and the others store theirs from slot 0 on
-    float acc = 0.0f;
-    const bool keep = !QS::kPack || q != 0;
-    const int sb = QS::kPack ? s0 - (total >> 2) : s0;
-    for (int t = 0; t < tmax; t += kU) {
-      float v[kU];
+    // kU terms of the lane's run from its t-th on (finished lanes load +0.0f)
+    auto step = [&](int t, float* v) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int j = __builtin_ctz(bits | 0x100000u);  // < 21
@@ -605,54 +695,106 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         bits = z ? (nxt & 0xfffffu) : bits;
         cL = z ? ncl : cL;
         if (QS::kPack) {
-          rowo = z ? gb + 64u * 5u * (nxt >> 20) : rowo;
-          eb = z && eb < eblast ? eb + 64u : eb;
+          rowo = z ? gb | ((nxt >> 20) << 6) : rowo;
+          eb = z ? eb + 64u : eb;
           nxt = *reinterpret_cast<const uint32_t*>(ldsb + eb);
           ncl = *reinterpret_cast<const uint32_t*>(ldsb + eb + 64 * (QS::kRowCL - QS::kRowTab));
         } else {
           e = z ? min(e + 1, QS::kLastE) : e;
-          rowb = z ? 64 * 5 * (int)(nxt >> 20) : rowb;
+          rowb = z ? 64 * (int)(nxt >> 20) : rowb;
           nxt = rowtab[16 * min(e + 1, QS::kLastE)];
           ncl = clc[64 * ((e + 1) >> 2) + ((e + 1) & 3)];
         }
       }
+    };
+    float MI = 0.0f;
+    if constexpr (QS::kPack) {
+      // Terms stay in registers (no LDS slots: 164 words per pair, 15
+      // workgroups per CU instead of 9).  Lane q's terms are T[0, nq), then
+      // +0.0f up to tmax.  The pair's terms left to right
+      // (mutual_information.cpp:78-84) are lane 0's, then lane 1's, 2's, 3's:
+      // every lane adds the quad's lane-qq terms by a DPP broadcast, and
+      // adding the +0.0f tail leaves a sum unchanged (no term and no partial
+      // sum is -0.0f: pJ > 0 and log2f(x) = +0.0f only at x = 1).
+      float T[QS::kMaxT];
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (QS::kPack) acc += vp[u];
-        if (keep && t - kU + u >= 0 && t - kU + u < nq) slots[16 * (sb + t - kU + u)] = vp[u];
+      for (int t = 0; t < QS::kMaxT; t += kU) {
+        if (t < tmax) {  // (wave-uniform; no early exit: a break copies T at every exit)
+          step(t, T + t);
+        } else {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) T[t + u] = 0.0f;
+        }
       }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) vp[u] = v[u];
-    }
-    {
-      const int t = (tmax + kU - 1) / kU * kU;
+      for (int t = 0; t < QS::kMaxT; ++t) {
+        if (t >= tmax) break;
+        MI += T[t];
+      }
 #pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        if (QS::kPack) acc += vp[u];
-        if (keep && t - kU + u >= 0 && t - kU + u < nq) slots[16 * (sb + t - kU + u)] = vp[u];
+      for (int t = 0; t < QS::kMaxT; ++t) {
+        if (t >= tmax) break;
+        MI += __builtin_bit_cast(float, (int)quad_perm<0x55>(__builtin_bit_cast(uint32_t, T[t])));
+      }
+#pragma unroll
+      for (int t = 0; t < QS::kMaxT; ++t) {
+        if (t >= tmax) break;
+        MI += __builtin_bit_cast(float, (int)quad_perm<0xAA>(__builtin_bit_cast(uint32_t, T[t])));
+      }
+#pragma unroll
+      for (int t = 0; t < QS::kMaxT; ++t) {
+        if (t >= tmax) break;
+        MI += __builtin_bit_cast(float, (int)quad_perm<0xFF>(__builtin_bit_cast(uint32_t, T[t])));
+      }
+      wave_sync();  // the walk's joint reads precede the clears
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        uint32_t* row = hg + 16 * 5 * (q + 4 * kk);
+#pragma unroll
+        for (int m = 0; m < 5; ++m) row[16 * m] = 0u;
+      }
+    } else {
+      // unpacked (N > 127): each lane stores its terms in the pair's slots, lane 0 sums them in order
+      float* slots = reinterpret_cast<float*>(hg + 16 * QS::kTerms);
+      float vp[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) vp[u] = 0.0f;
+      for (int t = 0; t < tmax; t += kU) {
+        float v[kU];
+        step(t, v);
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) vp[u] = v[u];
+      }
+      {
+        const int t = (tmax + kU - 1) / kU * kU;
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (t - kU + u >= 0 && t - kU + u < nq) slots[16 * (s0 + t - kU + u)] = vp[u];
+      }
+      wave_sync();  // the walk's joint reads precede the clears
+#pragma unroll
+      for (int kk = 0; kk < 5; ++kk) {
+        uint32_t* row = hg + 16 * 5 * (q + 4 * kk);
+#pragma unroll
+        for (int m = 0; m < 5; ++m) row[16 * m] = 0u;
+      }
+      wave_sync();  // slots written by the quad
+      if (q == 0) {
+        int s = 0;
+        for (; s + 8 <= total; s += 8) {
+          float x[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) x[u] = slots[16 * (s + u)];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) MI += x[u];
+        }
+        for (; s < total; ++s) MI += slots[16 * s];
       }
     }
-    wave_sync();  // the walk's joint reads precede the clears
-    // clear the lane's joint rows for the next pair
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      uint32_t* row = hg + 16 * 5 * (q + 4 * kk);
-#pragma unroll
-      for (int m = 0; m < 5; ++m) row[16 * m] = 0u;
-    }
-    wave_sync();  // slots written by the quad
     if (q == 0) {
-      float MI = acc;
-      const int ns = QS::kPack ? total - (total >> 2) : total;
-      int s = 0;
-      for (; s + 8 <= ns; s += 8) {
-        float x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = slots[16 * (s + u)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) MI += x[u];
-      }
-      for (; s < ns; ++s) MI += slots[16 * s];
       if (EPI) {
         if (k < ntot) em.sc[k] = live ? (double)MI : -INFINITY;
       } else if (k < n) {
@@ -915,7 +1057,19 @@ extern "C" int me_mi_epipolar_match_count(me_ctx* c, const uint8_t* imgL, const 
                          unique, ratio, margin, xr_out, ok_out);
 }
 
-// Shared launcher (also used by scale.hip for raw device buffers).
+// Batch form (host only): bin the images first when the patches read every
+// pixel at least twice over (the two bin passes read W H bytes and write
+// 4 W H; the binned histogram saves ~6 VALU per patch pixel) and the batch
+// takes the quad kernel with a binned shape (11x11, 10x10).
+#ifndef ME_MI_BIN
+#define ME_MI_BIN 1  // (0: measurement build without the bin pass, tools/build_variant.sh)
+#endif
+extern "C" int me_mi_binned(int n, int pw, int ph, int width, int height) {
+  const bool shape = ME_MI_BIN && ((pw == 11 && ph == 11) || (pw == 10 && ph == 10));
+  return shape && n >= kGroupThreshold && (long)n * pw * ph >= 2L * width * height ? 1 : 0;
+}
+
+// Batch launcher.
 int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, int width, int height,
                        const int32_t* dxyL, const int32_t* dxyR, int n, int pw, int ph, float* dout) {
   if (n <= 0) return ME_OK;
@@ -944,6 +1098,25 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
   if (!mi_use_lane_kernel()) {
     const int qb = (int)std::min<long>(((long)n + kQuadGroups - 1) / kQuadGroups, 16384);
     const int tb = (int)(4 * mi_tab_size(npx));
+    if (me_mi_binned(n, pw, ph, width, height)) {
+      // bin both images once (mi_bin_kernel), then the histogram is three VALU per pixel
+      const int os = (width + 1) & ~1;
+      const size_t plane = 2 * (size_t)os * height;
+      void* bins;
+      ME_TRY(me_scratch(c, SLOT_MI_BIN, 2 * plane + 128, &bins));
+      uint8_t* bl = static_cast<uint8_t*>(bins);
+      uint8_t* br = bl + plane + 64;  // 64 bytes past each plane: the last row's 6-dword loads
+      hipLaunchKernelGGL(mi_bin_kernel, dim3((os / 4 + 1 + 255) / 256, height, 2), dim3(256), 0, c->stream, dL, sL, dR,
+                         sR, width, height, os, reinterpret_cast<uint32_t*>(bl), reinterpret_cast<uint32_t*>(br));
+      ME_TRY(me_check_launch(c, "mi_bin_kernel"));
+      if (pw == 11)
+        hipLaunchKernelGGL((mi_quad_kernel<11, 11, false, true>), dim3(qb), dim3(kQuadBlock), 0, c->stream, bl, os, br,
+                           os, 0L, 0L, dxyL, dxyR, n, pw, ph, tab, tb, dout);
+      else
+        hipLaunchKernelGGL((mi_quad_kernel<10, 10, false, true>), dim3(qb), dim3(kQuadBlock), 0, c->stream, bl, os, br,
+                           os, 0L, 0L, dxyL, dxyR, n, pw, ph, tab, tb, dout);
+      return me_check_launch(c, "mi_quad_kernel<bin>");
+    }
     if (pw == 11 && ph == 11)
       hipLaunchKernelGGL((mi_quad_kernel<11, 11>), dim3(qb), dim3(kQuadBlock), 0, c->stream, dL, sL, dR, sR,
                          img_bytes_L, img_bytes_R, dxyL, dxyR, n, pw, ph, tab, tb, dout);
