@@ -121,11 +121,6 @@ int me_hbm_copy_gbs(me_ctx* ctx, size_t bytes, int reps, double* gbs);
 int me_mi_scores(me_ctx* ctx, me_mem mem, const uint8_t* imgL, int strideL, const uint8_t* imgR, int strideR,
                  int width, int height, const int32_t* xyL, const int32_t* xyR, int n, int patch_w, int patch_h,
                  float* mi_out);
-/* 1 when me_mi_scores bins both images once before the batch (11x11 or
-   10x10 patches, n >= 32 768 pairs, n patch_w patch_h >= 2 width height:
-   every pixel read twice over), else 0.  Same results either way (bit-exact);
-   host only, a throughput choice with no environment override. */
-int me_mi_binned(int n, int patch_w, int patch_h, int width, int height);
 /* Whole-patch form (any size, the literal computeMutualInformation(L, R)). */
 int me_mutual_information(me_ctx* ctx, me_mem mem, const uint8_t* L, int strideL, const uint8_t* R, int strideR,
                           int w, int h, float* mi_out);

@@ -49,30 +49,6 @@ def test_mi_large_batch_bit_exact(ctx, oracle, patch):
     assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
 
 
-@pytest.mark.parametrize("patch", [(11, 11), (10, 10)])
-def test_mi_binned_and_direct_batches_bit_exact(ctx, oracle, patch):
-    """The batch kernel reads binned images (one u16 joint-update word per
-    pixel) when the patches cover every pixel twice over, else the u8 images:
-    both forms against the oracle, corners on every image edge (the binned
-    rows' 6-dword loads of the last pixels read into the planes' padding)."""
-    from uasl_motion_estimation_amd import _lib
-    from uasl_motion_estimation_amd.mutual_information import mi_scores
-
-    lib = _lib.load_library()
-    pw, ph = patch
-    for (W, H, n), binned in (((1920, 1080, 32768), 0), ((333, 211, 50000), 1), ((1281, 720, 40000), 1)):
-        assert lib.me_mi_binned(n, pw, ph, W, H) == binned
-        L, R, xyL, xyR = S.random_patches(300 + W, W, H, n, pw, ph)
-        xyL[:300, 0] = W - pw
-        xyL[300:600, 1] = H - ph
-        xyR[600:900] = [W - pw, H - ph]
-        xyR[900:1200] = [0, 0]
-        xyL[1200:1500, 0] = np.arange(300) % 2  # both pixel parities at the left edge
-        got = mi_scores(L, R, xyL, xyR, patch, ctx=ctx)
-        ref = oracle.mi_scores(L, R, xyL, xyR, pw, ph)
-        assert np.array_equal(bits(got), bits(ref)), (W, H, np.flatnonzero(bits(got) != bits(ref))[:10])
-
-
 def test_mi_edge_patches(ctx, oracle):
     from uasl_motion_estimation_amd.mutual_information import computeEntropy, computeMutualInformation
 

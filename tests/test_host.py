@@ -188,18 +188,3 @@ def test_scale_lm_launch_form_selection():
     assert "ME_SCALE_BLOCKS" not in src and "getenv(\"ME_SCALE" not in src
     assert "ME_SCALE_BLOCKS" not in open(os.path.join(ROOT, "bench.py")).read()
 
-
-def test_mi_binned_batch_selection():
-    """me_mi_binned (host only): the batch bins both images first for the
-    11x11 / 10x10 quad-kernel shapes when n >= 32 768 and the patches cover
-    every pixel at least twice (n pw ph >= 2 W H), otherwise it reads the u8
-    images directly."""
-    lib = _lib.load_library()
-    assert lib.me_mi_binned(1 << 20, 11, 11, 1280, 720) == 1  # bench: 1 M pairs on 720p
-    assert lib.me_mi_binned(1 << 20, 10, 10, 1280, 720) == 1
-    assert lib.me_mi_binned(32767, 11, 11, 64, 64) == 0  # below the quad-kernel batch size
-    assert lib.me_mi_binned(32768, 11, 11, 1920, 1080) == 0  # 3.96 M patch px < 2 x 2.07 M
-    assert lib.me_mi_binned(34274, 11, 11, 1920, 1080) == 0  # 4 147 154 < 4 147 200
-    assert lib.me_mi_binned(34275, 11, 11, 1920, 1080) == 1  # 4 147 275
-    assert lib.me_mi_binned(1 << 20, 12, 12, 64, 64) == 0  # generic shape
-    assert lib.me_mi_binned(1 << 20, 11, 10, 64, 64) == 0

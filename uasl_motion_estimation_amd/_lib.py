@@ -153,7 +153,7 @@ EXPORTS = [
     "me_get_stream", "me_set_cu_mask", "me_stream_flags", "me_cu_count", "me_synchronize", "me_malloc", "me_free", "me_memcpy_h2d", "me_memcpy_d2h", "me_memcpy_d2d",
     "me_memcpy_async", "me_host_alloc", "me_host_free", "me_hbm_copy_gbs",
     "me_timing_enable", "me_timing_read", "me_timing_reset", "me_timing_sample",
-    "me_mi_scores", "me_mi_binned", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
+    "me_mi_scores", "me_mutual_information", "me_entropy", "me_mi_epipolar_match", "me_mi_epipolar_match_count", "me_vo_new_cells", "me_compare_pc", "me_ccoeff_normed", "me_quantise",
     "me_optim_default_params", "me_scale_residuals", "me_scale_normal_equations", "me_scale_jacobian",
     "me_scale_optimise", "me_scale_last_counters", "me_scale_persistent", "me_scale_state_mi", "me_scale_inliers",
     "me_ba_default_options", "me_ba_solve", "me_ba_cost", "me_ba_evaluate", "me_ba_reduced_system",
@@ -254,7 +254,6 @@ def load_library(path: str | None = None):
                                       P(c_double), c_int, P(c_long)]),
         "me_scale_last_counters": (c_int, [c_void_p, P(c_long), P(c_long), P(c_long), P(c_long)]),
         "me_scale_persistent": (c_int, [c_int, c_int]),
-        "me_mi_binned": (c_int, [c_int, c_int, c_int, c_int, c_int]),
         "me_scale_state_mi": (c_int, [c_void_p, P(ScaleStateC), P(c_double), P(c_int)]),
         "me_scale_inliers": (c_int, [c_void_p, P(ScaleStateC), c_int, c_double, P(c_int), c_int, P(c_int)]),
         "me_ba_default_options": (None, [P(BAOptionsC)]),

@@ -121,6 +121,6 @@ struct me_ktimer {
 enum {
   SLOT_IMG_L = 0, SLOT_IMG_R, SLOT_XY_L, SLOT_XY_R, SLOT_MI_OUT, SLOT_RED, SLOT_GENERIC,
   SLOT_SC_TRACKS, SLOT_SC_RES, SLOT_SC_RES2, SLOT_SC_NEQ, SLOT_SC_IMGL, SLOT_SC_IMGR,
-  SLOT_KLT_PYR, SLOT_KLT_PTS, SLOT_NMS, SLOT_VO, SLOT_EPI, SLOT_MONO, SLOT_MI_BIN,
+  SLOT_KLT_PYR, SLOT_KLT_PTS, SLOT_NMS, SLOT_VO, SLOT_EPI, SLOT_MONO,
   SLOT_COUNT
 };

@@ -365,6 +365,12 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t quad_perm(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
 }
+// lane QQ of each quad's value, to all four lanes
+template <int QQ>
+__device__ __forceinline__ float bcast_lane(float v) {
+  // (old = +0.0f, the add's identity: the DPP folds into the consuming v_add_f32)
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), QQ * 0x55, 0xf, 0xf, false));
+}
 __device__ __forceinline__ uint32_t quad_sum(uint32_t v) {
   v += quad_perm<0xB1>(v);     // lanes [1,0,3,2]
   return v + quad_perm<0x4E>(v);  // lanes [2,3,0,1]
@@ -425,94 +431,7 @@ __device__ __forceinline__ void quad_hist(uint32_t* hg, const uint8_t* __restric
   }
 }
 
-// Binned images for large batches (every pixel is read by ~n pw ph / (W H)
-// patches: at 1 M 11x11 pairs on 720p, 130 times).  One pass writes a u16
-// word per pixel whose sum over a left / right pixel pair IS the joint update:
-//   left  320 bl                              (= 64 x the row's first word, 5 bl)
-//   right 64 (br >> 2) | 8 (br & 3)           (word within the row, byte shift)
-// so s = L + R has the LDS byte offset of word 5 bl + br / 4 in bits 6.. and
-// the byte's shift in bits 0..4 (bit 5 clear): ds_add at (s & ~63) | 4 g of
-// 1 << s -- three VALU per pixel instead of nine (two byte multiplies, two
-// shifts, the code, its word, its shift), and one 32-bit add sums two pixels
-// (each half <= 6 080 + 280 < 2^16: no carry crosses).
-__device__ __forceinline__ uint32_t mi_bin_word(uint32_t b, bool right) {
-  return right ? ((b >> 2) << 6) | ((b & 3) << 3) : 320u * b;
-}
-
-// Both images in one launch (blockIdx.z: left / right), four pixels per lane.
-__global__ void mi_bin_kernel(const uint8_t* __restrict__ imgL, int strideL, const uint8_t* __restrict__ imgR,
-                              int strideR, int width, int height, int ostride, uint32_t* __restrict__ outL,
-                              uint32_t* __restrict__ outR) {
-  const bool right = blockIdx.z != 0;
-  const uint8_t* row = (right ? imgR : imgL) + (long)blockIdx.y * (right ? strideR : strideL);
-  uint32_t* orow = (right ? outR : outL) + (long)blockIdx.y * (ostride >> 1);
-  const int x = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
-  if (x >= ostride) return;
-  uint32_t px = 0;
-  if (x + 3 < width && ((uintptr_t)(row + x) & 3) == 0) {
-    px = *reinterpret_cast<const uint32_t*>(row + x);
-  } else {
-#pragma unroll
-    for (int h = 0; h < 4; ++h)
-      if (x + h < width) px |= (uint32_t)row[x + h] << (8 * h);
-  }
-  uint32_t w[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-    w[h] = mi_bin_word((uint32_t)bin20((int)((px >> (16 * h)) & 0xff)), right) |
-           (mi_bin_word((uint32_t)bin20((int)((px >> (16 * h + 8)) & 0xff)), right) << 16);
-  orow[x >> 1] = w[0];
-  if (x + 2 < ostride) orow[(x >> 1) + 1] = w[1];
-}
-
-// One patch's histogram from the binned images (u16 rows of ostride words,
-// every row start 4-byte aligned; the scratch holds 64 bytes past the last
-// row): lane q takes rows q, q + 4, ...  Each row is 6 aligned dwords from the
-// pixel's dword down, realigned by its 0 / 2-byte offset.
-template <int PW, int PH>
-__device__ __forceinline__ void quad_hist_bin(uint8_t* ldsb, const uint16_t* __restrict__ bL,
-                                              const uint16_t* __restrict__ bR, int ostride, long oL, long oR, int q,
-                                              uint32_t gb) {
-  static_assert(PW >= 2 && PW <= 11 && PH > 0, "binned rows: 6 dwords");
-  constexpr int kRows = (PH + 3) / 4, kD = (PW + 1) / 2;
-  uint32_t dl[kRows][6], dr[kRows][6], al[kRows], ar[kRows];
-#pragma unroll
-  for (int rr = 0; rr < kRows; ++rr) {
-    const int r = q + 4 * rr;
-    if (r < PH) {
-      const char* pl = reinterpret_cast<const char*>(bL + oL + (long)r * ostride);
-      const char* pr = reinterpret_cast<const char*>(bR + oR + (long)r * ostride);
-      al[rr] = (uint32_t)(uintptr_t)pl & 3u;
-      ar[rr] = (uint32_t)(uintptr_t)pr & 3u;
-      // (pointer arithmetic, not an integer round trip: the loads stay global_load)
-      const uint32_t* ql = reinterpret_cast<const uint32_t*>(pl - al[rr]);
-      const uint32_t* qr = reinterpret_cast<const uint32_t*>(pr - ar[rr]);
-#pragma unroll
-      for (int d = 0; d < 6; ++d) {
-        dl[rr][d] = ql[d];
-        dr[rr][d] = qr[d];
-      }
-    }
-  }
-#pragma unroll
-  for (int rr = 0; rr < kRows; ++rr) {
-    if (q + 4 * rr < PH) {
-#pragma unroll
-      for (int d = 0; d < kD; ++d) {
-        const uint32_t l = __builtin_amdgcn_alignbyte(dl[rr][d + 1 < 6 ? d + 1 : d], dl[rr][d], al[rr]);
-        const uint32_t r = __builtin_amdgcn_alignbyte(dr[rr][d + 1 < 6 ? d + 1 : d], dr[rr][d], ar[rr]);
-        const uint32_t s = l + r;  // two pixels' joint updates
-        atomicAdd(reinterpret_cast<uint32_t*>(ldsb + ((s & 0xffc0u) | gb)), 1u << (s & 31u));
-        if (2 * d + 1 < PW) {
-          const uint32_t t = s >> 16;
-          atomicAdd(reinterpret_cast<uint32_t*>(ldsb + ((t & 0xffc0u) | gb)), 1u << (t & 31u));
-        }
-      }
-    }
-  }
-}
-
-template <int PW, int PH, bool EPI = false, bool BIN = false>
+template <int PW, int PH, bool EPI = false>
 __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __restrict__ imgL, int strideL,
                                                              const uint8_t* __restrict__ imgR, int strideR,
                                                              long bytesL, long bytesR,
@@ -553,11 +472,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
       oR = (long)cr.y * strideR + cr.x;
     }
     wave_sync();  // the previous pair's clears and slot reads precede this pair's updates
-    if constexpr (BIN) {
-      if (live)
-        quad_hist_bin<PW, PH>(reinterpret_cast<uint8_t*>(lds), reinterpret_cast<const uint16_t*>(imgL),
-                              reinterpret_cast<const uint16_t*>(imgR), strideL, oL, oR, q, 4u * (uint32_t)g);
-    } else if (live) {
+    if (live) {
       const int rows = PH > 0 ? PH : ph;
       const bool fast = oL >= 3 && oR >= 3 && oL + (long)(rows - 1) * strideL + 16 <= bytesL &&
                         oR + (long)(rows - 1) * strideR + 16 <= bytesR;
@@ -646,7 +561,7 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
     }
     wave_sync();  // right marginal, row table and starts visible to the quad
     const int s0 = (q * total) >> 2, nq = (((q + 1) * total) >> 2) - s0;
-    const int tmax = wave_max(nq);
+    const int tmax = __builtin_amdgcn_readfirstlane(wave_max(nq));  // (uniform: scalar branches)
     const uint8_t* crb = reinterpret_cast<const uint8_t*>(hg + 16 * QS::kCR);
     const uint32_t* colw = hg + 16 * QS::kCR;  // (packed layout)
     const uint8_t* jnt = reinterpret_cast<const uint8_t*>(hg);
@@ -727,24 +642,32 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
         }
       }
 #pragma unroll
-      for (int t = 0; t < QS::kMaxT; ++t) {
-        if (t >= tmax) break;
-        MI += T[t];
+      for (int t = 0; t < QS::kMaxT; t += kU) {
+        if (t < tmax) {  // (uniform guards, not breaks: the sums stay unrolled, T stays in registers)
+#pragma unroll
+          for (int u = 0; u < kU; ++u) MI += T[t + u];
+        }
       }
 #pragma unroll
-      for (int t = 0; t < QS::kMaxT; ++t) {
-        if (t >= tmax) break;
-        MI += __builtin_bit_cast(float, (int)quad_perm<0x55>(__builtin_bit_cast(uint32_t, T[t])));
+      for (int t = 0; t < QS::kMaxT; t += kU) {
+        if (t < tmax) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) MI += bcast_lane<1>(T[t + u]);
+        }
       }
 #pragma unroll
-      for (int t = 0; t < QS::kMaxT; ++t) {
-        if (t >= tmax) break;
-        MI += __builtin_bit_cast(float, (int)quad_perm<0xAA>(__builtin_bit_cast(uint32_t, T[t])));
+      for (int t = 0; t < QS::kMaxT; t += kU) {
+        if (t < tmax) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) MI += bcast_lane<2>(T[t + u]);
+        }
       }
 #pragma unroll
-      for (int t = 0; t < QS::kMaxT; ++t) {
-        if (t >= tmax) break;
-        MI += __builtin_bit_cast(float, (int)quad_perm<0xFF>(__builtin_bit_cast(uint32_t, T[t])));
+      for (int t = 0; t < QS::kMaxT; t += kU) {
+        if (t < tmax) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) MI += bcast_lane<3>(T[t + u]);
+        }
       }
       wave_sync();  // the walk's joint reads precede the clears
 #pragma unroll
@@ -1057,18 +980,6 @@ extern "C" int me_mi_epipolar_match_count(me_ctx* c, const uint8_t* imgL, const 
                          unique, ratio, margin, xr_out, ok_out);
 }
 
-// Batch form (host only): bin the images first when the patches read every
-// pixel at least twice over (the two bin passes read W H bytes and write
-// 4 W H; the binned histogram saves ~6 VALU per patch pixel) and the batch
-// takes the quad kernel with a binned shape (11x11, 10x10).
-#ifndef ME_MI_BIN
-#define ME_MI_BIN 1  // (0: measurement build without the bin pass, tools/build_variant.sh)
-#endif
-extern "C" int me_mi_binned(int n, int pw, int ph, int width, int height) {
-  const bool shape = ME_MI_BIN && ((pw == 11 && ph == 11) || (pw == 10 && ph == 10));
-  return shape && n >= kGroupThreshold && (long)n * pw * ph >= 2L * width * height ? 1 : 0;
-}
-
 // Batch launcher.
 int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, int sR, int width, int height,
                        const int32_t* dxyL, const int32_t* dxyR, int n, int pw, int ph, float* dout) {
@@ -1098,25 +1009,6 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
   if (!mi_use_lane_kernel()) {
     const int qb = (int)std::min<long>(((long)n + kQuadGroups - 1) / kQuadGroups, 16384);
     const int tb = (int)(4 * mi_tab_size(npx));
-    if (me_mi_binned(n, pw, ph, width, height)) {
-      // bin both images once (mi_bin_kernel), then the histogram is three VALU per pixel
-      const int os = (width + 1) & ~1;
-      const size_t plane = 2 * (size_t)os * height;
-      void* bins;
-      ME_TRY(me_scratch(c, SLOT_MI_BIN, 2 * plane + 128, &bins));
-      uint8_t* bl = static_cast<uint8_t*>(bins);
-      uint8_t* br = bl + plane + 64;  // 64 bytes past each plane: the last row's 6-dword loads
-      hipLaunchKernelGGL(mi_bin_kernel, dim3((os / 4 + 1 + 255) / 256, height, 2), dim3(256), 0, c->stream, dL, sL, dR,
-                         sR, width, height, os, reinterpret_cast<uint32_t*>(bl), reinterpret_cast<uint32_t*>(br));
-      ME_TRY(me_check_launch(c, "mi_bin_kernel"));
-      if (pw == 11)
-        hipLaunchKernelGGL((mi_quad_kernel<11, 11, false, true>), dim3(qb), dim3(kQuadBlock), 0, c->stream, bl, os, br,
-                           os, 0L, 0L, dxyL, dxyR, n, pw, ph, tab, tb, dout);
-      else
-        hipLaunchKernelGGL((mi_quad_kernel<10, 10, false, true>), dim3(qb), dim3(kQuadBlock), 0, c->stream, bl, os, br,
-                           os, 0L, 0L, dxyL, dxyR, n, pw, ph, tab, tb, dout);
-      return me_check_launch(c, "mi_quad_kernel<bin>");
-    }
     if (pw == 11 && ph == 11)
       hipLaunchKernelGGL((mi_quad_kernel<11, 11>), dim3(qb), dim3(kQuadBlock), 0, c->stream, dL, sL, dR, sR,
                          img_bytes_L, img_bytes_R, dxyL, dxyR, n, pw, ph, tab, tb, dout);
