@@ -439,7 +439,7 @@ def compare(g, o):
 # flops are the useful FP64 MFMA flops (no padding).  cam_solve (BA_SOLVE)
 # is a single-workgroup dependency chain with no HBM/MFMA roofline.
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-MI_COUNTERS = "r06_mi_base_sq"  # SQ counters of the current batch MI kernel (tools/gpu.sh sq)
+MI_COUNTERS = "r06_mi_reg"  # SQ counters of the current batch MI kernel (tools/gpu.sh sq)
 PEAK_F64_MFMA_TFS = 78.6   # MI355X FP64 matrix spec
 
 
