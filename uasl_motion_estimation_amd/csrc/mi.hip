@@ -603,8 +603,10 @@ __global__ __launch_bounds__(kQuadBlock) void mi_quad_kernel(const uint8_t* __re
           const int a = (int)max(cL, cR), b = (int)min(cL, cR);
           idx = mi_c3(a) + (int)(mul_u24((uint32_t)b, (uint32_t)(b - 1)) >> 1) + (int)cJ;
         }
-        const int off = t + u < nq ? 4 * (idx - 1) : 0x7ffffff0;
-        v[u] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, off, 0, 0));
+        // lanes past their run issue no gather (exec-masked: no address work in the TA)
+        float tv = 0.0f;
+        if (t + u < nq) tv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rtab, 4 * (idx - 1), 0, 0));
+        v[u] = tv;
         // next non-empty row of the compacted table (read one ahead)
         const bool z = bits == 0u;
         bits = z ? (nxt & 0xfffffu) : bits;
