@@ -49,6 +49,52 @@ def test_mi_large_batch_bit_exact(ctx, oracle, patch):
     assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
 
 
+def _tile_patterns(patterns, W, H, n, rng):
+    """Images holding the given 11x11 (L, R) patch patterns side by side, and
+    n corner pairs that each select one pattern (both images at the same spot)."""
+    L = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    R = rng.integers(0, 256, (H, W)).astype(np.uint8)
+    per_row = W // 11
+    corners = []
+    for i, (pl, pr) in enumerate(patterns):
+        y, x = 11 * (i // per_row), 11 * (i % per_row)
+        L[y:y + 11, x:x + 11] = pl
+        R[y:y + 11, x:x + 11] = pr
+        corners.append((x, y))
+    pick = rng.integers(0, len(corners), n)
+    xy = np.array(corners, np.int32)[pick]
+    return L, R, np.ascontiguousarray(xy), np.ascontiguousarray(xy.copy())
+
+
+def test_mi_batch_extreme_bin_patterns(ctx, oracle):
+    """The batch kernel's bounds: a pair with 121 distinct joint bins (a lane
+    run of 31 terms, the register array's limit), every one of the 20 rows
+    populated (the row table full, its two sentinels right after), a single
+    bin (one lane does all), one bin per row down the diagonal, and random
+    pairs, mixed in every 16-pair wave (>= 32768 pairs: the quad kernel)."""
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    rng = np.random.default_rng(11)
+    mid = lambda b: np.uint8(min(255, (64 * b + 63) // 5))  # noqa: E731  a value in bin b ((5 v) >> 6 == b)
+    assert all((5 * int(mid(b))) >> 6 == b for b in range(20))
+    pats = []
+    codes = rng.permutation(400)[:121]  # 121 distinct joint bins
+    pats.append((np.array([mid(c // 20) for c in codes], np.uint8).reshape(11, 11),
+                 np.array([mid(c % 20) for c in codes], np.uint8).reshape(11, 11)))
+    rows = np.concatenate([np.arange(20).repeat(6), [19]])  # all 20 rows, 6-7 pixels each, random columns
+    pats.append((np.array([mid(r) for r in rows], np.uint8).reshape(11, 11),
+                 np.array([mid(c) for c in rng.integers(0, 20, 121)], np.uint8).reshape(11, 11)))
+    pats.append((np.full((11, 11), mid(7), np.uint8), np.full((11, 11), mid(13), np.uint8)))  # one bin
+    diag = np.array([mid(r) for r in rows], np.uint8).reshape(11, 11)
+    pats.append((diag, diag.copy()))  # 20 rows, one bin each
+    for _ in range(4):
+        pats.append((rng.integers(0, 256, (11, 11)).astype(np.uint8), rng.integers(0, 256, (11, 11)).astype(np.uint8)))
+    L, R, xyL, xyR = _tile_patterns(pats, 11 * 8, 11 * 2, 40000, rng)
+    got = mi_scores(L, R, xyL, xyR, (11, 11), ctx=ctx)
+    ref = oracle.mi_scores(L, R, xyL, xyR, 11, 11)
+    assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
+
+
 def test_mi_edge_patches(ctx, oracle):
     from uasl_motion_estimation_amd.mutual_information import computeEntropy, computeMutualInformation
 
