@@ -185,23 +185,75 @@ struct GroupHist {
   uint32_t* h;  // kGroupWords words of this group: histogram then float terms
   int gl;       // lane within the group
   __device__ __forceinline__ void clear() {
-    for (int i = gl; i < kHistWords; i += G) h[i] = 0u;
+    for (int i = gl; i < 100; i += G) h[i] = 0u;  // the joint words (mi() rewrites the rest)
     wave_sync();
   }
+  // one packed-byte joint update per pixel; the marginals and the occupancy
+  // bitmap are derived from the joint words in mi() (round 6: the marginal and
+  // bitmap atomics, 16 lanes hammering 10 + 13 words, were three quarters of
+  // the LDS atomics)
   __device__ __forceinline__ void add(int vl, int vr) {
     int bl = bin20(vl), br = bin20(vr);
     int code = bl * 20 + br;
     atomicAdd(&h[code >> 2], 1u << ((code & 3) * 8));
-    atomicAdd(&h[100 + (bl >> 2)], 1u << ((bl & 3) * 8));
-    atomicAdd(&h[105 + (br >> 2)], 1u << ((br & 3) * 8));
-    atomicOr(&h[110 + (code >> 5)], 1u << (code & 31));
+  }
+  // packed-byte sum over the group's 16 lanes (one DPP row; every byte sum
+  // <= 121 pixels: no carry crosses a byte)
+  __device__ __forceinline__ static uint32_t row_sum_u8x4(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);   // quad [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);   // quad [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);  // row half mirror
+    v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false);  // row mirror
+    return v;
+  }
+  // Left marginals (row sums), right marginals (column sums) and the bitmap of
+  // non-empty bins from the joint words; returns this lane's bitmap word
+  // (codes 32 gl .. 32 gl + 31).  Called by all 16 lanes after a wave_sync.
+  __device__ __forceinline__ uint32_t derive() {
+    uint32_t col[5] = {0u, 0u, 0u, 0u, 0u};
+    uint8_t* lm = reinterpret_cast<uint8_t*>(h + 100);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int r = gl + 16 * k;
+      if (r < 20) {
+        uint32_t s = 0u;
+#pragma unroll
+        for (int m = 0; m < 5; ++m) {
+          const uint32_t w = h[5 * r + m];
+          s = __builtin_amdgcn_sad_u8(w, 0u, s);
+          col[m] += w;
+        }
+        lm[r] = (uint8_t)s;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 5; ++m) col[m] = row_sum_u8x4(col[m]);
+    if (gl < 5) {
+      uint32_t c = col[0];
+#pragma unroll
+      for (int m = 1; m < 5; ++m) c = gl == m ? col[m] : c;
+      h[105 + gl] = c;
+    }
+    uint32_t bits = 0u;
+    if (gl < 13) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int w8 = 8 * gl + k;
+        if (w8 < 100) {
+          const uint32_t f = (h[w8] + 0x7f7f7f7fu) & 0x80808080u;  // bit 7 of a byte: count > 0
+          bits |= ((f * 0x00204081u) >> 28) << (4 * k);
+        }
+      }
+    }
+    return bits;
   }
   // Returns the MI in lane gl == 0 of the group (other lanes: unspecified).
   // tab: the per-N term table (bit-identical values, one gather per term) or null.
   __device__ __forceinline__ float mi(float invN, const float* __restrict__ tab = nullptr) {
     wave_sync();
     float* terms = reinterpret_cast<float*>(h + kHistWords);
-    uint32_t bits = gl < 13 ? h[110 + gl] : 0u;
+    uint32_t bits = derive();
+    wave_sync();  // the marginals visible to the group
     const int cnt = __builtin_popcount(bits);
     int pre = cnt;
 #pragma unroll
