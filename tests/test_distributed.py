@@ -514,6 +514,7 @@ def test_bench_world2_gloo_sharded_branch(tmp_path):
     gi = sb["gate_inputs"]
     cal = gi["calibrated_exchange_us"]
     assert cal["system"] > 0 and cal["scalars"] > 0
-    assert gi["per_exchange_us"] == round(0.5 * (cal["system"] + cal["scalars"]), 2)
+    # (both sides rounded to 0.01 us: compare within one rounding step)
+    assert abs(gi["per_exchange_us"] - 0.5 * (cal["system"] + cal["scalars"])) <= 0.011
     from uasl_motion_estimation_amd.optimisation import shard_worthwhile
     assert sb["gate_would_shard"] == shard_worthwhile(100010, 2, 0.5 * (cal["system"] + cal["scalars"]))

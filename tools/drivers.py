@@ -255,6 +255,33 @@ def cmd_scale_ts(a):
     print(f"  ns per executed track evaluation: {1e3 * buf[2] / L / 100.0 / max(evals, 1):.2f}")
 
 
+def cmd_cam_ts(a):
+    """Camera (0, 0)'s assembly workgroup phases (a -DME_CAM_TS=1 build): the
+    slot loop (loads + residual/Jacobian + sums), block_sum<27>, partial stores +
+    arrival, and (when last) the camera reduce; s_memtime ticks per execution."""
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions
+    ctx = _setup(a.lib)
+    fn = ctx.lib.me_cam_ts
+    fn.argtypes = [ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+    buf = (ctypes.c_longlong * 8)()
+    d = DeviceBAProblem(_ba_problem(a.config), ctx)
+    o = SolverOptions.fixed_iterations(10)
+    for _ in range(3):
+        d.reset()
+        d.solve(o)
+    ctx.synchronize()
+    fn(buf, 1)
+    for _ in range(20):
+        d.reset()
+        d.solve(o)
+    ctx.synchronize()
+    fn(buf, 0)
+    n = max(buf[0], 1)
+    print(json.dumps({"executions": buf[0], "slot_loop": round(buf[1] / n), "block_sum27": round(buf[2] / n),
+                      "store_arrive": round(buf[3] / n), "times_last": buf[5],
+                      "reduce_when_last": round(buf[4] / max(buf[5], 1))}))
+
+
 def cmd_schur_stamps(a):
     from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
     ctx = _setup(a.lib)
@@ -288,6 +315,8 @@ def main():
     p.add_argument("configs", nargs="?", default="3,5")
     p = sub.add_parser("scale_ts")
     p.add_argument("--front", type=int, default=0)
+    p = sub.add_parser("cam_ts")
+    p.add_argument("--config", default="3")
     p = sub.add_parser("schur_stamps")
     p.add_argument("configs", nargs="?", default="3,4")
     a = ap.parse_args()

@@ -393,12 +393,32 @@ __device__ void cam_reduce_body(const Geo& g, const Bufs& b, int sharded, const 
 // workgroups of camera c to finish adds the ck partials in order.
 // Threads 0 .. kBlock-1 of the block take part (in a wider block the other
 // waves have exited: barriers count only live waves).
+#ifdef ME_CAM_TS  // timing experiment only: phase split of camera (0, 0)'s assembly workgroup, s_memtime ticks
+__device__ unsigned long long g_cam_ts[8];
+#define CAM_T(i)                                                                           \
+  do {                                                                                     \
+    if (ci == 0 && k == 0 && threadIdx.x == 0) {                                           \
+      const long long t_ = (long long)__builtin_amdgcn_s_memtime();                        \
+      if ((i) > 0) atomicAdd(&g_cam_ts[(i)], (unsigned long long)(t_ - cam_prev_));        \
+      else atomicAdd(&g_cam_ts[0], 1ull);                                                  \
+      cam_prev_ = t_;                                                                      \
+    }                                                                                      \
+  } while (0)
+#else
+#define CAM_T(i) \
+  do {           \
+  } while (0)
+#endif
 template <int OD>
 __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, double* cpart, int sharded,
                                                   double* colnorm, double* gc_raw, double* Uraw, int ci, int k) {
-  __shared__ double lds[4 * 27];
+  __shared__ double rows[kBlock / 16 * 27];
   const State* st = b.st;
   if (st->done || !st->need_lin) return;
+#ifdef ME_CAM_TS
+  long long cam_prev_ = 0;
+#endif
+  CAM_T(0);
   const int beg = b.c_off[ci], end = b.c_off[ci + 1];
   double v[27];
   for (int i = 0; i < 27; ++i) v[i] = 0;
@@ -422,14 +442,38 @@ __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, d
         v[u] += Jc[a] * Jc[c] + Jc[6 + a] * Jc[6 + c] + Jc[12 + a] * Jc[12 + c] + Jc[18 + a] * Jc[18 + c];
     for (int a = 0; a < 6; ++a) v[21 + a] += Jc[a] * r[0] + Jc[6 + a] * r[1] + Jc[12 + a] * r[2] + Jc[18 + a] * r[3];
   }
-  double out[27];
-  block_sum<27>(v, out, lds, kBlock / 64);
-  if (threadIdx.x == 0) {  // written through for the last of the camera's workgroups (no release per arrival)
-    double* P = cpart + 27 * ((long)ci * g.ck + k);
-    for (int u = 0; u < 27; ++u) a_st<true>(&P[u], out[u]);
+  CAM_T(1);
+  // the 27 sums: 16-lane row sums by DPP (VALU only), the 16 row sums of the
+  // block through LDS, thread u < 27 adds component u's in row order (round 6:
+  // 4.2 -> see DESIGN §5.4 us; six dependent lane-shuffle rounds per value before)
+#pragma unroll
+  for (int u = 0; u < 27; ++u) {
+    double x = v[u];
+    x += dpp_f64<kDppQuadSwap1>(x);
+    x += dpp_f64<kDppQuadSwap2>(x);
+    x += dpp_f64<kDppRowHalfMirror>(x);
+    x += dpp_f64<kDppRowMirror>(x);
+    v[u] = x;
   }
-  if (!last_arrival_wt(b.cnt + ci, g.ck)) return;
+  if ((threadIdx.x & 15) == 0)
+#pragma unroll
+    for (int u = 0; u < 27; ++u) rows[(threadIdx.x >> 4) * 27 + u] = v[u];
+  __syncthreads();
+  CAM_T(2);
+  if (threadIdx.x < 27) {  // written through for the last of the camera's workgroups (no release per arrival)
+    double sum = 0.0;
+#pragma unroll
+    for (int r = 0; r < kBlock / 16; ++r) sum += rows[r * 27 + threadIdx.x];
+    a_st<true>(&cpart[27 * ((long)ci * g.ck + k) + threadIdx.x], sum);  // (lanes of wave 0: its vmcnt drain covers them)
+  }
+  const bool last = last_arrival_wt(b.cnt + ci, g.ck);
+  CAM_T(3);
+  if (!last) return;
   cam_reduce_body(g, b, sharded, cpart, colnorm, gc_raw, Uraw, ci);
+  CAM_T(4);
+#ifdef ME_CAM_TS
+  if (ci == 0 && k == 0 && threadIdx.x == 0) atomicAdd(&g_cam_ts[5], 1ull);
+#endif
 }
 
 __global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, double* cpart, int sharded,
@@ -447,6 +491,7 @@ __global__ __launch_bounds__(kBlock) void cam_assemble_kernel(Geo g, Bufs b, dou
 struct CamArgs {
   double *cpart, *colnorm, *gc_raw, *Uraw;
   int on;
+  int ncam;  // leading workgroups of the launch that assemble cameras (m ck, padded to whole rounds of 8 XCDs)
 };
 
 // Sharded mode, first linearisation: the rank's input flags (bad index,
@@ -582,7 +627,7 @@ __device__ __forceinline__ int group_max(int x) {
 #ifdef ME_SCHUR_STAMPS  // timing experiment only (tools/drivers.py schur_stamps): workgroup 0's phase times in st->stamps[6..11]
 #define SCHUR_T(i)                                                                     \
   do {                                                                                 \
-    if (blockIdx.x == 0 && threadIdx.x == 0) {                                         \
+    if (sblk == 0 && threadIdx.x == 0) {                                               \
       const long long tt_ = (long long)__builtin_amdgcn_s_memtime();                   \
       if ((i) > 0) st->stamps[5 + (i)] += tt_ - sch_prev_;                             \
       sch_prev_ = tt_;                                                                 \
@@ -598,20 +643,25 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   constexpr int SL = BLK / PTS, NW = BLK / 64;  // lanes per landmark, waves
   extern __shared__ double smem[];
   __shared__ double red[8];
-  if (ca.on && (int)blockIdx.x >= g.ksplit) {  // camera-assembly blocks of a fused launch
+  // camera-assembly blocks of a fused launch come first: dispatched before the
+  // Schur runs, their longer chain (slot loop, 27-value reduce, camera reduce)
+  // no longer trails the runs (round 6: the launch 14.8 -> see DESIGN §5.4)
+  if (ca.on && (int)blockIdx.x < ca.ncam) {
     if (threadIdx.x >= kBlock) return;
-    const int q = blockIdx.x - g.ksplit;
+    const int q = blockIdx.x;
+    if (q >= g.m * g.ck) return;  // (padding to a multiple of 8)
     if (g.od == 4)
       cam_assemble_body<4>(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
     else
       cam_assemble_body<2>(g, b, ca.cpart, 0, ca.colnorm, ca.gc_raw, ca.Uraw, q / g.ck, q % g.ck);
     return;
   }
+  const int sblk = (int)blockIdx.x - (ca.on ? ca.ncam : 0);  // this workgroup's index among the Schur runs
   State* st = b.st;
   if (st->done) return;
 #ifdef ME_SCHUR_STAMPS
   long long sch_prev_ = 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st->stamps[12] += 1;
+  if (sblk == 0 && threadIdx.x == 0) st->stamps[12] += 1;
 #endif
   SCHUR_T(0);
   const int need_lin = st->need_lin, scaled = st->scaled, cur = st->cur;
@@ -621,22 +671,22 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   // all allowed steps taken: this pass only evaluates the gradient for the
   // closing test (Ceres HandleSuccessfulStep); no Schur complement is needed
   const bool final_pass = st->iterations >= o.max_num_iterations;
-  if (blockIdx.x == 0 && threadIdx.x == 0) st->final_pass = final_pass;
+  if (sblk == 0 && threadIdx.x == 0) st->final_pass = final_pass;
   const int P = g.spts, Rz = g.Rpad, rows = 3 * P, nks = rows / 4;
   // this workgroup's run and tile group; the run's tile set is [bA, bB] plus the z tile T - 1
   // Workgroups are dealt round-robin over the 8 XCDs: a run's tile groups sit
   // at blocks b, b + 8, ... so they share an XCD's L2 -- the second group's
   // reads of the run's slots (W, obsx) hit the lines the first one fetched.
-  const int sup = blockIdx.x / (8 * g.sgrp), r8 = blockIdx.x - sup * 8 * g.sgrp;
+  const int sup = sblk / (8 * g.sgrp), r8 = sblk - sup * 8 * g.sgrp;
   const int run = 8 * sup + (r8 & 7), tgrp = r8 >> 3;
   if (run >= g.nruns) {  // (uniform) padding of the last block of 8 runs
-    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = 0.0;
+    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + sblk] = 0.0;
     return;
   }
   const int bA = g.sorted ? b.rband[2 * run] : 0, bB = g.sorted ? b.rband[2 * run + 1] : g.T - 1;
   const int nb = bB - bA + 1, ns = nb + (bB < g.T - 1 ? 1 : 0), ntile = ns * (ns + 1) / 2;
   if (tgrp * g.stpw >= ntile) {  // (uniform) the run's tiles are all taken by lower groups
-    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = 0.0;
+    if (need_lin && threadIdx.x == 0) b.part[R_GMAX_PT * g.pstride + sblk] = 0.0;
     return;
   }
   const bool lead = tgrp == 0;  // the run's first group writes the per-landmark results (the others recompute them)
@@ -886,7 +936,7 @@ __global__ __launch_bounds__(BLK) void pt_schur_kernel(Geo g, Bufs b, Opts o, Ca
   SCHUR_T(4);  // MFMA contraction (barrier)
   if (need_lin) {
     const double r = block_max(gm, red);
-    if (tid == 0) b.part[R_GMAX_PT * g.pstride + blockIdx.x] = r;
+    if (tid == 0) b.part[R_GMAX_PT * g.pstride + sblk] = r;
   }
   if (final_pass) return;
 #pragma unroll
@@ -3341,7 +3391,7 @@ int enqueue_linearize(Plan& P) {
   const bool first = P.n_enq == 0;
   const bool fused = !first && g.m > 0 && !P.sequential;
   ++P.n_enq;
-  CamArgs ca{P.cpart, P.colnorm, P.gc_raw, P.Uraw, fused ? 1 : 0};
+  CamArgs ca{P.cpart, P.colnorm, P.gc_raw, P.Uraw, fused ? 1 : 0, fused ? (g.m * g.ck + 7) / 8 * 8 : 0};
   if (g.m > 0 && !fused)
     hipLaunchKernelGGL(cam_assemble_kernel, dim3(g.m, g.ck), dim3(kBlock), 0, s, g, P.b, P.cpart, sh ? 1 : 0,
                        P.colnorm, P.gc_raw, P.Uraw);
@@ -3363,7 +3413,7 @@ int enqueue_linearize(Plan& P) {
     // budget is 256 registers -- up to 5 tiles nothing spills (9 tiles spilled
     // 120 B); wider windows take more tile groups per run instead.
     const int pw8 = g.stpw / 8;
-    const dim3 grd(g.ksplit + (fused ? g.m * g.ck : 0));
+    const dim3 grd(g.ksplit + ca.ncam);
 #define ME_SCHUR(N)                                                                                          \
   do {                                                                                                       \
     if (g.spts == kSchurPtsWide)                                                                             \
@@ -4186,3 +4236,16 @@ extern "C" int me_debug_read(me_ctx* c, long long* out, int n) {
   std::memcpy(out, c->dbg, 8 * (size_t)n);
   return ME_OK;
 }
+
+#ifdef ME_CAM_TS
+extern "C" int me_cam_ts(long long* out, int reset) {
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cam_ts), sizeof h) != hipSuccess) return -1;
+  for (int i = 0; i < 8; ++i) out[i] = (long long)h[i];
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_cam_ts), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
