@@ -427,7 +427,8 @@ __device__ __forceinline__ void cam_assemble_body(const Geo& g, const Bufs& b, d
     // the observation's residual and Jacobian at the linearisation point, as
     // linearize_kernel forms them (same function, same Huber scaling: the same
     // pieces bit for bit), then Jc^T Jc (21) and Jc^T r (6)
-    const int o = b.c_obs[q], pi = b.c_pt[q], cam = ci + g.nf;  // (slot q of variable camera ci)
+    const int o = b.c_obs[q];
+    const int cam = b.cam_idx[o], pi = b.pt_idx[o];
     double r[4], Jc[24], Jp[12];
     obs_residual<OD>(g, b, o, b.cams[cur] + 6 * cam, b.pts[cur] + 3 * pi, r, Jc, Jp);
     const double s2 = r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + r[3] * r[3];
@@ -2811,7 +2812,6 @@ __global__ __launch_bounds__(kBlock) void plan_scatter_kernel(Geo g, Bufs b) {
       for (int k = 0; k < t; ++k) rank += scam[k] == ci;
       slot = w.blk_cam[(long)blk * g.nc + ci] + rank;
       b.c_obs[slot] = o;
-      b.c_pt[slot] = b.pt_idx[o];
     }
     b.cpos[o] = slot;
   }
@@ -3198,7 +3198,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(4 * (size_t)g.no, &b.p_cam);
   add(4 * (size_t)(g.m + 1), &b.c_off);
   add(4 * (size_t)g.no, &b.c_obs);
-  add(4 * (size_t)g.no, &b.c_pt);
   add(4 * (size_t)g.no, &b.tmp_obs);
   add(4 * (size_t)g.no, &b.cpos);
   add(8 * kObsxStride * (size_t)g.no, &b.obsx);

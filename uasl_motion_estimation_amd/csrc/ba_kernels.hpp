@@ -96,7 +96,6 @@ struct Bufs {
   int* p_cam;         // CSR slot -> variable camera index (-1 fixed)
   int* c_off;         // CSR by variable camera (original observation order inside a camera)
   int* c_obs;
-  int* c_pt;          // the point of camera slot q (c_obs order): the camera assembly's loads in two rounds
   int* tmp_obs;       // plan: unsorted CSR-by-point slots
   int* cpos;          // obs -> slot in c_obs (-1: fixed camera)
   double* obsx;       // no * 9  (V_o, g_o unscaled)
