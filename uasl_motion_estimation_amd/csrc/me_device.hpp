@@ -177,7 +177,7 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kGroupTerms = 256;  // >= max non-empty joint bins (<= pixels <= 255)
-constexpr int kGroupWords = kHistWords + kGroupTerms;
+constexpr int kGroupWords = kHistWords + kGroupTerms + 16;  // + the balanced walk's 16 start words
 
 template <int G>
 struct GroupHist {
@@ -262,17 +262,43 @@ struct GroupHist {
       if (gl >= off) pre += t;
     }
     const int total = __shfl(pre, G - 1, G);
-    int idx = pre - cnt;
-    // four set bits per pass: the four terms' independent chains (division,
+    const int excl = pre - cnt;
+    // Balanced walk (round 6): lane q takes the slots [q T / 16, (q + 1) T / 16)
+    // of the T non-empty bins in code order, crossing bitmap words, instead of
+    // the bins of its own word (a patch's bins crowd a few rows: a few lanes
+    // had all the terms).  Each word's owner leaves the lanes whose first slot
+    // falls in its word their start (word, bins to skip).
+    uint32_t* bmw = h + 110;                        // the bitmap words, for the walkers
+    uint32_t* starts = h + kHistWords + kGroupTerms;  // one start word per lane
+    if (gl < 13) {
+      bmw[gl] = bits;
+      if (cnt > 0) {
+        const int qlo = (16 * excl + total - 1) / total, qhi = min(16, (16 * (excl + cnt) + total - 1) / total);
+        for (int q = qlo; q < qhi; ++q) starts[q] = (uint32_t)gl | ((uint32_t)(((q * total) >> 4) - excl) << 8);
+      }
+    }
+    wave_sync();  // bitmap words and starts visible to the group
+    const int s0 = (gl * total) >> 4, nq = (((gl + 1) * total) >> 4) - s0;
+    int w = 0;
+    uint32_t cur = 0u;
+    if (nq > 0) {
+      const uint32_t st = starts[gl];
+      w = (int)(st & 0xffu);
+      cur = bmw[w];
+      for (uint32_t sk = st >> 8; sk > 0; --sk) cur &= cur - 1u;
+    }
+    int idx = s0;
+    // four bins per pass: the four terms' independent chains (division,
     // log2f table reads, polynomial) overlap instead of running back to back
-    while (bits) {
+    for (int t = 0; t < nq; t += 4) {
       int code[4];
       bool ok[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        ok[u] = bits != 0u;
-        code[u] = ok[u] ? gl * 32 + __builtin_ctz(bits) : 0;
-        bits &= bits - 1u;
+        ok[u] = t + u < nq;
+        while (ok[u] && cur == 0u && w < 12) cur = bmw[++w];  // next non-empty word
+        code[u] = ok[u] ? w * 32 + __builtin_ctz(cur | 0x80000000u) : 0;
+        if (ok[u]) cur &= cur - 1u;
       }
       float tv[4];
 #pragma unroll
