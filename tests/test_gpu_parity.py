@@ -49,6 +49,26 @@ def test_mi_large_batch_bit_exact(ctx, oracle, patch):
     assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
 
 
+@pytest.mark.parametrize("patch", [(11, 11), (12, 16), (5, 3), (13, 13)])
+def test_mi_small_batch_edges_bit_exact(ctx, oracle, patch):
+    """< 32768 pairs take the 16-lane group kernel: its row form loads each
+    patch row as a 16-byte window (inside both images), else per-pixel bytes;
+    corners on the last row / column and the image's last byte exercise the
+    bound (odd width: rows not 4-byte aligned)."""
+    from uasl_motion_estimation_amd.mutual_information import mi_scores
+
+    pw, ph = patch
+    W, H = 97, 61
+    L, R, xyL, xyR = S.random_patches(400 + pw, W, H, 3000, pw, ph)
+    xyL[:200, 0] = W - pw
+    xyL[200:400, 1] = H - ph
+    xyR[400:600] = [W - pw, H - ph]
+    xyL[600:800] = [W - pw, H - ph]
+    got = mi_scores(L, R, xyL, xyR, patch, ctx=ctx)
+    ref = oracle.mi_scores(L, R, xyL, xyR, pw, ph)
+    assert np.array_equal(bits(got), bits(ref)), np.flatnonzero(bits(got) != bits(ref))[:10]
+
+
 def _tile_patterns(patterns, W, H, n, rng):
     """Images holding the given 11x11 (L, R) patch patterns side by side, and
     n corner pairs that each select one pattern (both images at the same spot)."""

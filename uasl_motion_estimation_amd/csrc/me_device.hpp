@@ -333,12 +333,47 @@ struct GroupHist {
   }
 };
 
-// Patch pair MI by a 16-lane group; pixels strided over the group.
+// Patch pair MI by a 16-lane group.  Row form (patches up to 12 x 16 whose
+// 16-byte row windows lie inside both images, endA / endB = one past each
+// image's last byte): lane r loads row r of both patches as one aligned
+// 16-byte window each and adds its pixels -- two vector loads per lane instead
+// of two byte loads per pixel (round 6: the scattered byte gathers were the
+// group MI's address-unit work).  Otherwise pixels strided over the group.
 template <bool BIN>
 __device__ __forceinline__ float group_mi(GroupHist<16>& h, const uint8_t* A, long astride, const uint8_t* B,
                                           long bstride, int pw, int ph, float invN,
-                                          const float* __restrict__ tab = nullptr) {
+                                          const float* __restrict__ tab = nullptr, const uint8_t* endA = nullptr,
+                                          const uint8_t* endB = nullptr) {
   h.clear();
+  if (endA && endB && pw <= 12 && ph <= 16) {
+    const uint8_t* la = A + (long)(ph - 1) * astride;
+    const uint8_t* lb = B + (long)(ph - 1) * bstride;
+    if (la - ((uintptr_t)la & 3) + 16 <= endA && lb - ((uintptr_t)lb & 3) + 16 <= endB) {  // (group-uniform)
+      if (h.gl < ph) {
+        const uint8_t* ra = A + (long)h.gl * astride;
+        const uint8_t* rb = B + (long)h.gl * bstride;
+        const uint32_t sa = (uint32_t)(uintptr_t)ra & 3u, sb = (uint32_t)(uintptr_t)rb & 3u;
+        const uint4 va = *reinterpret_cast<const uint4*>(ra - sa);
+        const uint4 vb = *reinterpret_cast<const uint4*>(rb - sb);
+        const uint32_t pa[3] = {__builtin_amdgcn_alignbyte(va.y, va.x, sa), __builtin_amdgcn_alignbyte(va.z, va.y, sa),
+                                __builtin_amdgcn_alignbyte(va.w, va.z, sa)};
+        const uint32_t pb[3] = {__builtin_amdgcn_alignbyte(vb.y, vb.x, sb), __builtin_amdgcn_alignbyte(vb.z, vb.y, sb),
+                                __builtin_amdgcn_alignbyte(vb.w, vb.z, sb)};
+#pragma unroll
+        for (int x = 0; x < 12; ++x) {
+          if (x < pw) {
+            int a = (int)((pa[x >> 2] >> (8 * (x & 3))) & 0xffu), b = (int)((pb[x >> 2] >> (8 * (x & 3))) & 0xffu);
+            if (BIN) {
+              a = a ? 255 : 0;
+              b = b ? 255 : 0;
+            }
+            h.add(a, b);
+          }
+        }
+      }
+      return h.mi(invN, tab);
+    }
+  }
   const int npx = pw * ph;
   // Pixels in batches of 8 per lane: every load of a batch is issued before
   // the first histogram update (pixels past the patch alias pixel 0 and are

@@ -736,7 +736,7 @@ __global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8
                                                                      const int32_t* __restrict__ xyL,
                                                                      const int32_t* __restrict__ xyR, int n, int pw,
                                                                      int ph, float invN, const float* __restrict__ tab,
-                                                                     float* __restrict__ out) {
+                                                                     float* __restrict__ out, long bytesL, long bytesR) {
   __shared__ uint32_t lds[(kGroupBlock / 16) * kGroupWords];
   const int grp = threadIdx.x >> 4;
   GroupHist<16> h{&lds[grp * kGroupWords], (int)(threadIdx.x & 15)};
@@ -744,7 +744,8 @@ __global__ __launch_bounds__(kGroupBlock) void mi_pairs_group_kernel(const uint8
     const int2 cl = reinterpret_cast<const int2*>(xyL)[k];
     const int2 cr = reinterpret_cast<const int2*>(xyR)[k];
     const float mi = group_mi<false>(h, imgL + (long)cl.y * strideL + cl.x, strideL,
-                                     imgR + (long)cr.y * strideR + cr.x, strideR, pw, ph, invN, tab);
+                                     imgR + (long)cr.y * strideR + cr.x, strideR, pw, ph, invN, tab, imgL + bytesL,
+                                     imgR + bytesR);
     if (h.gl == 0) out[k] = mi;
   }
 }
@@ -849,8 +850,9 @@ __global__ __launch_bounds__(kEpiBlock) void mi_epi_score_kernel(
     const bool ok = fv && xr >= 0 && d <= d_max && x0 >= 0 && y0 >= 0 && x0 + patch <= width &&
                     y0 + patch <= height;  // (group-uniform; both patches inside the image)
     float s = 0.0f;
+    const long end = (long)(height - 1) * stride + width;  // one past each image's last byte
     if (ok) s = group_mi<false>(h, L + (long)y0 * stride + x0, stride, R + (long)y0 * stride + xr, stride, patch, patch,
-                                invN);
+                                invN, nullptr, L + end, R + end);
     if (h.gl == 0) sc[q] = ok ? (double)s : -INFINITY;
   }
 }
@@ -989,19 +991,21 @@ int me_launch_mi_pairs(me_ctx* c, const uint8_t* dL, int sL, const uint8_t* dR, 
   me_ktimer t(c, ME_KT_MI);
   const float* gtab;  // the group kernels' terms come from the same per-N table
   ME_TRY(me_mi_table(c, pw * ph, &gtab));
+  // one past each image's last byte (the row windows' bound)
+  const long endL = (long)sL * (height - 1) + width, endR = (long)sR * (height - 1) + width;
   if (n < kGroupThreshold) {
     // fewer pairs than lanes to fill the chip: 16 lanes per pair
     const int per = kGroupBlock / 16;
     int blocks = (n + per - 1) / per;
     hipLaunchKernelGGL(mi_pairs_group_kernel, dim3(blocks), dim3(kGroupBlock), 0, c->stream, dL, sL, dR, sR, dxyL,
-                       dxyR, n, pw, ph, inv_count((long)pw * ph), gtab, dout);
+                       dxyR, n, pw, ph, inv_count((long)pw * ph), gtab, dout, endL, endR);
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
   const int npx = pw * ph;
   if (pw > 12) {  // wider than one realigned 16-byte row load: the group kernel handles any shape
     const int per = kGroupBlock / 16;
     hipLaunchKernelGGL(mi_pairs_group_kernel, dim3((n + per - 1) / per), dim3(kGroupBlock), 0, c->stream, dL, sL, dR,
-                       sR, dxyL, dxyR, n, pw, ph, inv_count((long)npx), gtab, dout);
+                       sR, dxyL, dxyR, n, pw, ph, inv_count((long)npx), gtab, dout, endL, endR);
     return me_check_launch(c, "mi_pairs_group_kernel");
   }
   const float* tab;

@@ -270,8 +270,10 @@ constexpr int kTracksPerBlock = kScBlock / 16;
 
 template <bool BIN>
 __device__ __forceinline__ float grp_mi(GroupHist<16>& h, const uint8_t* A, int ax, int ay, const uint8_t* B, int bx,
-                                        int by, int stride, int P, float invN, const float* tab) {
-  return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN, tab);
+                                        int by, int stride, int P, float invN, const float* tab, int rows, int cols) {
+  const long end = (long)(rows - 1) * stride + cols;  // one past each image's last byte (the row form's bound)
+  return group_mi<BIN>(h, A + (long)ay * stride + ax, stride, B + (long)by * stride + bx, stride, P, P, invN, tab,
+                       A + end, B + end);
 }
 
 // Stores a later workgroup of the same launch reduces (residual rows, JJ / Je
@@ -313,10 +315,10 @@ __device__ void residual_track(const ScaleArgs& a, const TrackDev& td, int t, Gr
   float mi;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, lx, ly, P);
-    mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN, a.tab);
+    mi = grp_mi<false>(h, a.imgL, lx, ly, a.imgR, rx, ry, a.stride, P, a.invN, a.tab, a.rows, a.cols);
   } else {
     if (a.weighting) wv = sobel_weight(a.imgR, a.stride, a.cols, a.rows, rx, ry, P);
-    mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN, a.tab);
+    mi = grp_mi<false>(h, a.imgR, rx, ry, a.imgL, lx, ly, a.stride, P, a.invN, a.tab, a.rows, a.cols);
   }
   if (h.gl == 0) wt_store(&res[row], (double)mi * wv);
 }
@@ -368,8 +370,8 @@ __device__ void neq_track(const ScaleArgs& a, const TrackDev& td, int t, GroupHi
   const uint8_t* I0 = left ? a.imgL : a.imgR;
   const uint8_t* I1 = left ? a.imgR : a.imgL;
   double wv = a.weighting ? sobel_weight(I0, a.stride, a.cols, a.rows, x0x, x0y, P) : 1.0;
-  double MIp = grp_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN, a.tab);
-  double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN, a.tab);
+  double MIp = grp_mi<false>(h, I1, x2x, x2y, I0, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
+  double MIm = grp_mi<false>(h, I1, x1x, x1y, I0, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) {
     wt_store(&jj[t], J * J * wv);
@@ -425,12 +427,12 @@ __global__ __launch_bounds__(kScBlock) void scale_jac_kernel(ScaleArgs a, TrackD
   double MIp, MIm, wv = 1.0;
   if (left) {
     if (a.weighting) wv = sobel_weight(a.imgL, a.stride, a.cols, a.rows, x0x, x0y, P);
-    MIp = grp_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab);
-    MIm = grp_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab);
+    MIp = grp_mi<false>(h, a.imgR, x2x, x2y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
+    MIm = grp_mi<false>(h, a.imgR, x1x, x1y, a.imgL, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
   } else {
     if (a.weighting) wv = sobel_weight_bin(a.imgR, a.stride, x0x, x0y, P);
-    MIp = grp_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab);
-    MIm = grp_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab);
+    MIp = grp_mi<true>(h, a.imgL, x2x, x2y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
+    MIm = grp_mi<true>(h, a.imgL, x1x, x1y, a.imgR, x0x, x0y, a.stride, P, a.invN, a.tab, a.rows, a.cols);
   }
   double J = (MIp - MIm) / 1.0 * duds;
   if (h.gl == 0) jj[t] = J * J * wv;
