@@ -282,6 +282,34 @@ def cmd_cam_ts(a):
                       "reduce_when_last": round(buf[4] / max(buf[5], 1))}))
 
 
+def cmd_step_ts(a):
+    """pt_step workgroup 0's phases and the finalizing workgroup's tail (a
+    -DME_STEP_TS=1 build), s_memtime ticks per launch."""
+    from uasl_motion_estimation_amd.optimisation import DeviceBAProblem, SolverOptions
+    ctx = _setup(a.lib)
+    fn = ctx.lib.me_step_ts
+    fn.argtypes = [ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
+    buf = (ctypes.c_longlong * 8)()
+    d = DeviceBAProblem(_ba_problem(a.config), ctx)
+    o = SolverOptions.fixed_iterations(10)
+    for _ in range(3):
+        d.reset()
+        d.solve(o)
+    ctx.synchronize()
+    fn(buf, 1)
+    for _ in range(20):
+        d.reset()
+        d.solve(o)
+    ctx.synchronize()
+    fn(buf, 0)
+    n = max(buf[0], 1)
+    names = ["issue", "slot_sums", "point_solve", "cand_cost", "blocksum_store"]
+    out = {k: round(buf[i + 1] / n) for i, k in enumerate(names)}
+    out["launches"] = buf[0]
+    out["finalize"] = round(buf[6] / max(buf[7], 1))
+    print(json.dumps(out))
+
+
 def cmd_schur_stamps(a):
     from uasl_motion_estimation_amd.optimisation import SolverOptions, ba_solve
     ctx = _setup(a.lib)
@@ -315,6 +343,8 @@ def main():
     p.add_argument("configs", nargs="?", default="3,5")
     p = sub.add_parser("scale_ts")
     p.add_argument("--front", type=int, default=0)
+    p = sub.add_parser("step_ts")
+    p.add_argument("--config", default="3")
     p = sub.add_parser("cam_ts")
     p.add_argument("--config", default="3")
     p = sub.add_parser("schur_stamps")

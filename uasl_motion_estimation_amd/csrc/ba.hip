@@ -2384,6 +2384,33 @@ constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 // -(g_c.y_c + y_c^T U_c y_c / 2) (cam_solve).  The same quantity as the
 // per-observation form (rounding aside), without the per-observation Jacobian
 // traffic (320 B / observation written by linearize and read here before).
+#ifdef ME_STEP_TS  // timing experiment only: phase split of pt_step workgroup 0 (and of the finalizing workgroup)
+__device__ unsigned long long g_step_ts[8];
+#define STEP_T(i)                                                                          \
+  do {                                                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0) {                                             \
+      const long long t_ = (long long)__builtin_amdgcn_s_memtime();                        \
+      if ((i) > 0) atomicAdd(&g_step_ts[(i)], (unsigned long long)(t_ - step_prev_));      \
+      else atomicAdd(&g_step_ts[0], 1ull);                                                 \
+      step_prev_ = t_;                                                                     \
+    }                                                                                      \
+  } while (0)
+#define STEP_FIN_T(i)                                                                      \
+  do {                                                                                     \
+    if (threadIdx.x == 0) {                                                                \
+      const long long t_ = (long long)__builtin_amdgcn_s_memtime();                        \
+      atomicAdd(&g_step_ts[(i)], (unsigned long long)(t_ - fin_prev_));                    \
+      fin_prev_ = t_;                                                                      \
+    }                                                                                      \
+  } while (0)
+#else
+#define STEP_T(i) \
+  do {            \
+  } while (0)
+#define STEP_FIN_T(i) \
+  do {                \
+  } while (0)
+#endif
 template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
@@ -2392,6 +2419,10 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   // workgroup of the solve launch, late joiners included, has finished)
   if (blockIdx.x == 0 && threadIdx.x < 2) b.roster[threadIdx.x] = 0u;
   if (st->done) return;
+#ifdef ME_STEP_TS
+  long long step_prev_ = 0, fin_prev_ = 0;
+#endif
+  STEP_T(0);
   const int gl = threadIdx.x & (kStepG - 1);
   const int j = blockIdx.x * kStepPts + (threadIdx.x / kStepG);
   double mc = 0, cc = 0, s2 = 0, xn2 = 0;
@@ -2438,6 +2469,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     double cv0[6];
     if (has0)
       for (int a = 0; a < 6; ++a) cv0[a] = cams_c[6 * cam0 + a];
+    STEP_T(1);  // (the first round of loads issued; returns at first use below)
     // (1) sum over the point's slots of W_q^T (Dc y_c)
     double t[3] = {0.0, 0.0, 0.0};
     for (int q = q0; q < end; q += kStepG) {
@@ -2459,6 +2491,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       }
     }
     for (int c = 0; c < 3; ++c) t[c] = group_sum<kStepG>(t[c]);
+    STEP_T(2);  // slot sums (loads of the first slot returned)
     // (2) point step y_p = -(V + D/r)^-1 (g_p + sum) in the scaled space, candidate point
     double rhs[3];
     for (int c = 0; c < 3; ++c) rhs[c] = -gpv[c] - t[c] * psv[c];
@@ -2486,6 +2519,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       }
       mc = -(gy + 0.5 * yvy + cross);
     }
+    STEP_T(3);  // point solve, candidate point
     // (3) candidate cost of the point's observations
     for (int q = q0; q < end; q += kStepG) {
       const bool first = q == q0;
@@ -2513,6 +2547,7 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       cc += 0.5 * rho0;
     }
   }
+  STEP_T(4);  // candidate costs
   double v4[4] = {mc, cc, s2, xn2}, out[4];
   block_sum<4>(v4, out, lds);
   if (threadIdx.x == 0) {
@@ -2523,8 +2558,16 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
   }
   // the last workgroup to finish reduces the partials (step_finalize) and,
   // single-GPU, runs the Ceres step handling
+  STEP_T(5);  // block sum + partial stores
   if (!last_arrival_wt(b.cnt + g.m, gridDim.x)) return;
+#ifdef ME_STEP_TS
+  if (threadIdx.x == 0) fin_prev_ = (long long)__builtin_amdgcn_s_memtime();
+#endif
   step_finalize_body(g, b, o, do_decide);
+  STEP_FIN_T(6);  // the finalizing workgroup: partial reduce + decide
+#ifdef ME_STEP_TS
+  if (threadIdx.x == 0) atomicAdd(&g_step_ts[7], 1ull);
+#endif
 }
 
 __global__ void decide_kernel(Geo g, Bufs b, Opts o) {
@@ -4245,6 +4288,19 @@ extern "C" int me_cam_ts(long long* out, int reset) {
   if (reset) {
     const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_cam_ts), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
+#ifdef ME_STEP_TS
+extern "C" int me_step_ts(long long* out, int reset) {
+  unsigned long long h[8];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_step_ts), sizeof h) != hipSuccess) return -1;
+  for (int i = 0; i < 8; ++i) out[i] = (long long)h[i];
+  if (reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_ts), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;
 }
