@@ -289,7 +289,7 @@ def cmd_step_ts(a):
     ctx = _setup(a.lib)
     fn = ctx.lib.me_step_ts
     fn.argtypes = [ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]
-    buf = (ctypes.c_longlong * 8)()
+    buf = (ctypes.c_longlong * 12)()
     d = DeviceBAProblem(_ba_problem(a.config), ctx)
     o = SolverOptions.fixed_iterations(10)
     for _ in range(3):
@@ -303,10 +303,12 @@ def cmd_step_ts(a):
     ctx.synchronize()
     fn(buf, 0)
     n = max(buf[0], 1)
+    nf = max(buf[7], 1)
     names = ["issue", "slot_sums", "point_solve", "cand_cost", "blocksum_store"]
     out = {k: round(buf[i + 1] / n) for i, k in enumerate(names)}
     out["launches"] = buf[0]
-    out["finalize"] = round(buf[6] / max(buf[7], 1))
+    out["finalize"] = round(buf[6] / nf)
+    out["fin_loads"], out["fin_blocksum"], out["fin_decide"] = (round(buf[k] / nf) for k in (8, 9, 10))
     print(json.dumps(out))
 
 

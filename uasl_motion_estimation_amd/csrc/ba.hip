@@ -2289,103 +2289,90 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
 // in a collective the others no longer issue.
 constexpr double kSpinFlag = 65536.0;
 
-__device__ void decide(Bufs& b, const Opts& o) {
-  State* st = b.st;
-  st->accepted = 0;
-  if (b.scal[R_COUNT] >= kSpinFlag) {
-    st->spin_err = 1;
-    st->done = 1;
-    st->termination = 2;
+// The Ceres step handling on a State-like object (the device State itself,
+// or the finalizing thread's register copy) and the reduced step scalars.
+template <class S>
+__device__ __forceinline__ void decide_t(S& st, const double* scal, const Opts& o) {
+  st.accepted = 0;
+  if (scal[R_COUNT] >= kSpinFlag) {
+    st.spin_err = 1;
+    st.done = 1;
+    st.termination = 2;
     return;
   }
-  const double model_change = b.scal[R_MODEL];
-  const bool fail = st->fail || b.scal[R_COUNT] != 0.0;
-  st->fail = 0;  // consumed: the next iteration starts clean
+  const double model_change = scal[R_MODEL];
+  const bool fail = st.fail || scal[R_COUNT] != 0.0;
+  st.fail = 0;  // consumed: the next iteration starts clean
   if (fail || !(model_change > 0.0)) {
-    st->invalid_count += 1;
-    if (st->invalid_count >= o.max_invalid) {
-      st->done = 1;
-      st->termination = 2;
+    st.invalid_count += 1;
+    if (st.invalid_count >= o.max_invalid) {
+      st.done = 1;
+      st.termination = 2;
       return;
     }
-    st->radius = st->radius / st->decrease;
-    st->decrease *= 2.0;
+    st.radius = st.radius / st.decrease;
+    st.decrease *= 2.0;
     return;
   }
-  st->invalid_count = 0;
-  const double cand_cost = b.scal[R_CAND];
-  const double step_norm = sqrt(b.scal[R_STEP2] + st->cam_step2);
-  const double x_norm = sqrt(b.scal[R_XN2] + st->cam_xn2);
-  st->cand_cost = cand_cost;
-  st->model_change = model_change;
+  st.invalid_count = 0;
+  const double cand_cost = scal[R_CAND];
+  const double step_norm = sqrt(scal[R_STEP2] + st.cam_step2);
+  const double x_norm = sqrt(scal[R_XN2] + st.cam_xn2);
+  st.cand_cost = cand_cost;
+  st.model_change = model_change;
   if (step_norm <= o.parameter_tolerance * (x_norm + o.parameter_tolerance)) {
-    st->done = 1;
-    st->termination = 0;
+    st.done = 1;
+    st.termination = 0;
     return;
   }
-  if (fabs(st->x_cost - cand_cost) <= o.function_tolerance * st->x_cost) {
-    st->done = 1;
-    st->termination = 0;
+  if (fabs(st.x_cost - cand_cost) <= o.function_tolerance * st.x_cost) {
+    st.done = 1;
+    st.termination = 0;
     return;
   }
-  const double q = (st->x_cost - cand_cost) / model_change;
-  st->last_q = q;
+  const double q = (st.x_cost - cand_cost) / model_change;
+  st.last_q = q;
   if (q > o.min_rel_decrease) {
-    st->cur = 1 - st->cur;
-    st->x_cost = cand_cost;
-    st->successful += 1;
-    st->accepted = 1;
+    st.cur = 1 - st.cur;
+    st.x_cost = cand_cost;
+    st.successful += 1;
+    st.accepted = 1;
     const double t = 2.0 * q - 1.0;
-    st->radius = st->radius / fmax(1.0 / 3.0, 1.0 - pow(t, 3.0));
-    st->radius = fmin(o.max_radius, st->radius);
-    st->decrease = 2.0;
-    st->need_lin = 1;
+    st.radius = st.radius / fmax(1.0 / 3.0, 1.0 - pow(t, 3.0));
+    st.radius = fmin(o.max_radius, st.radius);
+    st.decrease = 2.0;
+    st.need_lin = 1;
   } else {
-    st->radius = st->radius / st->decrease;
-    st->decrease *= 2.0;
+    st.radius = st.radius / st.decrease;
+    st.decrease *= 2.0;
   }
 }
 
-__device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_decide) {
-  __shared__ double lds[32];
-  State* st = b.st;
-  double v[4] = {0, 0, 0, 0};
-  for (int i = threadIdx.x; i < g.nblk_step; i += blockDim.x) {  // (written through by pt_step's workgroups)
-    v[0] += a_ld<true>(&b.part[R_MODEL * g.pstride + i]);
-    v[1] += a_ld<true>(&b.part[R_CAND * g.pstride + i]);
-    v[2] += a_ld<true>(&b.part[R_STEP2 * g.pstride + i]);
-    v[3] += a_ld<true>(&b.part[R_XN2 * g.pstride + i]);
-  }
-  double out[4];
-  block_sum<4>(v, out, lds);
-  if (threadIdx.x == 0) {
-    b.scal[R_MODEL] = out[0] + st->cam_model;  // (+ this rank's camera part, cam_solve)
-    b.scal[R_CAND] = out[1];
-    b.scal[R_STEP2] = out[2];
-    b.scal[R_XN2] = out[3];
-    b.scal[R_COUNT] = st->fail ? (st->spin_err ? kSpinFlag : 1.0) : 0.0;
-    if (do_decide) decide(b, o);
-  }
-}
+__device__ void decide(Bufs& b, const Opts& o) { decide_t(*b.st, b.scal, o); }
 
-// (64-thread workgroups measured slower: 17.2 -> 21.6 us at config 3, the
-// last arrival then reduces 4x the partials)
-// (Measured and dropped, round 4 as in rounds 2-3: the step linearising
-// speculatively at its candidate into a second obsx / Wo set, removing the
-// linearize launch of every accepted step -- the step went 15.1 -> 28.7 us
-// for 9.3 us saved; config 3 BA 0.821 -> 0.894 ms per 10 iterations.)
-constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
+// The fields decide_t reads or writes, loaded by the finalizing thread in one
+// round before the partial reduce (round 6: the decision's dependent State
+// loads were half of the step's finalize tail, ME_STEP_TS)
+struct DecideState {
+  int cur, need_lin, done, termination, successful, invalid_count, fail, accepted, spin_err;
+  double radius, decrease, x_cost, cand_cost, model_change, cam_step2, cam_xn2, cam_model, last_q;
+  __device__ __forceinline__ void load(const State* st) {
+    cur = st->cur; need_lin = st->need_lin; done = st->done; termination = st->termination;
+    successful = st->successful; invalid_count = st->invalid_count; fail = st->fail; accepted = st->accepted;
+    spin_err = st->spin_err; radius = st->radius; decrease = st->decrease; x_cost = st->x_cost;
+    cand_cost = st->cand_cost; model_change = st->model_change; cam_step2 = st->cam_step2; cam_xn2 = st->cam_xn2;
+    cam_model = st->cam_model; last_q = st->last_q;
+  }
+  __device__ __forceinline__ void store(State* st) const {
+    st->cur = cur; st->need_lin = need_lin; st->done = done; st->termination = termination;
+    st->successful = successful; st->invalid_count = invalid_count; st->fail = fail; st->accepted = accepted;
+    st->spin_err = spin_err; st->radius = radius; st->decrease = decrease; st->x_cost = x_cost;
+    st->cand_cost = cand_cost; st->model_change = model_change; st->last_q = last_q;
+  }
+};
 
-// Model cost change in the normal-equation form (Ceres computes
-// -(J dx).(r + J dx / 2) per residual block; summed over the blocks that is
-// -(g.dx + dx^T J^T J dx / 2) with g = J^T r): per point, in the scaled space,
-// -(g_p.y_p + y_p^T V_p y_p / 2 + (D_p y_p).sum_q W_q^T (D_c y_c)) -- the last
-// sum is the one the point's back-substitution forms anyway -- and per camera
-// -(g_c.y_c + y_c^T U_c y_c / 2) (cam_solve).  The same quantity as the
-// per-observation form (rounding aside), without the per-observation Jacobian
-// traffic (320 B / observation written by linearize and read here before).
 #ifdef ME_STEP_TS  // timing experiment only: phase split of pt_step workgroup 0 (and of the finalizing workgroup)
-__device__ unsigned long long g_step_ts[8];
+__device__ unsigned long long g_step_ts[12];
 #define STEP_T(i)                                                                          \
   do {                                                                                     \
     if (blockIdx.x == 0 && threadIdx.x == 0) {                                             \
@@ -2411,6 +2398,89 @@ __device__ unsigned long long g_step_ts[8];
   do {                \
   } while (0)
 #endif
+__device__ void step_finalize_body(const Geo& g, Bufs b, const Opts& o, int do_decide) {
+  __shared__ double rows[1024 / 16 * 4];
+  State* st = b.st;
+#ifdef ME_STEP_TS
+  long long f0 = (long long)__builtin_amdgcn_s_memtime();
+#endif
+  // the decision's State fields, requested with the partials (one round)
+  DecideState ds;
+  if (threadIdx.x == 0) ds.load(st);
+  double v[4] = {0, 0, 0, 0};
+  for (int i = threadIdx.x; i < g.nblk_step; i += blockDim.x) {  // (written through by pt_step's workgroups)
+    v[0] += a_ld<true>(&b.part[R_MODEL * g.pstride + i]);
+    v[1] += a_ld<true>(&b.part[R_CAND * g.pstride + i]);
+    v[2] += a_ld<true>(&b.part[R_STEP2 * g.pstride + i]);
+    v[3] += a_ld<true>(&b.part[R_XN2 * g.pstride + i]);
+  }
+#ifdef ME_STEP_TS
+  if (threadIdx.x == 0) {
+    const long long t_ = (long long)__builtin_amdgcn_s_memtime();
+    atomicAdd(&g_step_ts[8], (unsigned long long)(t_ - f0));
+    f0 = t_;
+  }
+#endif
+  // the block's sums: 16-lane row sums by DPP, then the rows in order (VALU and
+  // one LDS round; round 6: six lane-shuffle rounds per value before)
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    double x = v[u];
+    x += dpp_f64<kDppQuadSwap1>(x);
+    x += dpp_f64<kDppQuadSwap2>(x);
+    x += dpp_f64<kDppRowHalfMirror>(x);
+    x += dpp_f64<kDppRowMirror>(x);
+    v[u] = x;
+  }
+  if ((threadIdx.x & 15) == 0)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) rows[(threadIdx.x >> 4) * 4 + u] = v[u];
+  __syncthreads();
+#ifdef ME_STEP_TS
+  if (threadIdx.x == 0) {
+    const long long t_ = (long long)__builtin_amdgcn_s_memtime();
+    atomicAdd(&g_step_ts[9], (unsigned long long)(t_ - f0));
+    f0 = t_;
+  }
+#endif
+  if (threadIdx.x == 0) {
+    double out[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int r = 0; r < (int)(blockDim.x >> 4); ++r)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) out[u] += rows[r * 4 + u];
+    double scal[R_COUNT + 1];
+    scal[R_MODEL] = out[0] + ds.cam_model;  // (+ this rank's camera part, cam_solve)
+    scal[R_CAND] = out[1];
+    scal[R_STEP2] = out[2];
+    scal[R_XN2] = out[3];
+    scal[R_COUNT] = ds.fail ? (ds.spin_err ? kSpinFlag : 1.0) : 0.0;
+    for (int k = R_MODEL; k <= R_COUNT; ++k) b.scal[k] = scal[k];
+    if (do_decide) {
+      decide_t(ds, scal, o);
+      ds.store(st);
+    }
+#ifdef ME_STEP_TS
+    atomicAdd(&g_step_ts[10], (unsigned long long)((long long)__builtin_amdgcn_s_memtime() - f0));
+#endif
+  }
+}
+
+// (64-thread workgroups measured slower: 17.2 -> 21.6 us at config 3, the
+// last arrival then reduces 4x the partials)
+// (Measured and dropped, round 4 as in rounds 2-3: the step linearising
+// speculatively at its candidate into a second obsx / Wo set, removing the
+// linearize launch of every accepted step -- the step went 15.1 -> 28.7 us
+// for 9.3 us saved; config 3 BA 0.821 -> 0.894 ms per 10 iterations.)
+constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
+
+// Model cost change in the normal-equation form (Ceres computes
+// -(J dx).(r + J dx / 2) per residual block; summed over the blocks that is
+// -(g.dx + dx^T J^T J dx / 2) with g = J^T r): per point, in the scaled space,
+// -(g_p.y_p + y_p^T V_p y_p / 2 + (D_p y_p).sum_q W_q^T (D_c y_c)) -- the last
+// sum is the one the point's back-substitution forms anyway -- and per camera
+// -(g_c.y_c + y_c^T U_c y_c / 2) (cam_solve).  The same quantity as the
+// per-observation form (rounding aside), without the per-observation Jacobian
+// traffic (320 B / observation written by linearize and read here before).
 template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
@@ -4295,11 +4365,11 @@ extern "C" int me_cam_ts(long long* out, int reset) {
 
 #ifdef ME_STEP_TS
 extern "C" int me_step_ts(long long* out, int reset) {
-  unsigned long long h[8];
+  unsigned long long h[12];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_step_ts), sizeof h) != hipSuccess) return -1;
-  for (int i = 0; i < 8; ++i) out[i] = (long long)h[i];
+  for (int i = 0; i < 12; ++i) out[i] = (long long)h[i];
   if (reset) {
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_step_ts), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;
