@@ -28,14 +28,13 @@ constexpr double kDblMin = 2.2250738585072014e-308;
 constexpr double kDblEps = 2.220446049250313e-16;
 
 // ---------------------------------------------------------------- helpers
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double x);
+__device__ __forceinline__ double wave_total(double x);
 template <int NV>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double* out, double* lds /* nw*NV */, int nw_active = 0) {
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    double x = v[i];
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-    v[i] = x;
-  }
+  for (int i = 0; i < NV; ++i) v[i] = wave_total(v[i]);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0)
 #pragma unroll
@@ -86,6 +85,22 @@ __device__ __forceinline__ double group_sum(double x) {
   if (W >= 32) x += __shfl_xor(x, 16, W);
   if (W >= 64) x += __shfl_xor(x, 32, W);
   return x;
+}
+
+// The wave's sum in every lane, VALU only: the 16-lane row sums by DPP
+// (quad swaps, half mirror, mirror), then the four row sums by readlane,
+// added in row order (round 6: six dependent ds_bpermute rounds per value
+// before -- 3.2k of the step finalize's 7.8k ticks, ME_STEP_TS).
+__device__ __forceinline__ double wave_total(double x) {
+  x += dpp_f64<kDppQuadSwap1>(x);
+  x += dpp_f64<kDppQuadSwap2>(x);
+  x += dpp_f64<kDppRowHalfMirror>(x);
+  x += dpp_f64<kDppRowMirror>(x);
+  auto row = [&](int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+  };
+  return ((row(0) + row(16)) + row(32)) + row(48);
 }
 
 __device__ __forceinline__ double block_max(double v, double* lds) {
