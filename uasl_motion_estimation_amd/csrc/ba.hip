@@ -1535,6 +1535,7 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
       np = me_roster::count_or_abandon<me_roster_dev>(b.roster);
       if (np < 0) {  // a first closer that never published (not reachable: it is running)
         b.st->spin_err = 1;
+        atomicOr(&b.st->pad[0], 1);  // spin site: worker roster count
         pid = -1;
       } else if (pid >= np) {
         pid = -1;  // the roster was abandoned (np = 0): block 0 updates every tile
@@ -1560,7 +1561,10 @@ __device__ void cam_solve_worker(const Geo& g, const Bufs& b, int nworkers) {
         __builtin_amdgcn_s_sleep(2);
       }
       sep = k == kSolveSpin ? kSolveTerm : e;
-      if (k == kSolveSpin) b.st->spin_err = 1;  // block 0 never published the step: the solve ends in error
+      if (k == kSolveSpin) {  // block 0 never published the step: the solve ends in error
+        b.st->spin_err = 1;
+        atomicOr(&b.st->pad[0], 2);  // spin site: worker step poll
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
     __syncthreads();
@@ -1727,8 +1731,20 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
     }
     __syncthreads();
     if (s_steal) {
+      __shared__ int s_taken;
       for (int u = 0; u < nasm; ++u) {
-        if (__hip_atomic_load(b.asm_claim + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= asm_gen) continue;
+        // one decision for the whole workgroup (thread 0's load, through LDS):
+        // per-wave loads could see an assembler's claim land between them, and
+        // waves that skipped the unit would then meet the others' barriers
+        // inside s_assemble_body at the wrong place (round 6: the count never
+        // completed -- an intermittent hand-off timeout with another process on
+        // the GPU)
+        if (threadIdx.x == 0)
+          s_taken = __hip_atomic_load(b.asm_claim + u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= asm_gen;
+        __syncthreads();
+        const bool taken = s_taken != 0;
+        __syncthreads();  // s_taken is rewritten for the next unit
+        if (taken) continue;
         const bool mine = s_assemble_body<kSolveBlock, true>(g, b, u, 0, b.xch ? SA_UNPACK : SA_SUM,
                                                              kLds || ME_SOLVE_IMG ? b.Abuf : nullptr, &o,
                                                              b.asm_claim + u, asm_gen);
@@ -1752,6 +1768,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
           // in error (a late count may still come, so the counter is not
           // re-armed: the next plan clears it)
           spin_timeout(b);
+          atomicOr(&b.st->pad[0], 4);  // spin site: fused assemblers' count
         } else {
           __hip_atomic_store(asm_cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next iteration
         }
@@ -1931,6 +1948,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
       if (k == kSolveSpin) {
         sfail = 1;
         st->spin_err = 1;
+        atomicOr(&st->pad[0], 8);  // spin site: LDS-form step flags (pflag / pdone)
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     };
@@ -2020,6 +2038,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         if (k == kSolveSpin) {  // a worker not co-resident (narrow CU mask, busy CUs): the solve ends in error
           sfail = 1;
           st->spin_err = 1;
+          atomicOr(&st->pad[0], 16);  // spin site: workers' step count
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the loads behind the poll
@@ -2191,6 +2210,7 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
         if (k == kSolveSpin) {
           sfail = 1;
           st->spin_err = 1;
+          atomicOr(&st->pad[0], 32);  // spin site: backward-solve block flags
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       }
@@ -3715,8 +3735,12 @@ int finish(Plan& P, me_ba_problem* p, me_ba_summary* sum, bool output_queued = f
   }
   if (st.bad_input) return me_set_error(c, ME_ERR_INVALID, "BA: an observation indexes outside the window");
   if (st.spin_err)
-    return me_set_error(c, ME_ERR_STATE, "BA: a cross-workgroup hand-off of the camera solve timed out "
-                                         "(workgroups not co-resident: CU mask or concurrent persistent kernels)");
+    return me_set_error(c, ME_ERR_STATE,
+                        "BA: a cross-workgroup hand-off of the camera solve timed out (workgroups not co-resident: "
+                        "CU mask or concurrent persistent kernels; wait sites 0x%x: 1 worker roster, 2 worker step "
+                        "poll, 4 fused assemblers, 8 LDS step flags, 16 workers' count, 32 backward flags, 0 the "
+                        "step exchange)",
+                        (unsigned)st.pad[0]);
   if (sum) {
     sum->termination = st.termination;
     sum->iterations = st.iterations;
