@@ -1695,17 +1695,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const bool fused = kMode != 2 && nasm > 0;
   STS_DECL;
   STS_BEGIN();
-  // the tail's camera part of the model cost change needs row r of U and
-  // g_c[r] (earlier launches): requested now, consumed after the backward
-  // solve, off its latency
-  const bool upre = g.n6 <= (int)blockDim.x;
-  double urow[6] = {0, 0, 0, 0, 0, 0}, gcr = 0.0;
-  if (upre && (int)threadIdx.x < g.n6) {
-    const double* Ur = b.U + 36 * (long)(threadIdx.x / 6) + 6 * (threadIdx.x % 6);
-#pragma unroll
-    for (int k = 0; k < 6; ++k) urow[k] = Ur[k];
-    gcr = b.gcs[threadIdx.x];
-  }
   __shared__ int s_steal;
   if (fused) {
     lin_finalize_body(g, b, o, gc_raw, red);
@@ -1794,16 +1783,6 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   const int fail_in = st->fail || st->spin_err || (fused ? (b.xch && b.xch[xo_fail(g)] != 0.0) : b.scal[R_COUNT] != 0.0) ||
                       (skip & 1024);  // (1024: test hook, a forced solve failure)
   const double radius = st->radius;
-  // the candidate-camera inputs (current cameras, Jacobi scales) are requested
-  // now; they are consumed after the factorisation, which hides their latency
-  const int cur = st->cur;
-  const int ncp = 6 * g.nc;
-  const bool pre = ncp <= nt;
-  double x_pre = 0.0, cs_pre = 1.0;
-  if (pre && tid < ncp) {
-    x_pre = b.cams[cur][tid];
-    if (tid >= 6 * g.nf) cs_pre = b.csc[tid - 6 * g.nf];
-  }
   // [S + D; -b^T]: every load of a batch is issued from a computed index
   // before the first use, so a batch costs one round of global latency.
   // (Per-element branches with the use inside them made the compiler wait on
@@ -2266,43 +2245,10 @@ __global__ __launch_bounds__(kSolveBlock) void cam_solve_kernel(Geo g, Bufs b, O
   }
   SOLVE_STAMP(5);
   STS(5);
+  // the scaled camera step; the candidate cameras and the camera part of the
+  // model cost change are pt_step's camera workgroup (cam_step_body), beside
+  // the points -- off this launch's serial tail
   for (int r = tid; r < n; r += nt) b.yc[r] = u[r];
-  // candidate cameras
-  const double* x = b.cams[cur];
-  double* xc = b.cams[1 - cur];
-  double s2 = 0, xn2 = 0;
-  for (int i = tid; i < ncp; i += nt) {
-    const double xi = pre ? x_pre : x[i];
-    const int ci = i / 6 - g.nf;
-    if (ci < 0) {
-      xc[i] = xi;
-      continue;
-    }
-    const double d = u[i - 6 * g.nf] * (pre ? cs_pre : b.csc[i - 6 * g.nf]);
-    b.dc[i - 6 * g.nf] = d;
-    const double v = xi + d;
-    xc[i] = v;
-    const double dd = v - xi;
-    s2 += dd * dd;
-    xn2 += xi * xi;
-  }
-  // camera part of the model cost change (scaled space; see pt_step_kernel)
-  double cm = 0;
-  for (int r = tid; r < n; r += nt) {
-    const double* U = b.U + 36 * (long)(r / 6) + 6 * (r % 6);
-    const int c0 = r - r % 6;
-    double uy = 0.0;
-#pragma unroll
-    for (int k = 0; k < 6; ++k) uy += (upre ? urow[k] : U[k]) * u[c0 + k];
-    cm += (upre ? gcr : b.gcs[r]) * u[r] + 0.5 * u[r] * uy;
-  }
-  double v2[3] = {s2, xn2, -cm}, out[3];
-  block_sum<3>(v2, out, red);
-  if (tid == 0) {
-    st->cam_step2 = out[0];
-    st->cam_xn2 = out[1];
-    st->cam_model = out[2];
-  }
   STS(6);
   STS_END();
 }
@@ -2395,8 +2341,11 @@ struct DecideState {
     cur = st->cur; need_lin = st->need_lin; done = st->done; termination = st->termination;
     successful = st->successful; invalid_count = st->invalid_count; fail = st->fail; accepted = st->accepted;
     spin_err = st->spin_err; radius = st->radius; decrease = st->decrease; x_cost = st->x_cost;
-    cand_cost = st->cand_cost; model_change = st->model_change; cam_step2 = st->cam_step2; cam_xn2 = st->cam_xn2;
-    cam_model = st->cam_model; last_q = st->last_q;
+    cand_cost = st->cand_cost; model_change = st->model_change; last_q = st->last_q;
+    // (written through by this launch's camera workgroup, cam_step_body)
+    cam_step2 = a_ld<true>(&st->cam_step2);
+    cam_xn2 = a_ld<true>(&st->cam_xn2);
+    cam_model = a_ld<true>(&st->cam_model);
   }
   __device__ __forceinline__ void store(State* st) const {
     st->cur = cur; st->need_lin = need_lin; st->done = done; st->termination = termination;
@@ -2516,6 +2465,59 @@ constexpr int kStepG = 16, kStepBlock = 256, kStepPts = kStepBlock / kStepG;
 // -(g_c.y_c + y_c^T U_c y_c / 2) (cam_solve).  The same quantity as the
 // per-observation form (rounding aside), without the per-observation Jacobian
 // traffic (320 B / observation written by linearize and read here before).
+
+// Candidate camera parameter: x + D_c y_c (ys = csc * yc), never contracted
+// into an FMA, so the camera workgroup's stored candidate and the point
+// workgroups' own copies agree bit for bit.
+__device__ __forceinline__ double cam_cand(double x, double ys) {
+#pragma clang fp contract(off)
+  return x + ys;
+}
+
+// The camera workgroup of pt_step (the last one): the candidate cameras and the
+// camera part of the step's scalars, |dx_c|^2, |x_c|^2 and the model change
+// -(g_c.y_c + y_c^T U_c y_c / 2) in the scaled space.  Round 6: this was the
+// camera solve's tail, on its one workgroup's serial path (1.7 us per
+// iteration at config 3, tools/drivers.py solve_ts); here it runs beside the
+// points.  The scalars are written through: this launch's finalizing workgroup
+// reads them (DecideState::load).
+__device__ void cam_step_body(const Geo& g, const Bufs& b, int cur, double* lds) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int n = g.n6, ncp = 6 * g.nc, f6 = 6 * g.nf;
+  const double* x = b.cams[cur];
+  double* xc = b.cams[1 - cur];
+  double s2 = 0.0, xn2 = 0.0, cm = 0.0;
+  for (int i = tid; i < ncp; i += nt) {
+    const double xi = x[i];
+    if (i < f6) {  // fixed camera
+      xc[i] = xi;
+      continue;
+    }
+    const double v = cam_cand(xi, b.csc[i - f6] * b.yc[i - f6]);
+    xc[i] = v;
+    const double dd = v - xi;
+    s2 += dd * dd;
+    xn2 += xi * xi;
+  }
+  for (int r = tid; r < n; r += nt) {
+    const double* U = b.U + 36 * (long)(r / 6) + 6 * (r % 6);
+    const double* y = b.yc + (r - r % 6);
+    const double yr = b.yc[r];
+    double uy = 0.0;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) uy += U[k] * y[k];
+    cm += b.gcs[r] * yr + 0.5 * yr * uy;
+  }
+  double v3[3] = {s2, xn2, -cm}, out[3];
+  block_sum<3>(v3, out, lds);
+  if (tid == 0) {
+    a_st<true>(&b.st->cam_step2, out[0]);
+    a_st<true>(&b.st->cam_xn2, out[1]);
+    a_st<true>(&b.st->cam_model, out[2]);
+  }
+}
+
+// Grid: g.nblk_step point workgroups + the camera workgroup (cam_step_body).
 template <int OD>
 __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts o, int do_decide) {
   __shared__ double lds[16];
@@ -2527,6 +2529,11 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
 #ifdef ME_STEP_TS
   long long step_prev_ = 0, fin_prev_ = 0;
 #endif
+  if ((int)blockIdx.x == g.nblk_step) {
+    // (a failed solve wrote no step; thread 0's scalar stores drain before its
+    // arrival, last_arrival_wt)
+    if (!st->fail) cam_step_body(g, b, st->cur, lds);
+  } else {
   STEP_T(0);
   const int gl = threadIdx.x & (kStepG - 1);
   const int j = blockIdx.x * kStepPts + (threadIdx.x / kStepG);
@@ -2561,7 +2568,9 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
       o0 = b.p_obs[q0];
       for (int i = 0; i < 18; ++i) W0[i] = Wo[18 * (long)q0 + i];  // (unused for a fixed camera)
     }
-    const double* cams_c = b.cams[1 - cur];
+    // candidate cameras x + D_c y_c formed here from the current ones (the
+    // camera workgroup stores the same values, cam_cand; not read back)
+    const double* cams_x = b.cams[cur];
     double ys0[6], f0[4];
     int cam0 = 0, right0 = 0;
     if (has0) {
@@ -2573,7 +2582,10 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     }
     double cv0[6];
     if (has0)
-      for (int a = 0; a < 6; ++a) cv0[a] = cams_c[6 * cam0 + a];
+      for (int a = 0; a < 6; ++a) {
+        const double xa = cams_x[6 * cam0 + a];
+        cv0[a] = ci0 >= 0 ? cam_cand(xa, ys0[a]) : xa;
+      }
     STEP_T(1);  // (the first round of loads issued; returns at first use below)
     // (1) sum over the point's slots of W_q^T (Dc y_c)
     double t[3] = {0.0, 0.0, 0.0};
@@ -2636,8 +2648,11 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
         right = right0;
       } else {
         const int o = b.p_obs[q];
-        const int cam = b.p_cam[q] + g.nf;
-        for (int a = 0; a < 6; ++a) cv[a] = cams_c[6 * cam + a];
+        const int ci = b.p_cam[q], cam = ci + g.nf;
+        for (int a = 0; a < 6; ++a) {
+          const double xa = cams_x[6 * cam + a];
+          cv[a] = ci >= 0 ? cam_cand(xa, b.csc[6 * ci + a] * b.yc[6 * ci + a]) : xa;
+        }
         for (int k = 0; k < OD; ++k) f[k] = b.obs[(long)OD * o + k];
         if (OD == 2) right = b.cam_id[o] != 0;
       }
@@ -2661,9 +2676,10 @@ __global__ __launch_bounds__(kStepBlock) void pt_step_kernel(Geo g, Bufs b, Opts
     a_st<true>(&b.part[R_STEP2 * g.pstride + blockIdx.x], out[2]);
     a_st<true>(&b.part[R_XN2 * g.pstride + blockIdx.x], out[3]);
   }
-  // the last workgroup to finish reduces the partials (step_finalize) and,
-  // single-GPU, runs the Ceres step handling
   STEP_T(5);  // block sum + partial stores
+  }  // (point workgroups)
+  // the last workgroup to finish (of either kind) reduces the partials
+  // (step_finalize) and, single-GPU, runs the Ceres step handling
   if (!last_arrival_wt(b.cnt + g.m, gridDim.x)) return;
 #ifdef ME_STEP_TS
   if (threadIdx.x == 0) fin_prev_ = (long long)__builtin_amdgcn_s_memtime();
@@ -2914,10 +2930,7 @@ __global__ __launch_bounds__(kScanBlock) void plan_scan_kernel(Geo g, Bufs b, Op
     const int k0 = min(g.nblk_obs, lane * bchunk), k1 = min(g.nblk_obs, k0 + bchunk);
     for (int k = k0; k < k1; ++k) w.blk_cam[(long)k * g.nc + g.nf + c] += ctot[c];
   }
-  for (int i = t; i < g.n6; i += kScanBlock) {
-    b.csc[i] = 0.0;
-    b.dc[i] = 0.0;
-  }
+  for (int i = t; i < g.n6; i += kScanBlock) b.csc[i] = 0.0;
   if (t == 0) {
     State* st = b.st;
     st->cur = 0;
@@ -3370,7 +3383,6 @@ int plan_build(me_ctx* c, const me_ba_problem* p, const me_ba_options* opt, Plan
   add(4 * (size_t)g.npairs, &b.tcnt);
   add(8 * (size_t)g.n6 * g.n6 + 8 * (size_t)(2 * g.n6 + 2), &b.S);  // S | b | diagU | fail (contiguous for all-reduce)
   add(8 * (size_t)g.n6, &b.yc);
-  add(8 * (size_t)g.n6, &b.dc);
   add(8 * 3 * (size_t)g.np, &b.dp);
   add(8 * R_COUNT * (size_t)nb, &b.part);
   add(8 * (R_COUNT + 2), &b.scal);
@@ -3685,9 +3697,9 @@ int enqueue_iteration(Plan& P, bool last = false) {
     me_ktimer t(c, ME_KT_BA_STEP);
     // (step partials reduced and, single-GPU, the step decided in its last workgroup)
     if (g.od == 4)
-      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
+      hipLaunchKernelGGL(pt_step_kernel<4>, dim3(g.nblk_step + 1), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
     else
-      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
+      hipLaunchKernelGGL(pt_step_kernel<2>, dim3(g.nblk_step + 1), dim3(kStepBlock), 0, s, g, P.b, P.o, sh ? 0 : 1);
   }
   if (sh) {
     ME_XCH(P.b.scal + R_MODEL, 5, ME_COMM_SUM);  // model change, candidate cost, step^2, |x|^2, failure count

@@ -122,7 +122,6 @@ struct Bufs {
   double* bvec;       // n6
   double* diagU;      // n6 (for the sharded all-reduce)
   double* yc;         // n6
-  double* dc;         // n6 camera step (unscaled)
   double* dp;         // 3np point step (unscaled)
   double* part;       // R_COUNT * max(nblk_obs, nblk_pts)
   double* scal;       // R_COUNT reduced scalars (all-reduce target in sharded mode)
